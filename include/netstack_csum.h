@@ -1,0 +1,170 @@
+/*
+ * netstack_csum.h — C ABI of the MI355X (gfx950) Internet-checksum engine.
+ *
+ * This is the drop-in boundary for google/netstack's checksum hot path.  A cgo
+ * shim in package `header` binds exactly these symbols;
+ * nothing here uses torch or HIP types (streams are passed as `void*`, which is
+ * a hipStream_t, NULL = the context's own stream).
+ *
+ * Reference interfaces replaced (google/netstack @ /root/reference):
+ *   header.Checksum              tcpip/header/checksum.go:52-55   -> ns_csum_checksum
+ *   header.ChecksumVV            tcpip/header/checksum.go:61-63   -> ns_csum_vv_with_offset(off=0,size=Size())
+ *   header.ChecksumVVWithOffset  tcpip/header/checksum.go:69-98   -> ns_csum_vv_with_offset
+ *   header.ChecksumCombine       tcpip/header/checksum.go:104-107 -> ns_csum_combine
+ *   header.PseudoHeaderChecksum  tcpip/header/checksum.go:112-122 -> ns_csum_pseudo_header
+ *   per-view restart loops       transport/udp/endpoint.go:811-813,
+ *                                header/icmpv4.go:158-160, icmpv6.go:210-212
+ *                                                                 -> ns_csum_views_restart
+ *   n x ChecksumVVWithOffset in  transport/tcp/connect.go:668-702 (sendTCPBatch,
+ *   buildTCPHdr :662) over stack.PacketDescriptor{Off,Size}
+ *   (stack/route.go:174-188)                                      -> ns_csum_vv_batch
+ *   the per-packet calculateChecksum (checksum.go:26-46) over a
+ *   device-resident batch                                         -> ns_csum_batch_dev / _host
+ *
+ * Semantics (bit-exact with checksum.go, including its un-folded uint32 wrap for
+ * buffers > 128 KiB): every descriptor d is one calculateChecksum call over
+ * arena[d.off, d.off+d.len) with odd = (d.flags & NS_DESC_ODD) and
+ * initial = d.initial, returning ChecksumCombine(uint16(v), uint16(v>>16)).
+ * A descriptor with NS_DESC_CONT takes as its initial the result of the
+ * descriptor before it (the `sum` chaining of checksum.go:89 / the
+ * `xsum = Checksum(v, xsum)` loops); its own `initial` field is ignored.
+ * Results are the UN-complemented sum, exactly like the Go functions; callers
+ * apply `^` (connect.go:663) or compare with 0xffff (segment.go:180).
+ *
+ * Errors: every function returns NS_OK (0) or a negative NS_E* code; nothing is
+ * silently recomputed on the host.  There is no CPU fallback in this library.
+ */
+#ifndef NETSTACK_CSUM_H_
+#define NETSTACK_CSUM_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NS_CSUM_ABI_VERSION 1
+
+/* ---- status codes ------------------------------------------------------- */
+#define NS_OK 0
+#define NS_EINVAL (-1)     /* bad argument (negative size, NULL pointer, ...)  */
+#define NS_ERANGE (-2)     /* a descriptor reaches past the arena              */
+#define NS_ENODEV (-3)     /* no HIP device / device id out of range           */
+#define NS_ENOMEM (-4)     /* device or pinned allocation failed               */
+#define NS_EHIP (-5)       /* any other HIP runtime error                      */
+
+/* ---- descriptor --------------------------------------------------------- */
+/* bit 0: the previous piece ended mid-word; this piece's first byte is the
+ *        LOW byte of a big-endian word (calculateChecksum's `odd` argument,
+ *        checksum.go:29-32).                                                 */
+#define NS_DESC_ODD 0x1u
+/* bit 1: chain: initial := result of the previous descriptor (checksum.go:89). */
+#define NS_DESC_CONT 0x2u
+
+/* One packet (or one piece of a chained packet).  16 bytes, little-endian,
+ * naturally aligned: maps 1:1 onto stack.PacketDescriptor{Off,Size}
+ * (stack/route.go:174-178) plus the pseudo-header sum as `initial`
+ * (stack/route.go:93-95) — the device-staged layout of tcpip/buffer.        */
+typedef struct ns_pkt_desc {
+  uint64_t off;     /* byte offset of the piece in the arena          */
+  uint32_t len;     /* byte length (0 allowed: result = initial)      */
+  uint16_t initial; /* starting sum (pseudo-header), ignored if CONT  */
+  uint16_t flags;   /* NS_DESC_*                                       */
+} ns_pkt_desc;
+
+/* batch_flags for ns_csum_batch_*: the table contains NS_DESC_CONT entries.
+ * Without it CONT bits are an error-free no-op (each entry is independent). */
+#define NS_BATCH_CHAINED 0x1u
+
+/* A borrowed host byte range: one buffer.View (tcpip/buffer/view.go:19). */
+typedef struct ns_view {
+  const uint8_t* data;
+  uint64_t len;
+} ns_view;
+
+/* One segment of a VectorisedView batch: the (Off, Size) of a
+ * stack.PacketDescriptor (route.go:174-178) plus its pseudo-header sum.     */
+typedef struct ns_seg {
+  int64_t off;
+  int64_t size;
+  uint16_t initial;
+  uint16_t pad0;
+  uint32_t pad1;
+} ns_seg;
+
+/* ---- context -------------------------------------------------------------*/
+typedef struct ns_csum_ctx ns_csum_ctx;
+
+typedef struct ns_csum_opts {
+  int32_t device;          /* HIP device ordinal                            */
+  uint32_t flags;          /* reserved, 0                                   */
+  uint64_t staging_bytes;  /* pinned host staging per buffer (0 = 64 MiB)   */
+} ns_csum_opts;
+
+int ns_csum_abi_version(void);
+const char* ns_csum_strerror(int status);
+int ns_csum_device_count(int* count);
+
+int ns_csum_init(const ns_csum_opts* opts, ns_csum_ctx** out);
+void ns_csum_destroy(ns_csum_ctx* ctx);
+
+/* Blocks until all work this context issued on `stream` is done; returns the
+ * number of out-of-range descriptors seen since the last call in *bad
+ * (descriptors past `arena_bytes` are summed as empty and counted).          */
+int ns_csum_sync(ns_csum_ctx* ctx, void* stream, uint64_t* bad);
+
+/* ---- device-resident batch (the hot path) --------------------------------
+ * d_arena/d_desc/d_out are device pointers on ctx's device; the call only
+ * enqueues kernels on `stream` and returns (asynchronous).  With
+ * NS_BATCH_CHAINED the context's scratch is used: calls with that flag on one
+ * context must be serialised by the caller's stream order.                  */
+int ns_csum_batch_dev(ns_csum_ctx* ctx, const uint8_t* d_arena,
+                      uint64_t arena_bytes, const ns_pkt_desc* d_desc,
+                      uint32_t n, uint16_t* d_out, uint32_t batch_flags,
+                      void* stream);
+
+/* Host-memory batch: H2D of arena and table, kernels, D2H of results,
+ * pipelined over two streams in chunks; synchronous.  Pageable host memory is
+ * bounced through the context's pinned staging.                             */
+int ns_csum_batch_host(ns_csum_ctx* ctx, const uint8_t* h_arena,
+                       uint64_t arena_bytes, const ns_pkt_desc* h_desc,
+                       uint32_t n, uint16_t* h_out, uint32_t batch_flags);
+
+/* ---- reference-shaped entry points (synchronous, device-computed) ------- */
+/* header.Checksum(buf, initial)                    checksum.go:52-55        */
+int ns_csum_checksum(ns_csum_ctx* ctx, const uint8_t* buf, uint64_t len,
+                     uint16_t initial, uint16_t* out);
+/* header.ChecksumVVWithOffset(vv, initial, off, size) checksum.go:69-98.
+ * ChecksumVV(vv, initial) == this with off = 0, size = vv.Size().
+ * size < 0 or off < 0 -> NS_EINVAL (Go panics on a negative slice bound). */
+int ns_csum_vv_with_offset(ns_csum_ctx* ctx, const ns_view* views,
+                           uint32_t nviews, uint16_t initial, int64_t off,
+                           int64_t size, uint16_t* out);
+/* n x ChecksumVVWithOffset(vv, segs[i].initial, segs[i].off, segs[i].size)
+ * in one device pass (sendTCPBatch, connect.go:668-702).                    */
+int ns_csum_vv_batch(ns_csum_ctx* ctx, const ns_view* views, uint32_t nviews,
+                     const ns_seg* segs, uint32_t nsegs, uint16_t* out);
+/* xsum = initial; for v in views: xsum = Checksum(v, xsum)
+ * (udp/endpoint.go:811-813, icmpv4.go:158-160): alignment restarts per view. */
+int ns_csum_views_restart(ns_csum_ctx* ctx, const ns_view* views,
+                          uint32_t nviews, uint16_t initial, uint16_t* out);
+/* header.PseudoHeaderChecksum(protocol, src, dst, totalLen) checksum.go:112-122 */
+int ns_csum_pseudo_header(ns_csum_ctx* ctx, uint32_t protocol,
+                          const uint8_t* src, uint32_t src_len,
+                          const uint8_t* dst, uint32_t dst_len,
+                          uint16_t total_len, uint16_t* out);
+/* header.ChecksumCombine(a, b)                     checksum.go:104-107      */
+uint16_t ns_csum_combine(uint16_t a, uint16_t b);
+
+/* ---- multi-GPU sharding -------------------------------------------------
+ * Splits n descriptors into `parts` contiguous ranges with near-equal payload
+ * bytes (prefix sum of len, cut at byte quantiles).  first[p] = index of the
+ * first descriptor of part p; first[parts] = n.  Pure host arithmetic.      */
+int ns_csum_shard_plan(const ns_pkt_desc* h_desc, uint32_t n, uint32_t parts,
+                       uint32_t* first);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NETSTACK_CSUM_H_ */

@@ -1,0 +1,144 @@
+"""ctypes binding of the C ABI in include/netstack_csum.h.
+
+The library is netstack_amd/lib/libnetstack_csum.so, built in-tree by
+``netstack_amd/csrc/Makefile`` (``__graft_entry__.build()``).  There is no
+fallback: if the library is missing or cannot be loaded, every entry point
+raises ``NativeLibraryError``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libnetstack_csum.so")
+CSRC = os.path.join(_HERE, "csrc")
+
+NS_OK = 0
+NS_EINVAL = -1
+NS_ERANGE = -2
+NS_ENODEV = -3
+NS_ENOMEM = -4
+NS_EHIP = -5
+
+NS_DESC_ODD = 0x1
+NS_DESC_CONT = 0x2
+NS_BATCH_CHAINED = 0x1
+
+# Every symbol include/netstack_csum.h declares (checked by the CPU tests).
+EXPORTED = (
+    "ns_csum_abi_version", "ns_csum_strerror", "ns_csum_device_count",
+    "ns_csum_init", "ns_csum_destroy", "ns_csum_sync", "ns_csum_batch_dev",
+    "ns_csum_batch_host", "ns_csum_checksum", "ns_csum_vv_with_offset",
+    "ns_csum_vv_batch", "ns_csum_views_restart", "ns_csum_pseudo_header",
+    "ns_csum_combine", "ns_csum_shard_plan",
+)
+
+
+class NativeLibraryError(RuntimeError):
+    """The HIP engine library is missing or failed to load."""
+
+
+class ChecksumError(RuntimeError):
+    """A C-ABI call returned a negative status."""
+
+    def __init__(self, status: int, what: str):
+        self.status = status
+        super().__init__(f"{what}: {strerror(status)} ({status})")
+
+
+class NsPktDesc(ctypes.Structure):
+    _fields_ = [("off", ctypes.c_uint64), ("len", ctypes.c_uint32),
+                ("initial", ctypes.c_uint16), ("flags", ctypes.c_uint16)]
+
+
+class NsView(ctypes.Structure):
+    _fields_ = [("data", ctypes.c_void_p), ("len", ctypes.c_uint64)]
+
+
+class NsSeg(ctypes.Structure):
+    _fields_ = [("off", ctypes.c_int64), ("size", ctypes.c_int64),
+                ("initial", ctypes.c_uint16), ("pad0", ctypes.c_uint16),
+                ("pad1", ctypes.c_uint32)]
+
+
+class NsOpts(ctypes.Structure):
+    _fields_ = [("device", ctypes.c_int32), ("flags", ctypes.c_uint32),
+                ("staging_bytes", ctypes.c_uint64)]
+
+
+assert ctypes.sizeof(NsPktDesc) == 16 and ctypes.sizeof(NsSeg) == 24
+
+_lock = threading.Lock()
+_lib = None
+
+
+def _declare(lib):
+    c = ctypes
+    vp, u8p = c.c_void_p, c.c_void_p
+    u16p = c.POINTER(c.c_uint16)
+    sig = {
+        "ns_csum_abi_version": (c.c_int, []),
+        "ns_csum_strerror": (c.c_char_p, [c.c_int]),
+        "ns_csum_device_count": (c.c_int, [c.POINTER(c.c_int)]),
+        "ns_csum_init": (c.c_int, [c.POINTER(NsOpts), c.POINTER(vp)]),
+        "ns_csum_destroy": (None, [vp]),
+        "ns_csum_sync": (c.c_int, [vp, vp, c.POINTER(c.c_uint64)]),
+        "ns_csum_batch_dev": (c.c_int, [vp, u8p, c.c_uint64, vp, c.c_uint32, vp, c.c_uint32, vp]),
+        "ns_csum_batch_host": (c.c_int, [vp, u8p, c.c_uint64, vp, c.c_uint32, vp, c.c_uint32]),
+        "ns_csum_checksum": (c.c_int, [vp, u8p, c.c_uint64, c.c_uint16, u16p]),
+        "ns_csum_vv_with_offset": (c.c_int, [vp, c.POINTER(NsView), c.c_uint32, c.c_uint16,
+                                             c.c_int64, c.c_int64, u16p]),
+        "ns_csum_vv_batch": (c.c_int, [vp, c.POINTER(NsView), c.c_uint32, c.POINTER(NsSeg),
+                                       c.c_uint32, u16p]),
+        "ns_csum_views_restart": (c.c_int, [vp, c.POINTER(NsView), c.c_uint32, c.c_uint16, u16p]),
+        "ns_csum_pseudo_header": (c.c_int, [vp, c.c_uint32, u8p, c.c_uint32, u8p, c.c_uint32,
+                                            c.c_uint16, u16p]),
+        "ns_csum_combine": (c.c_uint16, [c.c_uint16, c.c_uint16]),
+        "ns_csum_shard_plan": (c.c_int, [vp, c.c_uint32, c.c_uint32, c.POINTER(c.c_uint32)]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+
+
+def lib():
+    """Load (once) and return the HIP engine library; raise if unavailable."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise NativeLibraryError(
+                    f"{LIB_PATH} is missing: build it with `make -C {CSRC}` "
+                    "(or __graft_entry__.build()); there is no CPU fallback")
+            # Share one HIP runtime with torch when torch is present: importing
+            # torch first makes the loader reuse its libamdhip64.so.7.
+            try:
+                import torch  # noqa: F401
+            except Exception:  # pragma: no cover - torch is optional here
+                pass
+            try:
+                l = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+            except OSError as e:
+                raise NativeLibraryError(f"cannot load {LIB_PATH}: {e}") from e
+            _declare(l)
+            _lib = l
+    return _lib
+
+
+def strerror(status: int) -> str:
+    try:
+        return lib().ns_csum_strerror(status).decode()
+    except NativeLibraryError:
+        return f"status {status}"
+
+
+def check(status: int, what: str) -> None:
+    if status != NS_OK:
+        if status == NS_EINVAL:
+            raise ValueError(f"{what}: {strerror(status)}")
+        raise ChecksumError(status, what)

@@ -1,0 +1,544 @@
+// csum_api.cpp — the C ABI of include/netstack_csum.h on top of the gfx950
+// kernels.  Host-side work here is plumbing only: argument validation, the
+// gather of tcpip/buffer views into a pinned, contiguous staging arena plus a
+// descriptor table (the "device-staged layout" of north_star), H2D/D2H copies
+// and launches.  Every checksum is computed on the GPU; there is no host
+// fallback — a HIP failure is returned as a negative status.
+#include <hip/hip_runtime_api.h>
+
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <vector>
+
+#include "csum_kernels.h"
+#include "netstack_csum.h"
+
+static_assert(sizeof(ns_pkt_desc) == 16, "ns_pkt_desc must be 16 bytes");
+static_assert(sizeof(ns_seg) == 24, "ns_seg layout");
+
+namespace {
+
+// Largest run of VectorisedView pieces that may be merged into ONE descriptor
+// and still equal Go's per-view chain (checksum.go:89): with initial <= 0xFFFF
+// and L <= 131072 bytes the uint32 accumulator cannot wrap, neither in the
+// chain nor in the merged sum (65535 * (1 + 65536) = 2^32 - 1).  A single
+// piece is never split (its own wrap is reproduced exactly by the kernel).
+constexpr uint64_t kMergeMax = 131072;
+constexpr uint64_t kDefaultStaging = 64ull << 20;
+
+#define HIP_TRY(expr)                                   \
+  do {                                                  \
+    hipError_t e__ = (expr);                            \
+    if (e__ != hipSuccess) return map_hip_error(e__);   \
+  } while (0)
+
+int map_hip_error(hipError_t e) {
+  if (e == hipErrorOutOfMemory) return NS_ENOMEM;
+  if (e == hipErrorNoDevice || e == hipErrorInvalidDevice) return NS_ENODEV;
+  return NS_EHIP;
+}
+
+template <typename T>
+struct DevBuf {
+  T* p = nullptr;
+  size_t cap = 0;  // elements
+  int ensure(size_t n) {
+    if (n <= cap) return NS_OK;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t want = std::max<size_t>(n, 1);
+    HIP_TRY(hipMalloc(reinterpret_cast<void**>(&p), want * sizeof(T)));
+    cap = want;
+    return NS_OK;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+template <typename T>
+struct PinBuf {
+  T* p = nullptr;
+  size_t cap = 0;
+  int ensure(size_t n) {
+    if (n <= cap) return NS_OK;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t want = std::max<size_t>(n, 1);
+    HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&p), want * sizeof(T), hipHostMallocDefault));
+    cap = want;
+    return NS_OK;
+  }
+  void release() {
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+}  // namespace
+
+struct ns_csum_ctx {
+  int device = 0;
+  uint64_t staging = kDefaultStaging;
+  hipStream_t stream[2] = {nullptr, nullptr};
+  hipEvent_t done[2] = {nullptr, nullptr};
+  unsigned long long* d_err = nullptr;
+  std::mutex mu;  // guards everything below
+
+  DevBuf<uint32_t> partial;  // chained-batch scratch (device-resident API)
+  // host-path slots (double-buffered)
+  DevBuf<uint8_t> d_arena[2];
+  DevBuf<ns_pkt_desc> d_desc[2];
+  DevBuf<uint16_t> d_out[2];
+  DevBuf<uint32_t> d_part[2];
+  PinBuf<ns_pkt_desc> h_desc[2];
+  PinBuf<uint16_t> h_out[2];
+  // gather staging for the VectorisedView entry points
+  PinBuf<uint8_t> g_arena;
+  std::vector<ns_pkt_desc> g_desc;
+};
+
+namespace {
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+bool any_cont(const ns_pkt_desc* d, uint32_t n) {
+  for (uint32_t i = 0; i < n; ++i)
+    if (d[i].flags & NS_DESC_CONT) return true;
+  return false;
+}
+
+// Host batch core, caller holds ctx->mu and the device guard.  Pipelines
+// chunks of the descriptor table over the two slots/streams: H2D of chunk k+1
+// overlaps the kernel of chunk k.  Chunks never split a NS_DESC_CONT run.
+int run_host_batch(ns_csum_ctx* ctx, const uint8_t* h_arena, uint64_t arena_bytes,
+                   const ns_pkt_desc* h_desc, uint32_t n, uint16_t* h_out,
+                   bool chained) {
+  if (n == 0) return NS_OK;
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint64_t off = h_desc[i].off, len = h_desc[i].len;
+    if (off > arena_bytes || len > arena_bytes - off) return NS_ERANGE;
+  }
+  const uint64_t budget = ctx->staging;
+  struct Pending {
+    bool live = false;
+    uint32_t first = 0, count = 0;
+  } pend[2];
+  uint32_t k = 0;
+  int slot = 0;
+  while (k < n) {
+    // Grow the chunk while its byte span stays within budget.
+    uint64_t lo = UINT64_MAX, hi = 0;
+    uint32_t j = k;
+    uint32_t cut = k;  // last index (exclusive) at which we may cut
+    uint64_t cut_lo = 0, cut_hi = 0;
+    while (j < n) {
+      uint64_t nlo = lo, nhi = hi;  // empty descriptors do not widen the span
+      if (h_desc[j].len) {
+        nlo = std::min(lo, h_desc[j].off);
+        nhi = std::max(hi, h_desc[j].off + h_desc[j].len);
+      }
+      if (j > k && cut > k && nlo != UINT64_MAX && nhi - nlo > budget) break;
+      lo = nlo;
+      hi = nhi;
+      ++j;
+      if (j == n || !(chained && (h_desc[j].flags & NS_DESC_CONT))) {
+        cut = j;
+        cut_lo = lo;
+        cut_hi = hi;
+      }
+    }
+    if (cut == k) {  // only possible at the end: take everything left
+      cut = j;
+      cut_lo = lo;
+      cut_hi = hi;
+    }
+    const uint32_t cnt = cut - k;
+    if (cut_lo == UINT64_MAX || cut_hi < cut_lo) cut_lo = cut_hi = 0;
+    const uint64_t span = cut_hi - cut_lo;
+
+    // Retire the slot's previous chunk before reusing its staging.
+    if (pend[slot].live) {
+      HIP_TRY(hipEventSynchronize(ctx->done[slot]));
+      std::memcpy(h_out + pend[slot].first, ctx->h_out[slot].p, pend[slot].count * sizeof(uint16_t));
+      pend[slot].live = false;
+    }
+    int rc;
+    if ((rc = ctx->d_arena[slot].ensure(std::max<uint64_t>(span, 16))) != NS_OK) return rc;
+    if ((rc = ctx->d_desc[slot].ensure(cnt)) != NS_OK) return rc;
+    if ((rc = ctx->d_out[slot].ensure(cnt)) != NS_OK) return rc;
+    if ((rc = ctx->h_desc[slot].ensure(cnt)) != NS_OK) return rc;
+    if ((rc = ctx->h_out[slot].ensure(cnt)) != NS_OK) return rc;
+    if (chained && (rc = ctx->d_part[slot].ensure(cnt)) != NS_OK) return rc;
+    ns_pkt_desc* hd = ctx->h_desc[slot].p;
+    for (uint32_t q = 0; q < cnt; ++q) {
+      hd[q] = h_desc[k + q];
+      hd[q].off = hd[q].len ? hd[q].off - cut_lo : 0;
+    }
+    hipStream_t s = ctx->stream[slot];
+    if (span) HIP_TRY(hipMemcpyAsync(ctx->d_arena[slot].p, h_arena + cut_lo, span, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(ctx->d_desc[slot].p, hd, cnt * sizeof(ns_pkt_desc), hipMemcpyHostToDevice, s));
+    HIP_TRY(nsk::launch_batch(ctx->d_arena[slot].p, span, ctx->d_desc[slot].p, cnt, ctx->d_out[slot].p,
+                              chained ? ctx->d_part[slot].p : nullptr, ctx->d_err, s));
+    HIP_TRY(hipMemcpyAsync(ctx->h_out[slot].p, ctx->d_out[slot].p, cnt * sizeof(uint16_t), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipEventRecord(ctx->done[slot], s));
+    pend[slot].live = true;
+    pend[slot].first = k;
+    pend[slot].count = cnt;
+    k = cut;
+    slot ^= 1;
+  }
+  for (int s = 0; s < 2; ++s) {
+    int sl = slot ^ s ^ 1;  // older chunk first
+    if (pend[sl].live) {
+      HIP_TRY(hipEventSynchronize(ctx->done[sl]));
+      std::memcpy(h_out + pend[sl].first, ctx->h_out[sl].p, pend[sl].count * sizeof(uint16_t));
+      pend[sl].live = false;
+    }
+  }
+  return NS_OK;
+}
+
+// ---- gather of VectorisedView pieces (tcpip/buffer -> staging arena) -----
+struct Gather {
+  ns_csum_ctx* ctx;
+  std::vector<uint8_t> bytes;  // assembled here, then copied to pinned once
+  std::vector<ns_pkt_desc> desc;
+  std::vector<uint32_t> result_at;  // index of the descriptor holding each result
+
+  // Append one segment made of pieces (ptr,len) with Go VV semantics:
+  // odd-carry across pieces, merged into runs of <= kMergeMax bytes.
+  void segment(const std::vector<std::pair<const uint8_t*, uint64_t>>& pieces, uint16_t initial) {
+    bool first_desc = true;
+    uint64_t consumed = 0;  // bytes of this segment already described
+    ns_pkt_desc cur{};
+    bool open = false;
+    auto close = [&]() {
+      if (!open) return;
+      desc.push_back(cur);
+      open = false;
+    };
+    for (const auto& pc : pieces) {
+      const uint64_t len = pc.second;
+      if (len == 0) continue;
+      const bool big = len > kMergeMax;
+      if (open && (big || cur.len + len > kMergeMax)) close();
+      if (!open) {
+        cur.off = bytes.size();
+        cur.len = 0;
+        cur.initial = first_desc ? initial : 0;
+        cur.flags = (uint16_t)((first_desc ? 0u : NS_DESC_CONT) | ((consumed & 1) ? NS_DESC_ODD : 0u));
+        first_desc = false;
+        open = true;
+      }
+      bytes.insert(bytes.end(), pc.first, pc.first + len);
+      cur.len += (uint32_t)len;
+      consumed += len;
+      if (big) close();
+    }
+    close();
+    if (first_desc) {  // no bytes: result = initial (checksum.go:97)
+      ns_pkt_desc z{};
+      z.off = 0;
+      z.len = 0;
+      z.initial = initial;
+      z.flags = 0;
+      desc.push_back(z);
+    }
+    result_at.push_back((uint32_t)desc.size() - 1);
+  }
+
+  // Each view its own calculateChecksum with odd=false, chained
+  // (xsum = Checksum(v, xsum): udp/endpoint.go:811-813).
+  void restart_chain(const std::vector<std::pair<const uint8_t*, uint64_t>>& pieces, uint16_t initial) {
+    bool first = true;
+    for (const auto& pc : pieces) {
+      ns_pkt_desc d{};
+      d.off = bytes.size();
+      d.len = (uint32_t)pc.second;
+      d.initial = first ? initial : 0;
+      d.flags = first ? 0 : NS_DESC_CONT;
+      if (pc.second) bytes.insert(bytes.end(), pc.first, pc.first + pc.second);
+      desc.push_back(d);
+      first = false;
+    }
+    if (first) {
+      ns_pkt_desc z{};
+      z.initial = initial;
+      desc.push_back(z);
+    }
+    result_at.push_back((uint32_t)desc.size() - 1);
+  }
+
+  int run(uint16_t* out) {
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    DeviceGuard g(ctx->device);
+    int rc = ctx->g_arena.ensure(std::max<size_t>(bytes.size(), 16));
+    if (rc != NS_OK) return rc;
+    if (!bytes.empty()) std::memcpy(ctx->g_arena.p, bytes.data(), bytes.size());
+    std::vector<uint16_t> res(desc.size());
+    rc = run_host_batch(ctx, ctx->g_arena.p, bytes.size(), desc.data(), (uint32_t)desc.size(), res.data(),
+                        any_cont(desc.data(), (uint32_t)desc.size()));
+    if (rc != NS_OK) return rc;
+    for (size_t q = 0; q < result_at.size(); ++q) out[q] = res[result_at[q]];
+    return NS_OK;
+  }
+};
+
+// Clip a VectorisedView to [off, off+size) exactly like checksum.go:72-96.
+int clip_views(const ns_view* views, uint32_t nviews, int64_t off, int64_t size,
+               std::vector<std::pair<const uint8_t*, uint64_t>>* pieces) {
+  if (off < 0 || size < 0) return NS_EINVAL;
+  pieces->clear();
+  uint64_t o = (uint64_t)off, s = (uint64_t)size;
+  for (uint32_t k = 0; k < nviews; ++k) {
+    const uint64_t vl = views[k].len;
+    if (vl == 0) continue;  // :73-75
+    if (!views[k].data) return NS_EINVAL;
+    if (o >= vl) {  // :77-80
+      o -= vl;
+      continue;
+    }
+    const uint64_t l = std::min<uint64_t>(vl - o, s);  // :81-87
+    if (l > 0xFFFFFFFFull) return NS_EINVAL;
+    pieces->emplace_back(views[k].data + o, l);
+    s -= l;  // :91-94
+    if (s == 0) break;
+    o = 0;
+  }
+  return NS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ns_csum_abi_version(void) { return NS_CSUM_ABI_VERSION; }
+
+const char* ns_csum_strerror(int status) {
+  switch (status) {
+    case NS_OK: return "ok";
+    case NS_EINVAL: return "invalid argument";
+    case NS_ERANGE: return "descriptor outside the arena";
+    case NS_ENODEV: return "no HIP device";
+    case NS_ENOMEM: return "out of memory";
+    case NS_EHIP: return "HIP runtime error";
+    default: return "unknown status";
+  }
+}
+
+int ns_csum_device_count(int* count) {
+  if (!count) return NS_EINVAL;
+  *count = 0;
+  int c = 0;
+  hipError_t e = hipGetDeviceCount(&c);
+  if (e != hipSuccess) return (e == hipErrorNoDevice) ? NS_ENODEV : map_hip_error(e);
+  *count = c;
+  return NS_OK;
+}
+
+uint16_t ns_csum_combine(uint16_t a, uint16_t b) {  // checksum.go:104-107
+  const uint32_t v = (uint32_t)a + (uint32_t)b;
+  return (uint16_t)(v + (v >> 16));
+}
+
+int ns_csum_init(const ns_csum_opts* opts, ns_csum_ctx** out) {
+  if (!out) return NS_EINVAL;
+  *out = nullptr;
+  int ndev = 0;
+  int rc = ns_csum_device_count(&ndev);
+  if (rc != NS_OK) return rc;
+  const int dev = opts ? opts->device : 0;
+  if (dev < 0 || dev >= ndev) return NS_ENODEV;
+  ns_csum_ctx* ctx = new (std::nothrow) ns_csum_ctx();
+  if (!ctx) return NS_ENOMEM;
+  ctx->device = dev;
+  if (opts && opts->staging_bytes) ctx->staging = opts->staging_bytes;
+  DeviceGuard g(dev);
+  hipError_t e = hipSuccess;
+  for (int s = 0; s < 2 && e == hipSuccess; ++s) {
+    e = hipStreamCreateWithFlags(&ctx->stream[s], hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->done[s], hipEventDisableTiming);
+  }
+  if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&ctx->d_err), sizeof(unsigned long long));
+  if (e == hipSuccess) e = hipMemset(ctx->d_err, 0, sizeof(unsigned long long));
+  if (e != hipSuccess) {
+    ns_csum_destroy(ctx);
+    return map_hip_error(e);
+  }
+  *out = ctx;
+  return NS_OK;
+}
+
+void ns_csum_destroy(ns_csum_ctx* ctx) {
+  if (!ctx) return;
+  {
+    DeviceGuard g(ctx->device);
+    for (int s = 0; s < 2; ++s)
+      if (ctx->stream[s]) (void)hipStreamSynchronize(ctx->stream[s]);
+    ctx->partial.release();
+    for (int s = 0; s < 2; ++s) {
+      ctx->d_arena[s].release();
+      ctx->d_desc[s].release();
+      ctx->d_out[s].release();
+      ctx->d_part[s].release();
+      ctx->h_desc[s].release();
+      ctx->h_out[s].release();
+      if (ctx->done[s]) (void)hipEventDestroy(ctx->done[s]);
+      if (ctx->stream[s]) (void)hipStreamDestroy(ctx->stream[s]);
+    }
+    ctx->g_arena.release();
+    if (ctx->d_err) (void)hipFree(ctx->d_err);
+  }
+  delete ctx;
+}
+
+int ns_csum_sync(ns_csum_ctx* ctx, void* stream, uint64_t* bad) {
+  if (!ctx) return NS_EINVAL;
+  DeviceGuard g(ctx->device);
+  hipStream_t s = stream ? (hipStream_t)stream : ctx->stream[0];
+  HIP_TRY(hipStreamSynchronize(s));
+  unsigned long long v = 0;
+  {
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    HIP_TRY(hipMemcpy(&v, ctx->d_err, sizeof(v), hipMemcpyDeviceToHost));
+    if (v) HIP_TRY(hipMemset(ctx->d_err, 0, sizeof(v)));
+  }
+  if (bad) *bad = v;
+  return NS_OK;
+}
+
+int ns_csum_batch_dev(ns_csum_ctx* ctx, const uint8_t* d_arena, uint64_t arena_bytes,
+                      const ns_pkt_desc* d_desc, uint32_t n, uint16_t* d_out,
+                      uint32_t batch_flags, void* stream) {
+  if (!ctx || (n && (!d_desc || !d_out)) || (arena_bytes && !d_arena)) return NS_EINVAL;
+  if (n == 0) return NS_OK;
+  DeviceGuard g(ctx->device);
+  hipStream_t s = stream ? (hipStream_t)stream : ctx->stream[0];
+  uint32_t* part = nullptr;
+  if (batch_flags & NS_BATCH_CHAINED) {
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    int rc = ctx->partial.ensure(n);
+    if (rc != NS_OK) return rc;
+    part = ctx->partial.p;
+  }
+  HIP_TRY(nsk::launch_batch(d_arena, arena_bytes, d_desc, n, d_out, part, ctx->d_err, s));
+  return NS_OK;
+}
+
+int ns_csum_batch_host(ns_csum_ctx* ctx, const uint8_t* h_arena, uint64_t arena_bytes,
+                       const ns_pkt_desc* h_desc, uint32_t n, uint16_t* h_out,
+                       uint32_t batch_flags) {
+  if (!ctx || (n && (!h_desc || !h_out)) || (arena_bytes && !h_arena)) return NS_EINVAL;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  DeviceGuard g(ctx->device);
+  return run_host_batch(ctx, h_arena, arena_bytes, h_desc, n, h_out,
+                        (batch_flags & NS_BATCH_CHAINED) != 0);
+}
+
+int ns_csum_checksum(ns_csum_ctx* ctx, const uint8_t* buf, uint64_t len, uint16_t initial,
+                     uint16_t* out) {
+  if (!ctx || !out || (len && !buf) || len > 0xFFFFFFFFull) return NS_EINVAL;
+  Gather gt{ctx, {}, {}, {}};
+  std::vector<std::pair<const uint8_t*, uint64_t>> pieces;
+  if (len) pieces.emplace_back(buf, len);
+  gt.restart_chain(pieces, initial);  // one piece, odd = false: checksum.go:52-55
+  return gt.run(out);
+}
+
+int ns_csum_vv_with_offset(ns_csum_ctx* ctx, const ns_view* views, uint32_t nviews,
+                           uint16_t initial, int64_t off, int64_t size, uint16_t* out) {
+  if (!ctx || !out || (nviews && !views)) return NS_EINVAL;
+  std::vector<std::pair<const uint8_t*, uint64_t>> pieces;
+  int rc = clip_views(views, nviews, off, size, &pieces);
+  if (rc != NS_OK) return rc;
+  Gather gt{ctx, {}, {}, {}};
+  gt.segment(pieces, initial);
+  return gt.run(out);
+}
+
+int ns_csum_vv_batch(ns_csum_ctx* ctx, const ns_view* views, uint32_t nviews,
+                     const ns_seg* segs, uint32_t nsegs, uint16_t* out) {
+  if (!ctx || (nsegs && (!segs || !out)) || (nviews && !views)) return NS_EINVAL;
+  if (nsegs == 0) return NS_OK;
+  Gather gt{ctx, {}, {}, {}};
+  std::vector<std::pair<const uint8_t*, uint64_t>> pieces;
+  for (uint32_t q = 0; q < nsegs; ++q) {
+    int rc = clip_views(views, nviews, segs[q].off, segs[q].size, &pieces);
+    if (rc != NS_OK) return rc;
+    gt.segment(pieces, segs[q].initial);
+  }
+  return gt.run(out);
+}
+
+int ns_csum_views_restart(ns_csum_ctx* ctx, const ns_view* views, uint32_t nviews,
+                          uint16_t initial, uint16_t* out) {
+  if (!ctx || !out || (nviews && !views)) return NS_EINVAL;
+  std::vector<std::pair<const uint8_t*, uint64_t>> pieces;
+  for (uint32_t k = 0; k < nviews; ++k) {
+    if (views[k].len && !views[k].data) return NS_EINVAL;
+    if (views[k].len > 0xFFFFFFFFull) return NS_EINVAL;
+    pieces.emplace_back(views[k].data, views[k].len);
+  }
+  Gather gt{ctx, {}, {}, {}};
+  gt.restart_chain(pieces, initial);
+  return gt.run(out);
+}
+
+int ns_csum_pseudo_header(ns_csum_ctx* ctx, uint32_t protocol, const uint8_t* src,
+                          uint32_t src_len, const uint8_t* dst, uint32_t dst_len,
+                          uint16_t total_len, uint16_t* out) {
+  if (!ctx || !out || (src_len && !src) || (dst_len && !dst)) return NS_EINVAL;
+  // checksum.go:112-122: four chained Checksum calls, each restarting alignment.
+  const uint8_t lenbe[2] = {(uint8_t)(total_len >> 8), (uint8_t)total_len};
+  const uint8_t proto[2] = {0, (uint8_t)protocol};
+  std::vector<std::pair<const uint8_t*, uint64_t>> pieces = {
+      {src, src_len}, {dst, dst_len}, {lenbe, 2}, {proto, 2}};
+  Gather gt{ctx, {}, {}, {}};
+  gt.restart_chain(pieces, 0);
+  return gt.run(out);
+}
+
+int ns_csum_shard_plan(const ns_pkt_desc* h_desc, uint32_t n, uint32_t parts, uint32_t* first) {
+  if (!first || parts == 0 || (n && !h_desc)) return NS_EINVAL;
+  uint64_t total = 0;
+  for (uint32_t i = 0; i < n; ++i) total += h_desc[i].len;
+  first[0] = 0;
+  uint64_t run = 0;
+  uint32_t i = 0;
+  for (uint32_t p = 1; p < parts; ++p) {
+    // Cut at the first descriptor whose prefix reaches p/parts of the bytes;
+    // with all-empty tables fall back to equal descriptor counts.
+    const uint64_t target = total ? (total * p + parts - 1) / parts : 0;
+    if (total == 0) {
+      i = (uint32_t)(((uint64_t)n * p) / parts);
+    } else {
+      while (i < n && run + h_desc[i].len <= target) run += h_desc[i++].len;
+    }
+    // never split a chained run
+    while (i > 0 && i < n && (h_desc[i].flags & NS_DESC_CONT)) run += h_desc[i++].len;
+    first[p] = std::max(i, first[p - 1]);
+  }
+  first[parts] = n;
+  return NS_OK;
+}
+
+}  // extern "C"

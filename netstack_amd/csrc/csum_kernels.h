@@ -1,0 +1,20 @@
+// Internal launcher interface between the C ABI (csum_api.cpp) and the gfx950
+// kernels (csum_kernels.hip).  Not installed; the public boundary is
+// include/netstack_csum.h.
+#pragma once
+#include <hip/hip_runtime_api.h>
+#include <stdint.h>
+
+namespace nsk {
+
+// Enqueue the checksum of n descriptors (16-byte ns_pkt_desc, device memory)
+// over `arena` on `stream`.  With `partial` != nullptr the per-descriptor
+// 32-bit partial sums go to `partial` and a chain fix-up pass resolves
+// NS_DESC_CONT runs into `out`; otherwise every descriptor is independent.
+// Out-of-range descriptors are summed as empty and counted in *err.
+hipError_t launch_batch(const uint8_t* arena, uint64_t arena_bytes,
+                        const void* desc, uint32_t n, uint16_t* out,
+                        uint32_t* partial, unsigned long long* err,
+                        hipStream_t stream);
+
+}  // namespace nsk

@@ -1,0 +1,206 @@
+"""Engine: a Python handle on one ``ns_csum_ctx`` (one GPU).
+
+Thin wrappers over the C ABI (include/netstack_csum.h).  All checksum
+arithmetic happens in the gfx950 kernels; this module only marshals pointers.
+"""
+from __future__ import annotations
+
+import ctypes
+import threading
+
+import numpy as np
+
+from . import _lib
+from ._lib import NsOpts, NsSeg, NsView, check, lib
+
+DESC_DTYPE = np.dtype(
+    [("off", "<u8"), ("len", "<u4"), ("initial", "<u2"), ("flags", "<u2")], align=False)
+assert DESC_DTYPE.itemsize == 16
+
+ODD = _lib.NS_DESC_ODD
+CONT = _lib.NS_DESC_CONT
+
+
+def device_count() -> int:
+    n = ctypes.c_int(0)
+    rc = lib().ns_csum_device_count(ctypes.byref(n))
+    if rc == _lib.NS_ENODEV:
+        return 0
+    check(rc, "ns_csum_device_count")
+    return int(n.value)
+
+
+def _u8(buf) -> np.ndarray:
+    if isinstance(buf, np.ndarray):
+        return np.ascontiguousarray(buf.reshape(-1).view(np.uint8))
+    return np.frombuffer(memoryview(buf).cast("B"), dtype=np.uint8)
+
+
+def _ptr(a: np.ndarray):
+    return a.ctypes.data if a.size else None
+
+
+def _views(views):
+    """Marshal a sequence of byte buffers into an ns_view array (keep-alive
+    list returned alongside)."""
+    arrs = [_u8(v) for v in views]
+    arr_t = NsView * max(len(arrs), 1)
+    cv = arr_t(*[NsView(_ptr(a), a.size) for a in arrs])
+    return cv, arrs
+
+
+class Engine:
+    """One ns_csum_ctx bound to a HIP device."""
+
+    def __init__(self, device: int = 0, staging_bytes: int = 0):
+        self.device = device
+        opts = NsOpts(device, 0, staging_bytes)
+        h = ctypes.c_void_p()
+        check(lib().ns_csum_init(ctypes.byref(opts), ctypes.byref(h)), "ns_csum_init")
+        self._h = h
+
+    # -- lifetime -----------------------------------------------------------
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            lib().ns_csum_destroy(self._h)
+            self._h = None
+
+    def __del__(self):  # pragma: no cover - interpreter shutdown order
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # -- device-resident batch (the hot path) ------------------------------
+    def batch_dev(self, arena_ptr: int, arena_bytes: int, desc_ptr: int, n: int,
+                  out_ptr: int, chained: bool = False, stream: int | None = None) -> None:
+        """Enqueue (asynchronously) the batch on `stream` (hipStream_t as int)."""
+        check(lib().ns_csum_batch_dev(self._h, arena_ptr, arena_bytes, desc_ptr, n, out_ptr,
+                                      _lib.NS_BATCH_CHAINED if chained else 0, stream),
+              "ns_csum_batch_dev")
+
+    def batch_tensors(self, arena, desc, out=None, chained: bool = False, stream=None):
+        """torch front end: `arena` uint8 CUDA tensor, `desc` CUDA tensor whose
+        bytes are the 16-byte ns_pkt_desc table, `out` int16/uint16 CUDA tensor
+        of n elements (allocated if None).  Launches on `stream` (a
+        torch.cuda.Stream, default: torch's current stream) and returns `out`
+        without synchronising."""
+        import torch
+
+        if not (arena.is_cuda and desc.is_cuda):
+            raise ValueError("arena and desc must be device tensors")
+        if desc.numel() * desc.element_size() % 16:
+            raise ValueError("descriptor table must be a whole number of 16-byte entries")
+        n = desc.numel() * desc.element_size() // 16
+        if out is None:
+            out = torch.empty(n, dtype=torch.int16, device=arena.device)
+        if out.numel() < n or out.element_size() != 2:
+            raise ValueError("out must hold n 16-bit results")
+        if stream is None:
+            stream = torch.cuda.current_stream(arena.device)
+        self.batch_dev(arena.data_ptr(), arena.numel() * arena.element_size(), desc.data_ptr(), n,
+                       out.data_ptr(), chained, stream.cuda_stream)
+        return out
+
+    def sync(self, stream: int | None = None) -> int:
+        """Wait for `stream`; return the number of out-of-range descriptors."""
+        bad = ctypes.c_uint64(0)
+        check(lib().ns_csum_sync(self._h, stream, ctypes.byref(bad)), "ns_csum_sync")
+        return int(bad.value)
+
+    # -- host-memory batch ---------------------------------------------------
+    def batch_host(self, arena, desc: np.ndarray, chained: bool = False) -> np.ndarray:
+        a = _u8(arena)
+        d = np.ascontiguousarray(desc, dtype=DESC_DTYPE)
+        out = np.zeros(len(d), dtype=np.uint16)
+        check(lib().ns_csum_batch_host(self._h, _ptr(a), a.size, _ptr(d), len(d), _ptr(out),
+                                       _lib.NS_BATCH_CHAINED if chained else 0),
+              "ns_csum_batch_host")
+        return out
+
+    # -- reference-shaped entry points --------------------------------------
+    def checksum(self, buf, initial: int = 0) -> int:
+        a = _u8(buf)
+        r = ctypes.c_uint16(0)
+        check(lib().ns_csum_checksum(self._h, _ptr(a), a.size, initial & 0xFFFF, ctypes.byref(r)),
+              "ns_csum_checksum")
+        return int(r.value)
+
+    def vv_with_offset(self, views, initial: int, off: int, size: int) -> int:
+        cv, keep = _views(views)
+        r = ctypes.c_uint16(0)
+        check(lib().ns_csum_vv_with_offset(self._h, cv, len(keep), initial & 0xFFFF, off, size,
+                                           ctypes.byref(r)), "ns_csum_vv_with_offset")
+        return int(r.value)
+
+    def vv_batch(self, views, segs) -> np.ndarray:
+        """segs: iterable of (off, size, initial)."""
+        cv, keep = _views(views)
+        segs = list(segs)
+        st = (NsSeg * max(len(segs), 1))(*[NsSeg(o, s, i & 0xFFFF, 0, 0) for (o, s, i) in segs])
+        out = np.zeros(len(segs), dtype=np.uint16)
+        check(lib().ns_csum_vv_batch(self._h, cv, len(keep), st, len(segs),
+                                     out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint16))),
+              "ns_csum_vv_batch")
+        return out
+
+    def views_restart(self, views, initial: int) -> int:
+        cv, keep = _views(views)
+        r = ctypes.c_uint16(0)
+        check(lib().ns_csum_views_restart(self._h, cv, len(keep), initial & 0xFFFF, ctypes.byref(r)),
+              "ns_csum_views_restart")
+        return int(r.value)
+
+    def pseudo_header(self, protocol: int, src: bytes, dst: bytes, total_len: int) -> int:
+        s, d = _u8(bytes(src)), _u8(bytes(dst))
+        r = ctypes.c_uint16(0)
+        check(lib().ns_csum_pseudo_header(self._h, protocol, _ptr(s), s.size, _ptr(d), d.size,
+                                          total_len & 0xFFFF, ctypes.byref(r)),
+              "ns_csum_pseudo_header")
+        return int(r.value)
+
+
+def combine(a: int, b: int) -> int:
+    """header.ChecksumCombine (checksum.go:104-107), via the C ABI."""
+    return int(lib().ns_csum_combine(a & 0xFFFF, b & 0xFFFF))
+
+
+def shard_plan(desc: np.ndarray, parts: int) -> np.ndarray:
+    """Byte-balanced contiguous split of a descriptor table into `parts`
+    ranges (ns_csum_shard_plan); returns `parts+1` boundaries."""
+    d = np.ascontiguousarray(desc, dtype=DESC_DTYPE)
+    first = np.zeros(parts + 1, dtype=np.uint32)
+    check(lib().ns_csum_shard_plan(_ptr(d), len(d), parts,
+                                   first.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))),
+          "ns_csum_shard_plan")
+    return first
+
+
+_engines: dict[int, Engine] = {}
+_elock = threading.Lock()
+
+
+def default_engine(device: int | None = None) -> Engine:
+    """Process-wide engine per device (created once), as the Go shim would
+    keep one context per device behind package `header`."""
+    if device is None:
+        try:
+            import torch
+
+            device = torch.cuda.current_device() if torch.cuda.is_available() else 0
+        except Exception:
+            device = 0
+    e = _engines.get(device)
+    if e is None:
+        with _elock:
+            e = _engines.get(device)
+            if e is None:
+                e = Engine(device)
+                _engines[device] = e
+    return e

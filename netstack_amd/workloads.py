@@ -1,0 +1,176 @@
+"""Synthetic packet batches for the BASELINE.json configurations.
+
+Bytes come from splitmix64 (state_i = seed + (i+1)*0x9E3779B97F4A7C15, output
+little-endian), generated either with numpy on the host or with torch int64
+arithmetic directly in HBM — both produce the same bytes, so a device-generated
+arena can be checked against the host oracle on the same inputs.
+
+Layouts (BASELINE.md "CPU-baseline and measurement plan"):
+  cfg1  one 65,536-B buffer, seed 1, initial 0 (host only)
+  cfg2  1,048,576 x 1500 B, seed 2, 16-B-aligned starts (stride 1504)
+  cfg3  1,048,576 x 64 B, seed 3 (stride 64)
+  cfg4  1,048,576 packets, L = 64 + r, P(r) ~ (r+1)^-1.1, r in [0, 8936], seed 4
+  cfg5  8,388,608 x 1500 B, seed 5 (sharded over GPUs)
+Per-packet `initial` is a random uint16 (a stand-in for the pseudo-header sum)
+drawn from an independent splitmix64 stream.  Padding bytes between packets
+are random too, so a kernel that sums them fails parity.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+
+GAMMA = 0x9E3779B97F4A7C15
+M1 = 0xBF58476D1CE4E5B9
+M2 = 0x94D049BB133111EB
+MASK64 = (1 << 64) - 1
+
+DESC_DTYPE = np.dtype(
+    [("off", "<u8"), ("len", "<u4"), ("initial", "<u2"), ("flags", "<u2")], align=False)
+
+
+def splitmix64(seed: int, n: int, start: int = 0) -> np.ndarray:
+    """n outputs of splitmix64 starting at index `start` (numpy, host)."""
+    i = np.arange(start + 1, start + n + 1, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        z = i * np.uint64(GAMMA) + np.uint64(seed & MASK64)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(M1)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(M2)
+        z = z ^ (z >> np.uint64(31))
+    return z
+
+
+def random_bytes(seed: int, nbytes: int, chunk: int = 1 << 24) -> np.ndarray:
+    """nbytes of splitmix64 output (host), generated in chunks of `chunk` words."""
+    words = (nbytes + 7) // 8
+    out = np.empty(words * 8, dtype=np.uint8)
+    o64 = out.view(np.uint64)
+    for s in range(0, words, chunk):
+        e = min(words, s + chunk)
+        o64[s:e] = splitmix64(seed, e - s, s)
+    return out[:nbytes]
+
+
+def _s64(x: int) -> int:
+    x &= MASK64
+    return x - (1 << 64) if x >> 63 else x
+
+
+def random_bytes_torch(seed: int, nbytes: int, device, chunk: int = 1 << 26):
+    """Same bytes as random_bytes(), generated in HBM with torch int64 ops
+    (two's-complement wrap; logical shifts emulated with masks)."""
+    import torch
+
+    words = (nbytes + 7) // 8
+    out = torch.empty(words * 8, dtype=torch.uint8, device=device)
+    o64 = out.view(torch.int64)
+    g, m1, m2, sd = _s64(GAMMA), _s64(M1), _s64(M2), _s64(seed)
+
+    def lsr(z, k):
+        return (z >> k) & ((1 << (64 - k)) - 1)
+
+    for s in range(0, words, chunk):
+        e = min(words, s + chunk)
+        z = torch.arange(s + 1, e + 1, dtype=torch.int64, device=device)
+        z = z * g + sd
+        z = (z ^ lsr(z, 30)) * m1
+        z = (z ^ lsr(z, 27)) * m2
+        o64[s:e] = z ^ lsr(z, 31)
+    return out[:nbytes]
+
+
+def zipf_lengths(seed: int, n: int, lo: int = 64, hi: int = 9000, alpha: float = 1.1) -> np.ndarray:
+    """L = lo + r, r in [0, hi-lo], P(r) ~ (r+1)^-alpha, by inverse CDF."""
+    r = np.arange(hi - lo + 1, dtype=np.float64)
+    w = (r + 1.0) ** (-alpha)
+    cdf = np.cumsum(w)
+    cdf /= cdf[-1]
+    u = (splitmix64(seed ^ 0x5A5A5A5A, n) >> np.uint64(11)).astype(np.float64) * (1.0 / (1 << 53))
+    idx = np.searchsorted(cdf, u, side="right")
+    idx = np.minimum(idx, len(cdf) - 1)
+    return (lo + idx).astype(np.uint32)
+
+
+@dataclass
+class Batch:
+    """A packet batch: descriptor table + how to make its arena."""
+
+    name: str
+    seed: int
+    desc: np.ndarray  # DESC_DTYPE
+    arena_bytes: int
+
+    @property
+    def n(self) -> int:
+        return len(self.desc)
+
+    @property
+    def payload_bytes(self) -> int:
+        return int(self.desc["len"].sum(dtype=np.uint64))
+
+    @property
+    def algorithmic_bytes(self) -> int:
+        """Σlen + 18·N: payload read + 16-B descriptor read + 2-B result
+        write."""
+        return self.payload_bytes + 18 * self.n
+
+    def arena_host(self) -> np.ndarray:
+        return random_bytes(self.seed, self.arena_bytes)
+
+    def arena_device(self, device):
+        return random_bytes_torch(self.seed, self.arena_bytes, device)
+
+
+def make_desc(lengths: np.ndarray, initial: np.ndarray, align: int = 16, base: int = 0,
+              flags: np.ndarray | None = None) -> tuple[np.ndarray, int]:
+    """Pack packets back to back with starts aligned to `align` bytes."""
+    n = len(lengths)
+    lengths = lengths.astype(np.uint64)
+    stride = ((lengths + np.uint64(align - 1)) // np.uint64(align)) * np.uint64(align) if align > 1 else lengths
+    off = np.zeros(n, dtype=np.uint64)
+    if n:
+        off[1:] = np.cumsum(stride[:-1], dtype=np.uint64)
+    off += np.uint64(base)
+    d = np.zeros(n, dtype=DESC_DTYPE)
+    d["off"] = off
+    d["len"] = lengths.astype(np.uint32)
+    d["initial"] = initial.astype(np.uint16)
+    if flags is not None:
+        d["flags"] = flags.astype(np.uint16)
+    end = int(off[-1] + lengths[-1]) if n else base
+    return d, end
+
+
+def _initials(seed: int, n: int) -> np.ndarray:
+    return (splitmix64(seed ^ 0x1D1D1D1D, n) >> np.uint64(48)).astype(np.uint16)
+
+
+def uniform(name: str, seed: int, n: int, length: int, align: int = 16) -> Batch:
+    lengths = np.full(n, length, dtype=np.uint32)
+    d, end = make_desc(lengths, _initials(seed, n), align)
+    return Batch(name, seed, d, ((end + 15) // 16) * 16)
+
+
+def zipf(name: str, seed: int, n: int, align: int = 16) -> Batch:
+    lengths = zipf_lengths(seed, n)
+    d, end = make_desc(lengths, _initials(seed, n), align)
+    return Batch(name, seed, d, ((end + 15) // 16) * 16)
+
+
+def config(k: int, n: int | None = None) -> Batch:
+    """BASELINE.json configs[k-1] (k = 1..5); `n` overrides the packet count
+    (for parity-test subsets with the same layout rule)."""
+    if k == 1:
+        b = uniform("cfg1_64KiB", 1, 1, 65536)
+        b.desc["initial"] = 0
+        return b
+    if k == 2:
+        return uniform("cfg2_1Mx1500", 2, n or (1 << 20), 1500)
+    if k == 3:
+        return uniform("cfg3_1Mx64", 3, n or (1 << 20), 64)
+    if k == 4:
+        return zipf("cfg4_1Mzipf", 4, n or (1 << 20))
+    if k == 5:
+        return uniform("cfg5_8Mx1500", 5, n or (8 << 20), 1500)
+    raise ValueError(k)

@@ -1,0 +1,38 @@
+/* ORACLE — TEST INFRASTRUCTURE ONLY (see csum_oracle.c). */
+#ifndef CSUM_ORACLE_H_
+#define CSUM_ORACLE_H_
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Same 16-byte layout as ns_pkt_desc (include/netstack_csum.h). */
+typedef struct oracle_desc {
+  uint64_t off;
+  uint32_t len;
+  uint16_t initial;
+  uint16_t flags; /* bit0 odd, bit1 chain */
+} oracle_desc;
+
+uint16_t oracle_combine(uint16_t a, uint16_t b);
+uint16_t oracle_calculate_checksum(const uint8_t* buf, uint64_t len, int odd,
+                                   uint32_t initial, int* odd_out);
+uint16_t oracle_checksum(const uint8_t* buf, uint64_t len, uint16_t initial);
+int oracle_vv_with_offset(const uint8_t* const* views, const uint64_t* lens,
+                          uint32_t nviews, uint16_t initial, int64_t off,
+                          int64_t size, uint16_t* out);
+uint16_t oracle_views_restart(const uint8_t* const* views, const uint64_t* lens,
+                              uint32_t nviews, uint16_t initial);
+uint16_t oracle_pseudo_header(uint32_t protocol, const uint8_t* src,
+                              uint32_t src_len, const uint8_t* dst,
+                              uint32_t dst_len, uint16_t total_len);
+int oracle_batch(const uint8_t* arena, uint64_t arena_bytes,
+                 const oracle_desc* d, uint32_t n, uint16_t* out, int chained);
+int oracle_batch_mt(const uint8_t* arena, const oracle_desc* d, uint32_t n,
+                    uint16_t* out, int nthreads);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,278 @@
+"""GPU: the HIP engine (through the C ABI) against the oracle and the golden
+vectors — bit-exact, every result.  Run on an MI355X: pytest -m gpu."""
+import numpy as np
+import pytest
+
+from make_golden import materialize
+
+pytestmark = pytest.mark.gpu
+
+
+def _torch():
+    import torch
+
+    assert torch.cuda.is_available(), "GPU tests need a HIP device"
+    return torch
+
+
+def dev_batch(engine, arena_np, desc_np, chained=False, arena_offset=0, stream=None):
+    """Run a batch device-resident; arena placed `arena_offset` bytes into a
+    device buffer (so its base need not be 16-byte aligned)."""
+    torch = _torch()
+    buf = torch.empty(arena_offset + max(arena_np.size, 1), dtype=torch.uint8, device="cuda")
+    if arena_np.size:
+        buf[arena_offset:arena_offset + arena_np.size].copy_(torch.from_numpy(arena_np))
+    arena = buf[arena_offset:arena_offset + arena_np.size]
+    desc = torch.from_numpy(np.ascontiguousarray(desc_np).view(np.uint8).copy()).cuda()
+    out = engine.batch_tensors(arena, desc, chained=chained, stream=stream)
+    torch.cuda.synchronize()
+    return out.cpu().numpy().view(np.uint16)
+
+
+# ---- reference KATs through the tcpip/header mirror ------------------------
+def test_reference_kats(kat, engine):
+    from netstack_amd import header
+    from netstack_amd.buffer import NewVectorisedView, NewViewFromBytes
+
+    for c in kat["vv_with_offset"]:
+        vv = NewVectorisedView(0, [NewViewFromBytes(bytes.fromhex(v)) for v in c["views"]])
+        # checksum_test.go:98
+        assert header.ChecksumVVWithOffset(vv, c["initial"], c["off"], c["size"]) == c["want"], c["name"]
+        # checksum_test.go:101-105
+        v = vv.ToView()
+        v.TrimFront(c["off"])
+        v.CapLength(c["size"])
+        assert header.Checksum(v, c["initial"]) == c["want"], c["name"]
+    for c in kat["checksum"]:
+        assert header.Checksum(bytes.fromhex(c["buf"]), c["initial"]) == c["want"], c["name"]
+
+
+def test_golden_vectors(vectors, engine):
+    from netstack_amd import header
+    from netstack_amd.buffer import NewVectorisedView
+
+    for c in vectors["checksum"]:
+        assert header.Checksum(materialize(c["buf"]), c["initial"]) == c["want"], c["name"]
+    for c in vectors["vv_with_offset"]:
+        views = [materialize(v) for v in c["views"]]
+        vv = NewVectorisedView(sum(map(len, views)), views)
+        assert header.ChecksumVVWithOffset(vv, c["initial"], c["off"], c["size"]) == c["want"], c["name"]
+    for c in vectors["views_restart"]:
+        assert header.ChecksumViews([materialize(v) for v in c["views"]], c["initial"]) == c["want"], c["name"]
+    for c in vectors["pseudo_header"]:
+        got = header.PseudoHeaderChecksum(c["protocol"], bytes.fromhex(c["src"]), bytes.fromhex(c["dst"]),
+                                          c["total_len"])
+        assert got == c["want"], c["name"]
+
+
+def test_golden_batches_dev_and_host(vectors, engine):
+    import oracle as O
+
+    for c in vectors["batch"]:
+        arena = np.frombuffer(materialize(c["arena"]), dtype=np.uint8).copy()
+        d = np.array([tuple(x) for x in c["desc"]], dtype=O.DESC_DTYPE)
+        for off in (0, 1, 3, 8):
+            assert dev_batch(engine, arena, d, c["chained"], arena_offset=off).tolist() == c["want"], c["name"]
+        assert engine.batch_host(arena, d, c["chained"]).tolist() == c["want"], c["name"]
+
+
+# ---- BASELINE.json layouts, subsets and full size -------------------------
+@pytest.mark.parametrize("cfg,n", [(2, 65536), (3, 65536), (4, 65536), (1, None)])
+def test_config_subsets(engine, cfg, n):
+    import oracle as O
+    from netstack_amd import workloads as W
+
+    b = W.config(cfg, n)
+    arena = b.arena_host()
+    want, bad = O.c_batch(arena, b.desc)
+    assert bad == 0
+    got = dev_batch(engine, arena, b.desc)
+    assert np.array_equal(got, want)
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("cfg", [2, 3, 4])
+def test_config_full_size(engine, cfg):
+    """Full BASELINE.json batch, generated in HBM; every result vs the C oracle
+    on the same bytes (copied back), multi-threaded."""
+    torch = _torch()
+    import os
+
+    import oracle as O
+    from netstack_amd import workloads as W
+
+    b = W.config(cfg)
+    arena = b.arena_device("cuda")
+    desc = torch.from_numpy(b.desc.view(np.uint8).copy()).cuda()
+    out = engine.batch_tensors(arena, desc)
+    torch.cuda.synchronize()
+    assert engine.sync() == 0
+    got = out.cpu().numpy().view(np.uint16)
+    host = arena.cpu().numpy()
+    want = O.c_batch_mt(host, b.desc, min(16, os.cpu_count() or 1))
+    assert np.array_equal(got, want), f"{int((got != want).sum())} mismatches"
+
+    # size-independent property: append ^sum (big-endian) after each even-length
+    # packet and re-sum: every packet must verify as 0xffff (segment.go:180).
+    if cfg in (2, 3):
+        L = int(b.desc["len"][0])
+        offs = torch.from_numpy(b.desc["off"].astype(np.int64)).cuda()
+        comp = (~out.to(torch.int32)) & 0xFFFF
+        arena[offs + L] = (comp >> 8).to(torch.uint8)
+        arena[offs + L + 1] = (comp & 0xFF).to(torch.uint8)
+        d2 = b.desc.copy()
+        d2["len"] = L + 2
+        out2 = engine.batch_tensors(arena, torch.from_numpy(d2.view(np.uint8).copy()).cuda())
+        torch.cuda.synchronize()
+        assert bool((out2.cpu().numpy().view(np.uint16) == 0xFFFF).all())
+
+
+# ---- layout edge cases -----------------------------------------------------
+def test_unaligned_packed_with_odd_flags(engine):
+    import oracle as O
+    from netstack_amd import workloads as W
+
+    rng = np.random.default_rng(1)
+    n = 20000
+    lengths = rng.integers(0, 3000, n).astype(np.uint32)
+    lengths[::13] = rng.integers(0, 20, len(lengths[::13]))
+    init = rng.integers(0, 65536, n).astype(np.uint16)
+    flags = rng.integers(0, 2, n).astype(np.uint16)
+    d, end = W.make_desc(lengths, init, align=1, base=5, flags=flags)
+    arena = W.random_bytes(99, end + 7)
+    want, _ = O.c_batch(arena, d)
+    for off in (0, 1, 2, 7, 15):
+        assert np.array_equal(dev_batch(engine, arena, d, arena_offset=off), want)
+
+
+def test_random_overlapping_descriptors(engine):
+    import oracle as O
+
+    rng = np.random.default_rng(2)
+    arena = rng.integers(0, 256, 1 << 20, dtype=np.uint8)
+    n = 50000
+    d = np.zeros(n, dtype=O.DESC_DTYPE)
+    d["off"] = rng.integers(0, arena.size, n)
+    d["len"] = np.minimum(rng.integers(0, 70000, n), arena.size - d["off"])
+    d["len"][rng.random(n) < 0.5] %= 97
+    d["initial"] = rng.integers(0, 65536, n)
+    d["flags"] = rng.integers(0, 2, n)
+    want, _ = O.c_batch(arena, d)
+    assert np.array_equal(dev_batch(engine, arena, d), want)
+
+
+def test_chained_runs(engine):
+    import oracle as O
+
+    rng = np.random.default_rng(3)
+    n = 30000
+    lengths = rng.integers(0, 400, n)
+    d = np.zeros(n, dtype=O.DESC_DTYPE)
+    pos = np.concatenate([[0], np.cumsum(lengths[:-1])])
+    d["off"], d["len"] = pos, lengths
+    d["initial"] = rng.integers(0, 65536, n)
+    cont = rng.random(n) < 0.8
+    d["flags"] = (cont * 2) | (pos & 1)
+    arena = rng.integers(0, 256, int(lengths.sum()) + 1, dtype=np.uint8)
+    want, _ = O.c_batch(arena, d, chained=True)
+    assert np.array_equal(dev_batch(engine, arena, d, chained=True), want)
+    assert np.array_equal(engine.batch_host(arena, d, chained=True), want)
+
+
+def test_large_single_descriptors_wrap(engine):
+    import oracle as O
+
+    for L, fill, init in [(200000, 0xFF, 0), (131074, 0xFF, 0), (1 << 22, 0xFF, 0xFFFF), (3_000_001, None, 7)]:
+        arena = np.full(L, fill, dtype=np.uint8) if fill is not None else \
+            np.random.default_rng(L).integers(0, 256, L, dtype=np.uint8)
+        d = np.zeros(1, dtype=O.DESC_DTYPE)
+        d[0] = (0, L, init, 0)
+        want, _ = O.c_batch(arena, d)
+        assert dev_batch(engine, arena, d).tolist() == want.tolist()
+
+
+def test_out_of_range_descriptors_counted(engine):
+    import oracle as O
+
+    arena = np.arange(1000, dtype=np.uint8)
+    d = np.zeros(4, dtype=O.DESC_DTYPE)
+    d[0] = (0, 1000, 1, 0)
+    d[1] = (999, 2, 2, 0)     # past the end
+    d[2] = (5000, 1, 3, 0)    # past the end
+    d[3] = (1000, 0, 4, 0)    # empty at the end: fine
+    engine.sync()
+    got = dev_batch(engine, arena, d)
+    assert engine.sync() == 2
+    want, bad = O.c_batch(arena, d)
+    assert bad == 2 and got.tolist() == want.tolist()
+    from netstack_amd._lib import ChecksumError
+
+    with pytest.raises(ChecksumError):
+        engine.batch_host(arena, d)
+
+
+def test_empty_batch_and_empty_packets(engine):
+    import oracle as O
+
+    arena = np.zeros(16, dtype=np.uint8)
+    d = np.zeros(0, dtype=O.DESC_DTYPE)
+    assert engine.batch_host(arena, d).size == 0
+    d = np.zeros(300, dtype=O.DESC_DTYPE)
+    d["initial"] = np.arange(300)
+    assert dev_batch(engine, arena, d).tolist() == list(range(300))
+
+
+def test_vv_batch_matches_oracle(engine):
+    """sendTCPBatch: n x ChecksumVVWithOffset over one GSO payload VV."""
+    import oracle as O
+    from netstack_amd import header
+    from netstack_amd.buffer import NewVectorisedView
+
+    rng = np.random.default_rng(4)
+    for trial in range(10):
+        views = [rng.integers(0, 256, int(rng.integers(0, 9000)), dtype=np.uint8).tobytes()
+                 for _ in range(int(rng.integers(1, 12)))]
+        total = sum(map(len, views))
+        mss = int(rng.integers(1, 1461))
+        segs, off = [], 0
+        while off < total:
+            sz = min(mss, total - off)
+            segs.append((off, sz, int(rng.integers(0, 65536))))
+            off += sz
+        segs.append((total + 5, 10, 3))  # past the end -> initial
+        vv = NewVectorisedView(total, views)
+        got = header.ChecksumVVBatch(vv, segs)
+        want = [O.c_checksum_vv_with_offset(views, i, o, s) for (o, s, i) in segs]
+        assert got == want
+
+
+def test_on_side_stream(engine):
+    torch = _torch()
+    import oracle as O
+    from netstack_amd import workloads as W
+
+    b = W.config(2, 4096)
+    arena = b.arena_host()
+    want, _ = O.c_batch(arena, b.desc)
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        got = dev_batch(engine, arena, b.desc, stream=s)
+    assert np.array_equal(got, want)
+
+
+def test_fuzz_small(engine):
+    import oracle as O
+
+    rng = np.random.default_rng(7)
+    for trial in range(30):
+        size = int(rng.integers(1, 5000))
+        arena = rng.integers(0, 256, size, dtype=np.uint8)
+        n = int(rng.integers(1, 700))
+        d = np.zeros(n, dtype=O.DESC_DTYPE)
+        d["off"] = rng.integers(0, size + 1, n)
+        d["len"] = [int(rng.integers(0, size - o + 1)) for o in d["off"]]
+        d["initial"] = rng.integers(0, 65536, n)
+        d["flags"] = rng.integers(0, 4, n)
+        chained = bool(trial % 2)
+        want, _ = O.c_batch(arena, d, chained)
+        assert np.array_equal(dev_batch(engine, arena, d, chained, arena_offset=trial % 16), want), trial

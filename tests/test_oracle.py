@@ -1,0 +1,119 @@
+"""CPU: the oracle (both restatements) against the pinned known answers and the
+golden vectors, plus the invariants the reference's tests rely on."""
+import numpy as np
+import pytest
+
+from make_golden import materialize
+
+
+def test_reference_kats_vv(kat, oracle_mod):
+    O = oracle_mod
+    for c in kat["vv_with_offset"]:
+        views = [bytes.fromhex(v) for v in c["views"]]
+        # checksum_test.go:98 — through ChecksumVVWithOffset
+        assert O.py_checksum_vv_with_offset(views, c["initial"], c["off"], c["size"]) == c["want"], c["name"]
+        assert O.c_checksum_vv_with_offset(views, c["initial"], c["off"], c["size"]) == c["want"], c["name"]
+        # checksum_test.go:101-105 — through Checksum on the flattened view
+        flat = b"".join(views)[c["off"]:][: c["size"]]
+        assert O.py_checksum(flat, c["initial"]) == c["want"], c["name"]
+        assert O.c_checksum(flat, c["initial"]) == c["want"], c["name"]
+
+
+def test_public_kats(kat, oracle_mod):
+    for c in kat["checksum"]:
+        buf = bytes.fromhex(c["buf"])
+        assert oracle_mod.py_checksum(buf, c["initial"]) == c["want"], c["name"]
+        assert oracle_mod.c_checksum(buf, c["initial"]) == c["want"], c["name"]
+
+
+def test_c_matches_python_on_vectors(vectors, oracle_mod):
+    O = oracle_mod
+    for c in vectors["checksum"]:
+        assert O.c_checksum(materialize(c["buf"]), c["initial"]) == c["want"], c["name"]
+    for c in vectors["vv_with_offset"]:
+        views = [materialize(v) for v in c["views"]]
+        assert O.c_checksum_vv_with_offset(views, c["initial"], c["off"], c["size"]) == c["want"], c["name"]
+    for c in vectors["views_restart"]:
+        views = [materialize(v) for v in c["views"]]
+        assert O.c_views_restart(views, c["initial"]) == c["want"], c["name"]
+    for c in vectors["pseudo_header"]:
+        got = O.c_pseudo_header(c["protocol"], bytes.fromhex(c["src"]), bytes.fromhex(c["dst"]), c["total_len"])
+        assert got == c["want"], c["name"]
+    for c in vectors["batch"]:
+        arena = np.frombuffer(materialize(c["arena"]), dtype=np.uint8)
+        d = np.array([tuple(x) for x in c["desc"]], dtype=O.DESC_DTYPE)
+        got, bad = O.c_batch(arena, d, c["chained"])
+        assert bad == 0
+        assert got.tolist() == c["want"], c["name"]
+
+
+def test_wrap_quirk(oracle_mod):
+    # Go's un-folded uint32 wraps past 128 KiB.
+    buf = b"\xff" * 200000
+    assert oracle_mod.py_checksum(buf) == 0xFFFE
+    assert oracle_mod.c_checksum(buf) == 0xFFFE
+    # RFC 1071 (exact one's complement) would give 0xFFFF here.
+    assert oracle_mod.c_checksum(b"\xff" * 131072, 0xFFFF) == 0xFFFF
+
+
+def test_zero_representation(oracle_mod):
+    O = oracle_mod
+    assert O.c_checksum(bytes(1500), 0) == 0
+    assert O.c_checksum(bytes(1500), 0xFFFF) == 0xFFFF
+    assert O.c_checksum(bytes.fromhex("fffe0001"), 0) == 0xFFFF
+
+
+def test_vv_equals_flattened_property(oracle_mod):
+    """checksum_test.go:98-106 as a property: VV == Checksum(flattened) while no
+    single view wraps."""
+    O = oracle_mod
+    rng = np.random.default_rng(3)
+    for _ in range(200):
+        views = [rng.integers(0, 256, int(rng.integers(0, 50)), dtype=np.uint8).tobytes()
+                 for _ in range(int(rng.integers(1, 8)))]
+        tot = sum(map(len, views))
+        off = int(rng.integers(0, tot + 1))
+        size = int(rng.integers(0, tot - off + 1))
+        init = int(rng.integers(0, 65536))
+        flat = b"".join(views)[off:off + size]
+        assert O.c_checksum_vv_with_offset(views, init, off, size) == O.c_checksum(flat, init)
+
+
+def test_tcp_segment_verify_and_corrupt(oracle_mod):
+    """tcp_test.go:2214-2245 (data[i]=byte(i) segments verify) and
+    tcp_test.go:3246-3254 (one corrupted payload byte must fail)."""
+    O = oracle_mod
+    src, dst = bytes([10, 0, 0, 1]), bytes([10, 0, 0, 2])
+    payload = bytes(i & 0xFF for i in range(1000))
+    hdr = bytearray(20)
+    hdr[0:2], hdr[2:4], hdr[12] = (1234).to_bytes(2, "big"), (80).to_bytes(2, "big"), 5 << 4
+    length = len(hdr) + len(payload)
+    x = O.c_pseudo_header(6, src, dst, length)
+    x = O.c_checksum(payload, x)
+    x = O.c_checksum(bytes(hdr), x)
+    hdr[16:18] = ((~x) & 0xFFFF).to_bytes(2, "big")  # tcp.SetChecksum(^...)
+    # receiver (segment.go:174-180): pseudo + header + payload == 0xffff
+    r = O.c_checksum(payload, O.c_checksum(bytes(hdr), O.c_pseudo_header(6, src, dst, length)))
+    assert r == 0xFFFF
+    bad = bytearray(payload)
+    bad[0] = 0x4
+    r = O.c_checksum(bytes(bad), O.c_checksum(bytes(hdr), O.c_pseudo_header(6, src, dst, length)))
+    assert r != 0xFFFF
+
+
+def test_negative_bounds_raise(oracle_mod):
+    with pytest.raises(ValueError):
+        oracle_mod.py_checksum_vv_with_offset([b"ab"], 0, 0, -1)
+    with pytest.raises(ValueError):
+        oracle_mod.c_checksum_vv_with_offset([b"ab"], 0, -1, 1)
+
+
+def test_batch_mt_matches(oracle_mod):
+    from netstack_amd import workloads as W
+
+    b = W.config(4, n=4000)
+    arena = b.arena_host()
+    want, bad = oracle_mod.c_batch(arena, b.desc)
+    assert bad == 0
+    got = oracle_mod.c_batch_mt(arena, b.desc, 4)
+    assert (got == want).all()
