@@ -4,7 +4,7 @@
  * This is the drop-in boundary for google/netstack's checksum hot path.  A cgo
  * shim in package `header` binds exactly these symbols;
  * nothing here uses torch or HIP types (streams are passed as `void*`, which is
- * a hipStream_t, NULL = the context's own stream).
+ * a hipStream_t; NULL = the HIP null stream, as in the HIP runtime API).
  *
  * Reference interfaces replaced (google/netstack @ /root/reference):
  *   header.Checksum              tcpip/header/checksum.go:52-55   -> ns_csum_checksum
@@ -109,7 +109,7 @@ int ns_csum_device_count(int* count);
 int ns_csum_init(const ns_csum_opts* opts, ns_csum_ctx** out);
 void ns_csum_destroy(ns_csum_ctx* ctx);
 
-/* Blocks until all work this context issued on `stream` is done; returns the
+/* Blocks until `stream` is idle (NULL: the whole device); returns the
  * number of out-of-range descriptors seen since the last call in *bad
  * (descriptors past `arena_bytes` are summed as empty and counted).          */
 int ns_csum_sync(ns_csum_ctx* ctx, void* stream, uint64_t* bad);

@@ -414,8 +414,11 @@ void ns_csum_destroy(ns_csum_ctx* ctx) {
 int ns_csum_sync(ns_csum_ctx* ctx, void* stream, uint64_t* bad) {
   if (!ctx) return NS_EINVAL;
   DeviceGuard g(ctx->device);
-  hipStream_t s = stream ? (hipStream_t)stream : ctx->stream[0];
-  HIP_TRY(hipStreamSynchronize(s));
+  if (stream) {
+    HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+  } else {
+    HIP_TRY(hipDeviceSynchronize());
+  }
   unsigned long long v = 0;
   {
     std::lock_guard<std::mutex> lk(ctx->mu);
@@ -432,7 +435,7 @@ int ns_csum_batch_dev(ns_csum_ctx* ctx, const uint8_t* d_arena, uint64_t arena_b
   if (!ctx || (n && (!d_desc || !d_out)) || (arena_bytes && !d_arena)) return NS_EINVAL;
   if (n == 0) return NS_OK;
   DeviceGuard g(ctx->device);
-  hipStream_t s = stream ? (hipStream_t)stream : ctx->stream[0];
+  hipStream_t s = (hipStream_t)stream;  // NULL = the HIP null stream
   uint32_t* part = nullptr;
   if (batch_flags & NS_BATCH_CHAINED) {
     std::lock_guard<std::mutex> lk(ctx->mu);

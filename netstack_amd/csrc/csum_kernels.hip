@@ -20,16 +20,30 @@
 // is byte-masked.  An aligned 16-byte chunk never crosses a page, and each
 // chunk read holds at least one byte of the packet, so no read can fault.
 //
-// Work decomposition ("chunk stream").  A 256-thread workgroup owns a tile of
-// 256 descriptors.  It scans their chunk counts into a virtual chunk space of
-// the tile (LDS), then streams that space: each lane takes U consecutive
-// chunks per step (so a lane's chunks almost always belong to one packet and
-// are summed in registers), finds their packet by a binary search of the
-// scan, issues all U 16-byte loads, then masks / splits the bytes into E/O
-// lanes of a packed 2x16-bit accumulator (v_and / v_perm / v_add3) and, on a
-// packet change, adds the packet's 32-bit partial into an LDS accumulator
-// (ds_add_u32).  The tile epilogue folds initial+acc and writes one u16 per
-// packet (coalesced).  No MFMA: this is a byte sum, HBM-bound.
+// Work decomposition.  A 256-thread workgroup owns a tile of P = 256*D
+// descriptors (D = 1 for MTU-sized packets, 4 for small ones).  The prologue
+// reads the tile's descriptors once, scans them in LDS and picks one of two
+// block-uniform paths:
+//
+//  * dense path — the tile's packets are sorted and non-overlapping in the
+//    arena with little padding (a packed batch, what tcpip/buffer staging and
+//    the benchmarks produce).  The tile's byte span is streamed directly:
+//    every lane owns runs of UD consecutive 16-byte chunks (a wave-instruction's
+//    lanes 64 B apart, which streams at the coalesced rate on gfx950), loads are
+//    nontemporal and software-pipelined one step ahead because their addresses
+//    do not depend on any lookup; packet attribution (a binary search of the
+//    packets' end offsets in LDS, then a forward walk with byte masks) runs
+//    while the next step's loads are in flight.
+//  * general path — any table (unsorted, overlapping, sparse, giant
+//    descriptors): the tile's chunk counts are scanned into a virtual chunk
+//    space; each lane takes UG consecutive virtual chunks, finds their packet
+//    by binary search and loads them.
+//
+// Both paths split each chunk into even/odd byte lanes of packed 2x16-bit
+// accumulators, flush a packet's 32-bit partial into an LDS accumulator
+// (ds_add_u32) when the lane moves past it, and the epilogue folds
+// initial + partial and writes one u16 per packet (coalesced).  No MFMA: this
+// is a byte sum, HBM-bound.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -70,144 +84,443 @@ __device__ __forceinline__ uint32_t partial_of(uint32_t e, uint32_t o, uint32_t 
   return phase ? (E + (O << 8)) : ((E << 8) + O);
 }
 
-// meta word: bits 0-3 = first byte within first chunk, 4-7 = last byte within
-// last chunk, bit 8 = phase.
-template <int WG, int U>
-__global__ __launch_bounds__(WG) void csum_tiles(
+// meta word (general path): bits 0-3 = first byte within first chunk,
+// 4-7 = last byte within last chunk, bit 8 = phase.  Dense path: bit 8 only.
+constexpr uint32_t kPhaseBit = 1u << 8;
+
+template <bool NT>
+__device__ __forceinline__ uint4 load16(const uint4* p) {
+  if constexpr (NT) {
+    uint4 v;
+    v.x = __builtin_nontemporal_load(&p->x);
+    v.y = __builtin_nontemporal_load(&p->y);
+    v.z = __builtin_nontemporal_load(&p->z);
+    v.w = __builtin_nontemporal_load(&p->w);
+    return v;
+  } else {
+    return *p;
+  }
+}
+
+__device__ __forceinline__ uint4 mask_chunk(uint4 w, int lo, int hi) {
+  w.x &= dword_mask(lo, hi, 0);
+  w.y &= dword_mask(lo, hi, 1);
+  w.z &= dword_mask(lo, hi, 2);
+  w.w &= dword_mask(lo, hi, 3);
+  return w;
+}
+
+__device__ __forceinline__ void flush(uint32_t* s_acc, const uint32_t* s_meta, int pk,
+                                      uint32_t e, uint32_t o) {
+  if (e | o) atomicAdd(&s_acc[pk], partial_of(e, o, s_meta[pk] & kPhaseBit));
+}
+
+// ---- general path: virtual chunk space ------------------------------------
+template <int P, int U, bool NT>
+__device__ __forceinline__ void general_step(const uint4* __restrict__ chunks,
+                                             const uint64_t* __restrict__ s_cstart,
+                                             const uint64_t* __restrict__ s_cbase,
+                                             const uint32_t* __restrict__ s_meta,
+                                             uint32_t* __restrict__ s_acc, uint64_t C,
+                                             uint64_t c0, int& pk_floor) {
+  constexpr int LOGP = __builtin_ctz(P);
+  // Largest pk with s_cstart[pk] <= c0 (that packet is non-empty); the lane's
+  // packet only moves forward, so search [pk_floor, P).
+  int lo = pk_floor, hi = P;
+#pragma unroll
+  for (int s = 0; s < LOGP; ++s) {
+    const int mid = (lo + hi) >> 1;
+    if (hi - lo > 1) {
+      if (s_cstart[mid] <= c0) lo = mid; else hi = mid;
+    }
+  }
+  int pk = lo;
+  pk_floor = lo;
+  uint64_t pstart = s_cstart[pk], pend = s_cstart[pk + 1], pbase = s_cbase[pk];
+  uint4 v[U];
+  int pid[U];
+  uint32_t firstm = 0, lastm = 0;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const uint64_t c = c0 + u;
+    pid[u] = -1;
+    v[u] = make_uint4(0, 0, 0, 0);
+    if (c < C) {
+      while (c >= pend) {
+        ++pk;
+        pstart = pend;
+        pend = s_cstart[pk + 1];
+        pbase = s_cbase[pk];
+      }
+      pid[u] = pk;
+      if (c == pstart) firstm |= 1u << u;
+      if (c + 1 == pend) lastm |= 1u << u;
+      v[u] = load16<NT>(chunks + (pbase + c));
+    }
+  }
+  int cur = pid[0];
+  uint32_t e = 0, o = 0;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    if (pid[u] < 0) break;
+    if (pid[u] != cur) {
+      flush(s_acc, s_meta, cur, e, o);
+      e = 0;
+      o = 0;
+      cur = pid[u];
+    }
+    uint4 w = v[u];
+    if ((firstm | lastm) & (1u << u)) {
+      const uint32_t m = s_meta[cur];
+      const int blo = (firstm >> u) & 1u ? (int)(m & 15u) : 0;
+      const int bhi = (lastm >> u) & 1u ? (int)((m >> 4) & 15u) + 1 : 16;
+      w = mask_chunk(w, blo, bhi);
+    }
+    acc_chunk(w, e, o);
+  }
+  flush(s_acc, s_meta, cur, e, o);
+}
+
+// ---- dense path: stream the tile's byte span --------------------------------
+// Loads go through a buffer resource (SRD) whose range is the tile span:
+// measured on MI355X, per-lane runs of 4 chunks stream at 6.26 TB/s through
+// buffer_load_dwordx4 but only 5.46 TB/s through global_load_dwordx4, and the
+// SRD range check returns zeros past the span (no clamping, no branches).
+// AUX = cache-policy bits (0 default; 2 nt helps only fully coalesced reads).
+template <int U, int AUX>
+__device__ __forceinline__ void dense_load(__amdgpu_buffer_rsrc_t rsrc, uint32_t q0, uint4 (&v)[U]) {
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    auto x = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (int)((q0 + u) * 16u), 0, AUX);
+    v[u] = *reinterpret_cast<uint4*>(&x);
+  }
+}
+
+// Attribute one lane run [16*q0, 16*(q0+U)) of the tile span to packets.
+// s_S/s_E: packet start/end byte offsets in the span (both non-decreasing;
+// empty packets have S == E).
+template <int P, int U>
+__device__ __forceinline__ void dense_consume(const uint4 (&v)[U], uint32_t q0, uint32_t C,
+                                              const uint32_t* __restrict__ s_S,
+                                              const uint32_t* __restrict__ s_E,
+                                              const uint32_t* __restrict__ s_meta,
+                                              uint32_t* __restrict__ s_acc, int& pk_floor) {
+  constexpr int LOGP = __builtin_ctz(P);
+  if (q0 >= C) return;
+  const uint32_t rb = q0 * 16u;
+  // First packet with E > rb, in [pk_floor, P].
+  int lo = pk_floor, hi = P;
+#pragma unroll
+  for (int s = 0; s <= LOGP; ++s) {
+    if (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (s_E[mid] > rb) hi = mid; else lo = mid + 1;
+    }
+  }
+  int cur = lo;
+  pk_floor = lo;
+  if (cur >= P) return;
+  uint32_t S = s_S[cur], E = s_E[cur];
+  uint32_t e = 0, o = 0;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const uint32_t cb = rb + 16u * u;
+    if (q0 + u >= C) break;
+    const uint4 w = v[u];
+    while (S < cb + 16u) {
+      if (S <= cb && E >= cb + 16u) {
+        acc_chunk(w, e, o);  // the whole chunk belongs to `cur`
+      } else {
+        const int blo = (int)(max(S, cb) - cb);
+        const int bhi = (int)(min(E, cb + 16u) - cb);
+        if (bhi > blo) acc_chunk(mask_chunk(w, blo, bhi), e, o);
+      }
+      if (E > cb + 16u) break;  // `cur` continues into the next chunk
+      flush(s_acc, s_meta, cur, e, o);
+      e = 0;
+      o = 0;
+      if (++cur >= P) break;
+      S = s_S[cur];
+      E = s_E[cur];
+    }
+    if (cur >= P) break;
+  }
+  if (cur < P) flush(s_acc, s_meta, cur, e, o);
+}
+
+// ---- dense path, LDS-DMA ring variant ---------------------------------------
+// Each wave streams its share of the tile span in windows of 64*U chunks.  A
+// window is fetched by U global_load_lds_dwordx4 (1 KiB each, fully coalesced,
+// nontemporal) into a wave-private ring slot, NB slots deep, then every lane
+// reads its run of U consecutive chunks back with ds_read_b128.  The source
+// permutation below makes those reads bank-conflict-free: LDS position
+// p = m + (64/U)*j of block b holds window chunk b*64 + U*m + j, so the 16
+// lanes of a ds_read_b128 group hit 16 distinct 16-byte bank slots.
+template <int U>
+__device__ __forceinline__ uint32_t ring_src(int u, int lane) {
+  constexpr int G = 64 / U;
+  return (uint32_t)(u * 64 + U * (lane % G) + lane / G);
+}
+template <int U>
+__device__ __forceinline__ uint32_t ring_pos(int lane, int j) {
+  constexpr int G = 64 / U;
+  return (uint32_t)(((lane * U) / 64) * 64 + (lane % G) + G * j);
+}
+
+// One 16-byte-per-lane LDS-DMA (global_load_lds_dwordx4): lane i's 16 bytes
+// land at lds_dst + 16*i.  Issued from inline asm so that hipcc does not
+// count it: otherwise it drains every in-flight DMA (vmcnt(0)) in front of any
+// LDS store or atomic it cannot prove disjoint from the ring.  Completion is
+// waited for explicitly with wait_vmcnt<N>() (cdna_hip_programming.md §5.7).
+template <bool NT>
+__device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_dst) {
+  unsigned keep;
+  if constexpr (NT) {
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(gsrc), "s"(lds_dst)
+        : "memory");
+  } else {
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(gsrc), "s"(lds_dst)
+        : "memory");
+  }
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
+}
+
+// Template parameters: WG threads, D descriptors per thread (tile P = WG*D),
+// UG / UD chunks per lane run on the general / dense path, NT nontemporal
+// loads (each byte is read exactly once).
+template <int WG, int D, int UG, int UD, bool NT, int DM = 0, int NB = 3>
+__global__ __launch_bounds__(WG) void csum_batch(
     const uint8_t* __restrict__ arena, uint64_t arena_bytes,
     const uint4* __restrict__ desc, uint32_t n, uint16_t* __restrict__ out,
     uint32_t* __restrict__ partial, unsigned long long* __restrict__ err) {
-  constexpr int P = WG;  // descriptors per tile
+  constexpr int P = WG * D;
   constexpr int NW = WG / 64;
-  static_assert(U * 1020 < 65536, "packed 16-bit lanes would overflow");
-  __shared__ uint64_t s_cstart[P + 1];  // virtual chunk start per packet
-  __shared__ uint64_t s_cbase[P];       // absolute chunk index - s_cstart
+  static_assert((P & (P - 1)) == 0, "tile must be a power of two");
+  static_assert(UG * 1020 < 65536 && UD * 1020 < 65536, "packed 16-bit lanes would overflow");
+  __shared__ uint64_t s_cstart[P + 1];  // general: virtual chunk start per packet
+  __shared__ uint64_t s_cbase[P];       // general: chunk index - s_cstart; dense: S|E
   __shared__ uint32_t s_meta[P];
   __shared__ uint32_t s_acc[P];
-  __shared__ uint64_t s_wtot[NW];
+  __shared__ uint64_t s_wsum[NW], s_wmax[NW], s_wmin[NW], s_wpay[NW];
+  // dense path ring (DM == 1): NW waves x NB slots x 64*UD chunks
+  __shared__ uint4 s_ring[DM == 1 ? NW * NB * 64 * UD : 1];
 
   const int t = threadIdx.x;
   const int lane = t & 63;
   const int wv = t >> 6;
-  const uint64_t i = (uint64_t)blockIdx.x * P + t;
+  const uint64_t i0 = (uint64_t)blockIdx.x * P + (uint64_t)t * D;
+  const uint64_t abase = (uint64_t)(uintptr_t)arena & 15u;  // arena-aligned coordinates
 
-  uint64_t nch = 0, cb = 0;
-  uint32_t meta = 0, init = 0;
-  if (i < n) {
-    const uint4 raw = desc[i];
-    const uint64_t off = (uint64_t)raw.x | ((uint64_t)raw.y << 32);
-    uint32_t len = raw.z;
-    init = raw.w & 0xFFFFu;
-    const uint32_t odd = (raw.w >> 16) & 1u;
-    if (off > arena_bytes || (uint64_t)len > arena_bytes - off) {
-      len = 0;
-      atomicAdd(err, 1ull);
+  uint64_t a[D], nch[D];
+  uint32_t len[D], meta[D], init[D];
+  uint64_t tsum = 0, tpay = 0, tmax = 0, tmin = ~0ull;
+  bool sorted = true;
+#pragma unroll
+  for (int k = 0; k < D; ++k) {
+    a[k] = 0;
+    nch[k] = 0;
+    len[k] = 0;
+    meta[k] = 0;
+    init[k] = 0;
+    const uint64_t i = i0 + k;
+    if (i < n) {
+      const uint4 raw = desc[i];
+      const uint64_t off = (uint64_t)raw.x | ((uint64_t)raw.y << 32);
+      uint32_t l = raw.z;
+      init[k] = raw.w & 0xFFFFu;
+      const uint32_t odd = (raw.w >> 16) & 1u;
+      if (off > arena_bytes || (uint64_t)l > arena_bytes - off) {
+        l = 0;
+        atomicAdd(err, 1ull);
+      }
+      if (l) {
+        const uint64_t s = abase + off;
+        const uint64_t last = s + l - 1;
+        a[k] = s;
+        len[k] = l;
+        nch[k] = (last >> 4) - (s >> 4) + 1;
+        meta[k] = (uint32_t)(s & 15u) | ((uint32_t)(last & 15u) << 4) |
+                  ((uint32_t)((s + odd) & 1u) << 8);
+        sorted = sorted && (s >= tmax);
+        tmax = s + l;
+        tmin = min(tmin, s);
+        tpay += l;
+      }
     }
-    if (len) {
-      // chunk coordinates relative to the 16-byte-aligned arena base (keeps
-      // the loads in the global address space; parity is unchanged).
-      const uint64_t a = ((uint64_t)(uintptr_t)arena & 15u) + off;
-      const uint64_t last = a + len - 1;
-      nch = (last >> 4) - (a >> 4) + 1;
-      cb = a >> 4;
-      meta = (uint32_t)(a & 15u) | ((uint32_t)(last & 15u) << 4) |
-             ((uint32_t)((a + odd) & 1u) << 8);
-    }
+    tsum += nch[k];
   }
 
-  // Block-wide exclusive scan of the chunk counts.
-  uint64_t incl = nch;
+  // Wave scans (sum of chunk counts, max of ends) and reductions.
+  uint64_t isum = tsum, imax = tmax, rmin = tmin, rpay = tpay;
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
-    const uint64_t y = __shfl_up(incl, d, 64);
-    if (lane >= d) incl += y;
-  }
-  if (lane == 63) s_wtot[wv] = incl;
-  s_acc[t] = 0u;
-  __syncthreads();
-  uint64_t wbase = 0;
-#pragma unroll
-  for (int w = 0; w < NW; ++w)
-    if (w < wv) wbase += s_wtot[w];
-  const uint64_t excl = wbase + incl - nch;
-  s_cstart[t] = excl;
-  s_cbase[t] = cb - excl;
-  s_meta[t] = meta;
-  if (t == P - 1) s_cstart[P] = excl + nch;
-  __syncthreads();
-
-  const uint4* __restrict__ chunks =
-      reinterpret_cast<const uint4*>(arena - ((uintptr_t)arena & 15u));
-  const uint64_t C = s_cstart[P];
-  for (uint64_t base = 0; base < C; base += (uint64_t)WG * U) {
-    const uint64_t c0 = base + (uint64_t)t * U;
-    if (c0 >= C) break;
-    // Largest pk with s_cstart[pk] <= c0 (that packet is non-empty).
-    int lo = 0, hi = P;
-#pragma unroll
-    for (int s = 0; s < 8; ++s) {  // log2(P) steps (P = 256)
-      const int mid = (lo + hi) >> 1;
-      if (s_cstart[mid] <= c0) lo = mid; else hi = mid;
+    const uint64_t ys = __shfl_up(isum, d, 64);
+    const uint64_t ym = __shfl_up(imax, d, 64);
+    if (lane >= d) {
+      isum += ys;
+      imax = max(imax, ym);
     }
-    int pk = lo;
-    uint64_t pstart = s_cstart[pk];
-    uint64_t pend = s_cstart[pk + 1];
-    uint64_t pbase = s_cbase[pk];
-
-    uint4 v[U];
-    int pid[U];
-    uint32_t firstm = 0, lastm = 0;
+    rmin = min(rmin, __shfl_xor(rmin, d, 64));
+    rpay += __shfl_xor(rpay, d, 64);
+  }
+  // Exclusive max of ends before this thread, within the wave.
+  uint64_t xmax = __shfl_up(imax, 1, 64);
+  if (lane == 0) xmax = 0;
+  if (lane == 63) {
+    s_wsum[wv] = isum;
+    s_wmax[wv] = imax;
+    s_wmin[wv] = rmin;
+    s_wpay[wv] = rpay;
+  }
+  // First non-empty start of this thread vs everything before it.
+  uint64_t first = ~0ull;
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint64_t c = c0 + u;
-      if (c < C) {
-        while (c >= pend) {
-          ++pk;
-          pstart = pend;
-          pend = s_cstart[pk + 1];
-          pbase = s_cbase[pk];
-        }
-        pid[u] = pk;
-        if (c == pstart) firstm |= 1u << u;
-        if (c + 1 == pend) lastm |= 1u << u;
-        v[u] = chunks[pbase + c];
+  for (int k = D - 1; k >= 0; --k)
+    if (len[k]) first = a[k];
+  __syncthreads();
+  uint64_t run = isum - tsum, tot = 0, maxend = 0, minstart = ~0ull, pay = 0;
+#pragma unroll
+  for (int w = 0; w < NW; ++w) {
+    if (w < wv) {
+      run += s_wsum[w];
+      xmax = max(xmax, s_wmax[w]);
+    }
+    tot += s_wsum[w];
+    maxend = max(maxend, s_wmax[w]);
+    minstart = min(minstart, s_wmin[w]);
+    pay += s_wpay[w];
+  }
+  if (first != ~0ull && first < xmax) sorted = false;
+  const bool all_sorted = __syncthreads_and(sorted);
+  const uint64_t tbase = (minstart == ~0ull) ? 0 : (minstart & ~15ull);
+  const uint64_t span = (minstart == ~0ull) ? 0 : maxend - tbase;
+  const bool dense = all_sorted && pay != 0 && span < (1ull << 31) &&
+                     span <= pay + (pay >> 3) + 64ull * P;
+
+  uint32_t* s_S = reinterpret_cast<uint32_t*>(s_cbase);
+  uint32_t* s_E = s_S + P;
+  if (dense) {
+    uint64_t rm = xmax;  // running max end before descriptor k
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+      const int idx = t * D + k;
+      if (len[k]) {
+        s_S[idx] = (uint32_t)(a[k] - tbase);
+        s_E[idx] = (uint32_t)(a[k] + len[k] - tbase);
+        rm = a[k] + len[k];
       } else {
-        pid[u] = -1;
-        v[u] = make_uint4(0, 0, 0, 0);
+        const uint32_t z = rm > tbase ? (uint32_t)(rm - tbase) : 0u;
+        s_S[idx] = z;
+        s_E[idx] = z;
       }
+      s_meta[idx] = meta[k] & kPhaseBit;
+      s_acc[idx] = 0u;
     }
-
-    int cur = pid[0];
-    uint32_t e = 0, o = 0;
+  } else {
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if (pid[u] < 0) break;
-      if (pid[u] != cur) {
-        atomicAdd(&s_acc[cur], partial_of(e, o, (s_meta[cur] >> 8) & 1u));
-        e = 0;
-        o = 0;
-        cur = pid[u];
-      }
-      uint4 w = v[u];
-      if ((firstm | lastm) & (1u << u)) {
-        const uint32_t m = s_meta[cur];
-        const int blo = (firstm >> u) & 1u ? (int)(m & 15u) : 0;
-        const int bhi = (lastm >> u) & 1u ? (int)((m >> 4) & 15u) + 1 : 16;
-        w.x &= dword_mask(blo, bhi, 0);
-        w.y &= dword_mask(blo, bhi, 1);
-        w.z &= dword_mask(blo, bhi, 2);
-        w.w &= dword_mask(blo, bhi, 3);
-      }
-      acc_chunk(w, e, o);
+    for (int k = 0; k < D; ++k) {
+      const int idx = t * D + k;
+      s_cstart[idx] = run;
+      s_cbase[idx] = (len[k] ? (a[k] >> 4) : 0) - run;
+      s_meta[idx] = meta[k];
+      s_acc[idx] = 0u;
+      run += nch[k];
     }
-    atomicAdd(&s_acc[cur], partial_of(e, o, (s_meta[cur] >> 8) & 1u));
+    if (t == WG - 1) s_cstart[P] = run;
   }
   __syncthreads();
 
-  if (i < n) {
-    const uint32_t s = s_acc[t];
-    if (partial) partial[i] = s;
-    else out[i] = (uint16_t)fold1(init + s);
+  const uint4* __restrict__ chunks = reinterpret_cast<const uint4*>(arena - abase);
+  if (dense && DM == 1) {
+    const uint32_t C = (uint32_t)((span + 15) >> 4);
+    const uint4* __restrict__ tb = chunks + (tbase >> 4);
+    constexpr uint32_t WIN = 64u * UD;
+    const uint32_t nwin = (C + WIN - 1) / WIN;
+    const int w = __builtin_amdgcn_readfirstlane(wv);
+    const uint32_t k0 = (uint32_t)(((uint64_t)nwin * w) / NW);
+    const uint32_t k1 = (uint32_t)(((uint64_t)nwin * (w + 1)) / NW);
+    uint4* ring = s_ring + (size_t)w * NB * WIN;
+    // LDS byte offset of this wave's ring (wave-uniform, in an SGPR).
+    const uint32_t ring_lds = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint4*)ring;
+    auto issue = [&](uint32_t k) {
+      const uint32_t slot = __builtin_amdgcn_readfirstlane(ring_lds + (k % NB) * WIN * 16u);
+#pragma unroll
+      for (int u = 0; u < UD; ++u) {
+        // Out-of-range lanes re-read the last chunk instead of being masked
+        // off, so every wave-instruction issues and the vmcnt counts hold.
+        const uint32_t src = min(k * WIN + ring_src<UD>(u, lane), C - 1);
+        glds16<NT>(tb + src, slot + u * 1024u);
+      }
+    };
+#pragma unroll
+    for (int a0 = 0; a0 < NB - 1; ++a0)
+      if (k0 + a0 < k1) issue(k0 + a0);
+    int pk_floor = 0;
+    for (uint32_t k = k0; k < k1; ++k) {
+      if (k + NB - 1 < k1) {
+        issue(k + NB - 1);
+        wait_vmcnt<(NB - 1) * UD>();
+      } else {
+        wait_vmcnt<0>();
+      }
+      const uint4* slot = ring + (k % NB) * WIN;
+      uint4 v[UD];
+#pragma unroll
+      for (int j = 0; j < UD; ++j) v[j] = slot[ring_pos<UD>(lane, j)];
+      dense_consume<P, UD>(v, k * WIN + (uint32_t)lane * UD, C, s_S, s_E, s_meta, s_acc, pk_floor);
+    }
+  } else if (dense) {
+    const uint32_t C = (uint32_t)((span + 15) >> 4);
+    // Wave-uniform SRD over the tile span (readfirstlane: T20, no waterfall).
+    const uint64_t tbp = (uint64_t)(uintptr_t)(chunks + (tbase >> 4));
+    const uint32_t lo32 = __builtin_amdgcn_readfirstlane((uint32_t)tbp);
+    const uint32_t hi32 = __builtin_amdgcn_readfirstlane((uint32_t)(tbp >> 32));
+    const uint32_t nrec = __builtin_amdgcn_readfirstlane(C * 16u);
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(((uint64_t)hi32 << 32) | lo32), (short)0, (int)nrec, 0x00020000);
+    constexpr uint32_t STEP = (uint32_t)WG * UD;
+    constexpr int AUX = NT ? 2 : 0;
+    int pk_floor = 0;
+    uint4 va[UD], vb[UD];
+    uint32_t q = (uint32_t)t * UD;
+    dense_load<UD, AUX>(rsrc, q, va);
+    while (q < C) {
+      dense_load<UD, AUX>(rsrc, q + STEP, vb);
+      dense_consume<P, UD>(va, q, C, s_S, s_E, s_meta, s_acc, pk_floor);
+      q += STEP;
+      if (q >= C) break;
+      dense_load<UD, AUX>(rsrc, q + STEP, va);
+      dense_consume<P, UD>(vb, q, C, s_S, s_E, s_meta, s_acc, pk_floor);
+      q += STEP;
+    }
+  } else {
+    int pk_floor = 0;
+    for (uint64_t c0 = (uint64_t)t * UG; c0 < tot; c0 += (uint64_t)WG * UG)
+      general_step<P, UG, NT>(chunks, s_cstart, s_cbase, s_meta, s_acc, tot, c0, pk_floor);
+  }
+  __syncthreads();
+
+#pragma unroll
+  for (int k = 0; k < D; ++k) {
+    const uint64_t i = i0 + k;
+    if (i < n) {
+      const uint32_t sacc = s_acc[t * D + k];
+      if (partial) partial[i] = sacc;
+      else out[i] = (uint16_t)fold1(init[k] + sacc);
+    }
   }
 }
 
@@ -235,19 +548,27 @@ __global__ void csum_chain(const uint4* __restrict__ desc, uint32_t n,
 // ---- launchers (C++ linkage, used by csum_api.cpp) ------------------------
 namespace nsk {
 
-static constexpr int kWG = 256;
-static constexpr int kU = 8;
+template <int D, int UD>
+static hipError_t launch_tiles(const uint8_t* arena, uint64_t arena_bytes, const void* desc,
+                               uint32_t n, uint16_t* out, uint32_t* partial,
+                               unsigned long long* err, hipStream_t stream) {
+  constexpr int WG = 256;
+  const uint32_t tiles = (uint32_t)(((uint64_t)n + WG * D - 1) / (WG * D));
+  hipLaunchKernelGGL((csum_batch<WG, D, 2, UD, false>), dim3(tiles), dim3(WG), 0, stream, arena,
+                     arena_bytes, reinterpret_cast<const uint4*>(desc), n, out, partial, err);
+  return hipGetLastError();
+}
 
 hipError_t launch_batch(const uint8_t* arena, uint64_t arena_bytes,
                         const void* desc, uint32_t n, uint16_t* out,
                         uint32_t* partial, unsigned long long* err,
                         hipStream_t stream) {
   if (n == 0) return hipSuccess;
-  const uint32_t tiles = (n + kWG - 1) / kWG;
-  hipLaunchKernelGGL((csum_tiles<kWG, kU>), dim3(tiles), dim3(kWG), 0, stream,
-                     arena, arena_bytes, reinterpret_cast<const uint4*>(desc), n,
-                     out, partial, err);
-  hipError_t e = hipGetLastError();
+  // Dense-path run length by the mean arena bytes per descriptor (tools/tune.py
+  // on MI355X: 8 chunks per lane for MTU-sized packets, 4 for small/mixed).
+  const bool big = arena_bytes / n >= 1024;
+  hipError_t e = big ? launch_tiles<1, 8>(arena, arena_bytes, desc, n, out, partial, err, stream)
+                     : launch_tiles<1, 4>(arena, arena_bytes, desc, n, out, partial, err, stream);
   if (e != hipSuccess || partial == nullptr) return e;
   const uint32_t blocks = (n + 255) / 256;
   hipLaunchKernelGGL(csum_chain, dim3(blocks), dim3(256), 0, stream,

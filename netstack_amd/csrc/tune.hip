@@ -1,0 +1,170 @@
+// tune.hip — NOT part of the product ABI.  Builds libns_tune.so: every
+// template variant of the checksum kernel behind one index, plus read-stream
+// calibration kernels, so tools/tune.py can A/B them in one process
+// (cdna_hip_programming.md §5.4 rule 24) and bench.py can report the roofline
+// against a same-run calibration.
+#include "csum_kernels.hip"
+
+namespace nsk {
+
+// Pure streaming read of `bytes` (multiple of 16): grid-stride, 4 x 16-B loads
+// in flight per lane per iteration, fully coalesced.  One u32 per block out.
+__global__ __launch_bounds__(256) void calib_read(const uint4* __restrict__ p, uint64_t n16,
+                                                  uint32_t* __restrict__ out) {
+  uint32_t acc = 0;
+  const uint64_t stride = (uint64_t)gridDim.x * 256;
+  uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  for (; i + 3 * stride < n16; i += 4 * stride) {
+    const uint4 a = p[i], b = p[i + stride], c = p[i + 2 * stride], d = p[i + 3 * stride];
+    acc += a.x ^ a.y ^ a.z ^ a.w;
+    acc += b.x ^ b.y ^ b.z ^ b.w;
+    acc += c.x ^ c.y ^ c.z ^ c.w;
+    acc += d.x ^ d.y ^ d.z ^ d.w;
+  }
+  for (; i < n16; i += stride) {
+    const uint4 a = p[i];
+    acc += a.x ^ a.y ^ a.z ^ a.w;
+  }
+  for (int d = 32; d > 0; d >>= 1) acc += __shfl_xor(acc, d, 64);
+  if ((threadIdx.x & 63) == 0) atomicAdd(&out[blockIdx.x], acc);
+}
+
+// Same bytes, but each lane reads U consecutive 16-B chunks (lanes U*16 B
+// apart): the access shape of csum_tiles' per-lane runs.
+template <int U, bool NT = false>
+__global__ __launch_bounds__(256) void calib_read_runs(const uint4* __restrict__ p, uint64_t n16,
+                                                       uint32_t* __restrict__ out) {
+  uint32_t acc = 0;
+  const uint64_t step = (uint64_t)gridDim.x * 256 * U;
+  for (uint64_t b = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * U; b < n16; b += step) {
+    uint4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = (b + u < n16) ? load16<NT>(p + b + u) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc += v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+  }
+  for (int d = 32; d > 0; d >>= 1) acc += __shfl_xor(acc, d, 64);
+  if ((threadIdx.x & 63) == 0) atomicAdd(&out[blockIdx.x], acc);
+}
+
+// Coalesced read with 8 x 16-B loads in flight per lane; NT = nontemporal.
+template <bool NT>
+__global__ __launch_bounds__(256) void calib_read8(const uint4* __restrict__ p, uint64_t n16,
+                                                   uint32_t* __restrict__ out) {
+  uint32_t acc = 0;
+  const uint64_t stride = (uint64_t)gridDim.x * 256;
+  uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  for (; i + 7 * stride < n16; i += 8 * stride) {
+    uint4 v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      if constexpr (NT) {
+        const uint4* q = &p[i + k * stride];
+        v[k].x = __builtin_nontemporal_load(&q->x);
+        v[k].y = __builtin_nontemporal_load(&q->y);
+        v[k].z = __builtin_nontemporal_load(&q->z);
+        v[k].w = __builtin_nontemporal_load(&q->w);
+      } else {
+        v[k] = p[i + k * stride];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc += v[k].x ^ v[k].y ^ v[k].z ^ v[k].w;
+  }
+  for (; i < n16; i += stride) {
+    const uint4 a = p[i];
+    acc += a.x ^ a.y ^ a.z ^ a.w;
+  }
+  for (int d = 32; d > 0; d >>= 1) acc += __shfl_xor(acc, d, 64);
+  if ((threadIdx.x & 63) == 0) atomicAdd(&out[blockIdx.x], acc);
+}
+
+// Runs of U consecutive chunks per lane (U = 1: coalesced) through raw buffer
+// loads with cache-policy bits AUX (1 = sc0, 2 = nt, 16 = sc1).
+template <int U, int AUX>
+__global__ __launch_bounds__(256) void calib_buf(const uint4* __restrict__ p, uint64_t n16,
+                                                 uint32_t* __restrict__ out) {
+  uint32_t acc = 0;
+  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, (int)0x7FFFFFF0, 0x00020000);
+  const uint64_t step = (uint64_t)gridDim.x * 256 * U;
+  const uint64_t lim = min<uint64_t>(n16, 0x7FFFFFF0ull / 16);
+  for (uint64_t b = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * U; b + U <= lim; b += step) {
+    uint4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      auto x = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (int)((b + u) * 16), 0, AUX);
+      v[u] = *reinterpret_cast<uint4*>(&x);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc += v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+  }
+  for (int d = 32; d > 0; d >>= 1) acc += __shfl_xor(acc, d, 64);
+  if ((threadIdx.x & 63) == 0) atomicAdd(&out[blockIdx.x], acc);
+}
+
+template <int D, int UG, int UD, bool NT, int DM = 0, int NB = 3>
+hipError_t launch_v(const uint8_t* arena, uint64_t arena_bytes, const void* desc, uint32_t n,
+                    uint16_t* out, unsigned long long* err, hipStream_t s) {
+  const uint32_t tiles = (n + 256 * D - 1) / (256 * D);
+  hipLaunchKernelGGL((csum_batch<256, D, UG, UD, NT, DM, NB>), dim3(tiles), dim3(256), 0, s, arena, arena_bytes,
+                     reinterpret_cast<const uint4*>(desc), n, out, nullptr, err);
+  return hipGetLastError();
+}
+
+typedef hipError_t (*launch_fn)(const uint8_t*, uint64_t, const void*, uint32_t, uint16_t*,
+                                unsigned long long*, hipStream_t);
+struct Variant {
+  const char* name;
+  launch_fn fn;
+};
+static const Variant kVariants[] = {
+    {"buf_D1_U4", launch_v<1, 2, 4, false>},    {"buf_D1_U2", launch_v<1, 2, 2, false>},
+    {"buf_D1_U8", launch_v<1, 2, 8, false>},    {"buf_D1_U4_nt", launch_v<1, 2, 4, true>},
+    {"buf_D2_U4", launch_v<2, 2, 4, false>},    {"buf_D4_U4", launch_v<4, 2, 4, false>},
+    {"buf_D4_U2", launch_v<4, 2, 2, false>},    {"buf_D1_U2_nt", launch_v<1, 2, 2, true>},
+};
+
+}  // namespace nsk
+
+extern "C" {
+
+int nsk_tune_count(void) { return (int)(sizeof(nsk::kVariants) / sizeof(nsk::kVariants[0])); }
+
+const char* nsk_tune_name(int v) {
+  return (v >= 0 && v < nsk_tune_count()) ? nsk::kVariants[v].name : "";
+}
+
+int nsk_tune_launch(int v, const uint8_t* arena, uint64_t arena_bytes, const void* desc, uint32_t n,
+                    uint16_t* out, unsigned long long* err, void* stream) {
+  if (v < 0 || v >= nsk_tune_count()) return -1;
+  return nsk::kVariants[v].fn(arena, arena_bytes, desc, n, out, err, (hipStream_t)stream) == hipSuccess
+             ? 0
+             : -5;
+}
+
+// mode 0: coalesced grid-stride read; mode 4/8/16: per-lane runs of U chunks.
+int nsk_calib_launch(int mode, const void* p, uint64_t bytes, uint32_t* out, uint32_t blocks,
+                     void* stream) {
+  const uint64_t n16 = bytes / 16;
+  hipStream_t s = (hipStream_t)stream;
+  const auto* q = reinterpret_cast<const uint4*>(p);
+  switch (mode) {
+    case 0: hipLaunchKernelGGL(nsk::calib_read, dim3(blocks), dim3(256), 0, s, q, n16, out); break;
+    case 4: hipLaunchKernelGGL(nsk::calib_read_runs<4>, dim3(blocks), dim3(256), 0, s, q, n16, out); break;
+    case 8: hipLaunchKernelGGL(nsk::calib_read_runs<8>, dim3(blocks), dim3(256), 0, s, q, n16, out); break;
+    case 16: hipLaunchKernelGGL(nsk::calib_read_runs<16>, dim3(blocks), dim3(256), 0, s, q, n16, out); break;
+    case 5: hipLaunchKernelGGL((nsk::calib_read_runs<4, true>), dim3(blocks), dim3(256), 0, s, q, n16, out); break;
+    case 6: hipLaunchKernelGGL((nsk::calib_read_runs<2, true>), dim3(blocks), dim3(256), 0, s, q, n16, out); break;
+    case 1: hipLaunchKernelGGL(nsk::calib_read8<false>, dim3(blocks), dim3(256), 0, s, q, n16, out); break;
+    case 2: hipLaunchKernelGGL(nsk::calib_read8<true>, dim3(blocks), dim3(256), 0, s, q, n16, out); break;
+#define NSK_CB(m, U, A) case m: hipLaunchKernelGGL((nsk::calib_buf<U, A>), dim3(blocks), dim3(256), 0, s, q, n16, out); break;
+    NSK_CB(100, 1, 0) NSK_CB(101, 1, 1) NSK_CB(102, 1, 2) NSK_CB(103, 1, 3) NSK_CB(116, 1, 16) NSK_CB(118, 1, 18) NSK_CB(119, 1, 19)
+    NSK_CB(200, 2, 0) NSK_CB(201, 2, 1) NSK_CB(202, 2, 2) NSK_CB(203, 2, 3) NSK_CB(216, 2, 16) NSK_CB(218, 2, 18) NSK_CB(219, 2, 19)
+    NSK_CB(400, 4, 0) NSK_CB(401, 4, 1) NSK_CB(402, 4, 2) NSK_CB(403, 4, 3) NSK_CB(416, 4, 16) NSK_CB(418, 4, 18) NSK_CB(419, 4, 19)
+#undef NSK_CB
+    default: return -1;
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+}  // extern "C"

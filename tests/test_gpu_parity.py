@@ -112,9 +112,12 @@ def test_config_full_size(engine, cfg):
     want = O.c_batch_mt(host, b.desc, min(16, os.cpu_count() or 1))
     assert np.array_equal(got, want), f"{int((got != want).sum())} mismatches"
 
-    # size-independent property: append ^sum (big-endian) after each even-length
-    # packet and re-sum: every packet must verify as 0xffff (segment.go:180).
-    if cfg in (2, 3):
+    # size-independent property: write ^sum (big-endian) into the 4 padding
+    # bytes after each 1500-B packet and re-sum the 1502 bytes: every packet
+    # must verify as 0xffff (segment.go:180).  Only cfg2 has padding (stride
+    # 1504); the writes stay inside each packet's own slot.
+    if cfg == 2:
+        assert int(b.desc["off"][-1]) + int(b.desc["len"][-1]) + 2 <= b.arena_bytes
         L = int(b.desc["len"][0])
         offs = torch.from_numpy(b.desc["off"].astype(np.int64)).cuda()
         comp = (~out.to(torch.int32)) & 0xFFFF
@@ -276,3 +279,33 @@ def test_fuzz_small(engine):
         chained = bool(trial % 2)
         want, _ = O.c_batch(arena, d, chained)
         assert np.array_equal(dev_batch(engine, arena, d, chained, arena_offset=trial % 16), want), trial
+
+
+def test_sorted_dense_tiles_with_gaps_and_empties(engine):
+    """Packed (sorted, non-overlapping) tables exercise the dense path: mixed
+    gaps, zero-length descriptors (also leading ones), multiple packets per
+    16-byte chunk, odd flags, and tiles that fall back to the general path
+    because their gaps are too large."""
+    import oracle as O
+
+    rng = np.random.default_rng(8)
+    for trial in range(12):
+        n = int(rng.integers(1, 5000))
+        lens = rng.integers(0, [8, 64, 1600, 9000][trial % 4], n)
+        lens[rng.random(n) < 0.1] = 0
+        if trial % 3 == 0:
+            lens[: min(n, 300)] = 0  # a whole leading tile of empties
+        gaps = rng.integers(0, [1, 4, 16, 5000][(trial // 4) % 4], n)
+        d = np.zeros(n, dtype=O.DESC_DTYPE)
+        pos = 0
+        for i in range(n):
+            pos += int(gaps[i])
+            d[i] = (pos if lens[i] else int(rng.integers(0, 1 << 20)), int(lens[i]),
+                    int(rng.integers(0, 65536)), int(rng.integers(0, 2)))
+            pos += int(lens[i])
+        arena = rng.integers(0, 256, pos + 64, dtype=np.uint8)
+        d["off"] = np.minimum(d["off"], arena.size)  # empty ones anywhere inside
+        want, bad = O.c_batch(arena, d)
+        assert bad == 0
+        for off in (0, 5):
+            assert np.array_equal(dev_batch(engine, arena, d, arena_offset=off), want), (trial, off)

@@ -1,0 +1,147 @@
+#!/usr/bin/env python3
+"""A/B the checksum kernel variants of libns_tune.so in ONE process,
+interleaved rounds (cdna_hip_programming.md §5.4 rule 24), on the
+BASELINE.json layouts; every variant is parity-checked against the product
+kernel's results.  Also times the read-stream calibration kernels.
+
+  python tools/tune.py [--configs 2,3,4] [--rounds 5] [--reps 10] [--variants all]
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402  (load torch's HIP runtime first)
+
+from netstack_amd import Engine  # noqa: E402
+from netstack_amd import workloads as W  # noqa: E402
+
+TUNE = os.path.join(ROOT, "netstack_amd", "lib", "libns_tune.so")
+
+
+def load():
+    L = ctypes.CDLL(TUNE)
+    L.nsk_tune_count.restype = ctypes.c_int
+    L.nsk_tune_name.restype = ctypes.c_char_p
+    L.nsk_tune_name.argtypes = [ctypes.c_int]
+    L.nsk_tune_launch.restype = ctypes.c_int
+    L.nsk_tune_launch.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                  ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    L.nsk_calib_launch.restype = ctypes.c_int
+    L.nsk_calib_launch.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                   ctypes.c_uint32, ctypes.c_void_p]
+    return L
+
+
+def time_launches(fn, reps, stream):
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    for a, b in ev:
+        a.record(stream)
+        fn()
+        b.record(stream)
+    torch.cuda.synchronize()
+    return [a.elapsed_time(b) * 1e3 for a, b in ev]  # us
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--configs", default="2,3,4")
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--variants", default="all")
+    ap.add_argument("--calib", action="store_true")
+    ap.add_argument("--calib-modes", default="2,4,5,6")
+    ap.add_argument("--calib-blocks", default="4096,8192,16384")
+    ap.add_argument("--json", default="")
+    args = ap.parse_args()
+
+    L = load()
+    names = [L.nsk_tune_name(v).decode() for v in range(L.nsk_tune_count())]
+    sel = list(range(len(names))) if args.variants == "all" else \
+        [names.index(x) for x in args.variants.split(",")]
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.current_stream(dev)
+    sp = stream.cuda_stream
+    eng = Engine(0)
+    err = torch.zeros(1, dtype=torch.int64, device=dev)
+    report = {"variants": {}, "calib": {}}
+
+    for cfg in [int(c) for c in args.configs.split(",")]:
+        b = W.config(cfg)
+        rot = 4 if cfg == 3 else 1
+        arenas = [b.arena_device(dev)] + [W.random_bytes_torch(b.seed + 77 * r, b.arena_bytes, dev)
+                                          for r in range(1, rot)]
+        desc = torch.from_numpy(b.desc.view(np.uint8).copy()).to(dev)
+        ref = eng.batch_tensors(arenas[0], desc)
+        torch.cuda.synchronize()
+        ref = ref.cpu()
+        out = torch.empty(b.n, dtype=torch.int16, device=dev)
+        ab = b.algorithmic_bytes
+        res = {v: [] for v in sel}
+        state = {"k": 0}
+
+        def launcher(v):
+            def f():
+                a = arenas[state["k"] % rot]
+                state["k"] += 1
+                rc = L.nsk_tune_launch(v, a.data_ptr(), b.arena_bytes, desc.data_ptr(), b.n,
+                                       out.data_ptr(), err.data_ptr(), sp)
+                assert rc == 0
+            return f
+
+        for v in sel:  # warm + parity
+            f = launcher(v)
+            state["k"] = 0
+            f()
+            torch.cuda.synchronize()
+            ok = torch.equal(out.cpu(), ref)
+            if not ok:
+                print(f"PARITY FAIL cfg{cfg} {names[v]}", flush=True)
+            for _ in range(2):
+                f()
+        for r in range(args.rounds):
+            for v in sel:
+                res[v] += time_launches(launcher(v), args.reps, stream)
+        print(f"== cfg{cfg} {b.name}: n={b.n} algorithmic={ab/1e6:.1f} MB", flush=True)
+        rows = []
+        for v in sel:
+            med = float(np.median(res[v]))
+            rows.append((med, names[v], float(np.min(res[v]))))
+            report["variants"].setdefault(f"cfg{cfg}", {})[names[v]] = {
+                "median_us": med, "min_us": float(np.min(res[v])), "GBps": ab / med / 1e3}
+        for med, nm, mn in sorted(rows):
+            print(f"  {nm:16s} median {med:9.1f} us  min {mn:9.1f}  -> {ab / med / 1e3:7.0f} GB/s "
+                  f"({ab / med / 1e3 / 8000 * 100:5.1f}% of 8 TB/s)", flush=True)
+        del arenas
+
+    if args.calib:
+        nbytes = (1 << 31) - 4096  # ~2 GiB, well past the 256 MiB MALL
+        buf = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+        buf.fill_(1)
+        outb = torch.zeros(65536, dtype=torch.int32, device=dev)
+        for mode in [int(x) for x in args.calib_modes.split(",")]:
+            for blocks in [int(x) for x in args.calib_blocks.split(",")]:
+                f = lambda: L.nsk_calib_launch(mode, buf.data_ptr(), nbytes, outb.data_ptr(), blocks, sp)
+                f()
+                ts = []
+                for _ in range(args.rounds):
+                    ts += time_launches(f, args.reps, stream)
+                med = float(np.median(ts))
+                report["calib"][f"mode{mode}_b{blocks}"] = {"median_us": med, "GBps": nbytes / med / 1e3}
+                print(f"  calib mode {mode:2d} blocks {blocks:5d}: {med:9.1f} us  {nbytes / med / 1e3:7.0f} GB/s",
+                      flush=True)
+    if args.json:
+        with open(args.json, "w") as f:
+            json.dump(report, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
