@@ -247,7 +247,7 @@ def main():
             "unit": "GB/s",
             "frac": achieved_gbs / HBM_PEAK_GBS,
             "traffic": traffic,
-            "kernel": "nsk::csum_batch<256,1,2,8,false> (dense path)" if cfg == 2 else "nsk::csum_batch<256,1,2,4,false> (dense path)",
+            "kernel": "nsk::csum_runs<256,4,true>",
             "algorithmic_bytes_per_launch": algo_bytes,
             "avg_launch_us": kern_avg_s * 1e6,
         },

@@ -103,6 +103,9 @@ typedef struct ns_csum_opts {
 } ns_csum_opts;
 
 int ns_csum_abi_version(void);
+/* hipError_t of the last failed HIP call on this thread (0 if none); set
+ * NS_CSUM_DEBUG=1 in the environment to also print it to stderr.          */
+int ns_csum_last_hip_error(void);
 const char* ns_csum_strerror(int status);
 int ns_csum_device_count(int* count);
 

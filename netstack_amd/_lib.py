@@ -28,7 +28,7 @@ NS_BATCH_CHAINED = 0x1
 
 # Every symbol include/netstack_csum.h declares (checked by the CPU tests).
 EXPORTED = (
-    "ns_csum_abi_version", "ns_csum_strerror", "ns_csum_device_count",
+    "ns_csum_abi_version", "ns_csum_last_hip_error", "ns_csum_strerror", "ns_csum_device_count",
     "ns_csum_init", "ns_csum_destroy", "ns_csum_sync", "ns_csum_batch_dev",
     "ns_csum_batch_host", "ns_csum_checksum", "ns_csum_vv_with_offset",
     "ns_csum_vv_batch", "ns_csum_views_restart", "ns_csum_pseudo_header",
@@ -45,7 +45,11 @@ class ChecksumError(RuntimeError):
 
     def __init__(self, status: int, what: str):
         self.status = status
-        super().__init__(f"{what}: {strerror(status)} ({status})")
+        try:
+            self.hip_error = int(lib().ns_csum_last_hip_error())
+        except Exception:
+            self.hip_error = None
+        super().__init__(f"{what}: {strerror(status)} ({status}, hipError {self.hip_error})")
 
 
 class NsPktDesc(ctypes.Structure):
@@ -80,6 +84,7 @@ def _declare(lib):
     u16p = c.POINTER(c.c_uint16)
     sig = {
         "ns_csum_abi_version": (c.c_int, []),
+        "ns_csum_last_hip_error": (c.c_int, []),
         "ns_csum_strerror": (c.c_char_p, [c.c_int]),
         "ns_csum_device_count": (c.c_int, [c.POINTER(c.c_int)]),
         "ns_csum_init": (c.c_int, [c.POINTER(NsOpts), c.POINTER(vp)]),

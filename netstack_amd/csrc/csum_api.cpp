@@ -7,6 +7,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -29,16 +30,29 @@ namespace {
 constexpr uint64_t kMergeMax = 131072;
 constexpr uint64_t kDefaultStaging = 64ull << 20;
 
-#define HIP_TRY(expr)                                   \
-  do {                                                  \
-    hipError_t e__ = (expr);                            \
-    if (e__ != hipSuccess) return map_hip_error(e__);   \
+thread_local hipError_t g_last_hip = hipSuccess;
+
+// Records the failing HIP call (ns_csum_last_hip_error) and, with
+// NS_CSUM_DEBUG set in the environment, prints it.
+int report_hip(hipError_t e, const char* expr, const char* file, int line);
+
+#define HIP_TRY(expr)                                                        \
+  do {                                                                       \
+    hipError_t e__ = (expr);                                                 \
+    if (e__ != hipSuccess) return report_hip(e__, #expr, __FILE__, __LINE__); \
   } while (0)
 
 int map_hip_error(hipError_t e) {
   if (e == hipErrorOutOfMemory) return NS_ENOMEM;
   if (e == hipErrorNoDevice || e == hipErrorInvalidDevice) return NS_ENODEV;
   return NS_EHIP;
+}
+
+int report_hip(hipError_t e, const char* expr, const char* file, int line) {
+  g_last_hip = e;
+  static const bool dbg = std::getenv("NS_CSUM_DEBUG") != nullptr;
+  if (dbg) std::fprintf(stderr, "netstack_csum: %s:%d: %s -> %s\n", file, line, expr, hipGetErrorString(e));
+  return map_hip_error(e);
 }
 
 template <typename T>
@@ -333,6 +347,8 @@ extern "C" {
 
 int ns_csum_abi_version(void) { return NS_CSUM_ABI_VERSION; }
 
+int ns_csum_last_hip_error(void) { return (int)g_last_hip; }
+
 const char* ns_csum_strerror(int status) {
   switch (status) {
     case NS_OK: return "ok";
@@ -382,7 +398,7 @@ int ns_csum_init(const ns_csum_opts* opts, ns_csum_ctx** out) {
   if (e == hipSuccess) e = hipMemset(ctx->d_err, 0, sizeof(unsigned long long));
   if (e != hipSuccess) {
     ns_csum_destroy(ctx);
-    return map_hip_error(e);
+    return report_hip(e, "ns_csum_init", __FILE__, __LINE__);
   }
   *out = ctx;
   return NS_OK;

@@ -524,6 +524,212 @@ __global__ __launch_bounds__(WG) void csum_batch(
   }
 }
 
+// ===========================================================================
+// csum_runs — the production kernel (arena < 4 GiB).
+//
+// Each packet is split into   head | body | tail:
+//   head = its first 16-byte chunk if the packet does not start on a chunk
+//          boundary (byte-masked), tail = its last chunk if it does not end on
+//          one (byte-masked); a packet inside one chunk is a lone head;
+//   body = the chunks it covers completely — no masking ever needed.
+// The thread that owns a descriptor loads head and tail itself in the prologue
+// (their latency hides under the whole tile) and adds them in the epilogue.
+// Body chunks are cut into packet-aligned runs of U chunks; the tile's runs
+// are scanned into LDS and each lane takes one run per step: one binary
+// search for its packet, U buffer_load_dwordx4 of consecutive chunks (lanes
+// U*16 B apart: the run shape that streams at ~6.3 TB/s through buffer loads
+// on MI355X), then 2 VALU per dword:
+//   T += v_sad_u8(w, 0)   (sum of the 4 bytes)
+//   W += v_sad_u16(w, 0)  (sum of the 2 little-endian 16-bit words)
+// and the big-endian word sum of checksum.go:41-43 is
+//   S = 256*E + O = 257*T - W   (first byte at an even address, phase 0)
+//   S = E + 256*O = W           (phase 1)
+// with E/O the bytes at even/odd addresses — all mod 2^32, so bit-exact
+// including the > 128 KiB wrap.  A run never crosses a packet, so each run
+// ends in exactly one ds_add_u32 into its packet's LDS accumulator.
+// Out-of-range run slots load from offset num_records (the SRD's own size):
+// out of range under both "offset >= size" and "offset + 16 > size" checks and
+// far from 32-bit wrap, so the hardware returns zeros without touching memory.
+// (An offset near 2^32 is NOT safe: offset + 16 wraps and passes the check.)
+// ===========================================================================
+constexpr uint64_t kMaxSrdBytes = 0xFFFF0000ull;  // arenas at or above: launch_general
+
+__device__ __forceinline__ uint4 bload(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  auto x = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0);
+  return *reinterpret_cast<uint4*>(&x);
+}
+
+__device__ __forceinline__ void sad_chunk(const uint4 w, uint32_t& T, uint32_t& W) {
+  T = __builtin_amdgcn_sad_u8(w.x, 0u, T);
+  W = __builtin_amdgcn_sad_u16(w.x, 0u, W);
+  T = __builtin_amdgcn_sad_u8(w.y, 0u, T);
+  W = __builtin_amdgcn_sad_u16(w.y, 0u, W);
+  T = __builtin_amdgcn_sad_u8(w.z, 0u, T);
+  W = __builtin_amdgcn_sad_u16(w.z, 0u, W);
+  T = __builtin_amdgcn_sad_u8(w.w, 0u, T);
+  W = __builtin_amdgcn_sad_u16(w.w, 0u, W);
+}
+
+__device__ __forceinline__ uint32_t s_of(uint32_t T, uint32_t W, uint32_t phase) {
+  return phase ? W : (257u * T - W);
+}
+
+template <int WG, int U, bool PIPE = true>
+__global__ __launch_bounds__(WG) void csum_runs(
+    const uint8_t* __restrict__ arena, uint64_t arena_bytes,
+    const uint4* __restrict__ desc, uint32_t n, uint16_t* __restrict__ out,
+    uint32_t* __restrict__ partial, unsigned long long* __restrict__ err) {
+  constexpr int P = WG;
+  constexpr int NW = WG / 64;
+  static_assert((P & (P - 1)) == 0, "tile must be a power of two");
+  __shared__ uint64_t s_rstart[P + 1];  // first run of each packet (tile-relative)
+  __shared__ uint32_t s_body[P];        // byte offset (SRD) of the packet's first body chunk
+  __shared__ uint32_t s_nb[P];          // body chunks | phase << 31
+  __shared__ uint32_t s_acc[P];
+  __shared__ uint64_t s_wtot[NW];
+
+  const int t = threadIdx.x;
+  const int lane = t & 63;
+  const int wv = t >> 6;
+  const uint64_t i = (uint64_t)blockIdx.x * P + t;
+
+  // SRD over the whole arena, from its 16-byte-aligned base (host guarantees
+  // the rounded size is below kMaxSrdBytes).
+  const uint64_t abase = (uint64_t)(uintptr_t)arena & 15u;
+  const uint64_t sb = (uint64_t)(uintptr_t)arena - abase;
+  const uint32_t nrec = (uint32_t)((abase + arena_bytes + 15) & ~15ull);
+  // readfirstlane returns int: widen through uint32_t (a sign-extended low
+  // word would corrupt the base's high bits).
+  const uint32_t sb_lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)sb);
+  const uint32_t sb_hi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(sb >> 32));
+  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(((uint64_t)sb_hi << 32) | (uint64_t)sb_lo), (short)0,
+      (int)__builtin_amdgcn_readfirstlane(nrec), 0x00020000);
+
+  const uint32_t oob = (uint32_t)__builtin_amdgcn_readfirstlane(nrec);
+  uint32_t init = 0, phase = 0, nb = 0, body = 0;
+  uint32_t hoff = oob, toff = oob;
+  int hlo = 0, hhi = 16, thi = 16;
+  if (i < n) {
+    const uint4 raw = desc[i];
+    const uint64_t off = (uint64_t)raw.x | ((uint64_t)raw.y << 32);
+    uint32_t len = raw.z;
+    init = raw.w & 0xFFFFu;
+    const uint32_t odd = (raw.w >> 16) & 1u;
+    if (off > arena_bytes || (uint64_t)len > arena_bytes - off) {
+      len = 0;
+      atomicAdd(err, 1ull);
+    }
+    if (len) {
+      const uint32_t a = (uint32_t)(abase + off);
+      const uint32_t e = a + len;          // exclusive end
+      const uint32_t cf = a >> 4, cl = (e - 1) >> 4;
+      const uint32_t lo = a & 15u, hiex = ((e - 1) & 15u) + 1u;
+      phase = (a + odd) & 1u;
+      if (cf == cl) {                     // inside one chunk: a lone head
+        hoff = cf * 16u;
+        hlo = (int)lo;
+        hhi = (int)hiex;
+      } else {
+        if (lo) {
+          hoff = cf * 16u;
+          hlo = (int)lo;
+        }
+        if (hiex != 16u) {
+          toff = cl * 16u;
+          thi = (int)hiex;
+        }
+        const uint32_t bf = cf + (lo ? 1u : 0u);
+        const uint32_t bl = cl - (hiex != 16u ? 1u : 0u);
+        nb = bl + 1u - bf;                // >= 0 since cl > cf
+        body = bf * 16u;
+      }
+    }
+  }
+  // Edge chunks: issued now, consumed in the epilogue.
+  const uint4 hv = bload(rsrc, hoff);
+  const uint4 tv = bload(rsrc, toff);
+
+  // Block-wide exclusive scan of run counts.
+  const uint64_t nr = (nb + (U - 1)) / U;
+  uint64_t incl = nr;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint64_t y = __shfl_up(incl, d, 64);
+    if (lane >= d) incl += y;
+  }
+  if (lane == 63) s_wtot[wv] = incl;
+  __syncthreads();
+  uint64_t excl = incl - nr;
+#pragma unroll
+  for (int w = 0; w < NW; ++w)
+    if (w < wv) excl += s_wtot[w];
+  s_rstart[t] = excl;
+  s_body[t] = body;
+  s_nb[t] = nb | (phase << 31);
+  s_acc[t] = 0u;
+  if (t == WG - 1) s_rstart[P] = excl + nr;
+  __syncthreads();
+
+  const uint64_t R = s_rstart[P];
+  // One run: packet lookup + U loads (stage), then SAD + one LDS add (consume).
+  auto stage = [&](uint64_t q, uint4 (&v)[U], int& pk) {
+    // Largest p with s_rstart[p] <= q (that packet has a run q): fixed-step,
+    // branch-free search (s_rstart[0] = 0 <= q always holds).
+    int lo = 0;
+#pragma unroll
+    for (int step = P / 2; step >= 1; step >>= 1)
+      lo = (s_rstart[lo + step] <= q) ? lo + step : lo;
+    const uint32_t k = (uint32_t)(q - s_rstart[lo]);
+    const uint32_t c0 = k * U;
+    const uint32_t nvalid = min((uint32_t)U, (s_nb[lo] & 0x7FFFFFFFu) - c0);
+    const uint32_t base = s_body[lo] + c0 * 16u;
+#pragma unroll
+    for (int j = 0; j < U; ++j) v[j] = bload(rsrc, (uint32_t)j < nvalid ? base + 16u * j : oob);
+    pk = lo;
+  };
+  auto consume = [&](const uint4 (&v)[U], int pk) {
+    uint32_t T = 0, W = 0;
+#pragma unroll
+    for (int j = 0; j < U; ++j) sad_chunk(v[j], T, W);
+    atomicAdd(&s_acc[pk], s_of(T, W, s_nb[pk] >> 31));
+  };
+  if constexpr (PIPE) {
+    // Software pipeline: run q+WG is looked up and its loads issued before
+    // run q is consumed (two register stages, unrolled by 2).
+    uint4 va[U], vb[U];
+    int pa = 0, pb = 0;
+    uint64_t q = (uint64_t)t;
+    if (q < R) stage(q, va, pa);
+    while (q < R) {
+      if (q + WG < R) stage(q + WG, vb, pb);
+      consume(va, pa);
+      q += WG;
+      if (q >= R) break;
+      if (q + WG < R) stage(q + WG, va, pa);
+      consume(vb, pb);
+      q += WG;
+    }
+  } else {
+    for (uint64_t q = (uint64_t)t; q < R; q += WG) {
+      uint4 v[U];
+      int pk;
+      stage(q, v, pk);
+      consume(v, pk);
+    }
+  }
+  __syncthreads();
+
+  if (i < n) {
+    uint32_t T = 0, W = 0;
+    sad_chunk(mask_chunk(hv, hlo, hhi), T, W);
+    sad_chunk(mask_chunk(tv, 0, thi), T, W);
+    const uint32_t sacc = s_acc[t] + s_of(T, W, phase);
+    if (partial) partial[i] = sacc;
+    else out[i] = (uint16_t)fold1(init + sacc);
+  }
+}
+
 // Sequential chain fix-up for NS_DESC_CONT runs (checksum.go:89 / the
 // `xsum = Checksum(v, xsum)` loops): out[k] = fold1(out[k-1] + S_k).
 __global__ void csum_chain(const uint4* __restrict__ desc, uint32_t n,
@@ -548,13 +754,23 @@ __global__ void csum_chain(const uint4* __restrict__ desc, uint32_t n,
 // ---- launchers (C++ linkage, used by csum_api.cpp) ------------------------
 namespace nsk {
 
-template <int D, int UD>
-static hipError_t launch_tiles(const uint8_t* arena, uint64_t arena_bytes, const void* desc,
-                               uint32_t n, uint16_t* out, uint32_t* partial,
-                               unsigned long long* err, hipStream_t stream) {
+template <int U>
+static hipError_t launch_runs(const uint8_t* arena, uint64_t arena_bytes, const void* desc,
+                              uint32_t n, uint16_t* out, uint32_t* partial,
+                              unsigned long long* err, hipStream_t stream) {
   constexpr int WG = 256;
-  const uint32_t tiles = (uint32_t)(((uint64_t)n + WG * D - 1) / (WG * D));
-  hipLaunchKernelGGL((csum_batch<WG, D, 2, UD, false>), dim3(tiles), dim3(WG), 0, stream, arena,
+  const uint32_t tiles = (uint32_t)(((uint64_t)n + WG - 1) / WG);
+  hipLaunchKernelGGL((csum_runs<WG, U, true>), dim3(tiles), dim3(WG), 0, stream, arena, arena_bytes,
+                     reinterpret_cast<const uint4*>(desc), n, out, partial, err);
+  return hipGetLastError();
+}
+
+static hipError_t launch_general(const uint8_t* arena, uint64_t arena_bytes, const void* desc,
+                                 uint32_t n, uint16_t* out, uint32_t* partial,
+                                 unsigned long long* err, hipStream_t stream) {
+  constexpr int WG = 256;
+  const uint32_t tiles = (uint32_t)(((uint64_t)n + WG - 1) / WG);
+  hipLaunchKernelGGL((csum_batch<WG, 1, 2, 4, false>), dim3(tiles), dim3(WG), 0, stream, arena,
                      arena_bytes, reinterpret_cast<const uint4*>(desc), n, out, partial, err);
   return hipGetLastError();
 }
@@ -564,11 +780,15 @@ hipError_t launch_batch(const uint8_t* arena, uint64_t arena_bytes,
                         uint32_t* partial, unsigned long long* err,
                         hipStream_t stream) {
   if (n == 0) return hipSuccess;
-  // Dense-path run length by the mean arena bytes per descriptor (tools/tune.py
-  // on MI355X: 8 chunks per lane for MTU-sized packets, 4 for small/mixed).
-  const bool big = arena_bytes / n >= 1024;
-  hipError_t e = big ? launch_tiles<1, 8>(arena, arena_bytes, desc, n, out, partial, err, stream)
-                     : launch_tiles<1, 4>(arena, arena_bytes, desc, n, out, partial, err, stream);
+  hipError_t e;
+  if (arena_bytes + 64 >= kMaxSrdBytes) {
+    // Arenas of 4 GiB and more: 64-bit addressing, global loads.
+    e = launch_general(arena, arena_bytes, desc, n, out, partial, err, stream);
+  } else {
+    // Runs of 4 chunks, software-pipelined: best or tied on every BASELINE
+    // layout in tools/tune.py on MI355X (1500 B, 64 B, Zipf 64-9000 B).
+    e = launch_runs<4>(arena, arena_bytes, desc, n, out, partial, err, stream);
+  }
   if (e != hipSuccess || partial == nullptr) return e;
   const uint32_t blocks = (n + 255) / 256;
   hipLaunchKernelGGL(csum_chain, dim3(blocks), dim3(256), 0, stream,

@@ -111,6 +111,15 @@ hipError_t launch_v(const uint8_t* arena, uint64_t arena_bytes, const void* desc
   return hipGetLastError();
 }
 
+template <int U, bool PIPE = true>
+hipError_t launch_r(const uint8_t* arena, uint64_t arena_bytes, const void* desc, uint32_t n,
+                    uint16_t* out, unsigned long long* err, hipStream_t s) {
+  const uint32_t tiles = (n + 255) / 256;
+  hipLaunchKernelGGL((csum_runs<256, U, PIPE>), dim3(tiles), dim3(256), 0, s, arena, arena_bytes,
+                     reinterpret_cast<const uint4*>(desc), n, out, nullptr, err);
+  return hipGetLastError();
+}
+
 typedef hipError_t (*launch_fn)(const uint8_t*, uint64_t, const void*, uint32_t, uint16_t*,
                                 unsigned long long*, hipStream_t);
 struct Variant {
@@ -118,10 +127,9 @@ struct Variant {
   launch_fn fn;
 };
 static const Variant kVariants[] = {
-    {"buf_D1_U4", launch_v<1, 2, 4, false>},    {"buf_D1_U2", launch_v<1, 2, 2, false>},
-    {"buf_D1_U8", launch_v<1, 2, 8, false>},    {"buf_D1_U4_nt", launch_v<1, 2, 4, true>},
-    {"buf_D2_U4", launch_v<2, 2, 4, false>},    {"buf_D4_U4", launch_v<4, 2, 4, false>},
-    {"buf_D4_U2", launch_v<4, 2, 2, false>},    {"buf_D1_U2_nt", launch_v<1, 2, 2, true>},
+    {"runs_U4_pipe", launch_r<4, true>},  {"runs_U4", launch_r<4, false>},
+    {"runs_U8_pipe", launch_r<8, true>},  {"runs_U2_pipe", launch_r<2, true>},
+    {"dense_U8", launch_v<1, 2, 8, false>},
 };
 
 }  // namespace nsk
@@ -160,7 +168,7 @@ int nsk_calib_launch(int mode, const void* p, uint64_t bytes, uint32_t* out, uin
 #define NSK_CB(m, U, A) case m: hipLaunchKernelGGL((nsk::calib_buf<U, A>), dim3(blocks), dim3(256), 0, s, q, n16, out); break;
     NSK_CB(100, 1, 0) NSK_CB(101, 1, 1) NSK_CB(102, 1, 2) NSK_CB(103, 1, 3) NSK_CB(116, 1, 16) NSK_CB(118, 1, 18) NSK_CB(119, 1, 19)
     NSK_CB(200, 2, 0) NSK_CB(201, 2, 1) NSK_CB(202, 2, 2) NSK_CB(203, 2, 3) NSK_CB(216, 2, 16) NSK_CB(218, 2, 18) NSK_CB(219, 2, 19)
-    NSK_CB(400, 4, 0) NSK_CB(401, 4, 1) NSK_CB(402, 4, 2) NSK_CB(403, 4, 3) NSK_CB(416, 4, 16) NSK_CB(418, 4, 18) NSK_CB(419, 4, 19)
+    NSK_CB(800, 8, 0) NSK_CB(400, 4, 0) NSK_CB(401, 4, 1) NSK_CB(402, 4, 2) NSK_CB(403, 4, 3) NSK_CB(416, 4, 16) NSK_CB(418, 4, 18) NSK_CB(419, 4, 19)
 #undef NSK_CB
     default: return -1;
   }

@@ -1,0 +1,73 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 counter CSVs written by tools/profile.sh.
+
+Dispatches of calib_buf / csum_batch are matched in order to the LABEL lines
+of tools/pmc_run.py (REPS each).  HBM bytes per launch follow
+MI355X_MICROARCH.md §HBM: FETCH_SIZE (KiB) is calibrated against a read of a
+known byte count in the same access shape (runs of 8 chunks for cfg2's
+kernel, runs of 4 for cfg3/cfg4) because gfx950 under-reports wide streaming
+reads; the raw values are kept beside the corrected ones.
+
+  python tools/pmc_parse.py OUTDIR LOGFILE > summary.json
+"""
+import csv
+import glob
+import json
+import os
+import re
+import sys
+from collections import defaultdict
+
+REPS = 3
+
+
+def load(outdir):
+    rows = []
+    for f in glob.glob(os.path.join(outdir, "**", "*counter_collection.csv"), recursive=True):
+        rows += list(csv.DictReader(open(f)))
+    return rows
+
+
+def main():
+    outdir, log = sys.argv[1], sys.argv[2]
+    labels = []
+    for line in open(log):
+        if line.startswith("LABEL "):
+            parts = line.split()
+            labels.append((parts[1], dict(p.split("=") for p in parts[2:])))
+    rows = load(outdir)
+    # per dispatch: {counter: value}
+    disp = defaultdict(dict)
+    names = {}
+    for r in rows:
+        k = int(r["Dispatch_Id"])
+        disp[k][r["Counter_Name"]] = disp[k].get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+        names[k] = r["Kernel_Name"]
+    ours = [k for k in sorted(disp) if ("calib_buf" in names[k] or "csum_batch" in names[k])]
+    out = {}
+    for i, (lab, meta) in enumerate(labels):
+        ks = ours[i * REPS:(i + 1) * REPS]
+        if len(ks) < REPS:
+            break
+        counters = sorted({c for k in ks for c in disp[k]})
+        avg = {c: sum(disp[k].get(c, 0.0) for k in ks) / len(ks) for c in counters}
+        out[lab] = {"kernel": names[ks[0]][:80], "meta": meta, "avg": avg}
+    # FETCH_SIZE calibration per access shape
+    cal = {}
+    for m in ("calib800", "calib400", "calib102"):
+        if m in out and "FETCH_SIZE" in out[m]["avg"]:
+            cal[m] = float(out[m]["meta"]["bytes"]) / (out[m]["avg"]["FETCH_SIZE"] * 1024.0)
+    for lab, shape in (("cfg2", "calib800"), ("cfg3", "calib400"), ("cfg4", "calib400")):
+        if lab in out and "FETCH_SIZE" in out[lab]["avg"]:
+            raw = out[lab]["avg"]["FETCH_SIZE"] * 1024.0
+            f = cal.get(shape)
+            out[lab]["hbm_read_bytes_raw"] = raw
+            out[lab]["fetch_calibration"] = {"shape": shape, "factor": f}
+            out[lab]["hbm_bytes_per_launch"] = raw * f if f else None
+            if "WRITE_SIZE" in out[lab]["avg"]:
+                out[lab]["hbm_write_bytes"] = out[lab]["avg"]["WRITE_SIZE"] * 1024.0
+    json.dump(out, sys.stdout, indent=1)
+
+
+if __name__ == "__main__":
+    main()
