@@ -531,14 +531,14 @@ __global__ __launch_bounds__(WG) void csum_batch(
 //   head = its first 16-byte chunk if the packet does not start on a chunk
 //          boundary (byte-masked), tail = its last chunk if it does not end on
 //          one (byte-masked); a packet inside one chunk is a lone head;
-//   body = the chunks it covers completely — no masking ever needed.
-// The thread that owns a descriptor loads head and tail itself in the prologue
-// (their latency hides under the whole tile) and adds them in the epilogue.
-// Body chunks are cut into packet-aligned runs of U chunks; the tile's runs
-// are scanned into LDS and each lane takes one run per step: one binary
-// search for its packet, U buffer_load_dwordx4 of consecutive chunks (lanes
-// U*16 B apart: the run shape that streams at ~6.3 TB/s through buffer loads
-// on MI355X), then 2 VALU per dword:
+//   body = the chunks it covers completely — no masking.
+// Body chunks are cut into packet-aligned runs of U chunks (a packet with no
+// full chunk gets one empty run).  The tile's runs are scanned into LDS and
+// each lane takes one run per step: a branch-free binary search for its
+// packet, U buffer_load_dwordx4 of consecutive chunks (lanes U*16 B apart: the
+// run shape that streams at ~6.3 TB/s through buffer loads on MI355X), plus —
+// only on the packet's first / last run — the head / tail chunk, adjacent in
+// address and time so its 128-B line is fetched once.  Then 2 VALU per dword:
 //   T += v_sad_u8(w, 0)   (sum of the 4 bytes)
 //   W += v_sad_u16(w, 0)  (sum of the 2 little-endian 16-bit words)
 // and the big-endian word sum of checksum.go:41-43 is
@@ -546,10 +546,11 @@ __global__ __launch_bounds__(WG) void csum_batch(
 //   S = E + 256*O = W           (phase 1)
 // with E/O the bytes at even/odd addresses — all mod 2^32, so bit-exact
 // including the > 128 KiB wrap.  A run never crosses a packet, so each run
-// ends in exactly one ds_add_u32 into its packet's LDS accumulator.
-// Out-of-range run slots load from offset num_records (the SRD's own size):
-// out of range under both "offset >= size" and "offset + 16 > size" checks and
-// far from 32-bit wrap, so the hardware returns zeros without touching memory.
+// ends in exactly one ds_add_u32 into its packet's LDS accumulator.  Runs are
+// software-pipelined one step deep (PIPE).
+// Out-of-range slots load from offset num_records (the SRD's own size): out of
+// range under both "offset >= size" and "offset + 16 > size" checks and far
+// from 32-bit wrap, so the hardware returns zeros without touching memory.
 // (An offset near 2^32 is NOT safe: offset + 16 wraps and passes the check.)
 // ===========================================================================
 constexpr uint64_t kMaxSrdBytes = 0xFFFF0000ull;  // arenas at or above: launch_general
@@ -574,6 +575,21 @@ __device__ __forceinline__ uint32_t s_of(uint32_t T, uint32_t W, uint32_t phase)
   return phase ? W : (257u * T - W);
 }
 
+// Per-packet edge word (LDS): bit 0 head, bit 1 tail, head bytes [hlo, hhi),
+// tail bytes [0, thi), bit 31 phase.
+__device__ __forceinline__ uint32_t edge_word(uint32_t has_h, uint32_t has_t, uint32_t hlo,
+                                              uint32_t hhi, uint32_t thi, uint32_t phase) {
+  return has_h | (has_t << 1) | (hlo << 2) | (hhi << 7) | (thi << 12) | (phase << 31);
+}
+
+template <int U>
+struct RunStage {
+  uint4 v[U];
+  uint4 h, tl;   // head / tail chunk (zeros unless this run carries them)
+  uint32_t ew;   // the packet's edge word, with bits 0/1 cleared unless carried here
+  int pk;
+};
+
 template <int WG, int U, bool PIPE = true>
 __global__ __launch_bounds__(WG) void csum_runs(
     const uint8_t* __restrict__ arena, uint64_t arena_bytes,
@@ -583,8 +599,9 @@ __global__ __launch_bounds__(WG) void csum_runs(
   constexpr int NW = WG / 64;
   static_assert((P & (P - 1)) == 0, "tile must be a power of two");
   __shared__ uint64_t s_rstart[P + 1];  // first run of each packet (tile-relative)
-  __shared__ uint32_t s_body[P];        // byte offset (SRD) of the packet's first body chunk
-  __shared__ uint32_t s_nb[P];          // body chunks | phase << 31
+  __shared__ uint32_t s_body[P];        // SRD byte offset of the packet's first body chunk
+  __shared__ uint32_t s_nb[P];          // body chunks
+  __shared__ uint32_t s_edge[P];        // edge word
   __shared__ uint32_t s_acc[P];
   __shared__ uint64_t s_wtot[NW];
 
@@ -593,8 +610,8 @@ __global__ __launch_bounds__(WG) void csum_runs(
   const int wv = t >> 6;
   const uint64_t i = (uint64_t)blockIdx.x * P + t;
 
-  // SRD over the whole arena, from its 16-byte-aligned base (host guarantees
-  // the rounded size is below kMaxSrdBytes).
+  // SRD over the whole arena, from its 16-byte-aligned base (the launcher
+  // guarantees the rounded size is below kMaxSrdBytes).
   const uint64_t abase = (uint64_t)(uintptr_t)arena & 15u;
   const uint64_t sb = (uint64_t)(uintptr_t)arena - abase;
   const uint32_t nrec = (uint32_t)((abase + arena_bytes + 15) & ~15ull);
@@ -605,11 +622,9 @@ __global__ __launch_bounds__(WG) void csum_runs(
   const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(((uint64_t)sb_hi << 32) | (uint64_t)sb_lo), (short)0,
       (int)__builtin_amdgcn_readfirstlane(nrec), 0x00020000);
-
   const uint32_t oob = (uint32_t)__builtin_amdgcn_readfirstlane(nrec);
-  uint32_t init = 0, phase = 0, nb = 0, body = 0;
-  uint32_t hoff = oob, toff = oob;
-  int hlo = 0, hhi = 16, thi = 16;
+
+  uint32_t init = 0, nb = 0, body = 0, ew = 0, nr = 0;
   if (i < n) {
     const uint4 raw = desc[i];
     const uint64_t off = (uint64_t)raw.x | ((uint64_t)raw.y << 32);
@@ -622,36 +637,26 @@ __global__ __launch_bounds__(WG) void csum_runs(
     }
     if (len) {
       const uint32_t a = (uint32_t)(abase + off);
-      const uint32_t e = a + len;          // exclusive end
+      const uint32_t e = a + len;  // exclusive end
       const uint32_t cf = a >> 4, cl = (e - 1) >> 4;
       const uint32_t lo = a & 15u, hiex = ((e - 1) & 15u) + 1u;
-      phase = (a + odd) & 1u;
-      if (cf == cl) {                     // inside one chunk: a lone head
-        hoff = cf * 16u;
-        hlo = (int)lo;
-        hhi = (int)hiex;
+      const uint32_t phase = (a + odd) & 1u;
+      if (cf == cl) {  // inside one chunk: a lone head
+        ew = edge_word(1u, 0u, lo, hiex, 16u, phase);
+        body = (cf + 1u) * 16u;
+        nb = 0;
       } else {
-        if (lo) {
-          hoff = cf * 16u;
-          hlo = (int)lo;
-        }
-        if (hiex != 16u) {
-          toff = cl * 16u;
-          thi = (int)hiex;
-        }
-        const uint32_t bf = cf + (lo ? 1u : 0u);
-        const uint32_t bl = cl - (hiex != 16u ? 1u : 0u);
-        nb = bl + 1u - bf;                // >= 0 since cl > cf
+        const uint32_t hh = lo ? 1u : 0u, ht = hiex != 16u ? 1u : 0u;
+        ew = edge_word(hh, ht, lo, 16u, hiex, phase);
+        const uint32_t bf = cf + hh;
+        nb = (cl - ht) + 1u - bf;
         body = bf * 16u;
       }
+      nr = nb ? (nb + (U - 1)) / U : 1u;
     }
   }
-  // Edge chunks: issued now, consumed in the epilogue.
-  const uint4 hv = bload(rsrc, hoff);
-  const uint4 tv = bload(rsrc, toff);
 
   // Block-wide exclusive scan of run counts.
-  const uint64_t nr = (nb + (U - 1)) / U;
   uint64_t incl = nr;
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
@@ -666,65 +671,77 @@ __global__ __launch_bounds__(WG) void csum_runs(
     if (w < wv) excl += s_wtot[w];
   s_rstart[t] = excl;
   s_body[t] = body;
-  s_nb[t] = nb | (phase << 31);
+  s_nb[t] = nb;
+  s_edge[t] = ew;
   s_acc[t] = 0u;
   if (t == WG - 1) s_rstart[P] = excl + nr;
   __syncthreads();
 
   const uint64_t R = s_rstart[P];
-  // One run: packet lookup + U loads (stage), then SAD + one LDS add (consume).
-  auto stage = [&](uint64_t q, uint4 (&v)[U], int& pk) {
+  auto stage = [&](uint64_t q, RunStage<U>& st) {
     // Largest p with s_rstart[p] <= q (that packet has a run q): fixed-step,
     // branch-free search (s_rstart[0] = 0 <= q always holds).
     int lo = 0;
 #pragma unroll
     for (int step = P / 2; step >= 1; step >>= 1)
       lo = (s_rstart[lo + step] <= q) ? lo + step : lo;
-    const uint32_t k = (uint32_t)(q - s_rstart[lo]);
+    const uint64_t r0 = s_rstart[lo];
+    const uint32_t k = (uint32_t)(q - r0);
+    const uint32_t last = (uint32_t)(s_rstart[lo + 1] - r0) - 1u;
+    const uint32_t nbp = s_nb[lo];
     const uint32_t c0 = k * U;
-    const uint32_t nvalid = min((uint32_t)U, (s_nb[lo] & 0x7FFFFFFFu) - c0);
-    const uint32_t base = s_body[lo] + c0 * 16u;
+    const uint32_t nvalid = nbp > c0 ? min((uint32_t)U, nbp - c0) : 0u;
+    const uint32_t bo = s_body[lo];
+    const uint32_t base = bo + c0 * 16u;
 #pragma unroll
-    for (int j = 0; j < U; ++j) v[j] = bload(rsrc, (uint32_t)j < nvalid ? base + 16u * j : oob);
-    pk = lo;
+    for (int j = 0; j < U; ++j) st.v[j] = bload(rsrc, (uint32_t)j < nvalid ? base + 16u * j : oob);
+    uint32_t e = s_edge[lo];
+    if (k != 0) e &= ~1u;
+    if (k != last) e &= ~2u;
+    st.h = make_uint4(0, 0, 0, 0);
+    st.tl = make_uint4(0, 0, 0, 0);
+    if (e & 1u) st.h = bload(rsrc, bo - 16u);
+    if (e & 2u) st.tl = bload(rsrc, bo + nbp * 16u);
+    st.ew = e;
+    st.pk = lo;
   };
-  auto consume = [&](const uint4 (&v)[U], int pk) {
+  auto consume = [&](const RunStage<U>& st) {
     uint32_t T = 0, W = 0;
 #pragma unroll
-    for (int j = 0; j < U; ++j) sad_chunk(v[j], T, W);
-    atomicAdd(&s_acc[pk], s_of(T, W, s_nb[pk] >> 31));
+    for (int j = 0; j < U; ++j) sad_chunk(st.v[j], T, W);
+    const uint32_t e = st.ew;
+    if (e & 3u) {
+      sad_chunk(mask_chunk(st.h, (int)((e >> 2) & 31u), (int)((e >> 7) & 31u)), T, W);
+      sad_chunk(mask_chunk(st.tl, 0, (int)((e >> 12) & 31u)), T, W);
+    }
+    atomicAdd(&s_acc[st.pk], s_of(T, W, e >> 31));
   };
   if constexpr (PIPE) {
     // Software pipeline: run q+WG is looked up and its loads issued before
     // run q is consumed (two register stages, unrolled by 2).
-    uint4 va[U], vb[U];
-    int pa = 0, pb = 0;
+    RunStage<U> sa, sbg;
     uint64_t q = (uint64_t)t;
-    if (q < R) stage(q, va, pa);
+    if (q < R) stage(q, sa);
     while (q < R) {
-      if (q + WG < R) stage(q + WG, vb, pb);
-      consume(va, pa);
+      if (q + WG < R) stage(q + WG, sbg);
+      consume(sa);
       q += WG;
       if (q >= R) break;
-      if (q + WG < R) stage(q + WG, va, pa);
-      consume(vb, pb);
+      if (q + WG < R) stage(q + WG, sa);
+      consume(sbg);
       q += WG;
     }
   } else {
     for (uint64_t q = (uint64_t)t; q < R; q += WG) {
-      uint4 v[U];
-      int pk;
-      stage(q, v, pk);
-      consume(v, pk);
+      RunStage<U> st;
+      stage(q, st);
+      consume(st);
     }
   }
   __syncthreads();
 
   if (i < n) {
-    uint32_t T = 0, W = 0;
-    sad_chunk(mask_chunk(hv, hlo, hhi), T, W);
-    sad_chunk(mask_chunk(tv, 0, thi), T, W);
-    const uint32_t sacc = s_acc[t] + s_of(T, W, phase);
+    const uint32_t sacc = s_acc[t];
     if (partial) partial[i] = sacc;
     else out[i] = (uint16_t)fold1(init + sacc);
   }
@@ -754,13 +771,13 @@ __global__ void csum_chain(const uint4* __restrict__ desc, uint32_t n,
 // ---- launchers (C++ linkage, used by csum_api.cpp) ------------------------
 namespace nsk {
 
-template <int U>
+template <int U, bool PIPE>
 static hipError_t launch_runs(const uint8_t* arena, uint64_t arena_bytes, const void* desc,
                               uint32_t n, uint16_t* out, uint32_t* partial,
                               unsigned long long* err, hipStream_t stream) {
   constexpr int WG = 256;
   const uint32_t tiles = (uint32_t)(((uint64_t)n + WG - 1) / WG);
-  hipLaunchKernelGGL((csum_runs<WG, U, true>), dim3(tiles), dim3(WG), 0, stream, arena, arena_bytes,
+  hipLaunchKernelGGL((csum_runs<WG, U, PIPE>), dim3(tiles), dim3(WG), 0, stream, arena, arena_bytes,
                      reinterpret_cast<const uint4*>(desc), n, out, partial, err);
   return hipGetLastError();
 }
@@ -784,10 +801,13 @@ hipError_t launch_batch(const uint8_t* arena, uint64_t arena_bytes,
   if (arena_bytes + 64 >= kMaxSrdBytes) {
     // Arenas of 4 GiB and more: 64-bit addressing, global loads.
     e = launch_general(arena, arena_bytes, desc, n, out, partial, err, stream);
+  } else if (arena_bytes / n >= 256) {
+    // Runs of 4 chunks, software-pipelined (tools/tune.py on MI355X: best on
+    // 1500 B and Zipf 64-9000 B batches).
+    e = launch_runs<4, true>(arena, arena_bytes, desc, n, out, partial, err, stream);
   } else {
-    // Runs of 4 chunks, software-pipelined: best or tied on every BASELINE
-    // layout in tools/tune.py on MI355X (1500 B, 64 B, Zipf 64-9000 B).
-    e = launch_runs<4>(arena, arena_bytes, desc, n, out, partial, err, stream);
+    // Small packets: about one run per lane per tile, pipelining only costs.
+    e = launch_runs<4, false>(arena, arena_bytes, desc, n, out, partial, err, stream);
   }
   if (e != hipSuccess || partial == nullptr) return e;
   const uint32_t blocks = (n + 255) / 256;

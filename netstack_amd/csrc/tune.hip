@@ -128,7 +128,7 @@ struct Variant {
 };
 static const Variant kVariants[] = {
     {"runs_U4_pipe", launch_r<4, true>},  {"runs_U4", launch_r<4, false>},
-    {"runs_U8_pipe", launch_r<8, true>},  {"runs_U2_pipe", launch_r<2, true>},
+    {"runs_U2_pipe", launch_r<2, true>},  {"runs_U8", launch_r<8, false>},
     {"dense_U8", launch_v<1, 2, 8, false>},
 };
 

@@ -43,7 +43,7 @@ def main():
         k = int(r["Dispatch_Id"])
         disp[k][r["Counter_Name"]] = disp[k].get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
         names[k] = r["Kernel_Name"]
-    ours = [k for k in sorted(disp) if ("calib_buf" in names[k] or "csum_batch" in names[k])]
+    ours = [k for k in sorted(disp) if ("calib_buf" in names[k] or "nsk::csum_" in names[k])]
     out = {}
     for i, (lab, meta) in enumerate(labels):
         ks = ours[i * REPS:(i + 1) * REPS]
@@ -57,7 +57,7 @@ def main():
     for m in ("calib800", "calib400", "calib102"):
         if m in out and "FETCH_SIZE" in out[m]["avg"]:
             cal[m] = float(out[m]["meta"]["bytes"]) / (out[m]["avg"]["FETCH_SIZE"] * 1024.0)
-    for lab, shape in (("cfg2", "calib800"), ("cfg3", "calib400"), ("cfg4", "calib400")):
+    for lab, shape in (("cfg2", "calib400"), ("cfg3", "calib400"), ("cfg4", "calib400")):
         if lab in out and "FETCH_SIZE" in out[lab]["avg"]:
             raw = out[lab]["avg"]["FETCH_SIZE"] * 1024.0
             f = cal.get(shape)
