@@ -215,7 +215,9 @@ def main():
     if os.path.exists(args.pmc_json):
         try:
             pm = json.load(open(args.pmc_json))
-            traffic = pm.get(f"cfg{cfg}", {}).get("hbm_bytes_per_launch")
+            e = pm.get(f"cfg{cfg}", {})
+            if e.get("hbm_bytes_per_launch") is not None:
+                traffic = e["hbm_bytes_per_launch"] + e.get("write_bytes", 0.0)
         except Exception:
             traffic = None
 

@@ -161,6 +161,17 @@ int ns_csum_pseudo_header(ns_csum_ctx* ctx, uint32_t protocol,
 uint16_t ns_csum_combine(uint16_t a, uint16_t b);
 
 /* ---- multi-GPU sharding -------------------------------------------------
+ * ns_csum_batch_multi: one host batch over nctx contexts (normally one per
+ * device): the table is split by ns_csum_shard_plan, each shard runs
+ * ns_csum_batch_host on its own context from its own host thread, results
+ * land in h_out in table order.  Shards are independent (per-packet
+ * arithmetic): no collective, no peer traffic.  Synchronous.                */
+int ns_csum_batch_multi(ns_csum_ctx* const* ctxs, uint32_t nctx,
+                        const uint8_t* h_arena, uint64_t arena_bytes,
+                        const ns_pkt_desc* h_desc, uint32_t n, uint16_t* h_out,
+                        uint32_t batch_flags);
+
+/* ---- (sharding plan) ----------------------------------------------------
  * Splits n descriptors into `parts` contiguous ranges with near-equal payload
  * bytes (prefix sum of len, cut at byte quantiles).  first[p] = index of the
  * first descriptor of part p; first[parts] = n.  Pure host arithmetic.      */

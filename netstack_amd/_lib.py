@@ -32,7 +32,7 @@ EXPORTED = (
     "ns_csum_init", "ns_csum_destroy", "ns_csum_sync", "ns_csum_batch_dev",
     "ns_csum_batch_host", "ns_csum_checksum", "ns_csum_vv_with_offset",
     "ns_csum_vv_batch", "ns_csum_views_restart", "ns_csum_pseudo_header",
-    "ns_csum_combine", "ns_csum_shard_plan",
+    "ns_csum_combine", "ns_csum_shard_plan", "ns_csum_batch_multi",
 )
 
 
@@ -102,6 +102,8 @@ def _declare(lib):
                                             c.c_uint16, u16p]),
         "ns_csum_combine": (c.c_uint16, [c.c_uint16, c.c_uint16]),
         "ns_csum_shard_plan": (c.c_int, [vp, c.c_uint32, c.c_uint32, c.POINTER(c.c_uint32)]),
+        "ns_csum_batch_multi": (c.c_int, [c.POINTER(vp), c.c_uint32, u8p, c.c_uint64, vp, c.c_uint32,
+                                          vp, c.c_uint32]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

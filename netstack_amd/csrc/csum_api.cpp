@@ -12,6 +12,7 @@
 #include <cstring>
 #include <mutex>
 #include <new>
+#include <thread>
 #include <vector>
 
 #include "csum_kernels.h"
@@ -534,6 +535,38 @@ int ns_csum_pseudo_header(ns_csum_ctx* ctx, uint32_t protocol, const uint8_t* sr
   Gather gt{ctx, {}, {}, {}};
   gt.restart_chain(pieces, 0);
   return gt.run(out);
+}
+
+int ns_csum_batch_multi(ns_csum_ctx* const* ctxs, uint32_t nctx, const uint8_t* h_arena,
+                        uint64_t arena_bytes, const ns_pkt_desc* h_desc, uint32_t n,
+                        uint16_t* h_out, uint32_t batch_flags) {
+  if (!ctxs || nctx == 0 || (n && (!h_desc || !h_out)) || (arena_bytes && !h_arena)) return NS_EINVAL;
+  for (uint32_t c = 0; c < nctx; ++c)
+    if (!ctxs[c]) return NS_EINVAL;
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint64_t off = h_desc[i].off, len = h_desc[i].len;
+    if (off > arena_bytes || len > arena_bytes - off) return NS_ERANGE;
+  }
+  std::vector<uint32_t> first(nctx + 1);
+  int rc = ns_csum_shard_plan(h_desc, n, nctx, first.data());
+  if (rc != NS_OK) return rc;
+  // One host thread per shard (per device context); each runs the pipelined
+  // host path on its own streams.  Shards are independent: no collective.
+  std::vector<int> status(nctx, NS_OK);
+  std::vector<std::thread> th;
+  th.reserve(nctx);
+  for (uint32_t c = 0; c < nctx; ++c) {
+    th.emplace_back([&, c]() {
+      const uint32_t lo = first[c], hi = first[c + 1];
+      if (hi <= lo) return;
+      status[c] = ns_csum_batch_host(ctxs[c], h_arena, arena_bytes, h_desc + lo, hi - lo,
+                                     h_out + lo, batch_flags);
+    });
+  }
+  for (auto& t : th) t.join();
+  for (uint32_t c = 0; c < nctx; ++c)
+    if (status[c] != NS_OK) return status[c];
+  return NS_OK;
 }
 
 int ns_csum_shard_plan(const ns_pkt_desc* h_desc, uint32_t n, uint32_t parts, uint32_t* first) {

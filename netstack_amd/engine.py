@@ -182,6 +182,19 @@ def shard_plan(desc: np.ndarray, parts: int) -> np.ndarray:
     return first
 
 
+def batch_multi(engines, arena, desc: np.ndarray, chained: bool = False) -> np.ndarray:
+    """One host batch sharded over several engines (devices) by
+    ns_csum_batch_multi: byte-balanced contiguous shards, one host thread and
+    one device per shard, no collective."""
+    a = _u8(arena)
+    d = np.ascontiguousarray(desc, dtype=DESC_DTYPE)
+    out = np.zeros(len(d), dtype=np.uint16)
+    hs = (ctypes.c_void_p * len(engines))(*[e._h for e in engines])
+    check(lib().ns_csum_batch_multi(hs, len(engines), _ptr(a), a.size, _ptr(d), len(d), _ptr(out),
+                                    _lib.NS_BATCH_CHAINED if chained else 0), "ns_csum_batch_multi")
+    return out
+
+
 _engines: dict[int, Engine] = {}
 _elock = threading.Lock()
 

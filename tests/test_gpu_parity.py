@@ -309,3 +309,22 @@ def test_sorted_dense_tiles_with_gaps_and_empties(engine):
         assert bad == 0
         for off in (0, 5):
             assert np.array_equal(dev_batch(engine, arena, d, arena_offset=off), want), (trial, off)
+
+
+def test_batch_multi_shards_over_contexts(engine):
+    """ns_csum_batch_multi: one host batch split over several contexts (here
+    three contexts on the single test GPU, standing in for three devices)."""
+    import oracle as O
+    from netstack_amd import Engine, workloads as W
+    from netstack_amd.engine import batch_multi
+
+    b = W.config(4, n=20000)
+    arena = b.arena_host()
+    want, _ = O.c_batch(arena, b.desc)
+    extra = [Engine(0), Engine(0)]
+    try:
+        got = batch_multi([engine] + extra, arena, b.desc)
+    finally:
+        for e in extra:
+            e.close()
+    assert np.array_equal(got, want)
