@@ -97,3 +97,12 @@ def test_header_mirror_is_device_only():
             if fn.endswith((".py", ".cpp", ".hip", ".h")):
                 txt = open(os.path.join(dirpath, fn)).read()
                 assert "import oracle" not in txt and "oracle_" not in txt, fn
+
+
+def test_cpp_mirror_buffer_tables():
+    """The C++ mirror's view_test.go tables (no GPU needed)."""
+    exe = os.path.join(ROOT, "netstack_amd", "lib", "checksum_test")
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "netstack_amd", "csrc")], check=True)
+    r = subprocess.run([exe, "--cpu-only"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stdout + r.stderr

@@ -12,33 +12,45 @@ def flat(v):
     return b"".join(bytes(x) for x in v.Views())
 
 
+def _same(a, b):
+    return a.Size() == b.Size() and flat(a) == flat(b) and len(a.Views()) == len(b.Views())
+
+
 def test_cap_length():
+    # view_test.go:44-97 capLengthTestCases
     cases = [
-        (vv(2, "12"), 1, vv(1, "1")),
-        (vv(2, "12"), 0, vv(0)),
-        (vv(2, "12"), 2, vv(2, "12")),
-        (vv(4, "12", "34"), 3, vv(3, "12", "3")),
-        (vv(4, "12", "34"), 2, vv(2, "12")),
-        (vv(4, "12", "34"), 5, vv(4, "12", "34")),
-        (vv(4, "12", "34"), -1, vv(0)),
+        ("Simple case", vv(2, "12"), 1, vv(1, "1")),
+        ("Case spanning across two Views", vv(4, "123", "4"), 2, vv(2, "12")),
+        ("Corner case with negative length", vv(1, "1"), -1, vv(0)),
+        ("Corner case with length = 0", vv(3, "12", "3"), 0, vv(0)),
+        ("Corner case with length = size", vv(1, "1"), 1, vv(1, "1")),
+        ("Corner case with length > size", vv(1, "1"), 2, vv(1, "1")),
     ]
-    for v, n, want in cases:
+    for name, v, n, want in cases:
         v.CapLength(n)
-        assert v.Size() == want.Size() and flat(v) == flat(want) and len(v.Views()) == len(want.Views())
+        assert _same(v, want), name
 
 
 def test_trim_front():
+    # view_test.go:99-160 trimFrontTestCases
     cases = [
-        (vv(2, "12"), 1, vv(1, "2")),
-        (vv(2, "12"), 2, vv(0)),
-        (vv(4, "12", "34"), 1, vv(3, "2", "34")),
-        (vv(4, "12", "34"), 2, vv(2, "34")),
-        (vv(4, "12", "34"), 3, vv(1, "4")),
-        (vv(4, "12", "34"), 5, vv(0)),
+        ("Simple case", vv(2, "12"), 1, vv(1, "2")),
+        ("Case where we trim an entire View", vv(2, "1", "2"), 1, vv(1, "2")),
+        ("Case spanning across two Views", vv(3, "1", "23"), 2, vv(1, "3")),
+        ("Corner case with negative count", vv(1, "1"), -1, vv(1, "1")),
+        ("Corner case with count = 0", vv(1, "1"), 0, vv(1, "1")),
+        ("Corner case with count = size", vv(1, "1"), 1, vv(0)),
+        ("Corner case with count > size", vv(1, "1"), 2, vv(0)),
     ]
-    for v, n, want in cases:
+    for name, v, n, want in cases:
         v.TrimFront(n)
-        assert v.Size() == want.Size() and flat(v) == flat(want)
+        assert _same(v, want), name
+
+
+def test_to_view():
+    # view_test.go:162-190 toViewCases
+    for v, want in [(vv(2, "12"), b"12"), (vv(2, "1", "2"), b"12"), (vv(0), b"")]:
+        assert bytes(v.ToView()) == want
 
 
 def test_to_view_and_append():

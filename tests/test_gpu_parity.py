@@ -328,3 +328,17 @@ def test_batch_multi_shards_over_contexts(engine):
         for e in extra:
             e.close()
     assert np.array_equal(got, want)
+
+
+def test_cpp_mirror_reference_tests(engine):
+    """tests/cpp/checksum_test.cc: checksum_test.go's TestChecksumVVWithOffset
+    and protocol invariants through the C++ tcpip/header mirror."""
+    import os
+    import subprocess
+
+    from conftest import ROOT
+
+    exe = os.path.join(ROOT, "netstack_amd", "lib", "checksum_test")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "0 failed" in r.stdout
