@@ -111,13 +111,10 @@ hipError_t launch_v(const uint8_t* arena, uint64_t arena_bytes, const void* desc
   return hipGetLastError();
 }
 
-template <int U, bool PIPE = true>
+template <int U, bool PIPE = true, bool PERSIST = false>
 hipError_t launch_r(const uint8_t* arena, uint64_t arena_bytes, const void* desc, uint32_t n,
                     uint16_t* out, unsigned long long* err, hipStream_t s) {
-  const uint32_t tiles = (n + 255) / 256;
-  hipLaunchKernelGGL((csum_runs<256, U, PIPE>), dim3(tiles), dim3(256), 0, s, arena, arena_bytes,
-                     reinterpret_cast<const uint4*>(desc), n, out, nullptr, err);
-  return hipGetLastError();
+  return launch_runs<U, PIPE, PERSIST>(arena, arena_bytes, desc, n, out, nullptr, err, s);
 }
 
 typedef hipError_t (*launch_fn)(const uint8_t*, uint64_t, const void*, uint32_t, uint16_t*,
@@ -127,9 +124,8 @@ struct Variant {
   launch_fn fn;
 };
 static const Variant kVariants[] = {
-    {"runs_U4_pipe", launch_r<4, true>},  {"runs_U4", launch_r<4, false>},
-    {"runs_U2_pipe", launch_r<2, true>},  {"runs_U8", launch_r<8, false>},
-    {"dense_U8", launch_v<1, 2, 8, false>},
+    {"runs_U4_pipe", launch_r<4, true, false>},       {"runs_U4", launch_r<4, false, false>},
+    {"runs_U4_pipe_persist", launch_r<4, true, true>}, {"runs_U4_persist", launch_r<4, false, true>},
 };
 
 }  // namespace nsk

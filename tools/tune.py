@@ -61,6 +61,7 @@ def main():
     ap.add_argument("--calib-modes", default="2,4,5,6")
     ap.add_argument("--calib-blocks", default="4096,8192,16384")
     ap.add_argument("--json", default="")
+    ap.add_argument("--n", default="", help="packet counts per config, e.g. 2:2097152")
     args = ap.parse_args()
 
     L = load()
@@ -74,8 +75,9 @@ def main():
     err = torch.zeros(1, dtype=torch.int64, device=dev)
     report = {"variants": {}, "calib": {}}
 
+    nover = dict((int(k), int(v)) for k, v in (x.split(":") for x in args.n.split(",") if x))
     for cfg in [int(c) for c in args.configs.split(",")]:
-        b = W.config(cfg)
+        b = W.config(cfg, nover.get(cfg))
         rot = 4 if cfg == 3 else 1
         arenas = [b.arena_device(dev)] + [W.random_bytes_torch(b.seed + 77 * r, b.arena_bytes, dev)
                                           for r in range(1, rot)]
