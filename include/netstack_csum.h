@@ -157,6 +157,30 @@ int ns_csum_pseudo_header(ns_csum_ctx* ctx, uint32_t protocol,
                           const uint8_t* src, uint32_t src_len,
                           const uint8_t* dst, uint32_t dst_len,
                           uint16_t total_len, uint16_t* out);
+/* Chains of pieces: the general form every caller above reduces to.  A chain
+ * is a run of pieces ending with one flagged NS_PIECE_END; its result is
+ * emitted to out[] in chain order.  Per chain: sum = first piece's initial,
+ * odd = false; for each piece (sum, odd) = calculateChecksum(piece, odd', sum)
+ * (checksum.go:26-46) with odd' = false for a NS_PIECE_RESTART piece (the
+ * semantics of Checksum(v, sum), checksum.go:52-55) and odd' = odd otherwise
+ * (ChecksumVVWithOffset's view chaining, checksum.go:89; empty continue
+ * pieces are skipped as empty views are, :73-75).  One chain can therefore
+ * hold a TCP/UDP segment's whole checksum: pseudo-header fields (restart),
+ * payload views (first restart, then continue), transport header (restart) —
+ * buildTCPHdr (tcp/connect.go:634-666) and segment.parse (tcp/segment.go:
+ * 174-180) — and all chains of a batch run in one device pass.              */
+#define NS_PIECE_RESTART 0x1u
+#define NS_PIECE_END 0x2u
+typedef struct ns_piece {
+  const uint8_t* data;
+  uint64_t len;
+  uint16_t initial; /* used by the first piece of a chain */
+  uint16_t flags;   /* NS_PIECE_* */
+  uint32_t pad;
+} ns_piece;
+int ns_csum_chains(ns_csum_ctx* ctx, const ns_piece* pieces, uint32_t npieces,
+                   uint16_t* out, uint32_t nout);
+
 /* header.ChecksumCombine(a, b)                     checksum.go:104-107      */
 uint16_t ns_csum_combine(uint16_t a, uint16_t b);
 

@@ -32,8 +32,10 @@ EXPORTED = (
     "ns_csum_init", "ns_csum_destroy", "ns_csum_sync", "ns_csum_batch_dev",
     "ns_csum_batch_host", "ns_csum_checksum", "ns_csum_vv_with_offset",
     "ns_csum_vv_batch", "ns_csum_views_restart", "ns_csum_pseudo_header",
-    "ns_csum_combine", "ns_csum_shard_plan", "ns_csum_batch_multi",
+    "ns_csum_combine", "ns_csum_shard_plan", "ns_csum_batch_multi", "ns_csum_chains",
 )
+NS_PIECE_RESTART = 0x1
+NS_PIECE_END = 0x2
 
 
 class NativeLibraryError(RuntimeError):
@@ -67,12 +69,17 @@ class NsSeg(ctypes.Structure):
                 ("pad1", ctypes.c_uint32)]
 
 
+class NsPiece(ctypes.Structure):
+    _fields_ = [("data", ctypes.c_void_p), ("len", ctypes.c_uint64), ("initial", ctypes.c_uint16),
+                ("flags", ctypes.c_uint16), ("pad", ctypes.c_uint32)]
+
+
 class NsOpts(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int32), ("flags", ctypes.c_uint32),
                 ("staging_bytes", ctypes.c_uint64)]
 
 
-assert ctypes.sizeof(NsPktDesc) == 16 and ctypes.sizeof(NsSeg) == 24
+assert ctypes.sizeof(NsPktDesc) == 16 and ctypes.sizeof(NsSeg) == 24 and ctypes.sizeof(NsPiece) == 24
 
 _lock = threading.Lock()
 _lib = None
@@ -102,6 +109,7 @@ def _declare(lib):
                                             c.c_uint16, u16p]),
         "ns_csum_combine": (c.c_uint16, [c.c_uint16, c.c_uint16]),
         "ns_csum_shard_plan": (c.c_int, [vp, c.c_uint32, c.c_uint32, c.POINTER(c.c_uint32)]),
+        "ns_csum_chains": (c.c_int, [vp, c.POINTER(NsPiece), c.c_uint32, u16p, c.c_uint32]),
         "ns_csum_batch_multi": (c.c_int, [c.POINTER(vp), c.c_uint32, u8p, c.c_uint64, vp, c.c_uint32,
                                           vp, c.c_uint32]),
     }

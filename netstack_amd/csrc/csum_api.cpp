@@ -20,6 +20,7 @@
 
 static_assert(sizeof(ns_pkt_desc) == 16, "ns_pkt_desc must be 16 bytes");
 static_assert(sizeof(ns_seg) == 24, "ns_seg layout");
+static_assert(sizeof(ns_piece) == 24, "ns_piece layout");
 
 namespace {
 
@@ -303,6 +304,55 @@ struct Gather {
     result_at.push_back((uint32_t)desc.size() - 1);
   }
 
+  // A chain of pieces with per-piece restart/continue semantics
+  // (include/netstack_csum.h, ns_csum_chains).  Continue pieces merge into the
+  // open descriptor up to kMergeMax bytes (exact, see kMergeMax); a restart
+  // piece always opens a new descriptor with odd = 0.
+  void chain(const ns_piece* p, uint32_t np) {
+    bool first_desc = true;
+    uint32_t parity = 0;  // odd flag carried to the next continue piece
+    ns_pkt_desc cur{};
+    bool open = false;
+    uint16_t initial = np ? p[0].initial : 0;
+    auto close = [&]() {
+      if (!open) return;
+      desc.push_back(cur);
+      open = false;
+    };
+    for (uint32_t k = 0; k < np; ++k) {
+      const bool restart = (p[k].flags & NS_PIECE_RESTART) != 0;
+      const uint64_t len = p[k].len;
+      if (restart) {
+        close();
+        parity = 0;
+        if (len == 0) continue;  // Checksum(empty, x) == x, odd = false
+      } else if (len == 0) {
+        continue;  // empty views are skipped (checksum.go:73-75)
+      }
+      const bool big = len > kMergeMax;
+      if (open && (big || cur.len + len > kMergeMax)) close();
+      if (!open) {
+        cur.off = bytes.size();
+        cur.len = 0;
+        cur.initial = first_desc ? initial : 0;
+        cur.flags = (uint16_t)((first_desc ? 0u : NS_DESC_CONT) | (parity ? NS_DESC_ODD : 0u));
+        first_desc = false;
+        open = true;
+      }
+      bytes.insert(bytes.end(), p[k].data, p[k].data + len);
+      cur.len += (uint32_t)len;
+      parity ^= (uint32_t)(len & 1);
+      if (big) close();
+    }
+    close();
+    if (first_desc) {  // no bytes at all: result = initial
+      ns_pkt_desc z{};
+      z.initial = initial;
+      desc.push_back(z);
+    }
+    result_at.push_back((uint32_t)desc.size() - 1);
+  }
+
   int run(uint16_t* out) {
     std::lock_guard<std::mutex> lk(ctx->mu);
     DeviceGuard g(ctx->device);
@@ -520,6 +570,29 @@ int ns_csum_views_restart(ns_csum_ctx* ctx, const ns_view* views, uint32_t nview
   }
   Gather gt{ctx, {}, {}, {}};
   gt.restart_chain(pieces, initial);
+  return gt.run(out);
+}
+
+int ns_csum_chains(ns_csum_ctx* ctx, const ns_piece* pieces, uint32_t npieces, uint16_t* out,
+                   uint32_t nout) {
+  if (!ctx || (npieces && !pieces)) return NS_EINVAL;
+  uint32_t chains = 0;
+  for (uint32_t k = 0; k < npieces; ++k) {
+    if (pieces[k].len && !pieces[k].data) return NS_EINVAL;
+    if (pieces[k].len > 0xFFFFFFFFull) return NS_EINVAL;
+    if (pieces[k].flags & NS_PIECE_END) ++chains;
+  }
+  if (npieces && !(pieces[npieces - 1].flags & NS_PIECE_END)) return NS_EINVAL;  // unterminated
+  if (chains > nout || (chains && !out)) return NS_EINVAL;
+  if (chains == 0) return NS_OK;
+  Gather gt{ctx, {}, {}, {}};
+  uint32_t start = 0;
+  for (uint32_t k = 0; k < npieces; ++k) {
+    if (pieces[k].flags & NS_PIECE_END) {
+      gt.chain(pieces + start, k + 1 - start);
+      start = k + 1;
+    }
+  }
   return gt.run(out);
 }
 

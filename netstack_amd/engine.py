@@ -11,7 +11,7 @@ import threading
 import numpy as np
 
 from . import _lib
-from ._lib import NsOpts, NsSeg, NsView, check, lib
+from ._lib import NsOpts, NsPiece, NsSeg, NsView, check, lib
 
 DESC_DTYPE = np.dtype(
     [("off", "<u8"), ("len", "<u4"), ("initial", "<u2"), ("flags", "<u2")], align=False)
@@ -156,6 +156,31 @@ class Engine:
         check(lib().ns_csum_views_restart(self._h, cv, len(keep), initial & 0xFFFF, ctypes.byref(r)),
               "ns_csum_views_restart")
         return int(r.value)
+
+    def chains(self, chains) -> np.ndarray:
+        """ns_csum_chains: `chains` is a list of chains; a chain is a list of
+        (bytes_like, restart: bool) pieces, optionally with the chain's initial
+        as ("init", value) first.  Returns one u16 per chain (one device pass)."""
+        keep, flat = [], []
+        for ch in chains:
+            init = 0
+            items = list(ch)
+            if items and isinstance(items[0], tuple) and items[0][0] == "init":
+                init = items[0][1] & 0xFFFF
+                items = items[1:]
+            if not items:
+                items = [(b"", True)]
+            for k, (buf, restart) in enumerate(items):
+                a = _u8(buf)
+                keep.append(a)
+                fl = (_lib.NS_PIECE_RESTART if restart else 0) | (_lib.NS_PIECE_END if k == len(items) - 1 else 0)
+                flat.append(NsPiece(_ptr(a), a.size, init if k == 0 else 0, fl, 0))
+        out = np.zeros(len(chains), dtype=np.uint16)
+        arr = (NsPiece * max(len(flat), 1))(*flat)
+        check(lib().ns_csum_chains(self._h, arr, len(flat),
+                                   out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint16)), len(chains)),
+              "ns_csum_chains")
+        return out
 
     def pseudo_header(self, protocol: int, src: bytes, dst: bytes, total_len: int) -> int:
         s, d = _u8(bytes(src)), _u8(bytes(dst))
