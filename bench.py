@@ -153,6 +153,14 @@ def cpu_baseline(batch, seconds: float, threads: int):
         (arena, d, out)
 
 
+# The kernel launch_batch picks for each workload (csum_kernels.hip launch_batch).
+KERNELS = {
+    2: "nsk::csum_hyb<256,16,8,4,2>",
+    3: "nsk::csum_runs<256,4,false,true>",
+    4: "nsk::csum_hyb<256,16,8,4,2>",
+}
+
+
 def main():
     args = parse()
     import torch
@@ -249,7 +257,7 @@ def main():
             "unit": "GB/s",
             "frac": achieved_gbs / HBM_PEAK_GBS,
             "traffic": traffic,
-            "kernel": "nsk::csum_runs<256,4,true>",
+            "kernel": KERNELS[cfg],
             "algorithmic_bytes_per_launch": algo_bytes,
             "avg_launch_us": kern_avg_s * 1e6,
         },

@@ -559,8 +559,9 @@ __global__ __launch_bounds__(WG) void csum_batch(
 // ===========================================================================
 constexpr uint64_t kMaxSrdBytes = 0xFFFF0000ull;  // arenas at or above: launch_general
 
+template <int AUX = 0>
 __device__ __forceinline__ uint4 bload(__amdgpu_buffer_rsrc_t r, uint32_t off) {
-  auto x = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0);
+  auto x = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, AUX);
   return *reinterpret_cast<uint4*>(&x);
 }
 
@@ -765,6 +766,332 @@ __global__ __launch_bounds__(WG) void csum_runs(
   }  // sub-tiles
 }
 
+// ===========================================================================
+// csum_grp — lane groups over a packet's chunks (arena < 4 GiB).
+//
+// A packet covers chunks [cf, cl] of the arena (16-B aligned address space);
+// they are cut into packet-aligned runs of G*U chunks and a run belongs to a
+// group of G adjacent lanes: lane li loads chunks li, li+G, ..., li+(U-1)G of
+// the run, so every load instruction reads G*16 contiguous bytes per group —
+// for G = 8 one full 128-B line, the fully coalesced shape rather than the
+// per-lane run shape (lanes U*16 B apart) of csum_runs.  The packet's first
+// and last chunk are byte-masked where they are loaded (no separate edge
+// loads); the group's partials are summed with DPP (S is linear in T and W
+// for a fixed phase) and lane 0 of the group issues the one ds_add_u32.
+// ===========================================================================
+template <int G>
+__device__ __forceinline__ uint32_t group_sum(uint32_t s) {
+  static_assert(G == 1 || G == 2 || G == 4 || G == 8 || G == 16, "group of 1..16 lanes");
+  if constexpr (G >= 2) s += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)s, 0xB1, 0xF, 0xF, false);   // quad_perm 1,0,3,2
+  if constexpr (G >= 4) s += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)s, 0x4E, 0xF, 0xF, false);   // quad_perm 2,3,0,1
+  if constexpr (G >= 8) s += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)s, 0x141, 0xF, 0xF, false);  // row_half_mirror
+  if constexpr (G >= 16) s += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)s, 0x140, 0xF, 0xF, false); // row_mirror
+  return s;
+}
+
+template <int U>
+struct GrpStage {
+  uint4 v[U];
+  uint32_t ci0;  // chunk index (within the packet) of v[0]
+  uint32_t nch;  // the packet's chunk count
+  uint32_t ew;   // lo | hiex << 5 | phase << 31
+  int pk;
+};
+
+template <int WG, int G, int U, bool PIPE, int AUX = 0>
+__global__ __launch_bounds__(WG) void csum_grp(
+    const uint8_t* __restrict__ arena, uint64_t arena_bytes,
+    const uint4* __restrict__ desc, uint32_t n, uint16_t* __restrict__ out,
+    uint32_t* __restrict__ partial, unsigned long long* __restrict__ err) {
+  constexpr int P = WG;
+  constexpr int NW = WG / 64;
+  constexpr int NG = WG / G;     // groups per workgroup
+  constexpr uint32_t RC = G * U; // chunks per run
+  static_assert((P & (P - 1)) == 0, "tile must be a power of two");
+  __shared__ uint64_t s_rstart[P + 1];
+  __shared__ uint32_t s_first[P];  // SRD byte offset of chunk cf
+  __shared__ uint32_t s_nch[P];
+  __shared__ uint32_t s_edge[P];
+  __shared__ uint32_t s_acc[P];
+  __shared__ uint64_t s_wtot[NW];
+
+  const int t = threadIdx.x;
+  const int lane = t & 63;
+  const int wv = t >> 6;
+  const int grp = t / G;
+  const uint32_t li = (uint32_t)(t % G);
+
+  const uint64_t abase = (uint64_t)(uintptr_t)arena & 15u;
+  const uint64_t sb = (uint64_t)(uintptr_t)arena - abase;
+  const uint32_t nrec = (uint32_t)((abase + arena_bytes + 15) & ~15ull);
+  const uint32_t sb_lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)sb);
+  const uint32_t sb_hi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(sb >> 32));
+  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(((uint64_t)sb_hi << 32) | (uint64_t)sb_lo), (short)0,
+      (int)__builtin_amdgcn_readfirstlane(nrec), 0x00020000);
+  const uint32_t oob = (uint32_t)__builtin_amdgcn_readfirstlane(nrec);
+
+  const uint64_t tile_lo = (uint64_t)blockIdx.x * P;
+  const uint64_t i = tile_lo + t;
+  const uint64_t lim = min<uint64_t>(tile_lo + P, n);
+  uint32_t init = 0, nch = 0, first = 0, ew = 0, nr = 0;
+  if (i < lim) {
+    const uint4 raw = desc[i];
+    const uint64_t off = (uint64_t)raw.x | ((uint64_t)raw.y << 32);
+    uint32_t len = raw.z;
+    init = raw.w & 0xFFFFu;
+    const uint32_t odd = (raw.w >> 16) & 1u;
+    if (off > arena_bytes || (uint64_t)len > arena_bytes - off) {
+      len = 0;
+      atomicAdd(err, 1ull);
+    }
+    if (len) {
+      const uint32_t a = (uint32_t)(abase + off);
+      const uint32_t e = a + len;
+      const uint32_t cf = a >> 4, cl = (e - 1) >> 4;
+      nch = cl - cf + 1u;
+      first = cf * 16u;
+      ew = (a & 15u) | ((((e - 1) & 15u) + 1u) << 5) | (((a + odd) & 1u) << 31);
+      nr = (nch + RC - 1) / RC;
+    }
+  }
+
+  uint64_t incl = nr;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint64_t y = __shfl_up(incl, d, 64);
+    if (lane >= d) incl += y;
+  }
+  if (lane == 63) s_wtot[wv] = incl;
+  __syncthreads();
+  uint64_t excl = incl - nr;
+#pragma unroll
+  for (int w = 0; w < NW; ++w)
+    if (w < wv) excl += s_wtot[w];
+  s_rstart[t] = excl;
+  s_first[t] = first;
+  s_nch[t] = nch;
+  s_edge[t] = ew;
+  s_acc[t] = 0u;
+  if (t == WG - 1) s_rstart[P] = excl + nr;
+  __syncthreads();
+
+  const uint64_t R = s_rstart[P];
+  auto stage = [&](uint64_t q, GrpStage<U>& st) {
+    int lo = 0;
+#pragma unroll
+    for (int step = P / 2; step >= 1; step >>= 1)
+      lo = (s_rstart[lo + step] <= q) ? lo + step : lo;
+    const uint32_t k = (uint32_t)(q - s_rstart[lo]);
+    const uint32_t nc = s_nch[lo];
+    const uint32_t ci0 = k * RC + li;
+    const uint32_t base = s_first[lo] + ci0 * 16u;
+#pragma unroll
+    for (int j = 0; j < U; ++j)
+      st.v[j] = bload<AUX>(rsrc, ci0 + (uint32_t)(G * j) < nc ? base + (uint32_t)(16 * G * j) : oob);
+    st.ci0 = ci0;
+    st.nch = nc;
+    st.ew = s_edge[lo];
+    st.pk = lo;
+  };
+  auto consume = [&](const GrpStage<U>& st) {
+    uint32_t T = 0, W = 0;
+    const uint32_t lastc = st.nch - 1u;
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      const uint32_t ci = st.ci0 + (uint32_t)(G * j);
+      uint4 w = st.v[j];
+      if (ci == 0u || ci == lastc)
+        w = mask_chunk(w, ci == 0u ? (int)(st.ew & 31u) : 0, ci == lastc ? (int)((st.ew >> 5) & 31u) : 16);
+      sad_chunk(w, T, W);
+    }
+    const uint32_t s = group_sum<G>(s_of(T, W, st.ew >> 31));
+    if (li == 0) atomicAdd(&s_acc[st.pk], s);
+  };
+  if constexpr (PIPE) {
+    GrpStage<U> sa, sbg;
+    uint64_t q = (uint64_t)grp;
+    if (q < R) stage(q, sa);
+    while (q < R) {
+      if (q + NG < R) stage(q + NG, sbg);
+      consume(sa);
+      q += NG;
+      if (q >= R) break;
+      if (q + NG < R) stage(q + NG, sa);
+      consume(sbg);
+      q += NG;
+    }
+  } else {
+    for (uint64_t q = (uint64_t)grp; q < R; q += NG) {
+      GrpStage<U> st;
+      stage(q, st);
+      consume(st);
+    }
+  }
+  __syncthreads();
+
+  if (i < lim) {
+    const uint32_t sacc = s_acc[t];
+    if (partial) partial[i] = sacc;
+    else out[i] = (uint16_t)fold1(init + sacc);
+  }
+}
+
+// ===========================================================================
+// csum_hyb — two lane shapes in one tile, chosen per packet.
+//
+// Nontemporal loads stream at ~6.8 TB/s on MI355X when every 128-B line is
+// consumed by ONE wave instruction (groups of 16 lanes = 256 contiguous bytes
+// per instruction), and lose badly when a line is split across instructions
+// (the evicted line is fetched again).  So a packet of at least `big_chunks`
+// chunks goes to a group of GB = 16 lanes (runs of GB*UB chunks, nt loads),
+// and a smaller one to a single lane (runs of US consecutive chunks, default
+// policy — its lines are shared with neighbouring packets and must stay in L2).
+// One prologue scans both run counts (packed in a u64); two loops follow.
+// ===========================================================================
+template <int WG, int GB, int UB, int US, int AUXB>
+__global__ __launch_bounds__(WG) void csum_hyb(
+    const uint8_t* __restrict__ arena, uint64_t arena_bytes,
+    const uint4* __restrict__ desc, uint32_t n, uint16_t* __restrict__ out,
+    uint32_t* __restrict__ partial, unsigned long long* __restrict__ err, uint32_t big_chunks) {
+  constexpr int P = WG;
+  constexpr int NW = WG / 64;
+  constexpr int NG = WG / GB;
+  constexpr uint32_t RB = GB * UB;
+  static_assert((P & (P - 1)) == 0, "tile must be a power of two");
+  __shared__ uint32_t s_rb[P + 1];   // first big run of each packet
+  __shared__ uint32_t s_rs[P + 1];   // first small run of each packet
+  __shared__ uint32_t s_first[P];
+  __shared__ uint32_t s_nch[P];
+  __shared__ uint32_t s_edge[P];
+  __shared__ uint32_t s_acc[P];
+  __shared__ uint64_t s_wtot[NW];
+
+  const int t = threadIdx.x;
+  const int lane = t & 63;
+  const int wv = t >> 6;
+  const uint32_t li = (uint32_t)(t % GB);
+
+  const uint64_t abase = (uint64_t)(uintptr_t)arena & 15u;
+  const uint64_t sb = (uint64_t)(uintptr_t)arena - abase;
+  const uint32_t nrec = (uint32_t)((abase + arena_bytes + 15) & ~15ull);
+  const uint32_t sb_lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)sb);
+  const uint32_t sb_hi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(sb >> 32));
+  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(((uint64_t)sb_hi << 32) | (uint64_t)sb_lo), (short)0,
+      (int)__builtin_amdgcn_readfirstlane(nrec), 0x00020000);
+  const uint32_t oob = (uint32_t)__builtin_amdgcn_readfirstlane(nrec);
+
+  const uint64_t tile_lo = (uint64_t)blockIdx.x * P;
+  const uint64_t i = tile_lo + t;
+  const uint64_t lim = min<uint64_t>(tile_lo + P, n);
+  uint32_t init = 0, nch = 0, first = 0, ew = 0;
+  uint64_t nr = 0;  // big runs | small runs << 32
+  if (i < lim) {
+    const uint4 raw = desc[i];
+    const uint64_t off = (uint64_t)raw.x | ((uint64_t)raw.y << 32);
+    uint32_t len = raw.z;
+    init = raw.w & 0xFFFFu;
+    const uint32_t odd = (raw.w >> 16) & 1u;
+    if (off > arena_bytes || (uint64_t)len > arena_bytes - off) {
+      len = 0;
+      atomicAdd(err, 1ull);
+    }
+    if (len) {
+      const uint32_t a = (uint32_t)(abase + off);
+      const uint32_t e = a + len;
+      const uint32_t cf = a >> 4, cl = (e - 1) >> 4;
+      nch = cl - cf + 1u;
+      first = cf * 16u;
+      ew = (a & 15u) | ((((e - 1) & 15u) + 1u) << 5) | (((a + odd) & 1u) << 31);
+      // arena < 4 GiB: at most 2^28 chunks per packet, so a tile's big-run
+      // total stays below 2^32; small packets have < big_chunks chunks.
+      nr = nch >= big_chunks ? (uint64_t)((nch + RB - 1) / RB)
+                             : ((uint64_t)((nch + US - 1) / US) << 32);
+    }
+  }
+
+  uint64_t incl = nr;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint64_t y = __shfl_up(incl, d, 64);
+    if (lane >= d) incl += y;
+  }
+  if (lane == 63) s_wtot[wv] = incl;
+  __syncthreads();
+  uint64_t excl = incl - nr;
+#pragma unroll
+  for (int w = 0; w < NW; ++w)
+    if (w < wv) excl += s_wtot[w];
+  s_rb[t] = (uint32_t)excl;
+  s_rs[t] = (uint32_t)(excl >> 32);
+  s_first[t] = first;
+  s_nch[t] = nch;
+  s_edge[t] = ew;
+  s_acc[t] = 0u;
+  if (t == WG - 1) {
+    s_rb[P] = (uint32_t)(excl + nr);
+    s_rs[P] = (uint32_t)((excl + nr) >> 32);
+  }
+  __syncthreads();
+
+  auto search = [&](const uint32_t* s_r, uint32_t q) {
+    int lo = 0;
+#pragma unroll
+    for (int step = P / 2; step >= 1; step >>= 1)
+      lo = (s_r[lo + step] <= q) ? lo + step : lo;
+    return lo;
+  };
+  auto edge_mask = [&](uint4 w, uint32_t ci, uint32_t lastc, uint32_t e) {
+    if (ci == 0u || ci == lastc)
+      w = mask_chunk(w, ci == 0u ? (int)(e & 31u) : 0, ci == lastc ? (int)((e >> 5) & 31u) : 16);
+    return w;
+  };
+
+  // Big packets: groups of GB lanes, lane li takes chunks li + GB*j of a run.
+  const uint32_t RBt = s_rb[P];
+  for (uint32_t q = (uint32_t)(t / GB); q < RBt; q += NG) {
+    const int pk = search(s_rb, q);
+    const uint32_t nc = s_nch[pk];
+    const uint32_t ci0 = (q - s_rb[pk]) * RB + li;
+    const uint32_t base = s_first[pk] + ci0 * 16u;
+    uint4 v[UB];
+#pragma unroll
+    for (int j = 0; j < UB; ++j)
+      v[j] = bload<AUXB>(rsrc, ci0 + (uint32_t)(GB * j) < nc ? base + (uint32_t)(16 * GB * j) : oob);
+    const uint32_t e = s_edge[pk];
+    uint32_t T = 0, W = 0;
+#pragma unroll
+    for (int j = 0; j < UB; ++j) sad_chunk(edge_mask(v[j], ci0 + (uint32_t)(GB * j), nc - 1u, e), T, W);
+    const uint32_t s = group_sum<GB>(s_of(T, W, e >> 31));
+    if (li == 0) atomicAdd(&s_acc[pk], s);
+  }
+
+  // Small packets: one lane per run of US consecutive chunks.
+  const uint32_t RSt = s_rs[P];
+  for (uint32_t q = (uint32_t)t; q < RSt; q += WG) {
+    const int pk = search(s_rs, q);
+    const uint32_t nc = s_nch[pk];
+    const uint32_t ci0 = (q - s_rs[pk]) * US;
+    const uint32_t base = s_first[pk] + ci0 * 16u;
+    uint4 v[US];
+#pragma unroll
+    for (int j = 0; j < US; ++j) v[j] = bload(rsrc, ci0 + (uint32_t)j < nc ? base + 16u * j : oob);
+    const uint32_t e = s_edge[pk];
+    uint32_t T = 0, W = 0;
+#pragma unroll
+    for (int j = 0; j < US; ++j) sad_chunk(edge_mask(v[j], ci0 + (uint32_t)j, nc - 1u, e), T, W);
+    atomicAdd(&s_acc[pk], s_of(T, W, e >> 31));
+  }
+  __syncthreads();
+
+  if (i < lim) {
+    const uint32_t sacc = s_acc[t];
+    if (partial) partial[i] = sacc;
+    else out[i] = (uint16_t)fold1(init + sacc);
+  }
+}
+
 // Sequential chain fix-up for NS_DESC_CONT runs (checksum.go:89 / the
 // `xsum = Checksum(v, xsum)` loops): out[k] = fold1(out[k-1] + S_k).
 __global__ void csum_chain(const uint4* __restrict__ desc, uint32_t n,
@@ -823,6 +1150,29 @@ static hipError_t launch_runs(const uint8_t* arena, uint64_t arena_bytes, const 
   return hipGetLastError();
 }
 
+template <int G, int U, bool PIPE, int AUX = 0>
+static hipError_t launch_grp(const uint8_t* arena, uint64_t arena_bytes, const void* desc,
+                             uint32_t n, uint16_t* out, uint32_t* partial,
+                             unsigned long long* err, hipStream_t stream) {
+  constexpr int WG = 256;
+  const uint32_t grid = (uint32_t)(((uint64_t)n + WG - 1) / WG);
+  hipLaunchKernelGGL((csum_grp<WG, G, U, PIPE, AUX>), dim3(grid), dim3(WG), 0, stream, arena, arena_bytes,
+                     reinterpret_cast<const uint4*>(desc), n, out, partial, err);
+  return hipGetLastError();
+}
+
+template <int GB, int UB, int US, int AUXB>
+static hipError_t launch_hyb(const uint8_t* arena, uint64_t arena_bytes, const void* desc,
+                             uint32_t n, uint16_t* out, uint32_t* partial,
+                             unsigned long long* err, hipStream_t stream, uint32_t big_chunks) {
+  constexpr int WG = 256;
+  const uint32_t grid = (uint32_t)(((uint64_t)n + WG - 1) / WG);
+  hipLaunchKernelGGL((csum_hyb<WG, GB, UB, US, AUXB>), dim3(grid), dim3(WG), 0, stream, arena,
+                     arena_bytes, reinterpret_cast<const uint4*>(desc), n, out, partial, err,
+                     big_chunks);
+  return hipGetLastError();
+}
+
 static hipError_t launch_general(const uint8_t* arena, uint64_t arena_bytes, const void* desc,
                                  uint32_t n, uint16_t* out, uint32_t* partial,
                                  unsigned long long* err, hipStream_t stream) {
@@ -843,9 +1193,11 @@ hipError_t launch_batch(const uint8_t* arena, uint64_t arena_bytes,
     // Arenas of 4 GiB and more: 64-bit addressing, global loads.
     e = launch_general(arena, arena_bytes, desc, n, out, partial, err, stream);
   } else if (arena_bytes / n >= 256) {
-    // Runs of 4 chunks, software-pipelined (tools/tune.py on MI355X: best on
-    // 1500 B and Zipf 64-9000 B batches).
-    e = launch_runs<4, true, false>(arena, arena_bytes, desc, n, out, partial, err, stream);
+    // Packets of >= 64 chunks (~1 KiB) to 16-lane groups with nontemporal
+    // loads, smaller ones to per-lane runs of 4 (tools/tune.py on MI355X:
+    // 240 us on 1M x 1500 B = 82.8% of 8 TB/s, 118 us on the Zipf batch;
+    // profiles/r01/tune_hyb*.json).
+    e = launch_hyb<16, 8, 4, 2>(arena, arena_bytes, desc, n, out, partial, err, stream, 64u);
   } else {
     // Small packets: about one run per lane per tile, so pipelining only
     // costs; a persistent grid with equal shares removes the last-round tail

@@ -102,6 +102,30 @@ __global__ __launch_bounds__(256) void calib_buf(const uint4* __restrict__ p, ui
   if ((threadIdx.x & 63) == 0) atomicAdd(&out[blockIdx.x], acc);
 }
 
+// Lane groups of G over runs of G*U chunks: lane li of a group reads chunks
+// li, li+G, ... (the access shape of csum_grp).
+template <int G, int U, int AUX = 0>
+__global__ __launch_bounds__(256) void calib_grp(const uint4* __restrict__ p, uint64_t n16,
+                                                 uint32_t* __restrict__ out) {
+  uint32_t acc = 0;
+  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, (int)0x7FFFFFF0, 0x00020000);
+  const uint64_t lim = min<uint64_t>(n16, 0x7FFFFFF0ull / 16);
+  const uint64_t step = (uint64_t)gridDim.x * 256 * U;
+  const uint32_t li = threadIdx.x % G;
+  for (uint64_t b = ((uint64_t)blockIdx.x * (256 / G) + threadIdx.x / G) * G * U; b + G * U <= lim; b += step) {
+    uint4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      auto x = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (int)((b + li + G * u) * 16), 0, AUX);
+      v[u] = *reinterpret_cast<uint4*>(&x);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc += v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+  }
+  for (int d = 32; d > 0; d >>= 1) acc += __shfl_xor(acc, d, 64);
+  if ((threadIdx.x & 63) == 0) atomicAdd(&out[blockIdx.x], acc);
+}
+
 template <int D, int UG, int UD, bool NT, int DM = 0, int NB = 3>
 hipError_t launch_v(const uint8_t* arena, uint64_t arena_bytes, const void* desc, uint32_t n,
                     uint16_t* out, unsigned long long* err, hipStream_t s) {
@@ -117,6 +141,18 @@ hipError_t launch_r(const uint8_t* arena, uint64_t arena_bytes, const void* desc
   return launch_runs<U, PIPE, PERSIST>(arena, arena_bytes, desc, n, out, nullptr, err, s);
 }
 
+template <int G, int U, bool PIPE, int AUX = 0>
+hipError_t launch_g(const uint8_t* arena, uint64_t arena_bytes, const void* desc, uint32_t n,
+                    uint16_t* out, unsigned long long* err, hipStream_t s) {
+  return launch_grp<G, U, PIPE, AUX>(arena, arena_bytes, desc, n, out, nullptr, err, s);
+}
+
+template <int GB, int UB, int US, int AUXB, uint32_t BIG>
+hipError_t launch_h(const uint8_t* arena, uint64_t arena_bytes, const void* desc, uint32_t n,
+                    uint16_t* out, unsigned long long* err, hipStream_t s) {
+  return launch_hyb<GB, UB, US, AUXB>(arena, arena_bytes, desc, n, out, nullptr, err, s, BIG);
+}
+
 typedef hipError_t (*launch_fn)(const uint8_t*, uint64_t, const void*, uint32_t, uint16_t*,
                                 unsigned long long*, hipStream_t);
 struct Variant {
@@ -126,6 +162,28 @@ struct Variant {
 static const Variant kVariants[] = {
     {"runs_U4_pipe", launch_r<4, true, false>},       {"runs_U4", launch_r<4, false, false>},
     {"runs_U4_pipe_persist", launch_r<4, true, true>}, {"runs_U4_persist", launch_r<4, false, true>},
+    {"grp_G8_U4_pipe", launch_g<8, 4, true>},           {"grp_G8_U4", launch_g<8, 4, false>},
+    {"grp_G8_U2_pipe", launch_g<8, 2, true>},           {"grp_G16_U2_pipe", launch_g<16, 2, true>},
+    {"grp_G4_U4_pipe", launch_g<4, 4, true>},           {"grp_G4_U2_pipe", launch_g<4, 2, true>},
+    {"grp_G2_U4", launch_g<2, 4, false>},               {"grp_G1_U4", launch_g<1, 4, false>},
+    {"grp_G4_U1", launch_g<4, 1, false>},               {"grp_G16_U4_pipe", launch_g<16, 4, true>},
+    {"grp_G8_U4_nt", launch_g<8, 4, false, 2>},         {"grp_G8_U4_pipe_nt", launch_g<8, 4, true, 2>},
+    {"grp_G8_U8", launch_g<8, 8, false>},               {"grp_G16_U4", launch_g<16, 4, false>},
+    {"grp_G4_U4", launch_g<4, 4, false>},               {"grp_G16_U4_nt", launch_g<16, 4, false, 2>},
+    {"grp_G8_U8_nt", launch_g<8, 8, false, 2>},         {"grp_G4_U8", launch_g<4, 8, false>},
+    {"grp_G16_U8_nt", launch_g<16, 8, false, 2>},       {"grp_G16_U2_nt", launch_g<16, 2, false, 2>},
+    {"grp_G16_U4_pipe_nt", launch_g<16, 4, true, 2>},   {"grp_G16_U8", launch_g<16, 8, false>},
+    {"grp_G4_U8_nt", launch_g<4, 8, false, 2>},         {"grp_G4_U16", launch_g<4, 16, false>},
+    {"grp_G8_U16_nt", launch_g<8, 16, false, 2>},       {"grp_G2_U8", launch_g<2, 8, false>},
+    {"grp_G16_U1_nt", launch_g<16, 1, false, 2>},       {"grp_G16_U2_pipe_nt", launch_g<16, 2, true, 2>},
+    {"grp_G2_U8_nt", launch_g<2, 8, false, 2>},         {"grp_G1_U8", launch_g<1, 8, false>},
+    {"hyb_16x8nt_4_b16", launch_h<16, 8, 4, 2, 16>},     {"hyb_16x8nt_4_b32", launch_h<16, 8, 4, 2, 32>},
+    {"hyb_16x8nt_4_b64", launch_h<16, 8, 4, 2, 64>},     {"hyb_16x4nt_4_b16", launch_h<16, 4, 4, 2, 16>},
+    {"hyb_16x4nt_4_b32", launch_h<16, 4, 4, 2, 32>},     {"hyb_16x8nt_8_b32", launch_h<16, 8, 8, 2, 32>},
+    {"hyb_16x8nt_4_b8", launch_h<16, 8, 4, 2, 8>},       {"hyb_16x8_4_b16", launch_h<16, 8, 4, 0, 16>},
+    {"hyb_16x8nt_4_b96", launch_h<16, 8, 4, 2, 96>},     {"hyb_16x8nt_4_b128", launch_h<16, 8, 4, 2, 128>},
+    {"hyb_16x8nt_4_b192", launch_h<16, 8, 4, 2, 192>},   {"hyb_16x8nt_8_b96", launch_h<16, 8, 8, 2, 96>},
+    {"hyb_16x8nt_8_b128", launch_h<16, 8, 8, 2, 128>},   {"hyb_16x8nt_2_b64", launch_h<16, 8, 2, 2, 64>},
 };
 
 }  // namespace nsk
@@ -166,6 +224,12 @@ int nsk_calib_launch(int mode, const void* p, uint64_t bytes, uint32_t* out, uin
     NSK_CB(200, 2, 0) NSK_CB(201, 2, 1) NSK_CB(202, 2, 2) NSK_CB(203, 2, 3) NSK_CB(216, 2, 16) NSK_CB(218, 2, 18) NSK_CB(219, 2, 19)
     NSK_CB(800, 8, 0) NSK_CB(400, 4, 0) NSK_CB(401, 4, 1) NSK_CB(402, 4, 2) NSK_CB(403, 4, 3) NSK_CB(416, 4, 16) NSK_CB(418, 4, 18) NSK_CB(419, 4, 19)
 #undef NSK_CB
+#define NSK_CG(m, G, U) case m: hipLaunchKernelGGL((nsk::calib_grp<G, U>), dim3(blocks), dim3(256), 0, s, q, n16, out); break;
+    NSK_CG(1084, 8, 4) NSK_CG(1082, 8, 2) NSK_CG(1164, 16, 4) NSK_CG(1162, 16, 2) NSK_CG(1044, 4, 4) NSK_CG(1024, 2, 4)
+#undef NSK_CG
+#define NSK_CG(m, G, U) case m: hipLaunchKernelGGL((nsk::calib_grp<G, U, 2>), dim3(blocks), dim3(256), 0, s, q, n16, out); break;
+    NSK_CG(2084, 8, 4) NSK_CG(2164, 16, 4) NSK_CG(2088, 8, 8)
+#undef NSK_CG
     default: return -1;
   }
   return hipGetLastError() == hipSuccess ? 0 : -5;

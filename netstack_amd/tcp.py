@@ -92,13 +92,46 @@ class PacketDescriptor:
     Size: int = 0
 
 
+@dataclass
+class NetworkHeaderParams:
+    """stack.NetworkHeaderParams (stack/registration.go) plus the IPv4 id
+    counter addIPHeader draws from (ipv4.go:221-225): ``ID`` is the counter's
+    value before this batch; each packet longer than 68 B takes the next id."""
+
+    TTL: int = 64
+    TOS: int = 0
+    ID: int = 0
+
+
+IPV4_MINIMUM_SIZE = 20
+IPV4_MAXIMUM_HEADER_SIZE = 60
+
+
+def _ipv4_header(params: NetworkHeaderParams, length: int, src: bytes, dst: bytes) -> bytearray:
+    """addIPHeader's Encode (network/ipv4/ipv4.go:217-235), checksum left 0."""
+    ident = 0
+    if length > IPV4_MAXIMUM_HEADER_SIZE + 8:
+        params.ID = (params.ID + 1) & 0xFFFFFFFF
+        ident = params.ID
+    b = bytearray(IPV4_MINIMUM_SIZE)
+    struct.pack_into(">BBHHHBBH4s4s", b, 0, 0x45, params.TOS & 0xFF, length & 0xFFFF, ident & 0xFFFF,
+                     0, params.TTL & 0xFF, PROTOCOL_NUMBER, 0, bytes(src), bytes(dst))
+    return b
+
+
 def send_tcp_batch(data: VectorisedView, mss: int, local_addr: bytes, remote_addr: bytes,
                    src_port: int, dst_port: int, flags: int, seq: int, ack: int, rcv_wnd: int,
                    opts: bytes = b"", tx_checksum_offload: bool = False,
-                   gso_needs_csum: bool = False, engine=None) -> list[PacketDescriptor]:
+                   gso_needs_csum: bool = False, ipv4: NetworkHeaderParams | None = None,
+                   engine=None) -> list[PacketDescriptor]:
     """sendTCPBatch + buildTCPHdr (connect.go:634-702) for one GSO payload:
     returns the n PacketDescriptors with fully encoded, checksummed TCP
-    headers.  All n checksums come from one device pass."""
+    headers.  All n checksums come from one device pass.
+
+    With ``ipv4`` set, the IPv4 network endpoint's WritePackets step is fused
+    in (network/ipv4/ipv4.go:271-285 -> addIPHeader :217-238, SURVEY §8(f)
+    rank 3): every Hdr gets its 20-B IPv4 header prepended, and the n IPv4
+    header checksums ride in the same device pass as the n TCP checksums."""
     if rcv_wnd > 0xFFFF:
         rcv_wnd = 0xFFFF
     eng = engine or default_engine()
@@ -124,11 +157,21 @@ def send_tcp_batch(data: VectorisedView, mss: int, local_addr: bytes, remote_add
             chains.append(ch)
         off += psize
         seq = (seq + psize) & 0xFFFFFFFF
+    ntcp = len(chains)
+    ips = []
+    if ipv4 is not None:
+        for d in descs:
+            ip = _ipv4_header(ipv4, IPV4_MINIMUM_SIZE + len(d.Hdr) + d.Size, local_addr, remote_addr)
+            ips.append(ip)
+            chains.append([(bytes(ip), True)])          # ip.CalculateChecksum()
     if chains:
         sums = eng.chains(chains)
-        for d, s in zip(descs, sums):
+        for d, s in zip(descs, sums[:ntcp]):
             v = int(s) if gso_needs_csum else (~int(s)) & 0xFFFF
             struct.pack_into(">H", d.Hdr, TCP_CHECKSUM_OFFSET, v)  # tcp.SetChecksum
+        for d, ip, s in zip(descs, ips, sums[ntcp:]):
+            struct.pack_into(">H", ip, 10, (~int(s)) & 0xFFFF)     # ip.SetChecksum(^...)
+            d.Hdr[0:0] = ip                                        # hdr.Prepend
     return descs
 
 

@@ -156,3 +156,32 @@ def test_chains_api_semantics(engine):
         chains.append([("init", init)] + pieces)
         want.append(x)
     assert engine.chains(chains).tolist() == want
+
+
+def test_send_tcp_batch_fused_ipv4_headers(engine):
+    """WritePackets -> addIPHeader (network/ipv4/ipv4.go:217-238, 271-285)
+    fused into the TX pass: the IPv4 header checksums verify (ipv4_test.go:
+    140-142 style, header sums to 0xffff), ids advance only for packets > 68 B,
+    and the TCP part equals the unfused result."""
+    import oracle as O
+    from netstack_amd import tcp
+    from netstack_amd.buffer import NewVectorisedView, View
+
+    data = bytes(np.random.default_rng(13).integers(0, 256, 20000, dtype=np.uint8))
+    vv = NewVectorisedView(len(data), [View(bytearray(data[:7000])), View(bytearray(data[7000:]))])
+    plain = tcp.send_tcp_batch(vv, 1448, SRC, DST, 5, 6, 0x18, 9, 10, 500)
+    p = tcp.NetworkHeaderParams(TTL=63, TOS=0x10, ID=41)
+    fused = tcp.send_tcp_batch(vv, 1448, SRC, DST, 5, 6, 0x18, 9, 10, 500, ipv4=p)
+    assert p.ID == 41 + len(fused)
+    for k, (a, b) in enumerate(zip(plain, fused)):
+        ip = bytes(b.Hdr[:20])
+        assert b.Hdr[20:] == a.Hdr and (b.Off, b.Size) == (a.Off, a.Size)
+        assert O.c_checksum(ip, 0) == 0xFFFF
+        assert struct.unpack_from(">HH", ip, 2) == (20 + len(a.Hdr) + a.Size, 42 + k)
+        assert ip[8] == 63 and ip[1] == 0x10 and ip[9] == 6 and ip[12:16] == SRC and ip[16:20] == DST
+    # a bare ACK (68 B or less) takes no id
+    p2 = tcp.NetworkHeaderParams(ID=7)
+    one = tcp.send_tcp_batch(NewVectorisedView(1, [View(bytearray(b"x"))]), 1448, SRC, DST, 1, 2, 0x10, 0, 0, 1,
+                             ipv4=p2)
+    assert p2.ID == 7 and struct.unpack_from(">H", one[0].Hdr, 4)[0] == 0
+    assert O.c_checksum(bytes(one[0].Hdr[:20]), 0) == 0xFFFF

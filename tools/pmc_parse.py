@@ -5,8 +5,10 @@ Dispatches of calib_buf / csum_batch are matched in order to the LABEL lines
 of tools/pmc_run.py (REPS each).  HBM bytes per launch follow
 MI355X_MICROARCH.md §HBM: FETCH_SIZE (KiB) is calibrated against a read of a
 known byte count in the same access shape (runs of 8 chunks for cfg2's
-kernel, runs of 4 for cfg3/cfg4) because gfx950 under-reports wide streaming
-reads; the raw values are kept beside the corrected ones.
+kernel's 16-lane nontemporal groups, runs of 4 for per-lane runs; cfg4 mixes
+both, weighted by the payload share of each class) because gfx950
+under-reports wide streaming reads; the raw values are kept beside the
+corrected ones.
 
   python tools/pmc_parse.py OUTDIR LOGFILE > summary.json
 """
@@ -43,7 +45,7 @@ def main():
         k = int(r["Dispatch_Id"])
         disp[k][r["Counter_Name"]] = disp[k].get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
         names[k] = r["Kernel_Name"]
-    ours = [k for k in sorted(disp) if ("calib_buf" in names[k] or "nsk::csum_" in names[k])]
+    ours = [k for k in sorted(disp) if ("calib_" in names[k] or "nsk::csum_" in names[k])]
     out = {}
     for i, (lab, meta) in enumerate(labels):
         ks = ours[i * REPS:(i + 1) * REPS]
@@ -54,13 +56,17 @@ def main():
         out[lab] = {"kernel": names[ks[0]][:80], "meta": meta, "avg": avg}
     # FETCH_SIZE calibration per access shape
     cal = {}
-    for m in ("calib800", "calib400", "calib102"):
+    for m in ("calib800", "calib400", "calib102", "calib2164"):
         if m in out and "FETCH_SIZE" in out[m]["avg"]:
             cal[m] = float(out[m]["meta"]["bytes"]) / (out[m]["avg"]["FETCH_SIZE"] * 1024.0)
-    for lab, shape in (("cfg2", "calib400"), ("cfg3", "calib400"), ("cfg4", "calib400")):
+    for lab in ("cfg2", "cfg3", "cfg4"):
         if lab in out and "FETCH_SIZE" in out[lab]["avg"]:
             raw = out[lab]["avg"]["FETCH_SIZE"] * 1024.0
-            f = cal.get(shape)
+            big = float(out[lab]["meta"].get("big_share", 0.0)) if lab != "cfg3" else 0.0
+            shape = {"calib2164": big, "calib400": 1.0 - big}
+            f = None
+            if all(cal.get(m) for m, w in shape.items() if w > 0):
+                f = sum(w * cal[m] for m, w in shape.items() if w > 0)
             out[lab]["hbm_read_bytes_raw"] = raw
             out[lab]["fetch_calibration"] = {"shape": shape, "factor": f}
             out[lab]["hbm_bytes_per_launch"] = raw * f if f else None

@@ -29,7 +29,8 @@ def main():
     sp = torch.cuda.current_stream(dev).cuda_stream
     buf = torch.ones(CAL_BYTES, dtype=torch.uint8, device=dev)
     outb = torch.zeros(65536, dtype=torch.int32, device=dev)
-    for mode in (800, 400, 102):  # runs of 8 / 4 chunks (buffer, default), coalesced nt
+    # runs of 8 / 4 chunks (buffer, default), coalesced nt, 16-lane groups nt
+    for mode in (800, 400, 102, 2164):
         for _ in range(REPS):
             assert L.nsk_calib_launch(mode, buf.data_ptr(), CAL_BYTES, outb.data_ptr(), 8192, sp) == 0
         torch.cuda.synchronize()
@@ -44,8 +45,10 @@ def main():
         for _ in range(REPS):
             eng.batch_tensors(arena, desc, out)
         torch.cuda.synchronize()
+        # share of payload in packets csum_hyb sends to 16-lane groups (>= 64 chunks)
+        big = float(b.desc["len"][b.desc["len"] >= 1024 - 15].sum()) / max(b.payload_bytes, 1)
         print(f"LABEL cfg{cfg} algorithmic_bytes={b.algorithmic_bytes} payload={b.payload_bytes} "
-              f"arena={b.arena_bytes} n={b.n}", flush=True)
+              f"arena={b.arena_bytes} n={b.n} big_share={big:.4f}", flush=True)
         del arena, desc, out
 
 
