@@ -948,8 +948,15 @@ __global__ __launch_bounds__(WG) void csum_grp(
 // and a smaller one to a single lane (runs of US consecutive chunks, default
 // policy — its lines are shared with neighbouring packets and must stay in L2).
 // One prologue scans both run counts (packed in a u64); two loops follow.
+//
+// UD > 0 adds a direct path for tiles of small packets: when every packet of
+// the tile spans at most UD chunks (a block-wide vote), each lane loads its
+// own packet right after its descriptor — no scan, no search, no LDS atomics.
+// PERSIST sizes the grid to the resident workgroup slots; workgroup w owns
+// descriptors [n*w/G, n*(w+1)/G) in sub-tiles, and the next sub-tile's
+// descriptors are loaded while the current one streams.
 // ===========================================================================
-template <int WG, int GB, int UB, int US, int AUXB>
+template <int WG, int GB, int UB, int US, int AUXB, int UD = 0, bool PERSIST = false>
 __global__ __launch_bounds__(WG) void csum_hyb(
     const uint8_t* __restrict__ arena, uint64_t arena_bytes,
     const uint4* __restrict__ desc, uint32_t n, uint16_t* __restrict__ out,
@@ -982,13 +989,37 @@ __global__ __launch_bounds__(WG) void csum_hyb(
       (int)__builtin_amdgcn_readfirstlane(nrec), 0x00020000);
   const uint32_t oob = (uint32_t)__builtin_amdgcn_readfirstlane(nrec);
 
-  const uint64_t tile_lo = (uint64_t)blockIdx.x * P;
+  auto search = [&](const uint32_t* s_r, uint32_t q) {
+    int lo = 0;
+#pragma unroll
+    for (int step = P / 2; step >= 1; step >>= 1)
+      lo = (s_r[lo + step] <= q) ? lo + step : lo;
+    return lo;
+  };
+  auto edge_mask = [&](uint4 w, uint32_t ci, uint32_t lastc, uint32_t e) {
+    if (ci == 0u || ci == lastc)
+      w = mask_chunk(w, ci == 0u ? (int)(e & 31u) : 0, ci == lastc ? (int)((e >> 5) & 31u) : 16);
+    return w;
+  };
+
+  uint64_t tile_lo, tile_end;
+  if constexpr (PERSIST) {
+    tile_lo = (uint64_t)n * blockIdx.x / gridDim.x;
+    tile_end = (uint64_t)n * (blockIdx.x + 1) / gridDim.x;
+  } else {
+    tile_lo = (uint64_t)blockIdx.x * P;
+    tile_end = min<uint64_t>(tile_lo + P, n);
+  }
+  uint4 raw = make_uint4(0, 0, 0, 0);
+  if (tile_lo + t < tile_end) raw = desc[tile_lo + t];
+
+  if (tile_lo >= tile_end) return;
+  do {
   const uint64_t i = tile_lo + t;
-  const uint64_t lim = min<uint64_t>(tile_lo + P, n);
+  const uint64_t lim = min<uint64_t>(tile_end, tile_lo + P);
+  const bool mine = i < lim;
   uint32_t init = 0, nch = 0, first = 0, ew = 0;
-  uint64_t nr = 0;  // big runs | small runs << 32
-  if (i < lim) {
-    const uint4 raw = desc[i];
+  if (mine) {
     const uint64_t off = (uint64_t)raw.x | ((uint64_t)raw.y << 32);
     uint32_t len = raw.z;
     init = raw.w & 0xFFFFu;
@@ -1004,13 +1035,37 @@ __global__ __launch_bounds__(WG) void csum_hyb(
       nch = cl - cf + 1u;
       first = cf * 16u;
       ew = (a & 15u) | ((((e - 1) & 15u) + 1u) << 5) | (((a + odd) & 1u) << 31);
-      // arena < 4 GiB: at most 2^28 chunks per packet, so a tile's big-run
-      // total stays below 2^32; small packets have < big_chunks chunks.
-      nr = nch >= big_chunks ? (uint64_t)((nch + RB - 1) / RB)
-                             : ((uint64_t)((nch + US - 1) / US) << 32);
+    }
+  }
+  if constexpr (PERSIST) {  // prefetch the next sub-tile's descriptor
+    const uint64_t nx = tile_lo + P + t;
+    raw = nx < tile_end ? desc[nx] : make_uint4(0, 0, 0, 0);
+  }
+
+  if constexpr (UD > 0) {
+    if (__syncthreads_and(nch <= (uint32_t)UD)) {
+      // Direct path: this lane's packet, at most UD chunks.
+      uint4 v[UD];
+#pragma unroll
+      for (int j = 0; j < UD; ++j) v[j] = bload(rsrc, (uint32_t)j < nch ? first + 16u * j : oob);
+      uint32_t T = 0, W = 0;
+#pragma unroll
+      for (int j = 0; j < UD; ++j) sad_chunk(edge_mask(v[j], (uint32_t)j, nch - 1u, ew), T, W);
+      if (mine) {
+        const uint32_t sacc = s_of(T, W, ew >> 31);
+        if (partial) partial[i] = sacc;
+        else out[i] = (uint16_t)fold1(init + sacc);
+      }
+      tile_lo += P;
+      continue;
     }
   }
 
+  // arena < 4 GiB: at most 2^28 chunks per packet, so a tile's big-run total
+  // stays below 2^32; small packets have < big_chunks chunks.
+  const uint64_t nr = nch == 0 ? 0ull
+                      : nch >= big_chunks ? (uint64_t)((nch + RB - 1) / RB)
+                                          : ((uint64_t)((nch + US - 1) / US) << 32);
   uint64_t incl = nr;
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
@@ -1034,19 +1089,6 @@ __global__ __launch_bounds__(WG) void csum_hyb(
     s_rs[P] = (uint32_t)((excl + nr) >> 32);
   }
   __syncthreads();
-
-  auto search = [&](const uint32_t* s_r, uint32_t q) {
-    int lo = 0;
-#pragma unroll
-    for (int step = P / 2; step >= 1; step >>= 1)
-      lo = (s_r[lo + step] <= q) ? lo + step : lo;
-    return lo;
-  };
-  auto edge_mask = [&](uint4 w, uint32_t ci, uint32_t lastc, uint32_t e) {
-    if (ci == 0u || ci == lastc)
-      w = mask_chunk(w, ci == 0u ? (int)(e & 31u) : 0, ci == lastc ? (int)((e >> 5) & 31u) : 16);
-    return w;
-  };
 
   // Big packets: groups of GB lanes, lane li takes chunks li + GB*j of a run.
   const uint32_t RBt = s_rb[P];
@@ -1085,11 +1127,13 @@ __global__ __launch_bounds__(WG) void csum_hyb(
   }
   __syncthreads();
 
-  if (i < lim) {
+  if (mine) {
     const uint32_t sacc = s_acc[t];
     if (partial) partial[i] = sacc;
     else out[i] = (uint16_t)fold1(init + sacc);
   }
+  tile_lo += P;
+  } while (PERSIST && tile_lo < tile_end);  // sub-tiles
 }
 
 // Sequential chain fix-up for NS_DESC_CONT runs (checksum.go:89 / the
@@ -1161,15 +1205,19 @@ static hipError_t launch_grp(const uint8_t* arena, uint64_t arena_bytes, const v
   return hipGetLastError();
 }
 
-template <int GB, int UB, int US, int AUXB>
+template <int GB, int UB, int US, int AUXB, int UD = 0, bool PERSIST = false>
 static hipError_t launch_hyb(const uint8_t* arena, uint64_t arena_bytes, const void* desc,
                              uint32_t n, uint16_t* out, uint32_t* partial,
                              unsigned long long* err, hipStream_t stream, uint32_t big_chunks) {
   constexpr int WG = 256;
-  const uint32_t grid = (uint32_t)(((uint64_t)n + WG - 1) / WG);
-  hipLaunchKernelGGL((csum_hyb<WG, GB, UB, US, AUXB>), dim3(grid), dim3(WG), 0, stream, arena,
-                     arena_bytes, reinterpret_cast<const uint4*>(desc), n, out, partial, err,
-                     big_chunks);
+  const auto kfn = csum_hyb<WG, GB, UB, US, AUXB, UD, PERSIST>;
+  uint32_t grid = (uint32_t)(((uint64_t)n + WG - 1) / WG);
+  if (PERSIST) {
+    const uint32_t slots = resident_slots((const void*)kfn, 1000 + GB * 100 + UB * 10 + US + UD * 7);
+    if (slots) grid = std::min(grid, slots);
+  }
+  hipLaunchKernelGGL(kfn, dim3(grid), dim3(WG), 0, stream, arena, arena_bytes,
+                     reinterpret_cast<const uint4*>(desc), n, out, partial, err, big_chunks);
   return hipGetLastError();
 }
 
@@ -1195,14 +1243,15 @@ hipError_t launch_batch(const uint8_t* arena, uint64_t arena_bytes,
   } else if (arena_bytes / n >= 256) {
     // Packets of >= 64 chunks (~1 KiB) to 16-lane groups with nontemporal
     // loads, smaller ones to per-lane runs of 4 (tools/tune.py on MI355X:
-    // 240 us on 1M x 1500 B = 82.8% of 8 TB/s, 118 us on the Zipf batch;
-    // profiles/r01/tune_hyb*.json).
+    // 239 us on 1M x 1500 B = 83% of 8 TB/s, 118 us on the Zipf batch;
+    // profiles/r01/tune_*.json).
     e = launch_hyb<16, 8, 4, 2>(arena, arena_bytes, desc, n, out, partial, err, stream, 64u);
   } else {
-    // Small packets: about one run per lane per tile, so pipelining only
-    // costs; a persistent grid with equal shares removes the last-round tail
-    // (tools/tune.py: 18.2 vs 19.1 us on 1M x 64 B).
-    e = launch_runs<4, false, true>(arena, arena_bytes, desc, n, out, partial, err, stream);
+    // Small packets: the same kernel plus the direct path — a tile whose
+    // packets all span <= 5 chunks (any <= 65-B packet) has each lane read its
+    // own packet with no scan (16.9 us on 1M x 64 B vs 17.7 for the best
+    // run-based variant).
+    e = launch_hyb<16, 8, 4, 2, 5>(arena, arena_bytes, desc, n, out, partial, err, stream, 64u);
   }
   if (e != hipSuccess || partial == nullptr) return e;
   const uint32_t blocks = (n + 255) / 256;

@@ -147,10 +147,10 @@ hipError_t launch_g(const uint8_t* arena, uint64_t arena_bytes, const void* desc
   return launch_grp<G, U, PIPE, AUX>(arena, arena_bytes, desc, n, out, nullptr, err, s);
 }
 
-template <int GB, int UB, int US, int AUXB, uint32_t BIG>
+template <int GB, int UB, int US, int AUXB, uint32_t BIG, int UD = 0, bool PERSIST = false>
 hipError_t launch_h(const uint8_t* arena, uint64_t arena_bytes, const void* desc, uint32_t n,
                     uint16_t* out, unsigned long long* err, hipStream_t s) {
-  return launch_hyb<GB, UB, US, AUXB>(arena, arena_bytes, desc, n, out, nullptr, err, s, BIG);
+  return launch_hyb<GB, UB, US, AUXB, UD, PERSIST>(arena, arena_bytes, desc, n, out, nullptr, err, s, BIG);
 }
 
 typedef hipError_t (*launch_fn)(const uint8_t*, uint64_t, const void*, uint32_t, uint16_t*,
@@ -184,6 +184,9 @@ static const Variant kVariants[] = {
     {"hyb_16x8nt_4_b96", launch_h<16, 8, 4, 2, 96>},     {"hyb_16x8nt_4_b128", launch_h<16, 8, 4, 2, 128>},
     {"hyb_16x8nt_4_b192", launch_h<16, 8, 4, 2, 192>},   {"hyb_16x8nt_8_b96", launch_h<16, 8, 8, 2, 96>},
     {"hyb_16x8nt_8_b128", launch_h<16, 8, 8, 2, 128>},   {"hyb_16x8nt_2_b64", launch_h<16, 8, 2, 2, 64>},
+    {"hyb_d4", launch_h<16, 8, 4, 2, 64, 4>},             {"hyb_d5", launch_h<16, 8, 4, 2, 64, 5>},
+    {"hyb_d8", launch_h<16, 8, 4, 2, 64, 8>},             {"hyb_d4_persist", launch_h<16, 8, 4, 2, 64, 4, true>},
+    {"hyb_d5_persist", launch_h<16, 8, 4, 2, 64, 5, true>}, {"hyb_persist", launch_h<16, 8, 4, 2, 64, 0, true>},
 };
 
 }  // namespace nsk

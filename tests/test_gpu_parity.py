@@ -148,6 +148,27 @@ def test_unaligned_packed_with_odd_flags(engine):
         assert np.array_equal(dev_batch(engine, arena, d, arena_offset=off), want)
 
 
+@pytest.mark.parametrize("maxlen", [17, 66, 81, 300])
+def test_small_unaligned_packets(engine, maxlen):
+    """Small-packet batches (mean < 256 B/descriptor): tiles where every packet
+    spans <= 5 chunks take the direct path, others the scanned one."""
+    import oracle as O
+    from netstack_amd import workloads as W
+
+    rng = np.random.default_rng(maxlen)
+    n = 40000
+    lengths = rng.integers(0, maxlen, n).astype(np.uint32)
+    init = rng.integers(0, 65536, n).astype(np.uint16)
+    flags = rng.integers(0, 2, n).astype(np.uint16)
+    d, end = W.make_desc(lengths, init, align=1, base=3, flags=flags)
+    arena = W.random_bytes(7 + maxlen, end + 5)
+    want, _ = O.c_batch(arena, d)
+    for off in (0, 9):
+        assert np.array_equal(dev_batch(engine, arena, d, arena_offset=off), want)
+    perm = rng.permutation(n)  # unsorted table, same packets
+    assert np.array_equal(dev_batch(engine, arena, d[perm]), want[perm])
+
+
 def test_random_overlapping_descriptors(engine):
     import oracle as O
 
