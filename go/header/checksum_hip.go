@@ -25,6 +25,7 @@ import "C"
 import (
 	"encoding/binary"
 	"fmt"
+	"runtime"
 	"sync"
 	"unsafe"
 
@@ -67,19 +68,24 @@ func bytePtr(b []byte) *C.uint8_t {
 }
 
 // cViews copies the view headers into C memory (cgo forbids passing Go memory
-// that holds Go pointers); the bytes themselves are borrowed for the call.
+// that holds Go pointers); the bytes themselves are borrowed for the call and
+// pinned while their addresses sit in C memory (runtime.Pinner, Go 1.21+).
 func cViews(views []buffer.View) (*C.ns_view, func()) {
 	n := len(views)
 	if n == 0 {
 		return nil, func() {}
 	}
+	var pin runtime.Pinner
 	p := (*C.ns_view)(C.malloc(C.size_t(n) * C.size_t(unsafe.Sizeof(C.ns_view{}))))
 	arr := (*[1 << 28]C.ns_view)(unsafe.Pointer(p))[:n:n]
 	for i, v := range views {
+		if len(v) > 0 {
+			pin.Pin(&v[0])
+		}
 		arr[i].data = bytePtr(v)
 		arr[i].len = C.uint64_t(len(v))
 	}
-	return p, func() { C.free(unsafe.Pointer(p)) }
+	return p, func() { pin.Unpin(); C.free(unsafe.Pointer(p)) }
 }
 
 // Checksum calculates the checksum (as defined in RFC 1071) of the bytes in the
@@ -165,6 +171,72 @@ func ChecksumViews(views []buffer.View, initial uint16) uint16 {
 	var out C.uint16_t
 	must(C.ns_csum_views_restart(engine(), cv, C.uint32_t(len(views)), C.uint16_t(initial), &out), "ChecksumViews")
 	return uint16(out)
+}
+
+// ChecksumPiece is one buffer of a checksum chain.  Restart = a fresh
+// Checksum(Buf, xsum) call (alignment restarts, checksum.go:52-55); otherwise
+// the piece continues the previous one's byte stream with its odd-byte carry
+// (ChecksumVVWithOffset's view chaining, checksum.go:89).
+type ChecksumPiece struct {
+	Buf     []byte
+	Restart bool
+}
+
+// ChecksumChain is `xsum := Initial; for p := range Pieces { ... }`.
+type ChecksumChain struct {
+	Initial uint16
+	Pieces  []ChecksumPiece
+}
+
+// ChecksumChains evaluates every chain in one device pass (ns_csum_chains);
+// out[i] is chain i's un-complemented sum.  One chain can hold a whole TCP
+// segment checksum — pseudo-header fields, payload views, the TCP header —
+// so sendTCPBatch (connect.go:668-702) and a recvmmsg batch of
+// segment.parse checks (segment.go:174-180) each take one call.
+func ChecksumChains(chains []ChecksumChain, out []uint16) {
+	if len(out) < len(chains) {
+		panic("ChecksumChains: out too short")
+	}
+	if len(chains) == 0 {
+		return
+	}
+	n := 0
+	for _, ch := range chains {
+		if len(ch.Pieces) == 0 {
+			n++
+		}
+		n += len(ch.Pieces)
+	}
+	var pin runtime.Pinner
+	defer pin.Unpin()
+	cp := (*C.ns_piece)(C.malloc(C.size_t(n) * C.size_t(unsafe.Sizeof(C.ns_piece{}))))
+	defer C.free(unsafe.Pointer(cp))
+	arr := (*[1 << 28]C.ns_piece)(unsafe.Pointer(cp))[:n:n]
+	k := 0
+	for _, ch := range chains {
+		pieces := ch.Pieces
+		if len(pieces) == 0 {
+			pieces = []ChecksumPiece{{Restart: true}}
+		}
+		for j, pc := range pieces {
+			if len(pc.Buf) > 0 {
+				pin.Pin(&pc.Buf[0])
+			}
+			arr[k] = C.ns_piece{data: bytePtr(pc.Buf), len: C.uint64_t(len(pc.Buf))}
+			if j == 0 {
+				arr[k].initial = C.uint16_t(ch.Initial)
+			}
+			if pc.Restart {
+				arr[k].flags |= C.NS_PIECE_RESTART
+			}
+			if j == len(pieces)-1 {
+				arr[k].flags |= C.NS_PIECE_END
+			}
+			k++
+		}
+	}
+	must(C.ns_csum_chains(engine(), cp, C.uint32_t(n), (*C.uint16_t)(unsafe.Pointer(&out[0])),
+		C.uint32_t(len(chains))), "ChecksumChains")
 }
 
 var _ = binary.BigEndian // keep the reference file's import set
