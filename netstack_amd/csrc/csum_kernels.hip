@@ -949,6 +949,11 @@ __global__ __launch_bounds__(WG) void csum_grp(
 // policy — its lines are shared with neighbouring packets and must stay in L2).
 // One prologue scans both run counts (packed in a u64); two loops follow.
 //
+// LA: a big packet's body is cut at 128-B line boundaries — chunks [0, h) and
+// [ts, nch) (the partial lines it shares with its neighbours) go to the
+// default-policy lane runs, [h, ts) to the nontemporal groups, so every nt
+// instruction reads whole lines no other packet touches.
+//
 // UD > 0 adds a direct path for tiles of small packets: when every packet of
 // the tile spans at most UD chunks (a block-wide vote), each lane loads its
 // own packet right after its descriptor — no scan, no search, no LDS atomics.
@@ -956,38 +961,153 @@ __global__ __launch_bounds__(WG) void csum_grp(
 // descriptors [n*w/G, n*(w+1)/G) in sub-tiles, and the next sub-tile's
 // descriptors are loaded while the current one streams.
 // ===========================================================================
-template <int WG, int GB, int UB, int US, int AUXB, int UD = 0, bool PERSIST = false>
-__global__ __launch_bounds__(WG) void csum_hyb(
-    const uint8_t* __restrict__ arena, uint64_t arena_bytes,
-    const uint4* __restrict__ desc, uint32_t n, uint16_t* __restrict__ out,
-    uint32_t* __restrict__ partial, unsigned long long* __restrict__ err, uint32_t big_chunks) {
+
+// One descriptor, decoded: the chunks [cf, cf + nch) it covers (first = cf*16,
+// the SRD offset), its edge word (lo | hiex << 5 | phase << 31) and initial.
+struct PktInfo {
+  uint32_t init, nch, first, ew;
+};
+
+__device__ __forceinline__ PktInfo pkt_info(uint4 raw, bool mine, uint64_t abase,
+                                            uint64_t arena_bytes, unsigned long long* err) {
+  PktInfo p{0u, 0u, 0u, 0u};
+  if (!mine) return p;
+  const uint64_t off = (uint64_t)raw.x | ((uint64_t)raw.y << 32);
+  uint32_t len = raw.z;
+  p.init = raw.w & 0xFFFFu;
+  const uint32_t odd = (raw.w >> 16) & 1u;
+  if (off > arena_bytes || (uint64_t)len > arena_bytes - off) {
+    len = 0;
+    atomicAdd(err, 1ull);
+  }
+  if (len) {
+    const uint32_t a = (uint32_t)(abase + off);
+    const uint32_t e = a + len;
+    const uint32_t cf = a >> 4, cl = (e - 1) >> 4;
+    p.nch = cl - cf + 1u;
+    p.first = cf * 16u;
+    p.ew = (a & 15u) | ((((e - 1) & 15u) + 1u) << 5) | (((a + odd) & 1u) << 31);
+  }
+  return p;
+}
+
+__device__ __forceinline__ uint4 edge_mask(uint4 w, uint32_t ci, uint32_t lastc, uint32_t e) {
+  if (ci == 0u || ci == lastc)
+    w = mask_chunk(w, ci == 0u ? (int)(e & 31u) : 0, ci == lastc ? (int)((e >> 5) & 31u) : 16);
+  return w;
+}
+
+__device__ __forceinline__ void put_result(const PktInfo& p, uint32_t sacc, uint64_t i,
+                                           uint16_t* out, uint32_t* partial) {
+  if (partial) partial[i] = sacc;
+  else out[i] = (uint16_t)fold1(p.init + sacc);
+}
+
+template <int P, bool LA>
+struct HybLds {
+  uint32_t rb[P + 1];   // first big run of each packet
+  uint32_t rs[P + 1];   // first small run of each packet
+  uint32_t first[P];
+  uint32_t nch[P];
+  uint32_t edge[P];
+  uint32_t acc[P];
+  uint32_t hts[LA ? P : 1];  // LA: split | h << 1 | ts << 4 (0: not split)
+  uint64_t wtot[P / 64];
+};
+
+struct Srd {
+  __amdgpu_buffer_rsrc_t rsrc;
+  uint32_t oob;    // an offset the range check rejects: the SRD's own size
+  uint32_t sb_lo;  // low word of the 16-B-aligned base (128-B line phase)
+  uint64_t abase;  // arena - base (0..15)
+};
+
+__device__ __forceinline__ Srd make_srd(const uint8_t* arena, uint64_t arena_bytes) {
+  Srd r;
+  r.abase = (uint64_t)(uintptr_t)arena & 15u;
+  const uint64_t sb = (uint64_t)(uintptr_t)arena - r.abase;
+  const uint32_t nrec = (uint32_t)((r.abase + arena_bytes + 15) & ~15ull);
+  // readfirstlane returns int: widen through uint32_t (a sign-extended low
+  // word would corrupt the base's high bits).
+  r.sb_lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)sb);
+  const uint32_t sb_hi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(sb >> 32));
+  r.rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)sb_hi << 32) | (uint64_t)r.sb_lo),
+                                             (short)0, (int)__builtin_amdgcn_readfirstlane(nrec),
+                                             0x00020000);
+  r.oob = (uint32_t)__builtin_amdgcn_readfirstlane(nrec);
+  return r;
+}
+
+// The direct path's per-lane sum of one packet of at most UD chunks.
+template <int UD>
+__device__ __forceinline__ void direct_load(const Srd& r, const PktInfo& p, uint4 (&v)[UD]) {
+#pragma unroll
+  for (int j = 0; j < UD; ++j) v[j] = bload(r.rsrc, (uint32_t)j < p.nch ? p.first + 16u * j : r.oob);
+}
+
+template <int UD>
+__device__ __forceinline__ uint32_t direct_sum(const PktInfo& p, const uint4 (&v)[UD]) {
+  uint32_t T = 0, W = 0;
+#pragma unroll
+  for (int j = 0; j < UD; ++j) sad_chunk(edge_mask(v[j], (uint32_t)j, p.nch - 1u, p.ew), T, W);
+  return s_of(T, W, p.ew >> 31);
+}
+
+// One tile of WG descriptors through the scan path (thread t holds packet p of
+// global index i).  Every thread of the block must call it.
+template <int WG, int GB, int UB, int US, int AUXB, bool LA>
+__device__ __forceinline__ void hyb_scan_tile(HybLds<WG, LA>& L, const Srd& r, const PktInfo& p,
+                                              bool mine, uint64_t i, uint16_t* __restrict__ out,
+                                              uint32_t* __restrict__ partial, uint32_t big_chunks) {
   constexpr int P = WG;
   constexpr int NW = WG / 64;
   constexpr int NG = WG / GB;
   constexpr uint32_t RB = GB * UB;
-  static_assert((P & (P - 1)) == 0, "tile must be a power of two");
-  __shared__ uint32_t s_rb[P + 1];   // first big run of each packet
-  __shared__ uint32_t s_rs[P + 1];   // first small run of each packet
-  __shared__ uint32_t s_first[P];
-  __shared__ uint32_t s_nch[P];
-  __shared__ uint32_t s_edge[P];
-  __shared__ uint32_t s_acc[P];
-  __shared__ uint64_t s_wtot[NW];
-
   const int t = threadIdx.x;
   const int lane = t & 63;
   const int wv = t >> 6;
   const uint32_t li = (uint32_t)(t % GB);
+  const uint32_t nch = p.nch;
 
-  const uint64_t abase = (uint64_t)(uintptr_t)arena & 15u;
-  const uint64_t sb = (uint64_t)(uintptr_t)arena - abase;
-  const uint32_t nrec = (uint32_t)((abase + arena_bytes + 15) & ~15ull);
-  const uint32_t sb_lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)sb);
-  const uint32_t sb_hi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(sb >> 32));
-  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(((uint64_t)sb_hi << 32) | (uint64_t)sb_lo), (short)0,
-      (int)__builtin_amdgcn_readfirstlane(nrec), 0x00020000);
-  const uint32_t oob = (uint32_t)__builtin_amdgcn_readfirstlane(nrec);
+  uint32_t h = nch, ts = nch;
+  if (LA && nch >= big_chunks) {
+    const uint32_t cph = ((r.sb_lo >> 4) + (p.first >> 4)) & 7u;  // chunk slot in its 128-B line
+    h = (8u - cph) & 7u;
+    ts = ((cph + nch) & ~7u) - cph;
+  }
+  // arena < 4 GiB: at most 2^28 chunks per packet, so a tile's big-run total
+  // stays below 2^32; small packets have < big_chunks chunks.
+  const uint64_t nr = nch == 0 ? 0ull
+                      : !LA ? (nch >= big_chunks ? (uint64_t)((nch + RB - 1) / RB)
+                                                 : ((uint64_t)((nch + US - 1) / US) << 32))
+                      : nch >= big_chunks
+                          ? ((uint64_t)((ts - h + RB - 1) / RB) |
+                             ((uint64_t)((h + US - 1) / US + (nch - ts + US - 1) / US) << 32))
+                          : ((uint64_t)((nch + US - 1) / US) << 32);
+  uint64_t incl = nr;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint64_t y = __shfl_up(incl, d, 64);
+    if (lane >= d) incl += y;
+  }
+  if (lane == 63) L.wtot[wv] = incl;
+  __syncthreads();
+  uint64_t excl = incl - nr;
+#pragma unroll
+  for (int w = 0; w < NW; ++w)
+    if (w < wv) excl += L.wtot[w];
+  L.rb[t] = (uint32_t)excl;
+  L.rs[t] = (uint32_t)(excl >> 32);
+  L.first[t] = p.first;
+  L.nch[t] = nch;
+  L.edge[t] = p.ew;
+  if constexpr (LA) L.hts[t] = (nch >= big_chunks) ? (1u | (h << 1) | (ts << 4)) : 0u;
+  L.acc[t] = 0u;
+  if (t == WG - 1) {
+    L.rb[P] = (uint32_t)(excl + nr);
+    L.rs[P] = (uint32_t)((excl + nr) >> 32);
+  }
+  __syncthreads();
 
   auto search = [&](const uint32_t* s_r, uint32_t q) {
     int lo = 0;
@@ -996,11 +1116,72 @@ __global__ __launch_bounds__(WG) void csum_hyb(
       lo = (s_r[lo + step] <= q) ? lo + step : lo;
     return lo;
   };
-  auto edge_mask = [&](uint4 w, uint32_t ci, uint32_t lastc, uint32_t e) {
-    if (ci == 0u || ci == lastc)
-      w = mask_chunk(w, ci == 0u ? (int)(e & 31u) : 0, ci == lastc ? (int)((e >> 5) & 31u) : 16);
-    return w;
-  };
+
+  // Big packets: groups of GB lanes, lane li takes chunks li + GB*j of a run.
+  const uint32_t RBt = L.rb[P];
+  for (uint32_t q = (uint32_t)(t / GB); q < RBt; q += NG) {
+    const int pk = search(L.rb, q);
+    const uint32_t nc = L.nch[pk];
+    uint32_t ci0 = (q - L.rb[pk]) * RB + li, cend = nc;
+    if constexpr (LA) {  // every big packet is split: body [h, ts)
+      const uint32_t hts = L.hts[pk];
+      ci0 += (hts >> 1) & 7u;
+      cend = hts >> 4;
+    }
+    const uint32_t base = L.first[pk] + ci0 * 16u;
+    uint4 v[UB];
+#pragma unroll
+    for (int j = 0; j < UB; ++j)
+      v[j] = bload<AUXB>(r.rsrc, ci0 + (uint32_t)(GB * j) < cend ? base + (uint32_t)(16 * GB * j) : r.oob);
+    const uint32_t e = L.edge[pk];
+    uint32_t T = 0, W = 0;
+#pragma unroll
+    for (int j = 0; j < UB; ++j) sad_chunk(edge_mask(v[j], ci0 + (uint32_t)(GB * j), nc - 1u, e), T, W);
+    const uint32_t sg = group_sum<GB>(s_of(T, W, e >> 31));
+    if (li == 0) atomicAdd(&L.acc[pk], sg);
+  }
+
+  // Small packets (and split packets' edge lines): one lane per run of US
+  // consecutive chunks.
+  const uint32_t RSt = L.rs[P];
+  for (uint32_t q = (uint32_t)t; q < RSt; q += WG) {
+    const int pk = search(L.rs, q);
+    const uint32_t nc = L.nch[pk];
+    uint32_t ci0 = (q - L.rs[pk]) * US, cend = nc;
+    if constexpr (LA) {  // split big packet: head runs cover [0, h), tail runs [ts, nc)
+      const uint32_t hts = L.hts[pk];
+      if (hts & 1u) {
+        const uint32_t hh = (hts >> 1) & 7u, nh = (hh + US - 1) / US;
+        const uint32_t k = q - L.rs[pk];
+        if (k < nh) cend = hh;
+        else ci0 = (hts >> 4) + (k - nh) * US;
+      }
+    }
+    const uint32_t base = L.first[pk] + ci0 * 16u;
+    uint4 v[US];
+#pragma unroll
+    for (int j = 0; j < US; ++j) v[j] = bload(r.rsrc, ci0 + (uint32_t)j < cend ? base + 16u * j : r.oob);
+    const uint32_t e = L.edge[pk];
+    uint32_t T = 0, W = 0;
+#pragma unroll
+    for (int j = 0; j < US; ++j) sad_chunk(edge_mask(v[j], ci0 + (uint32_t)j, nc - 1u, e), T, W);
+    atomicAdd(&L.acc[pk], s_of(T, W, e >> 31));
+  }
+  __syncthreads();
+
+  if (mine) put_result(p, L.acc[t], i, out, partial);
+}
+
+template <int WG, int GB, int UB, int US, int AUXB, int UD = 0, bool PERSIST = false, bool LA = false>
+__global__ __launch_bounds__(WG) void csum_hyb(
+    const uint8_t* __restrict__ arena, uint64_t arena_bytes,
+    const uint4* __restrict__ desc, uint32_t n, uint16_t* __restrict__ out,
+    uint32_t* __restrict__ partial, unsigned long long* __restrict__ err, uint32_t big_chunks) {
+  constexpr int P = WG;
+  static_assert((P & (P - 1)) == 0, "tile must be a power of two");
+  __shared__ HybLds<P, LA> L;
+  const int t = threadIdx.x;
+  const Srd r = make_srd(arena, arena_bytes);
 
   uint64_t tile_lo, tile_end;
   if constexpr (PERSIST) {
@@ -1012,128 +1193,28 @@ __global__ __launch_bounds__(WG) void csum_hyb(
   }
   uint4 raw = make_uint4(0, 0, 0, 0);
   if (tile_lo + t < tile_end) raw = desc[tile_lo + t];
-
   if (tile_lo >= tile_end) return;
   do {
-  const uint64_t i = tile_lo + t;
-  const uint64_t lim = min<uint64_t>(tile_end, tile_lo + P);
-  const bool mine = i < lim;
-  uint32_t init = 0, nch = 0, first = 0, ew = 0;
-  if (mine) {
-    const uint64_t off = (uint64_t)raw.x | ((uint64_t)raw.y << 32);
-    uint32_t len = raw.z;
-    init = raw.w & 0xFFFFu;
-    const uint32_t odd = (raw.w >> 16) & 1u;
-    if (off > arena_bytes || (uint64_t)len > arena_bytes - off) {
-      len = 0;
-      atomicAdd(err, 1ull);
+    const uint64_t i = tile_lo + t;
+    const bool mine = i < min<uint64_t>(tile_end, tile_lo + P);
+    const PktInfo p = pkt_info(raw, mine, r.abase, arena_bytes, err);
+    if constexpr (PERSIST) {  // prefetch the next sub-tile's descriptor
+      const uint64_t nx = tile_lo + P + t;
+      raw = nx < tile_end ? desc[nx] : make_uint4(0, 0, 0, 0);
     }
-    if (len) {
-      const uint32_t a = (uint32_t)(abase + off);
-      const uint32_t e = a + len;
-      const uint32_t cf = a >> 4, cl = (e - 1) >> 4;
-      nch = cl - cf + 1u;
-      first = cf * 16u;
-      ew = (a & 15u) | ((((e - 1) & 15u) + 1u) << 5) | (((a + odd) & 1u) << 31);
-    }
-  }
-  if constexpr (PERSIST) {  // prefetch the next sub-tile's descriptor
-    const uint64_t nx = tile_lo + P + t;
-    raw = nx < tile_end ? desc[nx] : make_uint4(0, 0, 0, 0);
-  }
-
-  if constexpr (UD > 0) {
-    if (__syncthreads_and(nch <= (uint32_t)UD)) {
-      // Direct path: this lane's packet, at most UD chunks.
-      uint4 v[UD];
-#pragma unroll
-      for (int j = 0; j < UD; ++j) v[j] = bload(rsrc, (uint32_t)j < nch ? first + 16u * j : oob);
-      uint32_t T = 0, W = 0;
-#pragma unroll
-      for (int j = 0; j < UD; ++j) sad_chunk(edge_mask(v[j], (uint32_t)j, nch - 1u, ew), T, W);
-      if (mine) {
-        const uint32_t sacc = s_of(T, W, ew >> 31);
-        if (partial) partial[i] = sacc;
-        else out[i] = (uint16_t)fold1(init + sacc);
+    bool done = false;
+    if constexpr (UD > 0) {
+      if (__syncthreads_and(p.nch <= (uint32_t)UD)) {
+        uint4 v[UD];
+        direct_load<UD>(r, p, v);
+        const uint32_t sacc = direct_sum<UD>(p, v);
+        if (mine) put_result(p, sacc, i, out, partial);
+        done = true;
       }
-      tile_lo += P;
-      continue;
     }
-  }
-
-  // arena < 4 GiB: at most 2^28 chunks per packet, so a tile's big-run total
-  // stays below 2^32; small packets have < big_chunks chunks.
-  const uint64_t nr = nch == 0 ? 0ull
-                      : nch >= big_chunks ? (uint64_t)((nch + RB - 1) / RB)
-                                          : ((uint64_t)((nch + US - 1) / US) << 32);
-  uint64_t incl = nr;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint64_t y = __shfl_up(incl, d, 64);
-    if (lane >= d) incl += y;
-  }
-  if (lane == 63) s_wtot[wv] = incl;
-  __syncthreads();
-  uint64_t excl = incl - nr;
-#pragma unroll
-  for (int w = 0; w < NW; ++w)
-    if (w < wv) excl += s_wtot[w];
-  s_rb[t] = (uint32_t)excl;
-  s_rs[t] = (uint32_t)(excl >> 32);
-  s_first[t] = first;
-  s_nch[t] = nch;
-  s_edge[t] = ew;
-  s_acc[t] = 0u;
-  if (t == WG - 1) {
-    s_rb[P] = (uint32_t)(excl + nr);
-    s_rs[P] = (uint32_t)((excl + nr) >> 32);
-  }
-  __syncthreads();
-
-  // Big packets: groups of GB lanes, lane li takes chunks li + GB*j of a run.
-  const uint32_t RBt = s_rb[P];
-  for (uint32_t q = (uint32_t)(t / GB); q < RBt; q += NG) {
-    const int pk = search(s_rb, q);
-    const uint32_t nc = s_nch[pk];
-    const uint32_t ci0 = (q - s_rb[pk]) * RB + li;
-    const uint32_t base = s_first[pk] + ci0 * 16u;
-    uint4 v[UB];
-#pragma unroll
-    for (int j = 0; j < UB; ++j)
-      v[j] = bload<AUXB>(rsrc, ci0 + (uint32_t)(GB * j) < nc ? base + (uint32_t)(16 * GB * j) : oob);
-    const uint32_t e = s_edge[pk];
-    uint32_t T = 0, W = 0;
-#pragma unroll
-    for (int j = 0; j < UB; ++j) sad_chunk(edge_mask(v[j], ci0 + (uint32_t)(GB * j), nc - 1u, e), T, W);
-    const uint32_t s = group_sum<GB>(s_of(T, W, e >> 31));
-    if (li == 0) atomicAdd(&s_acc[pk], s);
-  }
-
-  // Small packets: one lane per run of US consecutive chunks.
-  const uint32_t RSt = s_rs[P];
-  for (uint32_t q = (uint32_t)t; q < RSt; q += WG) {
-    const int pk = search(s_rs, q);
-    const uint32_t nc = s_nch[pk];
-    const uint32_t ci0 = (q - s_rs[pk]) * US;
-    const uint32_t base = s_first[pk] + ci0 * 16u;
-    uint4 v[US];
-#pragma unroll
-    for (int j = 0; j < US; ++j) v[j] = bload(rsrc, ci0 + (uint32_t)j < nc ? base + 16u * j : oob);
-    const uint32_t e = s_edge[pk];
-    uint32_t T = 0, W = 0;
-#pragma unroll
-    for (int j = 0; j < US; ++j) sad_chunk(edge_mask(v[j], ci0 + (uint32_t)j, nc - 1u, e), T, W);
-    atomicAdd(&s_acc[pk], s_of(T, W, e >> 31));
-  }
-  __syncthreads();
-
-  if (mine) {
-    const uint32_t sacc = s_acc[t];
-    if (partial) partial[i] = sacc;
-    else out[i] = (uint16_t)fold1(init + sacc);
-  }
-  tile_lo += P;
-  } while (PERSIST && tile_lo < tile_end);  // sub-tiles
+    if (!done) hyb_scan_tile<WG, GB, UB, US, AUXB, LA>(L, r, p, mine, i, out, partial, big_chunks);
+    tile_lo += P;
+  } while (PERSIST && tile_lo < tile_end);
 }
 
 // Sequential chain fix-up for NS_DESC_CONT runs (checksum.go:89 / the
@@ -1205,12 +1286,12 @@ static hipError_t launch_grp(const uint8_t* arena, uint64_t arena_bytes, const v
   return hipGetLastError();
 }
 
-template <int GB, int UB, int US, int AUXB, int UD = 0, bool PERSIST = false>
+template <int GB, int UB, int US, int AUXB, int UD = 0, bool PERSIST = false, bool LA = false>
 static hipError_t launch_hyb(const uint8_t* arena, uint64_t arena_bytes, const void* desc,
                              uint32_t n, uint16_t* out, uint32_t* partial,
                              unsigned long long* err, hipStream_t stream, uint32_t big_chunks) {
   constexpr int WG = 256;
-  const auto kfn = csum_hyb<WG, GB, UB, US, AUXB, UD, PERSIST>;
+  const auto kfn = csum_hyb<WG, GB, UB, US, AUXB, UD, PERSIST, LA>;
   uint32_t grid = (uint32_t)(((uint64_t)n + WG - 1) / WG);
   if (PERSIST) {
     const uint32_t slots = resident_slots((const void*)kfn, 1000 + GB * 100 + UB * 10 + US + UD * 7);
@@ -1241,17 +1322,18 @@ hipError_t launch_batch(const uint8_t* arena, uint64_t arena_bytes,
     // Arenas of 4 GiB and more: 64-bit addressing, global loads.
     e = launch_general(arena, arena_bytes, desc, n, out, partial, err, stream);
   } else if (arena_bytes / n >= 256) {
-    // Packets of >= 64 chunks (~1 KiB) to 16-lane groups with nontemporal
-    // loads, smaller ones to per-lane runs of 4 (tools/tune.py on MI355X:
-    // 239 us on 1M x 1500 B = 83% of 8 TB/s, 118 us on the Zipf batch;
+    // Packets of >= 64 chunks (~1 KiB): their whole 128-B lines to 16-lane
+    // groups with nontemporal loads, their partial edge lines and all smaller
+    // packets to per-lane runs of 4 (tools/tune.py on MI355X: 233.5 us on
+    // 1M x 1500 B = 85% of 8 TB/s, 112 us on the Zipf batch;
     // profiles/r01/tune_*.json).
-    e = launch_hyb<16, 8, 4, 2>(arena, arena_bytes, desc, n, out, partial, err, stream, 64u);
+    e = launch_hyb<16, 8, 4, 2, 0, false, true>(arena, arena_bytes, desc, n, out, partial, err, stream, 64u);
   } else {
     // Small packets: the same kernel plus the direct path — a tile whose
     // packets all span <= 5 chunks (any <= 65-B packet) has each lane read its
     // own packet with no scan (16.9 us on 1M x 64 B vs 17.7 for the best
     // run-based variant).
-    e = launch_hyb<16, 8, 4, 2, 5>(arena, arena_bytes, desc, n, out, partial, err, stream, 64u);
+    e = launch_hyb<16, 8, 4, 2, 5, false, true>(arena, arena_bytes, desc, n, out, partial, err, stream, 64u);
   }
   if (e != hipSuccess || partial == nullptr) return e;
   const uint32_t blocks = (n + 255) / 256;

@@ -147,10 +147,10 @@ hipError_t launch_g(const uint8_t* arena, uint64_t arena_bytes, const void* desc
   return launch_grp<G, U, PIPE, AUX>(arena, arena_bytes, desc, n, out, nullptr, err, s);
 }
 
-template <int GB, int UB, int US, int AUXB, uint32_t BIG, int UD = 0, bool PERSIST = false>
+template <int GB, int UB, int US, int AUXB, uint32_t BIG, int UD = 0, bool PERSIST = false, bool LA = false>
 hipError_t launch_h(const uint8_t* arena, uint64_t arena_bytes, const void* desc, uint32_t n,
                     uint16_t* out, unsigned long long* err, hipStream_t s) {
-  return launch_hyb<GB, UB, US, AUXB, UD, PERSIST>(arena, arena_bytes, desc, n, out, nullptr, err, s, BIG);
+  return launch_hyb<GB, UB, US, AUXB, UD, PERSIST, LA>(arena, arena_bytes, desc, n, out, nullptr, err, s, BIG);
 }
 
 typedef hipError_t (*launch_fn)(const uint8_t*, uint64_t, const void*, uint32_t, uint16_t*,
@@ -187,6 +187,10 @@ static const Variant kVariants[] = {
     {"hyb_d4", launch_h<16, 8, 4, 2, 64, 4>},             {"hyb_d5", launch_h<16, 8, 4, 2, 64, 5>},
     {"hyb_d8", launch_h<16, 8, 4, 2, 64, 8>},             {"hyb_d4_persist", launch_h<16, 8, 4, 2, 64, 4, true>},
     {"hyb_d5_persist", launch_h<16, 8, 4, 2, 64, 5, true>}, {"hyb_persist", launch_h<16, 8, 4, 2, 64, 0, true>},
+    {"hyb_la", launch_h<16, 8, 4, 2, 64, 0, false, true>}, {"hyb_la_b32", launch_h<16, 8, 4, 2, 32, 0, false, true>},
+    {"hyb_la_u8", launch_h<16, 8, 8, 2, 64, 0, false, true>}, {"hyb_la_b128", launch_h<16, 8, 4, 2, 128, 0, false, true>},
+    {"hyb_d5_la", launch_h<16, 8, 4, 2, 64, 5, false, true>}, {"hyb_la_b48", launch_h<16, 8, 4, 2, 48, 0, false, true>},
+    {"hyb_la_b80", launch_h<16, 8, 4, 2, 80, 0, false, true>},
 };
 
 }  // namespace nsk
