@@ -1322,12 +1322,13 @@ hipError_t launch_batch(const uint8_t* arena, uint64_t arena_bytes,
     // Arenas of 4 GiB and more: 64-bit addressing, global loads.
     e = launch_general(arena, arena_bytes, desc, n, out, partial, err, stream);
   } else if (arena_bytes / n >= 256) {
-    // Packets of >= 64 chunks (~1 KiB): their whole 128-B lines to 16-lane
-    // groups with nontemporal loads, their partial edge lines and all smaller
-    // packets to per-lane runs of 4 (tools/tune.py on MI355X: 233.5 us on
-    // 1M x 1500 B = 85% of 8 TB/s, 112 us on the Zipf batch;
+    // Packets of >= 64 chunks (~1 KiB): their whole 128-B lines to 8-lane
+    // groups (one full line per group per load instruction, 16 loads per lane
+    // in flight) with nontemporal loads; their partial edge lines and all
+    // smaller packets to per-lane runs of 4 (tools/tune.py on MI355X: 227 us
+    // on 1M x 1500 B = 87.6% of 8 TB/s, 110 us on the Zipf batch;
     // profiles/r01/tune_*.json).
-    e = launch_hyb<16, 8, 4, 2, 0, false, true>(arena, arena_bytes, desc, n, out, partial, err, stream, 64u);
+    e = launch_hyb<8, 16, 4, 2, 0, false, true>(arena, arena_bytes, desc, n, out, partial, err, stream, 64u);
   } else {
     // Small packets: the same kernel plus the direct path — a tile whose
     // packets all span <= 5 chunks (any <= 65-B packet) has each lane read its

@@ -191,6 +191,13 @@ static const Variant kVariants[] = {
     {"hyb_la_u8", launch_h<16, 8, 8, 2, 64, 0, false, true>}, {"hyb_la_b128", launch_h<16, 8, 4, 2, 128, 0, false, true>},
     {"hyb_d5_la", launch_h<16, 8, 4, 2, 64, 5, false, true>}, {"hyb_la_b48", launch_h<16, 8, 4, 2, 48, 0, false, true>},
     {"hyb_la_b80", launch_h<16, 8, 4, 2, 80, 0, false, true>},
+    {"la_g8u8_b16", launch_h<8, 8, 4, 2, 16, 0, false, true>},   {"la_g8u8_b24", launch_h<8, 8, 4, 2, 24, 0, false, true>},
+    {"la_g8u8_b32", launch_h<8, 8, 4, 2, 32, 0, false, true>},   {"la_g8u16_b32", launch_h<8, 16, 4, 2, 32, 0, false, true>},
+    {"la_g8u8_b64", launch_h<8, 8, 4, 2, 64, 0, false, true>},   {"la_g16u4_b32", launch_h<16, 4, 4, 2, 32, 0, false, true>},
+    {"la_g8u4_b16", launch_h<8, 4, 4, 2, 16, 0, false, true>},
+    {"la_g8u16_b24", launch_h<8, 16, 4, 2, 24, 0, false, true>}, {"la_g8u16_b48", launch_h<8, 16, 4, 2, 48, 0, false, true>},
+    {"la_g8u16_b64", launch_h<8, 16, 4, 2, 64, 0, false, true>}, {"la_g8u12_b32", launch_h<8, 12, 4, 2, 32, 0, false, true>},
+    {"la_g16u16_b64", launch_h<16, 16, 4, 2, 64, 0, false, true>}, {"la_g8u16_b32_s8", launch_h<8, 16, 8, 2, 32, 0, false, true>},
 };
 
 }  // namespace nsk
