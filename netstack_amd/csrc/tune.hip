@@ -7,6 +7,20 @@
 
 namespace nsk {
 
+template <bool NT>
+__device__ __forceinline__ uint4 load16(const uint4* p) {
+  if constexpr (NT) {
+    uint4 v;
+    v.x = __builtin_nontemporal_load(&p->x);
+    v.y = __builtin_nontemporal_load(&p->y);
+    v.z = __builtin_nontemporal_load(&p->z);
+    v.w = __builtin_nontemporal_load(&p->w);
+    return v;
+  } else {
+    return *p;
+  }
+}
+
 // Pure streaming read of `bytes` (multiple of 16): grid-stride, 4 x 16-B loads
 // in flight per lane per iteration, fully coalesced.  One u32 per block out.
 __global__ __launch_bounds__(256) void calib_read(const uint4* __restrict__ p, uint64_t n16,
@@ -126,31 +140,10 @@ __global__ __launch_bounds__(256) void calib_grp(const uint4* __restrict__ p, ui
   if ((threadIdx.x & 63) == 0) atomicAdd(&out[blockIdx.x], acc);
 }
 
-template <int D, int UG, int UD, bool NT, int DM = 0, int NB = 3>
-hipError_t launch_v(const uint8_t* arena, uint64_t arena_bytes, const void* desc, uint32_t n,
-                    uint16_t* out, unsigned long long* err, hipStream_t s) {
-  const uint32_t tiles = (n + 256 * D - 1) / (256 * D);
-  hipLaunchKernelGGL((csum_batch<256, D, UG, UD, NT, DM, NB>), dim3(tiles), dim3(256), 0, s, arena, arena_bytes,
-                     reinterpret_cast<const uint4*>(desc), n, out, nullptr, err);
-  return hipGetLastError();
-}
-
-template <int U, bool PIPE = true, bool PERSIST = false>
-hipError_t launch_r(const uint8_t* arena, uint64_t arena_bytes, const void* desc, uint32_t n,
-                    uint16_t* out, unsigned long long* err, hipStream_t s) {
-  return launch_runs<U, PIPE, PERSIST>(arena, arena_bytes, desc, n, out, nullptr, err, s);
-}
-
-template <int G, int U, bool PIPE, int AUX = 0>
-hipError_t launch_g(const uint8_t* arena, uint64_t arena_bytes, const void* desc, uint32_t n,
-                    uint16_t* out, unsigned long long* err, hipStream_t s) {
-  return launch_grp<G, U, PIPE, AUX>(arena, arena_bytes, desc, n, out, nullptr, err, s);
-}
-
-template <int GB, int UB, int US, int AUXB, uint32_t BIG, int UD = 0, bool PERSIST = false, bool LA = false>
+template <int GB, int UB, int US, int AUXB, uint32_t BIG, int UD = 0, bool LA = true>
 hipError_t launch_h(const uint8_t* arena, uint64_t arena_bytes, const void* desc, uint32_t n,
                     uint16_t* out, unsigned long long* err, hipStream_t s) {
-  return launch_hyb<GB, UB, US, AUXB, UD, PERSIST, LA>(arena, arena_bytes, desc, n, out, nullptr, err, s, BIG);
+  return launch_hyb<GB, UB, US, AUXB, UD, LA>(arena, arena_bytes, desc, n, out, nullptr, err, s, BIG);
 }
 
 typedef hipError_t (*launch_fn)(const uint8_t*, uint64_t, const void*, uint32_t, uint16_t*,
@@ -159,45 +152,22 @@ struct Variant {
   const char* name;
   launch_fn fn;
 };
+// Earlier kernel families (csum_batch, csum_runs, csum_grp) were measured
+// against these and retired; their numbers are in profiles/r01/tune_*.json
+// and DESIGN.md §4.2.
 static const Variant kVariants[] = {
-    {"runs_U4_pipe", launch_r<4, true, false>},       {"runs_U4", launch_r<4, false, false>},
-    {"runs_U4_pipe_persist", launch_r<4, true, true>}, {"runs_U4_persist", launch_r<4, false, true>},
-    {"grp_G8_U4_pipe", launch_g<8, 4, true>},           {"grp_G8_U4", launch_g<8, 4, false>},
-    {"grp_G8_U2_pipe", launch_g<8, 2, true>},           {"grp_G16_U2_pipe", launch_g<16, 2, true>},
-    {"grp_G4_U4_pipe", launch_g<4, 4, true>},           {"grp_G4_U2_pipe", launch_g<4, 2, true>},
-    {"grp_G2_U4", launch_g<2, 4, false>},               {"grp_G1_U4", launch_g<1, 4, false>},
-    {"grp_G4_U1", launch_g<4, 1, false>},               {"grp_G16_U4_pipe", launch_g<16, 4, true>},
-    {"grp_G8_U4_nt", launch_g<8, 4, false, 2>},         {"grp_G8_U4_pipe_nt", launch_g<8, 4, true, 2>},
-    {"grp_G8_U8", launch_g<8, 8, false>},               {"grp_G16_U4", launch_g<16, 4, false>},
-    {"grp_G4_U4", launch_g<4, 4, false>},               {"grp_G16_U4_nt", launch_g<16, 4, false, 2>},
-    {"grp_G8_U8_nt", launch_g<8, 8, false, 2>},         {"grp_G4_U8", launch_g<4, 8, false>},
-    {"grp_G16_U8_nt", launch_g<16, 8, false, 2>},       {"grp_G16_U2_nt", launch_g<16, 2, false, 2>},
-    {"grp_G16_U4_pipe_nt", launch_g<16, 4, true, 2>},   {"grp_G16_U8", launch_g<16, 8, false>},
-    {"grp_G4_U8_nt", launch_g<4, 8, false, 2>},         {"grp_G4_U16", launch_g<4, 16, false>},
-    {"grp_G8_U16_nt", launch_g<8, 16, false, 2>},       {"grp_G2_U8", launch_g<2, 8, false>},
-    {"grp_G16_U1_nt", launch_g<16, 1, false, 2>},       {"grp_G16_U2_pipe_nt", launch_g<16, 2, true, 2>},
-    {"grp_G2_U8_nt", launch_g<2, 8, false, 2>},         {"grp_G1_U8", launch_g<1, 8, false>},
-    {"hyb_16x8nt_4_b16", launch_h<16, 8, 4, 2, 16>},     {"hyb_16x8nt_4_b32", launch_h<16, 8, 4, 2, 32>},
-    {"hyb_16x8nt_4_b64", launch_h<16, 8, 4, 2, 64>},     {"hyb_16x4nt_4_b16", launch_h<16, 4, 4, 2, 16>},
-    {"hyb_16x4nt_4_b32", launch_h<16, 4, 4, 2, 32>},     {"hyb_16x8nt_8_b32", launch_h<16, 8, 8, 2, 32>},
-    {"hyb_16x8nt_4_b8", launch_h<16, 8, 4, 2, 8>},       {"hyb_16x8_4_b16", launch_h<16, 8, 4, 0, 16>},
-    {"hyb_16x8nt_4_b96", launch_h<16, 8, 4, 2, 96>},     {"hyb_16x8nt_4_b128", launch_h<16, 8, 4, 2, 128>},
-    {"hyb_16x8nt_4_b192", launch_h<16, 8, 4, 2, 192>},   {"hyb_16x8nt_8_b96", launch_h<16, 8, 8, 2, 96>},
-    {"hyb_16x8nt_8_b128", launch_h<16, 8, 8, 2, 128>},   {"hyb_16x8nt_2_b64", launch_h<16, 8, 2, 2, 64>},
-    {"hyb_d4", launch_h<16, 8, 4, 2, 64, 4>},             {"hyb_d5", launch_h<16, 8, 4, 2, 64, 5>},
-    {"hyb_d8", launch_h<16, 8, 4, 2, 64, 8>},             {"hyb_d4_persist", launch_h<16, 8, 4, 2, 64, 4, true>},
-    {"hyb_d5_persist", launch_h<16, 8, 4, 2, 64, 5, true>}, {"hyb_persist", launch_h<16, 8, 4, 2, 64, 0, true>},
-    {"hyb_la", launch_h<16, 8, 4, 2, 64, 0, false, true>}, {"hyb_la_b32", launch_h<16, 8, 4, 2, 32, 0, false, true>},
-    {"hyb_la_u8", launch_h<16, 8, 8, 2, 64, 0, false, true>}, {"hyb_la_b128", launch_h<16, 8, 4, 2, 128, 0, false, true>},
-    {"hyb_d5_la", launch_h<16, 8, 4, 2, 64, 5, false, true>}, {"hyb_la_b48", launch_h<16, 8, 4, 2, 48, 0, false, true>},
-    {"hyb_la_b80", launch_h<16, 8, 4, 2, 80, 0, false, true>},
-    {"la_g8u8_b16", launch_h<8, 8, 4, 2, 16, 0, false, true>},   {"la_g8u8_b24", launch_h<8, 8, 4, 2, 24, 0, false, true>},
-    {"la_g8u8_b32", launch_h<8, 8, 4, 2, 32, 0, false, true>},   {"la_g8u16_b32", launch_h<8, 16, 4, 2, 32, 0, false, true>},
-    {"la_g8u8_b64", launch_h<8, 8, 4, 2, 64, 0, false, true>},   {"la_g16u4_b32", launch_h<16, 4, 4, 2, 32, 0, false, true>},
-    {"la_g8u4_b16", launch_h<8, 4, 4, 2, 16, 0, false, true>},
-    {"la_g8u16_b24", launch_h<8, 16, 4, 2, 24, 0, false, true>}, {"la_g8u16_b48", launch_h<8, 16, 4, 2, 48, 0, false, true>},
-    {"la_g8u16_b64", launch_h<8, 16, 4, 2, 64, 0, false, true>}, {"la_g8u12_b32", launch_h<8, 12, 4, 2, 32, 0, false, true>},
-    {"la_g16u16_b64", launch_h<16, 16, 4, 2, 64, 0, false, true>}, {"la_g8u16_b32_s8", launch_h<8, 16, 8, 2, 32, 0, false, true>},
+    {"prod_g8u16_b64", launch_h<8, 16, 4, 2, 64>},
+    {"prod_small_d5", launch_h<16, 8, 4, 2, 64, 5>},
+    {"g16u8_b64", launch_h<16, 8, 4, 2, 64>},
+    {"g8u8_b64", launch_h<8, 8, 4, 2, 64>},
+    {"g8u12_b32", launch_h<8, 12, 4, 2, 32>},
+    {"g8u16_b32", launch_h<8, 16, 4, 2, 32>},
+    {"g8u16_b48", launch_h<8, 16, 4, 2, 48>},
+    {"g8u16_d5", launch_h<8, 16, 4, 2, 64, 5>},
+    {"g16u8_b64_nola", launch_h<16, 8, 4, 2, 64, 0, false>},
+    {"g16u8_b64_default", launch_h<16, 8, 4, 0, 64>},
+    {"g16u8_d4", launch_h<16, 8, 4, 2, 64, 4>},
+    {"g16u8_d8", launch_h<16, 8, 4, 2, 64, 8>},
 };
 
 }  // namespace nsk
@@ -242,7 +212,8 @@ int nsk_calib_launch(int mode, const void* p, uint64_t bytes, uint32_t* out, uin
     NSK_CG(1084, 8, 4) NSK_CG(1082, 8, 2) NSK_CG(1164, 16, 4) NSK_CG(1162, 16, 2) NSK_CG(1044, 4, 4) NSK_CG(1024, 2, 4)
 #undef NSK_CG
 #define NSK_CG(m, G, U) case m: hipLaunchKernelGGL((nsk::calib_grp<G, U, 2>), dim3(blocks), dim3(256), 0, s, q, n16, out); break;
-    NSK_CG(2084, 8, 4) NSK_CG(2164, 16, 4) NSK_CG(2088, 8, 8)
+    NSK_CG(2084, 8, 4) NSK_CG(2164, 16, 4) NSK_CG(2088, 8, 8) NSK_CG(2816, 8, 16) NSK_CG(2832, 8, 32)
+    NSK_CG(2616, 16, 16) NSK_CG(2824, 8, 24)
 #undef NSK_CG
     default: return -1;
   }

@@ -169,6 +169,45 @@ def test_small_unaligned_packets(engine, maxlen):
     assert np.array_equal(dev_batch(engine, arena, d[perm]), want[perm])
 
 
+@pytest.mark.slow
+def test_arena_over_4gib_windowed_and_scattered(engine):
+    """A 4.5 GiB arena (288 GB HBM makes such batches natural): sorted tiles
+    take a per-tile SRD window anywhere in the arena, tiles whose packets
+    span >= 4 GiB take the 64-bit global-load path."""
+    torch = _torch()
+    import oracle as O
+
+    size = (9 << 29) + 12345                       # ~4.5 GiB, odd size
+    g = torch.Generator(device="cuda").manual_seed(45)
+    arena = torch.randint(0, 256, (size,), dtype=torch.uint8, device="cuda", generator=g)
+    host = arena.cpu().numpy()
+    rng = np.random.default_rng(45)
+    n = 60000
+    d = np.zeros(n, dtype=O.DESC_DTYPE)
+    # (a) sorted, sparse across the whole arena: every tile fits a window
+    d["off"][: n // 2] = np.sort(rng.integers(0, size - 10000, n // 2))
+    # (b) scattered over the whole arena: tiles span > 4 GiB
+    d["off"][n // 2:] = rng.integers(0, size - 10000, n - n // 2)
+    d["len"] = rng.integers(0, 9001, n)
+    d["len"][rng.random(n) < 0.3] %= 70
+    d["initial"] = rng.integers(0, 65536, n)
+    d["flags"] = rng.integers(0, 2, n)
+    want, bad = O.c_batch(host, d)
+    assert bad == 0
+    desc = torch.from_numpy(d.view(np.uint8).copy()).cuda()
+    got = engine.batch_tensors(arena, desc)
+    torch.cuda.synchronize()
+    assert engine.sync() == 0
+    assert np.array_equal(got.cpu().numpy().view(np.uint16), want)
+    # the last packet ends exactly at the arena's end
+    d2 = d[:300].copy()
+    d2["off"][-1], d2["len"][-1] = size - 4099, 4099
+    want2, _ = O.c_batch(host, d2)
+    got2 = engine.batch_tensors(arena, torch.from_numpy(d2.view(np.uint8).copy()).cuda())
+    torch.cuda.synchronize()
+    assert np.array_equal(got2.cpu().numpy().view(np.uint16), want2)
+
+
 def test_random_overlapping_descriptors(engine):
     import oracle as O
 
