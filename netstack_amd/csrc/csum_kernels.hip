@@ -27,6 +27,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
 #include <type_traits>
 
 #include "csum_kernels.h"
@@ -292,7 +293,7 @@ __device__ __forceinline__ uint32_t direct_sum(const Srd& r, const PktInfo& p) {
 // One tile through the scan path (thread t holds packet p of global index i).
 // GL = 64-bit global loads (tile span >= 4 GiB) instead of the window SRD.
 // Every thread of the block must call it.
-template <int WG, int GB, int UB, int US, int AUXB, bool LA, bool GL>
+template <int WG, int TP, int GB, int UB, int US, int AUXB, bool LA, bool GL>
 __device__ __forceinline__ void hyb_scan_tile(HybLds<WG>& L, const Srd& r, const PktInfo& p,
                                               bool mine, uint64_t i, uint16_t* __restrict__ out,
                                               uint32_t* __restrict__ partial, uint32_t big_chunks) {
@@ -350,10 +351,11 @@ __device__ __forceinline__ void hyb_scan_tile(HybLds<WG>& L, const Srd& r, const
   __syncthreads();
 
   auto search = [&](const uint32_t* s_r, uint32_t q) {
-    // Largest pk with s_r[pk] <= q: fixed-step, branch-free (s_r[0] = 0 <= q).
+    // Largest pk < TP with s_r[pk] <= q: fixed-step, branch-free
+    // (s_r[0] = 0 <= q; threads past TP hold no packet and no runs).
     int lo = 0;
 #pragma unroll
-    for (int step = P / 2; step >= 1; step >>= 1)
+    for (int step = TP / 2; step >= 1; step >>= 1)
       lo = (s_r[lo + step] <= q) ? lo + step : lo;
     return lo;
   };
@@ -425,7 +427,9 @@ __device__ __forceinline__ void hyb_scan_tile(HybLds<WG>& L, const Srd& r, const
 // WIN = false (arenas below 4 GiB): one SRD over the whole arena, no window
 // reduction — it costs a block barrier and ~1 us on latency-bound
 // small-packet batches.
-template <int WG, int GB, int UB, int US, int AUXB, int UD = 0, bool LA = true, bool WIN = false>
+// TP = descriptors per tile (<= WG): large packets get fewer per workgroup so
+// a batch of 64 KiB GSO buffers still spreads over every CU.
+template <int WG, int TP, int GB, int UB, int US, int AUXB, int UD = 0, bool LA = true, bool WIN = false>
 __global__ __launch_bounds__(WG) void csum_hyb(
     const uint8_t* __restrict__ arena, uint64_t arena_bytes,
     const uint4* __restrict__ desc, uint32_t n, uint16_t* __restrict__ out,
@@ -433,8 +437,8 @@ __global__ __launch_bounds__(WG) void csum_hyb(
   static_assert((WG & (WG - 1)) == 0, "tile must be a power of two");
   __shared__ HybLds<WG> L;
   const int t = threadIdx.x;
-  const uint64_t i = (uint64_t)blockIdx.x * WG + t;
-  const bool mine = i < n;
+  const uint64_t i = (uint64_t)blockIdx.x * TP + t;
+  const bool mine = t < TP && i < n;
   const uint4 raw = mine ? desc[i] : make_uint4(0, 0, 0, 0);
   const uint64_t arena_abs = (uint64_t)(uintptr_t)arena;
   const Pkt d = decode(raw, mine, arena_abs, arena_bytes, err);
@@ -455,13 +459,13 @@ __global__ __launch_bounds__(WG) void csum_hyb(
       if (mine) put_result(p.init, s, i, out, partial);
       return;
     }
-    hyb_scan_tile<WG, GB, UB, US, AUXB, LA, false>(L, r, p, mine, i, out, partial, big_chunks);
+    hyb_scan_tile<WG, TP, GB, UB, US, AUXB, LA, false>(L, r, p, mine, i, out, partial, big_chunks);
   } else if constexpr (WIN) {
     // The tile spans >= 4 GiB: 64-bit global loads, fewer in flight per lane
     // so this rarely taken path does not raise the kernel's register count.
     const Srd r = make_srd(0ull, 0ull);
     const PktInfo p = pkt_info(d, 0ull);
-    hyb_scan_tile<WG, 16, 4, 4, AUXB, LA, true>(L, r, p, mine, i, out, partial, big_chunks);
+    hyb_scan_tile<WG, TP, 16, 4, 4, AUXB, LA, true>(L, r, p, mine, i, out, partial, big_chunks);
   }
 }
 
@@ -489,22 +493,55 @@ __global__ void csum_chain(const uint4* __restrict__ desc, uint32_t n,
 // ---- launchers (C++ linkage, used by csum_api.cpp) ------------------------
 namespace nsk {
 
-template <int GB, int UB, int US, int AUXB, int UD = 0, bool LA = true>
-static hipError_t launch_hyb(const uint8_t* arena, uint64_t arena_bytes, const void* desc,
-                             uint32_t n, uint16_t* out, uint32_t* partial,
-                             unsigned long long* err, hipStream_t stream, uint32_t big_chunks) {
+template <int TP, int GB, int UB, int US, int AUXB, int UD, bool LA>
+static hipError_t launch_hyb_tp(const uint8_t* arena, uint64_t arena_bytes, const void* desc,
+                                uint32_t n, uint16_t* out, uint32_t* partial,
+                                unsigned long long* err, hipStream_t stream, uint32_t big_chunks) {
   constexpr int WG = 256;
-  const uint32_t grid = (uint32_t)(((uint64_t)n + WG - 1) / WG);
+  const uint32_t grid = (uint32_t)(((uint64_t)n + TP - 1) / TP);
   const uint4* d = reinterpret_cast<const uint4*>(desc);
   // One SRD over the whole arena when it fits (arena base rounded down to 16 B
   // plus the arena), else per-tile windows.
   if (((uintptr_t)arena & 15u) + arena_bytes + 64 < kMaxSrdBytes)
-    hipLaunchKernelGGL((csum_hyb<WG, GB, UB, US, AUXB, UD, LA, false>), dim3(grid), dim3(WG), 0, stream,
-                       arena, arena_bytes, d, n, out, partial, err, big_chunks);
+    hipLaunchKernelGGL((csum_hyb<WG, TP, GB, UB, US, AUXB, UD, LA, false>), dim3(grid), dim3(WG), 0,
+                       stream, arena, arena_bytes, d, n, out, partial, err, big_chunks);
   else
-    hipLaunchKernelGGL((csum_hyb<WG, GB, UB, US, AUXB, UD, LA, true>), dim3(grid), dim3(WG), 0, stream,
-                       arena, arena_bytes, d, n, out, partial, err, big_chunks);
+    hipLaunchKernelGGL((csum_hyb<WG, TP, GB, UB, US, AUXB, UD, LA, true>), dim3(grid), dim3(WG), 0,
+                       stream, arena, arena_bytes, d, n, out, partial, err, big_chunks);
   return hipGetLastError();
+}
+
+// Descriptors per workgroup: the largest power of two <= 128 KiB of payload
+// per workgroup, clamped to [1, 256] (tools/tune.py on MI355X: 1M x 1500 B
+// best at 64 = 223 us vs 229 at 256; the Zipf batch at 128; 16K x 64 KiB
+// at 2-4 = 155 us vs 495 at 256 — profiles/r01/tune_tp*.log).
+template <int GB, int UB, int US, int AUXB, int UD = 0, bool LA = true>
+static hipError_t launch_hyb(const uint8_t* arena, uint64_t arena_bytes, const void* desc,
+                             uint32_t n, uint16_t* out, uint32_t* partial,
+                             unsigned long long* err, hipStream_t stream, uint32_t big_chunks) {
+  const uint64_t avg = std::max<uint64_t>(arena_bytes / n, 1);
+  const uint64_t want = (128u << 10) / avg;
+#define NSK_TP(tp) \
+  if (want >= tp)              \
+  return launch_hyb_tp<tp, GB, UB, US, AUXB, UD, LA>(arena, arena_bytes, desc, n, out, partial, err, stream, big_chunks)
+  if constexpr (UD > 0) {
+    // The small-packet variant (launch_batch: < 256 B per descriptor) keeps
+    // full tiles: its direct path is one packet per lane.
+    return launch_hyb_tp<256, GB, UB, US, AUXB, UD, LA>(arena, arena_bytes, desc, n, out, partial, err,
+                                                        stream, big_chunks);
+  } else {
+    NSK_TP(256);
+    NSK_TP(128);
+    NSK_TP(64);
+    NSK_TP(32);
+    NSK_TP(16);
+    NSK_TP(8);
+    NSK_TP(4);
+    NSK_TP(2);
+    return launch_hyb_tp<1, GB, UB, US, AUXB, UD, LA>(arena, arena_bytes, desc, n, out, partial, err, stream,
+                                                      big_chunks);
+  }
+#undef NSK_TP
 }
 
 hipError_t launch_batch(const uint8_t* arena, uint64_t arena_bytes,

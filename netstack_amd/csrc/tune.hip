@@ -146,6 +146,12 @@ hipError_t launch_h(const uint8_t* arena, uint64_t arena_bytes, const void* desc
   return launch_hyb<GB, UB, US, AUXB, UD, LA>(arena, arena_bytes, desc, n, out, nullptr, err, s, BIG);
 }
 
+template <int TP, int GB, int UB>
+hipError_t launch_tp(const uint8_t* arena, uint64_t arena_bytes, const void* desc, uint32_t n,
+                     uint16_t* out, unsigned long long* err, hipStream_t s) {
+  return launch_hyb_tp<TP, GB, UB, 4, 2, 0, true>(arena, arena_bytes, desc, n, out, nullptr, err, s, 64u);
+}
+
 typedef hipError_t (*launch_fn)(const uint8_t*, uint64_t, const void*, uint32_t, uint16_t*,
                                 unsigned long long*, hipStream_t);
 struct Variant {
@@ -168,6 +174,13 @@ static const Variant kVariants[] = {
     {"g16u8_b64_default", launch_h<16, 8, 4, 0, 64>},
     {"g16u8_d4", launch_h<16, 8, 4, 2, 64, 4>},
     {"g16u8_d8", launch_h<16, 8, 4, 2, 64, 8>},
+    {"g8u16_tp256", launch_tp<256, 8, 16>},
+    {"g8u16_tp128", launch_tp<128, 8, 16>},
+    {"g8u16_tp32", launch_tp<32, 8, 16>},
+    {"g8u16_tp64", launch_tp<64, 8, 16>},
+    {"g8u16_tp16", launch_tp<16, 8, 16>},
+    {"g8u16_tp4", launch_tp<4, 8, 16>},
+    {"g8u16_tp1", launch_tp<1, 8, 16>},
 };
 
 }  // namespace nsk

@@ -159,7 +159,8 @@ def zipf(name: str, seed: int, n: int, align: int = 16) -> Batch:
 
 
 def config(k: int, n: int | None = None) -> Batch:
-    """BASELINE.json configs[k-1] (k = 1..5); `n` overrides the packet count
+    """BASELINE.json configs[k-1] (k = 1..5; 6 = bulk 64 KiB GSO buffers, not
+    a BASELINE config); `n` overrides the packet count
     (for parity-test subsets with the same layout rule)."""
     if k == 1:
         b = uniform("cfg1_64KiB", 1, 1, 65536)
@@ -173,4 +174,8 @@ def config(k: int, n: int | None = None) -> Batch:
         return zipf("cfg4_1Mzipf", 4, n or (1 << 20))
     if k == 5:
         return uniform("cfg5_8Mx1500", 5, n or (8 << 20), 1500)
+    if k == 6:
+        # Not a BASELINE config: 64 KiB GSO payloads (sendTCPBatch's largest
+        # write, connect.go:668-702) in bulk — the large-packet tile sizing case.
+        return uniform("gso_16Kx64KiB", 6, n or (16 << 10), 65536)
     raise ValueError(k)

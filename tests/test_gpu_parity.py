@@ -208,6 +208,23 @@ def test_arena_over_4gib_windowed_and_scattered(engine):
     assert np.array_equal(got2.cpu().numpy().view(np.uint16), want2)
 
 
+@pytest.mark.parametrize("lo,hi,n", [(60000, 70000, 3000), (100000, 400000, 300), (2000, 9000, 20000)])
+def test_large_packet_tiles(engine, lo, hi, n):
+    """Large packets get fewer descriptors per workgroup (launch_hyb's tile
+    sizing): every tile size bit-exact, unaligned starts, odd flags."""
+    import oracle as O
+    from netstack_amd import workloads as W
+
+    rng = np.random.default_rng(lo)
+    lengths = rng.integers(lo, hi, n).astype(np.uint32)
+    init = rng.integers(0, 65536, n).astype(np.uint16)
+    flags = rng.integers(0, 2, n).astype(np.uint16)
+    d, end = W.make_desc(lengths, init, align=1, base=7, flags=flags)
+    arena = W.random_bytes(lo + 1, end + 3)
+    want, _ = O.c_batch(arena, d)
+    assert np.array_equal(dev_batch(engine, arena, d, arena_offset=5), want)
+
+
 def test_random_overlapping_descriptors(engine):
     import oracle as O
 
