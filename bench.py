@@ -158,9 +158,9 @@ def cpu_baseline(batch, seconds: float, threads: int):
 
 # The kernel launch_batch picks for each workload (csum_kernels.hip launch_batch).
 KERNELS = {
-    2: "nsk::csum_hyb<256,8,16,4,2,0,false,true>",
-    3: "nsk::csum_hyb<256,16,8,4,2,5,false,true>",
-    4: "nsk::csum_hyb<256,8,16,4,2,0,false,true>",
+    2: "nsk::csum_hyb<256,64,8,16,4,2,0,true,false>",
+    3: "nsk::csum_hyb<256,256,16,8,4,2,5,true,false>",
+    4: "nsk::csum_hyb<256,128,8,16,4,2,0,true,false>",
 }
 
 
