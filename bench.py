@@ -37,6 +37,8 @@ WORKLOADS = {
     2: "cfg2: 1,048,576 x 1500 B TCP payloads per GPU, 16-B-aligned starts (BASELINE.json configs[1])",
     3: "cfg3: 1,048,576 x 64 B min-size packets per GPU, 4 rotating batches (BASELINE.json configs[2])",
     4: "cfg4: 1,048,576 Zipf(1.1) 64-9000 B packets per GPU (BASELINE.json configs[3])",
+    5: "cfg5: 8,388,608 x 1500 B packets in total, one contiguous shard of 8M/N per GPU "
+       "(BASELINE.json configs[4], strong scaling)",
 }
 
 
@@ -45,7 +47,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", type=int, default=2, choices=(2, 3, 4))
+    ap.add_argument("--config", type=int, default=2, choices=(2, 3, 4, 5))
     ap.add_argument("--mode", default="dev", choices=("dev", "host"))
     ap.add_argument("--rotate", type=int, default=0, help="distinct batches cycled per step (0 = auto)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline time budget")
@@ -118,10 +120,14 @@ def timed_region(step, sync, dist: Dist, steps: int, warmup: int, device=None):
     return dist.max(local, device), local
 
 
-def rank_batch(cfg: int, rank: int):
-    """This rank's batch: the config's layout, a distinct seed per rank."""
+def rank_batch(cfg: int, rank: int, world: int = 1):
+    """This rank's batch.  cfg 2-4 (weak scaling): the config's layout, a
+    distinct seed per rank.  cfg 5 (strong scaling): shard `rank` of `world`
+    contiguous packet ranges of the one 8M x 1500 B batch."""
     from netstack_amd import workloads as W
 
+    if cfg == 5:
+        return W.config(5).shard(rank, world)
     b = W.config(cfg)
     b.seed = b.seed + 1000 * rank
     return b
@@ -132,13 +138,12 @@ def rank_batch(cfg: int, rank: int):
 # ---------------------------------------------------------------------------
 def cpu_baseline(batch, seconds: float, threads: int):
     import oracle as O
-    from netstack_amd import workloads as W
 
     # bounded sample: the first packets of this rank's batch (same bytes)
     n_s = min(batch.n, 65536)
     d = batch.desc[:n_s].copy()
     span = int(d["off"][-1] + d["len"][-1])
-    arena = W.random_bytes(batch.seed, span)
+    arena = batch.host_bytes(0, span)
     payload = int(d["len"].sum())
     out = np.zeros(n_s, dtype=np.uint16)
     O.c_batch_mt(arena, d, threads, out)  # warm
@@ -156,12 +161,38 @@ def cpu_baseline(batch, seconds: float, threads: int):
         (arena, d, out)
 
 
-# The kernel launch_batch picks for each workload (csum_kernels.hip launch_batch).
-KERNELS = {
-    2: "nsk::csum_hyb<256,64,8,16,4,2,0,true,false>",
-    3: "nsk::csum_hyb<256,256,16,8,4,2,5,true,false>",
-    4: "nsk::csum_hyb<256,128,8,16,4,2,0,true,false>",
-}
+def parity_sample(batch, out_dev, k: int = 65536) -> dict:
+    """Bit-exact check of the measured launch's own results: the first and
+    the last k packets of this rank's batch against the oracle (C port of
+    checksum.go) on the same bytes, generated on the host."""
+    import oracle as O
+
+    got = out_dev.cpu().numpy().view(np.uint16)
+    n = batch.n
+    checked, ok = 0, True
+    for a, b in ((0, min(k, n)), (max(min(k, n), n - k), n)):
+        if b <= a:
+            continue
+        d = batch.desc[a:b].copy()
+        lo = (int(d["off"].min()) // 16) * 16
+        hi = int((d["off"] + d["len"].astype(np.uint64)).max())
+        d["off"] -= np.uint64(lo)
+        want, bad = O.c_batch(batch.host_bytes(lo, hi), d)
+        ok = ok and bad == 0 and bool(np.array_equal(got[a:b], want))
+        checked += b - a
+    return {"packets": checked, "bit_exact": ok,
+            "which": "first and last 65536 packets of the timed batch, results of the measured kernel"}
+
+
+def kernel_name(arena_bytes: int, n: int) -> str:
+    """The csum_hyb instance launch_batch picks (csum_kernels.hip
+    launch_batch / launch_hyb / launch_hyb_tp), as rocprofv3 names it."""
+    win = "true" if arena_bytes + 64 >= 0xFFFF0000 else "false"
+    if arena_bytes // n >= 256:
+        want = (128 << 10) // max(arena_bytes // n, 1)
+        tp = next((t for t in (256, 128, 64, 32, 16, 8, 4, 2) if want >= t), 1)
+        return f"nsk::csum_hyb<256,{tp},8,16,4,2,0,true,{win},2,false,0>"
+    return f"nsk::csum_hyb<256,256,16,8,4,2,5,true,{win},1,false,0>"
 
 
 def main():
@@ -178,8 +209,10 @@ def main():
     eng = Engine(dist.local)
 
     cfg = args.config
-    batch = rank_batch(cfg, dist.rank)
+    batch = rank_batch(cfg, dist.rank, dist.world)
     rotate = args.rotate or (4 if cfg == 3 else 1)
+    if cfg == 5 and rotate != 1:
+        raise SystemExit("--rotate applies to cfg 2-4 only")
     if args.mode == "host":
         return host_mode(args, dist, eng, batch, dev)
 
@@ -212,6 +245,13 @@ def main():
     bad = eng.sync()
     kern_avg_s = ev[0].elapsed_time(ev[1]) / 1e3 / args.steps
 
+    # parity of the measured kernel on this rank's batch (one more launch of
+    # the same instance over arenas[0], outside the timed region)
+    eng.batch_tensors(arenas[0], descs[0], out, stream=stream)
+    torch.cuda.synchronize()
+    par = parity_sample(batch, out)
+    par_fail = dist.sum(0.0 if par["bit_exact"] else 1.0, dev)
+
     # parity spot check of the last step's results against the oracle
     payload_rank = batch.payload_bytes
     total_payload = dist.sum(float(payload_rank), dev)
@@ -236,7 +276,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": wall / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if cfg == 5 else "weak",
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic (splitmix64 bytes, random per-packet initial), resident in HBM",
@@ -244,7 +284,7 @@ def main():
             "workload": WORKLOADS[cfg],
             "packets_per_gpu": batch.n,
             "payload_bytes_per_gpu": payload_rank,
-            "global_packets": batch.n * dist.world,
+            "global_packets": int(dist.sum(float(batch.n), dev)),
             "parallelism": f"shard{dist.world} (independent batches, no collective)",
             "rotating_batches": rotate,
         },
@@ -255,27 +295,21 @@ def main():
             "unit": "GB/s",
             "frac": achieved_gbs / HBM_PEAK_GBS,
             "traffic": traffic,
-            "kernel": KERNELS[cfg],
+            "kernel": kernel_name(batch.arena_bytes, batch.n),
             "algorithmic_bytes_per_launch": algo_bytes,
             "avg_launch_us": kern_avg_s * 1e6,
         },
         "bad_descriptors": bad,
+        "parity_sample": dict(par, ranks_failed=int(par_fail)),
     }
 
     if dist.rank == 0 and not args.no_cpu:
-        cb, (arena_s, d_s, out_s) = cpu_baseline(batch, args.cpu_seconds, 1)
+        cb, _ = cpu_baseline(batch, args.cpu_seconds, 1)
         result["cpu_baseline"] = cb
         if args.cpu_threads or True:
             th = args.cpu_threads or min(16, os.cpu_count() or 1)
             cbm, _ = cpu_baseline(batch, max(2.0, args.cpu_seconds / 4), th)
             result["cpu_baseline_multicore"] = cbm
-        # bit-exact spot check: GPU results of the sample packets vs the oracle
-        ns = len(d_s)
-        d0 = torch.from_numpy(d_s.view(np.uint8).copy()).to(dev)
-        chk = eng.batch_tensors(arenas[0], d0)
-        torch.cuda.synchronize()
-        g = chk.cpu().numpy().view(np.uint16)
-        result["parity_sample"] = {"packets": ns, "bit_exact": bool(np.array_equal(g, out_s))}
 
     if dist.rank == 0:
         print(json.dumps(result), flush=True)

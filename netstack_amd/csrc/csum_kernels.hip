@@ -283,7 +283,13 @@ template <int UD>
 __device__ __forceinline__ uint32_t direct_sum(const Srd& r, const PktInfo& p) {
   uint4 v[UD];
 #pragma unroll
-  for (int j = 0; j < UD; ++j) v[j] = bload(r.rsrc, (uint32_t)j < p.nch ? p.first + 16u * j : r.oob);
+  for (int j = 0; j < UD; ++j) {
+    // Chunks past the 4th only when some lane of the wave has them (a 64-B
+    // packet at a 16-B-aligned start spans exactly 4): an out-of-range load
+    // touches no memory but still costs issue and address slots.
+    v[j] = make_uint4(0, 0, 0, 0);
+    if (j < 4 || __any((uint32_t)j < p.nch)) v[j] = bload(r.rsrc, (uint32_t)j < p.nch ? p.first + 16u * j : r.oob);
+  }
   uint32_t T = 0, W = 0;
 #pragma unroll
   for (int j = 0; j < UD; ++j) sad_chunk(edge_mask(v[j], (uint32_t)j, p.nch - 1u, p.ew), T, W);
@@ -293,7 +299,7 @@ __device__ __forceinline__ uint32_t direct_sum(const Srd& r, const PktInfo& p) {
 // One tile through the scan path (thread t holds packet p of global index i).
 // GL = 64-bit global loads (tile span >= 4 GiB) instead of the window SRD.
 // Every thread of the block must call it.
-template <int WG, int TP, int GB, int UB, int US, int AUXB, bool LA, bool GL>
+template <int WG, int TP, int GB, int UB, int US, int AUXB, bool LA, bool GL, int SU = 1, bool PF = false>
 __device__ __forceinline__ void hyb_scan_tile(HybLds<WG>& L, const Srd& r, const PktInfo& p,
                                               bool mine, uint64_t i, uint16_t* __restrict__ out,
                                               uint32_t* __restrict__ partial, uint32_t big_chunks) {
@@ -368,6 +374,54 @@ __device__ __forceinline__ void hyb_scan_tile(HybLds<WG>& L, const Srd& r, const
     }
   };
 
+  // Small packets (and split packets' edge lines): one lane per run of US
+  // consecutive chunks.  A run is issued (search + loads) by small_issue and
+  // consumed by small_sum, so its loads can be in flight while other work
+  // runs: PF issues the lane's first run before the big loop, SU runs are
+  // issued per iteration of the small loop.
+  const uint32_t RSt = L.rs[P];
+  struct SRun {
+    int pk;
+    uint32_t ci0;
+    bool act;
+  };
+  auto small_issue = [&](uint32_t q, uint4 (&v)[US]) -> SRun {
+    SRun s{0, 0u, q < RSt};
+    uint32_t cend = 0u;
+    if (s.act) {
+      s.pk = search(L.rs, q);
+      const uint32_t nc = L.nch[s.pk];
+      s.ci0 = (q - L.rs[s.pk]) * US;
+      cend = nc;
+      if constexpr (LA) {  // split big packet: head runs cover [0, h), tail runs [ts, nc)
+        const uint32_t hts = L.hts[s.pk];
+        if (hts & 1u) {
+          const uint32_t hh = (hts >> 1) & 7u, nh = (hh + US - 1) / US;
+          const uint32_t k = q - L.rs[s.pk];
+          if (k < nh) cend = hh;
+          else s.ci0 = (hts >> 4) + (k - nh) * US;
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < US; ++j)
+      v[j] = load(s.pk, s.ci0 + (uint32_t)j, s.ci0 + (uint32_t)j < cend, std::integral_constant<bool, false>{});
+    return s;
+  };
+  auto small_sum = [&](const SRun& s, const uint4 (&v)[US]) {
+    if (!s.act) return;
+    const uint32_t e = L.edge[s.pk];
+    const uint32_t lastc = L.nch[s.pk] - 1u;
+    uint32_t T = 0, W = 0;
+#pragma unroll
+    for (int j = 0; j < US; ++j) sad_chunk(edge_mask(v[j], s.ci0 + (uint32_t)j, lastc, e), T, W);
+    atomicAdd(&L.acc[s.pk], s_of(T, W, e >> 31));
+  };
+
+  uint4 pv[PF ? US : 1];
+  SRun pr{0, 0u, false};
+  if constexpr (PF) pr = small_issue((uint32_t)t, pv);
+
   // Big packets: groups of GB lanes, lane li takes chunks li + GB*j of a run.
   const uint32_t RBt = L.rb[P];
   for (uint32_t q = (uint32_t)(t / GB); q < RBt; q += NG) {
@@ -393,31 +447,18 @@ __device__ __forceinline__ void hyb_scan_tile(HybLds<WG>& L, const Srd& r, const
     if (li == 0) atomicAdd(&L.acc[pk], sg);
   }
 
-  // Small packets (and split packets' edge lines): one lane per run of US
-  // consecutive chunks.
-  const uint32_t RSt = L.rs[P];
-  for (uint32_t q = (uint32_t)t; q < RSt; q += WG) {
-    const int pk = search(L.rs, q);
-    const uint32_t nc = L.nch[pk];
-    uint32_t ci0 = (q - L.rs[pk]) * US, cend = nc;
-    if constexpr (LA) {  // split big packet: head runs cover [0, h), tail runs [ts, nc)
-      const uint32_t hts = L.hts[pk];
-      if (hts & 1u) {
-        const uint32_t hh = (hts >> 1) & 7u, nh = (hh + US - 1) / US;
-        const uint32_t k = q - L.rs[pk];
-        if (k < nh) cend = hh;
-        else ci0 = (hts >> 4) + (k - nh) * US;
-      }
+  if constexpr (PF) small_sum(pr, pv);
+  for (uint32_t q = (uint32_t)t + (PF ? WG : 0); q < RSt; q += SU * WG) {
+    uint4 va[US];
+    const SRun ra = small_issue(q, va);
+    if constexpr (SU == 2) {
+      uint4 vb[US];
+      const SRun rb = small_issue(q + WG, vb);
+      small_sum(ra, va);
+      small_sum(rb, vb);
+    } else {
+      small_sum(ra, va);
     }
-    uint4 v[US];
-#pragma unroll
-    for (int j = 0; j < US; ++j)
-      v[j] = load(pk, ci0 + (uint32_t)j, ci0 + (uint32_t)j < cend, std::integral_constant<bool, false>{});
-    const uint32_t e = L.edge[pk];
-    uint32_t T = 0, W = 0;
-#pragma unroll
-    for (int j = 0; j < US; ++j) sad_chunk(edge_mask(v[j], ci0 + (uint32_t)j, nc - 1u, e), T, W);
-    atomicAdd(&L.acc[pk], s_of(T, W, e >> 31));
   }
   __syncthreads();
 
@@ -429,8 +470,12 @@ __device__ __forceinline__ void hyb_scan_tile(HybLds<WG>& L, const Srd& r, const
 // small-packet batches.
 // TP = descriptors per tile (<= WG): large packets get fewer per workgroup so
 // a batch of 64 KiB GSO buffers still spreads over every CU.
-template <int WG, int TP, int GB, int UB, int US, int AUXB, int UD = 0, bool LA = true, bool WIN = false>
-__global__ __launch_bounds__(WG) void csum_hyb(
+// SU = small runs issued per lane per iteration, PF = first small run issued
+// before the big loop, OCC = minimum waves per SIMD asked of the register
+// allocator (0: none).
+template <int WG, int TP, int GB, int UB, int US, int AUXB, int UD = 0, bool LA = true, bool WIN = false,
+          int SU = 1, bool PF = false, int OCC = 0>
+__global__ __launch_bounds__(WG, OCC ? OCC : 1) void csum_hyb(
     const uint8_t* __restrict__ arena, uint64_t arena_bytes,
     const uint4* __restrict__ desc, uint32_t n, uint16_t* __restrict__ out,
     uint32_t* __restrict__ partial, unsigned long long* __restrict__ err, uint32_t big_chunks) {
@@ -459,7 +504,7 @@ __global__ __launch_bounds__(WG) void csum_hyb(
       if (mine) put_result(p.init, s, i, out, partial);
       return;
     }
-    hyb_scan_tile<WG, TP, GB, UB, US, AUXB, LA, false>(L, r, p, mine, i, out, partial, big_chunks);
+    hyb_scan_tile<WG, TP, GB, UB, US, AUXB, LA, false, SU, PF>(L, r, p, mine, i, out, partial, big_chunks);
   } else if constexpr (WIN) {
     // The tile spans >= 4 GiB: 64-bit global loads, fewer in flight per lane
     // so this rarely taken path does not raise the kernel's register count.
@@ -493,7 +538,7 @@ __global__ void csum_chain(const uint4* __restrict__ desc, uint32_t n,
 // ---- launchers (C++ linkage, used by csum_api.cpp) ------------------------
 namespace nsk {
 
-template <int TP, int GB, int UB, int US, int AUXB, int UD, bool LA>
+template <int TP, int GB, int UB, int US, int AUXB, int UD, bool LA, int SU = 1, bool PF = false, int OCC = 0>
 static hipError_t launch_hyb_tp(const uint8_t* arena, uint64_t arena_bytes, const void* desc,
                                 uint32_t n, uint16_t* out, uint32_t* partial,
                                 unsigned long long* err, hipStream_t stream, uint32_t big_chunks) {
@@ -503,10 +548,10 @@ static hipError_t launch_hyb_tp(const uint8_t* arena, uint64_t arena_bytes, cons
   // One SRD over the whole arena when it fits (arena base rounded down to 16 B
   // plus the arena), else per-tile windows.
   if (((uintptr_t)arena & 15u) + arena_bytes + 64 < kMaxSrdBytes)
-    hipLaunchKernelGGL((csum_hyb<WG, TP, GB, UB, US, AUXB, UD, LA, false>), dim3(grid), dim3(WG), 0,
+    hipLaunchKernelGGL((csum_hyb<WG, TP, GB, UB, US, AUXB, UD, LA, false, SU, PF, OCC>), dim3(grid), dim3(WG), 0,
                        stream, arena, arena_bytes, d, n, out, partial, err, big_chunks);
   else
-    hipLaunchKernelGGL((csum_hyb<WG, TP, GB, UB, US, AUXB, UD, LA, true>), dim3(grid), dim3(WG), 0,
+    hipLaunchKernelGGL((csum_hyb<WG, TP, GB, UB, US, AUXB, UD, LA, true, SU, PF, OCC>), dim3(grid), dim3(WG), 0,
                        stream, arena, arena_bytes, d, n, out, partial, err, big_chunks);
   return hipGetLastError();
 }
@@ -515,7 +560,7 @@ static hipError_t launch_hyb_tp(const uint8_t* arena, uint64_t arena_bytes, cons
 // per workgroup, clamped to [1, 256] (tools/tune.py on MI355X: 1M x 1500 B
 // best at 64 = 223 us vs 229 at 256; the Zipf batch at 128; 16K x 64 KiB
 // at 2-4 = 155 us vs 495 at 256 — profiles/r01/tune_tp*.log).
-template <int GB, int UB, int US, int AUXB, int UD = 0, bool LA = true>
+template <int GB, int UB, int US, int AUXB, int UD = 0, bool LA = true, int SU = 1, bool PF = false, int OCC = 0>
 static hipError_t launch_hyb(const uint8_t* arena, uint64_t arena_bytes, const void* desc,
                              uint32_t n, uint16_t* out, uint32_t* partial,
                              unsigned long long* err, hipStream_t stream, uint32_t big_chunks) {
@@ -523,11 +568,11 @@ static hipError_t launch_hyb(const uint8_t* arena, uint64_t arena_bytes, const v
   const uint64_t want = (128u << 10) / avg;
 #define NSK_TP(tp) \
   if (want >= tp)              \
-  return launch_hyb_tp<tp, GB, UB, US, AUXB, UD, LA>(arena, arena_bytes, desc, n, out, partial, err, stream, big_chunks)
+  return launch_hyb_tp<tp, GB, UB, US, AUXB, UD, LA, SU, PF, OCC>(arena, arena_bytes, desc, n, out, partial, err, stream, big_chunks)
   if constexpr (UD > 0) {
     // The small-packet variant (launch_batch: < 256 B per descriptor) keeps
     // full tiles: its direct path is one packet per lane.
-    return launch_hyb_tp<256, GB, UB, US, AUXB, UD, LA>(arena, arena_bytes, desc, n, out, partial, err,
+    return launch_hyb_tp<256, GB, UB, US, AUXB, UD, LA, SU, PF, OCC>(arena, arena_bytes, desc, n, out, partial, err,
                                                         stream, big_chunks);
   } else {
     NSK_TP(256);
@@ -538,7 +583,7 @@ static hipError_t launch_hyb(const uint8_t* arena, uint64_t arena_bytes, const v
     NSK_TP(8);
     NSK_TP(4);
     NSK_TP(2);
-    return launch_hyb_tp<1, GB, UB, US, AUXB, UD, LA>(arena, arena_bytes, desc, n, out, partial, err, stream,
+    return launch_hyb_tp<1, GB, UB, US, AUXB, UD, LA, SU, PF, OCC>(arena, arena_bytes, desc, n, out, partial, err, stream,
                                                       big_chunks);
   }
 #undef NSK_TP
@@ -554,10 +599,10 @@ hipError_t launch_batch(const uint8_t* arena, uint64_t arena_bytes,
     // Packets of >= 64 chunks (~1 KiB): their whole 128-B lines to 8-lane
     // groups (one full line per group per load instruction, 16 loads per lane
     // in flight) with nontemporal loads; their partial edge lines and all
-    // smaller packets to per-lane runs of 4 (tools/tune.py on MI355X: 227 us
-    // on 1M x 1500 B = 87.6% of 8 TB/s, 110 us on the Zipf batch;
-    // profiles/r01/tune_*.json).
-    e = launch_hyb<8, 16, 4, 2, 0>(arena, arena_bytes, desc, n, out, partial, err, stream, 64u);
+    // smaller packets to per-lane runs of 4, two runs issued per lane per
+    // iteration (tools/tune.py on MI355X: 220.6 us on 1M x 1500 B = 90.2% of
+    // 8 TB/s, 107 us on the Zipf batch; profiles/r01/tune_*.json).
+    e = launch_hyb<8, 16, 4, 2, 0, true, 2>(arena, arena_bytes, desc, n, out, partial, err, stream, 64u);
   } else {
     // Small packets: the same kernel plus the direct path — a tile whose
     // packets all span <= 5 chunks (any <= 65-B packet) has each lane read its

@@ -140,10 +140,87 @@ __global__ __launch_bounds__(256) void calib_grp(const uint4* __restrict__ p, ui
   if ((threadIdx.x & 63) == 0) atomicAdd(&out[blockIdx.x], acc);
 }
 
-template <int GB, int UB, int US, int AUXB, uint32_t BIG, int UD = 0, bool LA = true>
+template <int GB, int UB, int US, int AUXB, uint32_t BIG, int UD = 0, bool LA = true, int SU = 1, bool PF = false,
+          int OCC = 0>
 hipError_t launch_h(const uint8_t* arena, uint64_t arena_bytes, const void* desc, uint32_t n,
                     uint16_t* out, unsigned long long* err, hipStream_t s) {
-  return launch_hyb<GB, UB, US, AUXB, UD, LA>(arena, arena_bytes, desc, n, out, nullptr, err, s, BIG);
+  return launch_hyb<GB, UB, US, AUXB, UD, LA, SU, PF, OCC>(arena, arena_bytes, desc, n, out, nullptr, err, s, BIG);
+}
+
+// Floor for the 1M x 64 B layout only (desc[i].off == 64 * i): the same
+// descriptor and payload bytes as the direct path, but the payload loads do
+// not wait for the descriptor.  Not a checksum kernel for any other layout.
+__global__ __launch_bounds__(256) void small_floor(const uint8_t* __restrict__ arena, uint64_t arena_bytes,
+                                                   const uint4* __restrict__ desc, uint32_t n,
+                                                   uint16_t* __restrict__ out) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)arena, (short)0, (int)0x7FFFFFF0, 0x00020000);
+  uint4 v[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) v[j] = bload(rsrc, (uint32_t)(i * 64 + 16 * j));
+  const uint4 raw = desc[i];
+  uint32_t T = 0, W = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) sad_chunk(v[j], T, W);
+  out[i] = (uint16_t)fold1((raw.w & 0xFFFFu) + s_of(T, W, (raw.w >> 16) & 1u));
+}
+
+// Quad-lane direct path (experiment; correct only when every packet spans
+// <= 4 chunks): lane l of a wave handles chunk (l & 3) of packet 16j + l/4 in
+// step j, so one load instruction reads 16 whole packets (1 KiB, coalesced
+// when packets are dense) instead of 64 lanes each reading one 16-B chunk of
+// its own packet.  Quad DPP sum, lane (l & 3) == 0 writes.
+__global__ __launch_bounds__(256) void quad_d4(const uint8_t* __restrict__ arena, uint64_t arena_bytes,
+                                               const uint4* __restrict__ desc, uint32_t n,
+                                               uint16_t* __restrict__ out) {
+  const uint32_t l = threadIdx.x & 63;
+  const uint64_t wbase = ((uint64_t)blockIdx.x * 256 + (threadIdx.x & ~63u));
+  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)arena, (short)0, (int)0x7FFFFFF0, 0x00020000);
+  uint4 raw[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const uint64_t pk = wbase + 16 * j + (l >> 2);
+    raw[j] = pk < n ? desc[pk] : make_uint4(0, 0, 0, 0);
+  }
+  uint4 v[4];
+  uint32_t ph[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const uint64_t off = (uint64_t)raw[j].x | ((uint64_t)raw[j].y << 32);
+    const uint64_t A = (uint64_t)(uintptr_t)arena + off;
+    const uint32_t len = raw[j].z;
+    const uint32_t nch = len ? (uint32_t)(((A + len - 1) >> 4) - (A >> 4) + 1) : 0u;
+    const uint32_t c = l & 3;
+    const uint32_t first = (uint32_t)((A & ~15ull) - (uint64_t)(uintptr_t)arena);
+    v[j] = bload(rsrc, c < nch ? first + 16u * c : 0x7FFFFFF0u);
+    const uint32_t lastc = nch - 1u;
+    const uint32_t lo = (uint32_t)(A & 15u), hi = (uint32_t)(((A + len - 1) & 15u) + 1u);
+    if (c == 0 || c == lastc) v[j] = mask_chunk(v[j], c == 0 ? (int)lo : 0, c == lastc ? (int)hi : 16);
+    ph[j] = (uint32_t)((A + ((raw[j].w >> 16) & 1u)) & 1u);
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    uint32_t T = 0, W = 0;
+    sad_chunk(v[j], T, W);
+    const uint32_t sq = group_sum<4>(s_of(T, W, ph[j]));
+    const uint64_t pk = wbase + 16 * j + (l >> 2);
+    if ((l & 3) == 0 && pk < n) out[pk] = (uint16_t)fold1((raw[j].w & 0xFFFFu) + sq);
+  }
+}
+
+hipError_t launch_quad(const uint8_t* arena, uint64_t arena_bytes, const void* desc, uint32_t n,
+                       uint16_t* out, unsigned long long* err, hipStream_t s) {
+  hipLaunchKernelGGL(quad_d4, dim3((n + 255) / 256), dim3(256), 0, s, arena, arena_bytes,
+                     reinterpret_cast<const uint4*>(desc), n, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_floor(const uint8_t* arena, uint64_t arena_bytes, const void* desc, uint32_t n,
+                        uint16_t* out, unsigned long long* err, hipStream_t s) {
+  hipLaunchKernelGGL(small_floor, dim3((n + 255) / 256), dim3(256), 0, s, arena, arena_bytes,
+                     reinterpret_cast<const uint4*>(desc), n, out);
+  return hipGetLastError();
 }
 
 template <int TP, int GB, int UB>
@@ -162,25 +239,19 @@ struct Variant {
 // against these and retired; their numbers are in profiles/r01/tune_*.json
 // and DESIGN.md §4.2.
 static const Variant kVariants[] = {
-    {"prod_g8u16_b64", launch_h<8, 16, 4, 2, 64>},
+    {"prod_g8u16_b64", launch_h<8, 16, 4, 2, 64, 0, true, 2>},
+    {"g8u16_su1", launch_h<8, 16, 4, 2, 64>},
     {"prod_small_d5", launch_h<16, 8, 4, 2, 64, 5>},
-    {"g16u8_b64", launch_h<16, 8, 4, 2, 64>},
-    {"g8u8_b64", launch_h<8, 8, 4, 2, 64>},
-    {"g8u12_b32", launch_h<8, 12, 4, 2, 32>},
-    {"g8u16_b32", launch_h<8, 16, 4, 2, 32>},
-    {"g8u16_b48", launch_h<8, 16, 4, 2, 48>},
-    {"g8u16_d5", launch_h<8, 16, 4, 2, 64, 5>},
-    {"g16u8_b64_nola", launch_h<16, 8, 4, 2, 64, 0, false>},
-    {"g16u8_b64_default", launch_h<16, 8, 4, 0, 64>},
-    {"g16u8_d4", launch_h<16, 8, 4, 2, 64, 4>},
-    {"g16u8_d8", launch_h<16, 8, 4, 2, 64, 8>},
-    {"g8u16_tp256", launch_tp<256, 8, 16>},
-    {"g8u16_tp128", launch_tp<128, 8, 16>},
-    {"g8u16_tp32", launch_tp<32, 8, 16>},
-    {"g8u16_tp64", launch_tp<64, 8, 16>},
-    {"g8u16_tp16", launch_tp<16, 8, 16>},
-    {"g8u16_tp4", launch_tp<4, 8, 16>},
-    {"g8u16_tp1", launch_tp<1, 8, 16>},
+    {"g8u16_pf", launch_h<8, 16, 4, 2, 64, 0, true, 1, true>},
+    {"g8u16_pf_su2", launch_h<8, 16, 4, 2, 64, 0, true, 2, true>},
+    {"g8u16_b32_pf", launch_h<8, 16, 4, 2, 32, 0, true, 1, true>},
+    {"small_d5_occ8", launch_h<16, 8, 4, 2, 64, 5, true, 1, false, 8>},
+    {"small_d5_pf", launch_h<16, 8, 4, 2, 64, 5, true, 1, true>},
+    {"floor_64B", launch_floor},
+    {"quad_d4", launch_quad},
+    {"g8u16_occ5", launch_h<8, 16, 4, 2, 64, 0, true, 1, false, 5>},
+    {"g8u12_occ5", launch_h<8, 12, 4, 2, 64, 0, true, 1, false, 5>},
+    {"g8u16_su2_occ5", launch_h<8, 16, 4, 2, 64, 0, true, 2, false, 5>},
 };
 
 }  // namespace nsk

@@ -41,14 +41,15 @@ def splitmix64(seed: int, n: int, start: int = 0) -> np.ndarray:
     return z
 
 
-def random_bytes(seed: int, nbytes: int, chunk: int = 1 << 24) -> np.ndarray:
-    """nbytes of splitmix64 output (host), generated in chunks of `chunk` words."""
+def random_bytes(seed: int, nbytes: int, chunk: int = 1 << 24, start_word: int = 0) -> np.ndarray:
+    """nbytes of splitmix64 output (host) from word `start_word` on, generated
+    in chunks of `chunk` words."""
     words = (nbytes + 7) // 8
     out = np.empty(words * 8, dtype=np.uint8)
     o64 = out.view(np.uint64)
     for s in range(0, words, chunk):
         e = min(words, s + chunk)
-        o64[s:e] = splitmix64(seed, e - s, s)
+        o64[s:e] = splitmix64(seed, e - s, start_word + s)
     return out[:nbytes]
 
 
@@ -57,7 +58,7 @@ def _s64(x: int) -> int:
     return x - (1 << 64) if x >> 63 else x
 
 
-def random_bytes_torch(seed: int, nbytes: int, device, chunk: int = 1 << 26):
+def random_bytes_torch(seed: int, nbytes: int, device, chunk: int = 1 << 26, start_word: int = 0):
     """Same bytes as random_bytes(), generated in HBM with torch int64 ops
     (two's-complement wrap; logical shifts emulated with masks)."""
     import torch
@@ -72,7 +73,7 @@ def random_bytes_torch(seed: int, nbytes: int, device, chunk: int = 1 << 26):
 
     for s in range(0, words, chunk):
         e = min(words, s + chunk)
-        z = torch.arange(s + 1, e + 1, dtype=torch.int64, device=device)
+        z = torch.arange(start_word + s + 1, start_word + e + 1, dtype=torch.int64, device=device)
         z = z * g + sd
         z = (z ^ lsr(z, 30)) * m1
         z = (z ^ lsr(z, 27)) * m2
@@ -100,6 +101,7 @@ class Batch:
     seed: int
     desc: np.ndarray  # DESC_DTYPE
     arena_bytes: int
+    base: int = 0  # byte offset of this arena in the seed's byte stream (multiple of 8)
 
     @property
     def n(self) -> int:
@@ -116,10 +118,32 @@ class Batch:
         return self.payload_bytes + 18 * self.n
 
     def arena_host(self) -> np.ndarray:
-        return random_bytes(self.seed, self.arena_bytes)
+        return random_bytes(self.seed, self.arena_bytes, start_word=self.base // 8)
 
     def arena_device(self, device):
-        return random_bytes_torch(self.seed, self.arena_bytes, device)
+        return random_bytes_torch(self.seed, self.arena_bytes, device, start_word=self.base // 8)
+
+    def host_bytes(self, lo: int, hi: int) -> np.ndarray:
+        """Arena bytes [lo, hi) on the host, without generating the rest."""
+        w0 = (self.base + lo) // 8
+        skip = (self.base + lo) - 8 * w0
+        return random_bytes(self.seed, hi - lo + skip, start_word=w0)[skip:]
+
+    def shard(self, part: int, parts: int) -> "Batch":
+        """Packets [part*n/parts, (part+1)*n/parts) as a batch of their own
+        (contiguous packet ranges, offsets rebased, no
+        collective).  The shard's arena is the same bytes as the whole
+        batch's arena over its range, so results equal the unsharded ones."""
+        n = self.n
+        a, b = part * n // parts, (part + 1) * n // parts
+        d = self.desc[a:b].copy()
+        if len(d) == 0:
+            return Batch(f"{self.name}_s{part}of{parts}", self.seed, d, 0, self.base)
+        lo = (int(d["off"][0]) // 16) * 16
+        hi = int((d["off"] + d["len"].astype(np.uint64)).max())
+        d["off"] -= np.uint64(lo)
+        return Batch(f"{self.name}_s{part}of{parts}", self.seed, d, ((hi - lo + 15) // 16) * 16,
+                     self.base + lo)
 
 
 def make_desc(lengths: np.ndarray, initial: np.ndarray, align: int = 16, base: int = 0,

@@ -84,3 +84,40 @@ def test_two_rank_gloo_sharded_bench_plumbing():
     # byte balance of the plan
     sizes = [int(b.desc["len"][r[1]:r[2]].sum()) for r in res]
     assert abs(sizes[0] - sizes[1]) <= 9000
+
+
+def test_cfg5_strong_scaling_shards_reproduce_the_whole_batch():
+    """bench.py --config 5: each of N ranks takes one contiguous shard of the
+    8M x 1500 B batch (here 4096 packets) with rebased offsets; the shards'
+    results concatenate to the unsharded ones, and bench.parity_sample passes
+    on correct results and catches a single wrong one."""
+    import torch
+
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import bench
+    import oracle as O
+    from netstack_amd import workloads as W
+
+    whole = W.config(5, n=4096)
+    arena = whole.arena_host()
+    want = O.c_batch(arena, whole.desc)[0]
+    for world in (1, 2, 4, 8):
+        got = []
+        for r in range(world):
+            s = whole.shard(r, world)
+            assert s.base % 8 == 0 and int(s.desc["off"].min()) < 16
+            sa = s.arena_host()
+            assert np.array_equal(sa, arena[s.base:s.base + s.arena_bytes])
+            res = O.c_batch(sa, s.desc)[0]
+            got.append(res)
+            out = torch.from_numpy(res.view(np.int16).copy())
+            p = bench.parity_sample(s, out, k=100)
+            assert p["bit_exact"] and p["packets"] == min(200, s.n)
+            bad = res.copy()
+            bad[-1] ^= 1
+            assert not bench.parity_sample(s, torch.from_numpy(bad.view(np.int16)), k=100)["bit_exact"]
+        assert np.array_equal(np.concatenate(got), want)
+    assert "true" in bench.kernel_name(12_583_000_000, 8 << 20)
+    assert bench.kernel_name(1_577_058_304, 1 << 20) == "nsk::csum_hyb<256,64,8,16,4,2,0,true,false,2,false,0>"
+    assert bench.kernel_name(67_108_864, 1 << 20) == "nsk::csum_hyb<256,256,16,8,4,2,5,true,false,1,false,0>"
