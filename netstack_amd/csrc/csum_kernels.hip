@@ -199,25 +199,60 @@ __device__ __forceinline__ uint4 edge_mask(uint4 w, uint32_t ci, uint32_t lastc,
   return w;
 }
 
-__device__ __forceinline__ void put_result(uint32_t init, uint32_t sacc, uint64_t i,
+__device__ __forceinline__ void put_result(uint32_t init, uint32_t s, uint64_t i,
                                            uint16_t* out, uint32_t* partial) {
-  if (partial) partial[i] = sacc;
-  else out[i] = (uint16_t)fold1(init + sacc);
+  if (partial) partial[i] = s;
+  else out[i] = (uint16_t)fold1(init + s);
 }
+
+// W-only accumulation.  The result fold1(initial + S) depends on S only
+// through S mod 65535 and whether initial + S == 0, as long as Go's uint32
+// accumulator does not wrap (initial + S < 2^32, i.e. packets of at most
+// 8190 chunks = 131,040 bytes).  Since 2^16 == 1 (mod 65535), the big-endian
+// word sum is S == 256*W (phase 0) or W (phase 1) (mod 65535), and S == 0 iff
+// every byte is 0 iff W == 0.  So those packets need only W — one v_sad_u16
+// per dword — and s_class() turns a packet's W total into a value with the
+// same fold1 behaviour as S (also as a chain partial: csum_chain adds it to a
+// u16).  Tiles holding a longer packet accumulate the exact S (EX = true).
+constexpr uint32_t kWOnlyMaxChunks = 8190;
+
+__device__ __forceinline__ uint32_t s_class(uint32_t W, uint32_t phase) {
+  const uint32_t w = fold1(W);
+  return phase ? w : fold1(w << 8);
+}
+
+template <bool EX>
+__device__ __forceinline__ void acc_chunk(const uint4 w, uint32_t& T, uint32_t& W) {
+  if constexpr (EX) {
+    sad_chunk(w, T, W);
+  } else {
+    W = __builtin_amdgcn_sad_u16(w.x, 0u, W);
+    W = __builtin_amdgcn_sad_u16(w.y, 0u, W);
+    W = __builtin_amdgcn_sad_u16(w.z, 0u, W);
+    W = __builtin_amdgcn_sad_u16(w.w, 0u, W);
+  }
+}
+
+template <bool EX>
+__device__ __forceinline__ uint32_t run_value(uint32_t T, uint32_t W, uint32_t phase) {
+  if constexpr (EX) return s_of(T, W, phase);
+  else return W;
+}
+
+// Edge word bits: lo (0-4) | hiex (5-9) | h (10-13) | split (14) | phase (31).
+constexpr uint32_t kSplitBit = 1u << 14;
 
 template <int P>
 struct HybLds {
-  uint32_t rb[P + 1];   // first big run of each packet
-  uint32_t rs[P + 1];   // first small run of each packet
-  uint32_t first[P];    // SRD offset of chunk 0 (window path)
+  uint4 info[P];        // {SRD offset of chunk 0, nch, edge word, ts}
   uint64_t g[P];        // absolute address of chunk 0 (64-bit path)
-  uint32_t nch[P];
-  uint32_t edge[P];
-  uint32_t acc[P];
-  uint32_t hts[P];      // split | h << 1 | ts << 4 (0: not split)
   uint64_t wtot[P / 64];
   uint64_t wmin[P / 64], wmax[P / 64];
+  uint32_t rb[P + 1];   // first big run of each packet
+  uint32_t rs[P + 1];   // first small run of each packet
+  uint32_t acc[P];
   uint32_t wsmall[P / 64];
+  uint32_t wex[P / 64];
 };
 
 struct Srd {
@@ -292,8 +327,8 @@ __device__ __forceinline__ uint32_t direct_sum(const Srd& r, const PktInfo& p) {
   }
   uint32_t T = 0, W = 0;
 #pragma unroll
-  for (int j = 0; j < UD; ++j) sad_chunk(edge_mask(v[j], (uint32_t)j, p.nch - 1u, p.ew), T, W);
-  return s_of(T, W, p.ew >> 31);
+  for (int j = 0; j < UD; ++j) acc_chunk<false>(edge_mask(v[j], (uint32_t)j, p.nch - 1u, p.ew), T, W);
+  return s_class(W, p.ew >> 31);
 }
 
 // One tile through the scan path (thread t holds packet p of global index i).
@@ -315,10 +350,16 @@ __device__ __forceinline__ void hyb_scan_tile(HybLds<WG>& L, const Srd& r, const
 
   // LA split of a big packet: lane runs over chunks [0, h) and [ts, nch), the
   // partial first and last 128-B lines; groups over the whole lines [h, ts).
+  // The body holds only whole chunks of the packet, so the group loop needs
+  // no byte masks: a partial first (last) chunk sends its whole line to the
+  // lane runs — a line it shares with the neighbouring packet anyway.
   uint32_t h = nch, ts = nch;
-  if (LA && nch >= big_chunks) {
+  const bool split = LA && nch >= big_chunks;
+  if (split) {
     h = (8u - p.lp) & 7u;
     ts = ((p.lp + nch) & ~7u) - p.lp;
+    if (h == 0u && (p.ew & 31u) != 0u) h = 8u;
+    if (ts == nch && ((p.ew >> 5) & 31u) != 16u) ts -= 8u;
   }
   // At most 2^28 chunks per packet (len is a u32), so a tile's big-run total
   // stays below 2^32 with RB >= 16; small runs per packet are bounded by
@@ -326,7 +367,7 @@ __device__ __forceinline__ void hyb_scan_tile(HybLds<WG>& L, const Srd& r, const
   const uint64_t nr = nch == 0 ? 0ull
                       : !LA ? (nch >= big_chunks ? (uint64_t)((nch + RB - 1) / RB)
                                                  : ((uint64_t)((nch + US - 1) / US) << 32))
-                      : nch >= big_chunks
+                      : split
                           ? ((uint64_t)((ts - h + RB - 1) / RB) |
                              ((uint64_t)((h + US - 1) / US + (nch - ts + US - 1) / US) << 32))
                           : ((uint64_t)((nch + US - 1) / US) << 32);
@@ -336,19 +377,23 @@ __device__ __forceinline__ void hyb_scan_tile(HybLds<WG>& L, const Srd& r, const
     const uint64_t y = __shfl_up(incl, d, 64);
     if (lane >= d) incl += y;
   }
-  if (lane == 63) L.wtot[wv] = incl;
+  const int wex = __any(nch > kWOnlyMaxChunks);
+  if (lane == 63) {
+    L.wtot[wv] = incl;
+    L.wex[wv] = (uint32_t)wex;
+  }
   __syncthreads();
   uint64_t excl = incl - nr;
+  bool exact = false;
 #pragma unroll
-  for (int w = 0; w < NW; ++w)
+  for (int w = 0; w < NW; ++w) {
     if (w < wv) excl += L.wtot[w];
+    exact = exact || L.wex[w];
+  }
   L.rb[t] = (uint32_t)excl;
   L.rs[t] = (uint32_t)(excl >> 32);
   if constexpr (GL) L.g[t] = p.g;
-  else L.first[t] = p.first;
-  L.nch[t] = nch;
-  L.edge[t] = p.ew;
-  if constexpr (LA) L.hts[t] = (nch >= big_chunks) ? (1u | (h << 1) | (ts << 4)) : 0u;
+  L.info[t] = make_uint4(p.first, nch, p.ew | (split ? (kSplitBit | (h << 10)) : 0u), ts);
   L.acc[t] = 0u;
   if (t == WG - 1) {
     L.rb[P] = (uint32_t)(excl + nr);
@@ -365,104 +410,116 @@ __device__ __forceinline__ void hyb_scan_tile(HybLds<WG>& L, const Srd& r, const
       lo = (s_r[lo + step] <= q) ? lo + step : lo;
     return lo;
   };
-  auto load = [&](int pk, uint32_t ci, bool valid, auto nt) -> uint4 {
-    constexpr bool NT = decltype(nt)::value;
-    if constexpr (GL) {
-      return valid ? gload<NT>(L.g[pk] + (uint64_t)ci * 16u) : make_uint4(0, 0, 0, 0);
-    } else {
-      return bload<NT ? AUXB : 0>(r.rsrc, valid ? L.first[pk] + ci * 16u : r.oob);
-    }
-  };
-
-  // Small packets (and split packets' edge lines): one lane per run of US
-  // consecutive chunks.  A run is issued (search + loads) by small_issue and
-  // consumed by small_sum, so its loads can be in flight while other work
-  // runs: PF issues the lane's first run before the big loop, SU runs are
-  // issued per iteration of the small loop.
+  const uint32_t RBt = L.rb[P];
   const uint32_t RSt = L.rs[P];
-  struct SRun {
-    int pk;
-    uint32_t ci0;
-    bool act;
-  };
-  auto small_issue = [&](uint32_t q, uint4 (&v)[US]) -> SRun {
-    SRun s{0, 0u, q < RSt};
-    uint32_t cend = 0u;
-    if (s.act) {
-      s.pk = search(L.rs, q);
-      const uint32_t nc = L.nch[s.pk];
-      s.ci0 = (q - L.rs[s.pk]) * US;
-      cend = nc;
-      if constexpr (LA) {  // split big packet: head runs cover [0, h), tail runs [ts, nc)
-        const uint32_t hts = L.hts[s.pk];
-        if (hts & 1u) {
-          const uint32_t hh = (hts >> 1) & 7u, nh = (hh + US - 1) / US;
-          const uint32_t k = q - L.rs[s.pk];
+
+  // The loops, with the exact (T, W) or the W-only accumulator for the whole
+  // tile.  Every load offset is a select (out-of-range slots read r.oob, which
+  // the buffer range check turns into zeros), so the descriptor fields come
+  // from one ds_read_b128 per run and no load sits behind a branch.
+  auto loops = [&](auto ex_tag) {
+    constexpr bool EX = decltype(ex_tag)::value;
+    // Small packets (and split packets' edge lines): one lane per run of US
+    // consecutive chunks.  A run is issued (search + loads) by small_issue and
+    // consumed by small_sum, so its loads can be in flight while other work
+    // runs: PF issues the lane's first run before the big loop, SU runs are
+    // issued per iteration of the small loop.
+    struct SRun {
+      int pk;
+      uint32_t ci0, lastc, ew;
+      bool act;
+    };
+    auto small_issue = [&](uint32_t q, uint4 (&v)[US]) -> SRun {
+      SRun sr{0, 0u, 0u, 0u, q < RSt};
+      uint32_t cend = 0u, base = 0u;
+      uint64_t gb = 0ull;
+      if (sr.act) {
+        sr.pk = search(L.rs, q);
+        const uint4 inf = L.info[sr.pk];
+        const uint32_t k = q - L.rs[sr.pk];
+        sr.ci0 = k * US;
+        sr.lastc = inf.y - 1u;
+        sr.ew = inf.z;
+        cend = inf.y;
+        if (LA && (inf.z & kSplitBit)) {  // head runs cover [0, h), tail runs [ts, nch)
+          const uint32_t hh = (inf.z >> 10) & 15u, nh = (hh + US - 1) / US;
           if (k < nh) cend = hh;
-          else s.ci0 = (hts >> 4) + (k - nh) * US;
+          else sr.ci0 = inf.w + (k - nh) * US;
         }
+        if constexpr (GL) gb = L.g[sr.pk] + (uint64_t)sr.ci0 * 16u;
+        else base = inf.x + sr.ci0 * 16u;
+      }
+#pragma unroll
+      for (int j = 0; j < US; ++j) {
+        const bool valid = sr.ci0 + (uint32_t)j < cend;
+        if constexpr (GL) v[j] = valid ? gload<false>(gb + 16u * j) : make_uint4(0, 0, 0, 0);
+        else v[j] = bload(r.rsrc, valid ? base + 16u * j : r.oob);
+      }
+      return sr;
+    };
+    auto small_sum = [&](const SRun& sr, const uint4 (&v)[US]) {
+      if (!sr.act) return;
+      uint32_t T = 0, W = 0;
+#pragma unroll
+      for (int j = 0; j < US; ++j) acc_chunk<EX>(edge_mask(v[j], sr.ci0 + (uint32_t)j, sr.lastc, sr.ew), T, W);
+      atomicAdd(&L.acc[sr.pk], run_value<EX>(T, W, sr.ew >> 31));
+    };
+
+    uint4 pv[PF ? US : 1];
+    SRun pr{0, 0u, 0u, 0u, false};
+    if constexpr (PF) pr = small_issue((uint32_t)t, pv);
+
+    // Big packets: groups of GB lanes, lane li takes chunks li + GB*j of a run.
+    for (uint32_t q = (uint32_t)(t / GB); q < RBt; q += NG) {
+      const int pk = search(L.rb, q);
+      const uint4 inf = L.info[pk];
+      uint32_t ci0 = (q - L.rb[pk]) * RB + li, cend = inf.y;
+      if constexpr (LA) {  // every big packet is split: body [h, ts)
+        ci0 += (inf.z >> 10) & 15u;
+        cend = inf.w;
+      }
+      uint4 v[UB];
+      if constexpr (GL) {
+        const uint64_t g0 = L.g[pk] + (uint64_t)ci0 * 16u;
+#pragma unroll
+        for (int j = 0; j < UB; ++j)
+          v[j] = ci0 + (uint32_t)(GB * j) < cend ? gload<AUXB != 0>(g0 + 16u * GB * j) : make_uint4(0, 0, 0, 0);
+      } else {
+        const uint32_t b0 = inf.x + ci0 * 16u;
+#pragma unroll
+        for (int j = 0; j < UB; ++j)
+          v[j] = bload<AUXB>(r.rsrc, ci0 + (uint32_t)(GB * j) < cend ? b0 + 16u * GB * j : r.oob);
+      }
+      uint32_t T = 0, W = 0;
+#pragma unroll
+      for (int j = 0; j < UB; ++j)
+        acc_chunk<EX>(LA ? v[j] : edge_mask(v[j], ci0 + (uint32_t)(GB * j), inf.y - 1u, inf.z), T, W);
+      const uint32_t sg = group_sum<GB>(run_value<EX>(T, W, inf.z >> 31));
+      if (li == 0) atomicAdd(&L.acc[pk], sg);
+    }
+
+    if constexpr (PF) small_sum(pr, pv);
+    for (uint32_t q = (uint32_t)t + (PF ? WG : 0); q < RSt; q += SU * WG) {
+      uint4 va[US];
+      const SRun ra = small_issue(q, va);
+      if constexpr (SU == 2) {
+        uint4 vb[US];
+        const SRun rb = small_issue(q + WG, vb);
+        small_sum(ra, va);
+        small_sum(rb, vb);
+      } else {
+        small_sum(ra, va);
       }
     }
-#pragma unroll
-    for (int j = 0; j < US; ++j)
-      v[j] = load(s.pk, s.ci0 + (uint32_t)j, s.ci0 + (uint32_t)j < cend, std::integral_constant<bool, false>{});
-    return s;
   };
-  auto small_sum = [&](const SRun& s, const uint4 (&v)[US]) {
-    if (!s.act) return;
-    const uint32_t e = L.edge[s.pk];
-    const uint32_t lastc = L.nch[s.pk] - 1u;
-    uint32_t T = 0, W = 0;
-#pragma unroll
-    for (int j = 0; j < US; ++j) sad_chunk(edge_mask(v[j], s.ci0 + (uint32_t)j, lastc, e), T, W);
-    atomicAdd(&L.acc[s.pk], s_of(T, W, e >> 31));
-  };
-
-  uint4 pv[PF ? US : 1];
-  SRun pr{0, 0u, false};
-  if constexpr (PF) pr = small_issue((uint32_t)t, pv);
-
-  // Big packets: groups of GB lanes, lane li takes chunks li + GB*j of a run.
-  const uint32_t RBt = L.rb[P];
-  for (uint32_t q = (uint32_t)(t / GB); q < RBt; q += NG) {
-    const int pk = search(L.rb, q);
-    const uint32_t nc = L.nch[pk];
-    uint32_t ci0 = (q - L.rb[pk]) * RB + li, cend = nc;
-    if constexpr (LA) {  // every big packet is split: body [h, ts)
-      const uint32_t hts = L.hts[pk];
-      ci0 += (hts >> 1) & 7u;
-      cend = hts >> 4;
-    }
-    uint4 v[UB];
-#pragma unroll
-    for (int j = 0; j < UB; ++j) {
-      const uint32_t ci = ci0 + (uint32_t)(GB * j);
-      v[j] = load(pk, ci, ci < cend, std::integral_constant<bool, AUXB != 0>{});
-    }
-    const uint32_t e = L.edge[pk];
-    uint32_t T = 0, W = 0;
-#pragma unroll
-    for (int j = 0; j < UB; ++j) sad_chunk(edge_mask(v[j], ci0 + (uint32_t)(GB * j), nc - 1u, e), T, W);
-    const uint32_t sg = group_sum<GB>(s_of(T, W, e >> 31));
-    if (li == 0) atomicAdd(&L.acc[pk], sg);
-  }
-
-  if constexpr (PF) small_sum(pr, pv);
-  for (uint32_t q = (uint32_t)t + (PF ? WG : 0); q < RSt; q += SU * WG) {
-    uint4 va[US];
-    const SRun ra = small_issue(q, va);
-    if constexpr (SU == 2) {
-      uint4 vb[US];
-      const SRun rb = small_issue(q + WG, vb);
-      small_sum(ra, va);
-      small_sum(rb, vb);
-    } else {
-      small_sum(ra, va);
-    }
-  }
+  if (exact) loops(std::true_type{});
+  else loops(std::false_type{});
   __syncthreads();
 
-  if (mine) put_result(p.init, L.acc[t], i, out, partial);
+  if (mine) {
+    const uint32_t acc = L.acc[t];
+    put_result(p.init, exact ? acc : s_class(acc, p.ew >> 31), i, out, partial);
+  }
 }
 
 // WIN = false (arenas below 4 GiB): one SRD over the whole arena, no window
