@@ -239,6 +239,49 @@ __device__ __forceinline__ uint32_t run_value(uint32_t T, uint32_t W, uint32_t p
   else return W;
 }
 
+// The bytes of a run that lie outside its packet: [0, lo) of the packet's
+// first chunk and [hiex, 16) of its last (edge word e).  A run sums its chunks
+// unmasked and subtracts these (S is linear in T and W for a fixed phase):
+// one masked chunk per partial edge, in a branch taken only by lanes whose run
+// holds such an edge — a 16-B-aligned packet start never has one, so the
+// per-chunk mask work of edge_mask() is gone from every run.
+__device__ __forceinline__ uint32_t bytes_below(int c) {  // bytes [0, c) of a dword, c clamped to [0, 4]
+  c = min(max(c, 0), 4);
+  return c >= 4 ? 0xFFFFFFFFu : ((1u << (8 * c)) - 1u);
+}
+
+template <bool EX, int U>
+__device__ __forceinline__ void sub_edges(const uint4 (&v)[U], uint32_t ci0, uint32_t lastc, uint32_t e,
+                                          uint32_t& T, uint32_t& W) {
+  const int lo = (int)(e & 31u), hx = (int)((e >> 5) & 31u);
+  uint32_t Tx = 0, Wx = 0;
+  if (ci0 == 0u && lo != 0) {
+    const uint4 w = v[0];
+    acc_chunk<EX>(make_uint4(w.x & bytes_below(lo), w.y & bytes_below(lo - 4), w.z & bytes_below(lo - 8),
+                             w.w & bytes_below(lo - 12)),
+                  Tx, Wx);
+  }
+  const uint32_t jl = lastc - ci0;
+  if (jl < (uint32_t)U && hx != 16) {
+    // The last chunk, picked with AND/OR masks (an if-chain on jl becomes a
+    // switch that LLVM lowers to a scratch-memory lookup of v[jl]).
+    uint4 w = make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      const uint32_t m = 0u - (uint32_t)(jl == (uint32_t)j);
+      w.x |= v[j].x & m;
+      w.y |= v[j].y & m;
+      w.z |= v[j].z & m;
+      w.w |= v[j].w & m;
+    }
+    acc_chunk<EX>(make_uint4(w.x & ~bytes_below(hx), w.y & ~bytes_below(hx - 4), w.z & ~bytes_below(hx - 8),
+                             w.w & ~bytes_below(hx - 12)),
+                  Tx, Wx);
+  }
+  T -= Tx;
+  W -= Wx;
+}
+
 // Edge word bits: lo (0-4) | hiex (5-9) | h (10-13) | split (14) | phase (31).
 constexpr uint32_t kSplitBit = 1u << 14;
 
@@ -327,7 +370,8 @@ __device__ __forceinline__ uint32_t direct_sum(const Srd& r, const PktInfo& p) {
   }
   uint32_t T = 0, W = 0;
 #pragma unroll
-  for (int j = 0; j < UD; ++j) acc_chunk<false>(edge_mask(v[j], (uint32_t)j, p.nch - 1u, p.ew), T, W);
+  for (int j = 0; j < UD; ++j) acc_chunk<false>(v[j], T, W);
+  sub_edges<false>(v, 0u, p.nch - 1u, p.ew, T, W);
   return s_class(W, p.ew >> 31);
 }
 
@@ -461,7 +505,8 @@ __device__ __forceinline__ void hyb_scan_tile(HybLds<WG>& L, const Srd& r, const
       if (!sr.act) return;
       uint32_t T = 0, W = 0;
 #pragma unroll
-      for (int j = 0; j < US; ++j) acc_chunk<EX>(edge_mask(v[j], sr.ci0 + (uint32_t)j, sr.lastc, sr.ew), T, W);
+      for (int j = 0; j < US; ++j) acc_chunk<EX>(v[j], T, W);
+      sub_edges<EX>(v, sr.ci0, sr.lastc, sr.ew, T, W);
       atomicAdd(&L.acc[sr.pk], run_value<EX>(T, W, sr.ew >> 31));
     };
 

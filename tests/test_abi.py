@@ -106,3 +106,31 @@ def test_cpp_mirror_buffer_tables():
         subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "netstack_amd", "csrc")], check=True)
     r = subprocess.run([exe, "--cpu-only"], capture_output=True, text=True, timeout=60)
     assert r.returncode == 0, r.stdout + r.stderr
+
+
+def test_product_kernels_never_spill_and_keep_occupancy():
+    """The build keeps hipcc's kernel resource report (netstack_amd/csrc/
+    Makefile).  No checksum kernel may use scratch memory: an if-chain over a
+    register array once compiled to a scratch lookup and cost 45% of the
+    bandwidth.  The group kernels must keep >= 6 waves per SIMD and the
+    small-packet kernels 8."""
+    rep = os.path.join(ROOT, "netstack_amd", "lib", "csum_kernels.resources.txt")
+    txt = open(rep).read()
+    kernels = {}
+    cur = None
+    for line in txt.splitlines():
+        m = re.search(r"Function Name: (\S+)", line)
+        if m:
+            cur = m.group(1)
+            kernels[cur] = {}
+            continue
+        m = re.search(r"(ScratchSize \[bytes/lane\]|Occupancy \[waves/SIMD\]|VGPRs): (\d+)", line)
+        if m and cur:
+            kernels[cur][m.group(1).split()[0]] = int(m.group(2))
+    hyb = {k: v for k, v in kernels.items() if "csum_hyb" in k}
+    assert len(hyb) >= 18, sorted(kernels)
+    for k, v in kernels.items():
+        assert v["ScratchSize"] == 0, (k, v)
+    for k, v in hyb.items():
+        small = "ILi256ELi256ELi16ELi8ELi4ELi2ELi5E" in k
+        assert v["Occupancy"] >= (8 if small else 6), (k, v)
