@@ -191,8 +191,8 @@ def kernel_name(arena_bytes: int, n: int) -> str:
     if arena_bytes // n >= 256:
         want = (128 << 10) // max(arena_bytes // n, 1)
         tp = next((t for t in (256, 128, 64, 32, 16, 8, 4, 2) if want >= t), 1)
-        return f"nsk::csum_hyb<256,{tp},8,16,4,2,0,true,{win},2,false,0>"
-    return f"nsk::csum_hyb<256,256,16,8,4,2,5,true,{win},1,false,0>"
+        return f"nsk::csum_hyb<256,{tp},8,16,4,2,0,true,{win},2>"
+    return f"nsk::csum_hyb<256,256,16,8,4,2,5,true,{win},1>"
 
 
 def main():

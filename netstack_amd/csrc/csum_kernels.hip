@@ -378,7 +378,7 @@ __device__ __forceinline__ uint32_t direct_sum(const Srd& r, const PktInfo& p) {
 // One tile through the scan path (thread t holds packet p of global index i).
 // GL = 64-bit global loads (tile span >= 4 GiB) instead of the window SRD.
 // Every thread of the block must call it.
-template <int WG, int TP, int GB, int UB, int US, int AUXB, bool LA, bool GL, int SU = 1, bool PF = false>
+template <int WG, int TP, int GB, int UB, int US, int AUXB, bool LA, bool GL, int SU>
 __device__ __forceinline__ void hyb_scan_tile(HybLds<WG>& L, const Srd& r, const PktInfo& p,
                                               bool mine, uint64_t i, uint16_t* __restrict__ out,
                                               uint32_t* __restrict__ partial, uint32_t big_chunks) {
@@ -466,8 +466,7 @@ __device__ __forceinline__ void hyb_scan_tile(HybLds<WG>& L, const Srd& r, const
     // Small packets (and split packets' edge lines): one lane per run of US
     // consecutive chunks.  A run is issued (search + loads) by small_issue and
     // consumed by small_sum, so its loads can be in flight while other work
-    // runs: PF issues the lane's first run before the big loop, SU runs are
-    // issued per iteration of the small loop.
+    // runs: SU runs are issued per iteration of the small loop.
     struct SRun {
       int pk;
       uint32_t ci0, lastc, ew;
@@ -479,8 +478,8 @@ __device__ __forceinline__ void hyb_scan_tile(HybLds<WG>& L, const Srd& r, const
       uint64_t gb = 0ull;
       if (sr.act) {
         sr.pk = search(L.rs, q);
-        const uint4 inf = L.info[sr.pk];
         const uint32_t k = q - L.rs[sr.pk];
+        const uint4 inf = L.info[sr.pk];
         sr.ci0 = k * US;
         sr.lastc = inf.y - 1u;
         sr.ew = inf.z;
@@ -509,10 +508,6 @@ __device__ __forceinline__ void hyb_scan_tile(HybLds<WG>& L, const Srd& r, const
       sub_edges<EX>(v, sr.ci0, sr.lastc, sr.ew, T, W);
       atomicAdd(&L.acc[sr.pk], run_value<EX>(T, W, sr.ew >> 31));
     };
-
-    uint4 pv[PF ? US : 1];
-    SRun pr{0, 0u, 0u, 0u, false};
-    if constexpr (PF) pr = small_issue((uint32_t)t, pv);
 
     // Big packets: groups of GB lanes, lane li takes chunks li + GB*j of a run.
     for (uint32_t q = (uint32_t)(t / GB); q < RBt; q += NG) {
@@ -543,8 +538,7 @@ __device__ __forceinline__ void hyb_scan_tile(HybLds<WG>& L, const Srd& r, const
       if (li == 0) atomicAdd(&L.acc[pk], sg);
     }
 
-    if constexpr (PF) small_sum(pr, pv);
-    for (uint32_t q = (uint32_t)t + (PF ? WG : 0); q < RSt; q += SU * WG) {
+    for (uint32_t q = (uint32_t)t; q < RSt; q += SU * WG) {
       uint4 va[US];
       const SRun ra = small_issue(q, va);
       if constexpr (SU == 2) {
@@ -572,12 +566,10 @@ __device__ __forceinline__ void hyb_scan_tile(HybLds<WG>& L, const Srd& r, const
 // small-packet batches.
 // TP = descriptors per tile (<= WG): large packets get fewer per workgroup so
 // a batch of 64 KiB GSO buffers still spreads over every CU.
-// SU = small runs issued per lane per iteration, PF = first small run issued
-// before the big loop, OCC = minimum waves per SIMD asked of the register
-// allocator (0: none).
+// SU = small runs issued per lane per iteration.
 template <int WG, int TP, int GB, int UB, int US, int AUXB, int UD = 0, bool LA = true, bool WIN = false,
-          int SU = 1, bool PF = false, int OCC = 0>
-__global__ __launch_bounds__(WG, OCC ? OCC : 1) void csum_hyb(
+          int SU = 1>
+__global__ __launch_bounds__(WG) void csum_hyb(
     const uint8_t* __restrict__ arena, uint64_t arena_bytes,
     const uint4* __restrict__ desc, uint32_t n, uint16_t* __restrict__ out,
     uint32_t* __restrict__ partial, unsigned long long* __restrict__ err, uint32_t big_chunks) {
@@ -606,13 +598,13 @@ __global__ __launch_bounds__(WG, OCC ? OCC : 1) void csum_hyb(
       if (mine) put_result(p.init, s, i, out, partial);
       return;
     }
-    hyb_scan_tile<WG, TP, GB, UB, US, AUXB, LA, false, SU, PF>(L, r, p, mine, i, out, partial, big_chunks);
+    hyb_scan_tile<WG, TP, GB, UB, US, AUXB, LA, false, SU>(L, r, p, mine, i, out, partial, big_chunks);
   } else if constexpr (WIN) {
     // The tile spans >= 4 GiB: 64-bit global loads, fewer in flight per lane
     // so this rarely taken path does not raise the kernel's register count.
     const Srd r = make_srd(0ull, 0ull);
     const PktInfo p = pkt_info(d, 0ull);
-    hyb_scan_tile<WG, TP, 16, 4, 4, AUXB, LA, true>(L, r, p, mine, i, out, partial, big_chunks);
+    hyb_scan_tile<WG, TP, 16, 4, 4, AUXB, LA, true, 1>(L, r, p, mine, i, out, partial, big_chunks);
   }
 }
 
@@ -640,7 +632,7 @@ __global__ void csum_chain(const uint4* __restrict__ desc, uint32_t n,
 // ---- launchers (C++ linkage, used by csum_api.cpp) ------------------------
 namespace nsk {
 
-template <int TP, int GB, int UB, int US, int AUXB, int UD, bool LA, int SU = 1, bool PF = false, int OCC = 0>
+template <int TP, int GB, int UB, int US, int AUXB, int UD, bool LA, int SU = 1>
 static hipError_t launch_hyb_tp(const uint8_t* arena, uint64_t arena_bytes, const void* desc,
                                 uint32_t n, uint16_t* out, uint32_t* partial,
                                 unsigned long long* err, hipStream_t stream, uint32_t big_chunks) {
@@ -650,10 +642,10 @@ static hipError_t launch_hyb_tp(const uint8_t* arena, uint64_t arena_bytes, cons
   // One SRD over the whole arena when it fits (arena base rounded down to 16 B
   // plus the arena), else per-tile windows.
   if (((uintptr_t)arena & 15u) + arena_bytes + 64 < kMaxSrdBytes)
-    hipLaunchKernelGGL((csum_hyb<WG, TP, GB, UB, US, AUXB, UD, LA, false, SU, PF, OCC>), dim3(grid), dim3(WG), 0,
+    hipLaunchKernelGGL((csum_hyb<WG, TP, GB, UB, US, AUXB, UD, LA, false, SU>), dim3(grid), dim3(WG), 0,
                        stream, arena, arena_bytes, d, n, out, partial, err, big_chunks);
   else
-    hipLaunchKernelGGL((csum_hyb<WG, TP, GB, UB, US, AUXB, UD, LA, true, SU, PF, OCC>), dim3(grid), dim3(WG), 0,
+    hipLaunchKernelGGL((csum_hyb<WG, TP, GB, UB, US, AUXB, UD, LA, true, SU>), dim3(grid), dim3(WG), 0,
                        stream, arena, arena_bytes, d, n, out, partial, err, big_chunks);
   return hipGetLastError();
 }
@@ -662,7 +654,7 @@ static hipError_t launch_hyb_tp(const uint8_t* arena, uint64_t arena_bytes, cons
 // per workgroup, clamped to [1, 256] (tools/tune.py on MI355X: 1M x 1500 B
 // best at 64 = 223 us vs 229 at 256; the Zipf batch at 128; 16K x 64 KiB
 // at 2-4 = 155 us vs 495 at 256 — profiles/r01/tune_tp*.log).
-template <int GB, int UB, int US, int AUXB, int UD = 0, bool LA = true, int SU = 1, bool PF = false, int OCC = 0>
+template <int GB, int UB, int US, int AUXB, int UD = 0, bool LA = true, int SU = 1>
 static hipError_t launch_hyb(const uint8_t* arena, uint64_t arena_bytes, const void* desc,
                              uint32_t n, uint16_t* out, uint32_t* partial,
                              unsigned long long* err, hipStream_t stream, uint32_t big_chunks) {
@@ -670,11 +662,11 @@ static hipError_t launch_hyb(const uint8_t* arena, uint64_t arena_bytes, const v
   const uint64_t want = (128u << 10) / avg;
 #define NSK_TP(tp) \
   if (want >= tp)              \
-  return launch_hyb_tp<tp, GB, UB, US, AUXB, UD, LA, SU, PF, OCC>(arena, arena_bytes, desc, n, out, partial, err, stream, big_chunks)
+  return launch_hyb_tp<tp, GB, UB, US, AUXB, UD, LA, SU>(arena, arena_bytes, desc, n, out, partial, err, stream, big_chunks)
   if constexpr (UD > 0) {
     // The small-packet variant (launch_batch: < 256 B per descriptor) keeps
     // full tiles: its direct path is one packet per lane.
-    return launch_hyb_tp<256, GB, UB, US, AUXB, UD, LA, SU, PF, OCC>(arena, arena_bytes, desc, n, out, partial, err,
+    return launch_hyb_tp<256, GB, UB, US, AUXB, UD, LA, SU>(arena, arena_bytes, desc, n, out, partial, err,
                                                         stream, big_chunks);
   } else {
     NSK_TP(256);
@@ -685,7 +677,7 @@ static hipError_t launch_hyb(const uint8_t* arena, uint64_t arena_bytes, const v
     NSK_TP(8);
     NSK_TP(4);
     NSK_TP(2);
-    return launch_hyb_tp<1, GB, UB, US, AUXB, UD, LA, SU, PF, OCC>(arena, arena_bytes, desc, n, out, partial, err, stream,
+    return launch_hyb_tp<1, GB, UB, US, AUXB, UD, LA, SU>(arena, arena_bytes, desc, n, out, partial, err, stream,
                                                       big_chunks);
   }
 #undef NSK_TP

@@ -140,11 +140,10 @@ __global__ __launch_bounds__(256) void calib_grp(const uint4* __restrict__ p, ui
   if ((threadIdx.x & 63) == 0) atomicAdd(&out[blockIdx.x], acc);
 }
 
-template <int GB, int UB, int US, int AUXB, uint32_t BIG, int UD = 0, bool LA = true, int SU = 1, bool PF = false,
-          int OCC = 0>
+template <int GB, int UB, int US, int AUXB, uint32_t BIG, int UD = 0, bool LA = true, int SU = 1>
 hipError_t launch_h(const uint8_t* arena, uint64_t arena_bytes, const void* desc, uint32_t n,
                     uint16_t* out, unsigned long long* err, hipStream_t s) {
-  return launch_hyb<GB, UB, US, AUXB, UD, LA, SU, PF, OCC>(arena, arena_bytes, desc, n, out, nullptr, err, s, BIG);
+  return launch_hyb<GB, UB, US, AUXB, UD, LA, SU>(arena, arena_bytes, desc, n, out, nullptr, err, s, BIG);
 }
 
 // Floor for the 1M x 64 B layout only (desc[i].off == 64 * i): the same
@@ -226,7 +225,7 @@ hipError_t launch_floor(const uint8_t* arena, uint64_t arena_bytes, const void* 
 template <int TP, int GB, int UB>
 hipError_t launch_tp(const uint8_t* arena, uint64_t arena_bytes, const void* desc, uint32_t n,
                      uint16_t* out, unsigned long long* err, hipStream_t s) {
-  return launch_hyb_tp<TP, GB, UB, 4, 2, 0, true>(arena, arena_bytes, desc, n, out, nullptr, err, s, 64u);
+  return launch_hyb_tp<TP, GB, UB, 4, 2, 0, true, 2>(arena, arena_bytes, desc, n, out, nullptr, err, s, 64u);
 }
 
 typedef hipError_t (*launch_fn)(const uint8_t*, uint64_t, const void*, uint32_t, uint16_t*,
@@ -242,16 +241,10 @@ static const Variant kVariants[] = {
     {"prod_g8u16_b64", launch_h<8, 16, 4, 2, 64, 0, true, 2>},
     {"g8u16_su1", launch_h<8, 16, 4, 2, 64>},
     {"prod_small_d5", launch_h<16, 8, 4, 2, 64, 5>},
-    {"g8u16_pf", launch_h<8, 16, 4, 2, 64, 0, true, 1, true>},
-    {"g8u16_pf_su2", launch_h<8, 16, 4, 2, 64, 0, true, 2, true>},
-    {"g8u16_b32_pf", launch_h<8, 16, 4, 2, 32, 0, true, 1, true>},
-    {"small_d5_occ8", launch_h<16, 8, 4, 2, 64, 5, true, 1, false, 8>},
-    {"small_d5_pf", launch_h<16, 8, 4, 2, 64, 5, true, 1, true>},
+    {"g8u16_b32", launch_h<8, 16, 4, 2, 32, 0, true, 2>},
+    {"g8u16_b48", launch_h<8, 16, 4, 2, 48, 0, true, 2>},
     {"floor_64B", launch_floor},
     {"quad_d4", launch_quad},
-    {"g8u16_occ5", launch_h<8, 16, 4, 2, 64, 0, true, 1, false, 5>},
-    {"g8u12_occ5", launch_h<8, 12, 4, 2, 64, 0, true, 1, false, 5>},
-    {"g8u16_su2_occ5", launch_h<8, 16, 4, 2, 64, 0, true, 2, false, 5>},
 };
 
 }  // namespace nsk
