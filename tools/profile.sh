@@ -12,7 +12,8 @@ mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd "$R"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv \
-  -- python3 bench.py --steps 20 --warmup 3 --no-cpu > "$OUT/bench_traced.log" 2>&1
+  -- python3 bench.py --steps 50 --warmup 5 --no-cpu > "$OUT/bench_traced.log" 2>&1
+python3 tools/trace_summary.py "$OUT/trace" --warmup 5 --steps 50 > "$OUT/trace_summary.json"
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run --output-format csv \
   -- python3 tools/pmc_run.py > "$OUT/pmc_fetch.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run --output-format csv \
