@@ -31,6 +31,12 @@ namespace {
 // piece is never split (its own wrap is reproduced exactly by the kernel).
 constexpr uint64_t kMergeMax = 131072;
 constexpr uint64_t kDefaultStaging = 64ull << 20;
+// Host batches whose staged bytes (table + results + arena span) fit here run
+// zero-copy: the kernel reads the table and the bytes from mapped pinned host
+// memory over PCIe and writes the results there, so a small synchronous call
+// is one CPU copy, one launch and one wait instead of three DMA operations,
+// a launch and a wait (tools/latency.cc).
+constexpr uint64_t kZeroCopyMax = 1ull << 20;
 
 thread_local hipError_t g_last_hip = hipSuccess;
 
@@ -78,23 +84,25 @@ struct DevBuf {
   }
 };
 
-template <typename T>
+template <typename T, unsigned FLAGS = hipHostMallocDefault>
 struct PinBuf {
   T* p = nullptr;
+  T* dev = nullptr;  // the same memory as a device pointer (mapped)
   size_t cap = 0;
   int ensure(size_t n) {
     if (n <= cap) return NS_OK;
     if (p) (void)hipHostFree(p);
-    p = nullptr;
+    p = dev = nullptr;
     cap = 0;
     size_t want = std::max<size_t>(n, 1);
-    HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&p), want * sizeof(T), hipHostMallocDefault));
+    HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&p), want * sizeof(T), FLAGS));
+    HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&dev), p, 0));
     cap = want;
     return NS_OK;
   }
   void release() {
     if (p) (void)hipHostFree(p);
-    p = nullptr;
+    p = dev = nullptr;
     cap = 0;
   }
 };
@@ -117,6 +125,9 @@ struct ns_csum_ctx {
   DevBuf<uint32_t> d_part[2];
   PinBuf<ns_pkt_desc> h_desc[2];
   PinBuf<uint16_t> h_out[2];
+  // zero-copy staging for small host batches: [table | results | arena],
+  // coherent so the kernel's loads and stores go straight to host memory
+  PinBuf<uint8_t, hipHostMallocMapped | hipHostMallocCoherent> z_buf;
   // gather staging for the VectorisedView entry points
   PinBuf<uint8_t> g_arena;
   std::vector<ns_pkt_desc> g_desc;
@@ -152,6 +163,39 @@ int run_host_batch(ns_csum_ctx* ctx, const uint8_t* h_arena, uint64_t arena_byte
   for (uint32_t i = 0; i < n; ++i) {
     const uint64_t off = h_desc[i].off, len = h_desc[i].len;
     if (off > arena_bytes || len > arena_bytes - off) return NS_ERANGE;
+  }
+  {  // small batch: zero-copy through mapped pinned memory
+    uint64_t lo = UINT64_MAX, hi = 0;
+    for (uint32_t i = 0; i < n; ++i)
+      if (h_desc[i].len) {
+        lo = std::min(lo, h_desc[i].off);
+        hi = std::max(hi, h_desc[i].off + h_desc[i].len);
+      }
+    if (lo == UINT64_MAX) lo = hi = 0;
+    const uint64_t span = hi - lo;
+    const uint64_t t_bytes = (uint64_t)n * sizeof(ns_pkt_desc);
+    const uint64_t o_off = t_bytes, a_off = (o_off + (uint64_t)n * 2 + 15) & ~15ull;
+    // NS_CSUM_NO_ZERO_COPY=1 forces the DMA pipeline (A/B diagnostics only).
+    static const bool zc_off = std::getenv("NS_CSUM_NO_ZERO_COPY") != nullptr;
+    if (!zc_off && a_off + span <= kZeroCopyMax) {
+      int rc;
+      if ((rc = ctx->z_buf.ensure(kZeroCopyMax)) != NS_OK) return rc;
+      if (chained && (rc = ctx->d_part[0].ensure(n)) != NS_OK) return rc;
+      uint8_t* z = ctx->z_buf.p;
+      ns_pkt_desc* zd = reinterpret_cast<ns_pkt_desc*>(z);
+      for (uint32_t q = 0; q < n; ++q) {
+        zd[q] = h_desc[q];
+        zd[q].off = zd[q].len ? zd[q].off - lo : 0;
+      }
+      if (span) std::memcpy(z + a_off, h_arena + lo, span);
+      uint8_t* zdev = ctx->z_buf.dev;
+      hipStream_t s = ctx->stream[0];
+      HIP_TRY(nsk::launch_batch(zdev + a_off, span, zdev, n, reinterpret_cast<uint16_t*>(zdev + o_off),
+                                chained ? ctx->d_part[0].p : nullptr, ctx->d_err, s));
+      HIP_TRY(hipStreamSynchronize(s));
+      std::memcpy(h_out, z + o_off, (size_t)n * 2);
+      return NS_OK;
+    }
   }
   const uint64_t budget = ctx->staging;
   struct Pending {
@@ -356,11 +400,18 @@ struct Gather {
   int run(uint16_t* out) {
     std::lock_guard<std::mutex> lk(ctx->mu);
     DeviceGuard g(ctx->device);
-    int rc = ctx->g_arena.ensure(std::max<size_t>(bytes.size(), 16));
-    if (rc != NS_OK) return rc;
-    if (!bytes.empty()) std::memcpy(ctx->g_arena.p, bytes.data(), bytes.size());
+    // Small gathers go zero-copy straight from `bytes` (run_host_batch copies
+    // them into the mapped staging); large ones are staged in pinned memory
+    // for the DMA pipeline.
+    const uint8_t* src = bytes.data();
+    int rc = NS_OK;
+    if (std::getenv("NS_CSUM_NO_ZERO_COPY") || bytes.size() + desc.size() * (sizeof(ns_pkt_desc) + 2) + 16 > kZeroCopyMax) {
+      if ((rc = ctx->g_arena.ensure(std::max<size_t>(bytes.size(), 16))) != NS_OK) return rc;
+      if (!bytes.empty()) std::memcpy(ctx->g_arena.p, bytes.data(), bytes.size());
+      src = ctx->g_arena.p;
+    }
     std::vector<uint16_t> res(desc.size());
-    rc = run_host_batch(ctx, ctx->g_arena.p, bytes.size(), desc.data(), (uint32_t)desc.size(), res.data(),
+    rc = run_host_batch(ctx, src, bytes.size(), desc.data(), (uint32_t)desc.size(), res.data(),
                         any_cont(desc.data(), (uint32_t)desc.size()));
     if (rc != NS_OK) return rc;
     for (size_t q = 0; q < result_at.size(); ++q) out[q] = res[result_at[q]];
@@ -462,6 +513,7 @@ void ns_csum_destroy(ns_csum_ctx* ctx) {
     for (int s = 0; s < 2; ++s)
       if (ctx->stream[s]) (void)hipStreamSynchronize(ctx->stream[s]);
     ctx->partial.release();
+    ctx->z_buf.release();
     for (int s = 0; s < 2; ++s) {
       ctx->d_arena[s].release();
       ctx->d_desc[s].release();

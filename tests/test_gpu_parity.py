@@ -419,3 +419,44 @@ def test_cpp_mirror_reference_tests(engine):
     r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "0 failed" in r.stdout
+
+
+@pytest.mark.parametrize("chained", [False, True])
+def test_w_only_threshold_and_zero_sums(engine, chained):
+    """csum_hyb accumulates only W for packets of <= 8190 chunks and the exact
+    (T, W) pair in tiles holding a longer one.  Packets on
+    both sides of the threshold at odd starts, all-0xFF bytes (largest sums),
+    all-zero bytes (S == 0 must stay distinguishable from S == 65535), initial
+    0 / 1 / 0xFFFF, odd flags, mixed into the same tiles as small packets —
+    plain and chained (the W-only class value as a csum_chain partial)."""
+    import oracle as O
+    from netstack_amd import workloads as W
+
+    rng = np.random.default_rng(8190)
+    big = [131008, 131024, 131039, 131040, 131041, 131055, 131056, 131057, 131072, 131073, 200000]
+    lengths, fills = [], []
+    for L in big:
+        lengths += [L] + list(rng.integers(1, 200, 150))
+        fills += ["ff"] + ["rnd"] * 150
+    for k in range(3000):  # tiles of small packets only: W-only
+        lengths.append(int(rng.integers(0, 300)))
+        fills.append(["zero", "ff", "rnd"][k % 3])
+    n = len(lengths)
+    lengths = np.array(lengths, dtype=np.uint32)
+    init = rng.choice(np.array([0, 1, 0xFFFF], dtype=np.uint16), n)
+    flags = rng.integers(0, 2, n).astype(np.uint16)
+    if chained:
+        flags = flags | (2 * (rng.random(n) < 0.6)).astype(np.uint16)
+    d, end = W.make_desc(lengths, init, align=1, base=3, flags=flags)
+    arena = rng.integers(0, 256, end + 5, dtype=np.uint8)
+    for i in range(n):
+        o, L = int(d["off"][i]), int(d["len"][i])
+        if fills[i] == "ff":
+            arena[o:o + L] = 0xFF
+        elif fills[i] == "zero":
+            arena[o:o + L] = 0
+    want, _ = O.c_batch(arena, d, chained=chained)
+    got = dev_batch(engine, arena, d, chained=chained, arena_offset=1)
+    assert np.array_equal(got, want), np.flatnonzero(got != want)[:10]
+    if not chained:
+        assert (want == 0).any() and (want == 0xFFFF).any()
