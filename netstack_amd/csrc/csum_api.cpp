@@ -7,8 +7,11 @@
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
+#include <chrono>
 #include <cstring>
 #include <mutex>
 #include <new>
@@ -31,12 +34,11 @@ namespace {
 // piece is never split (its own wrap is reproduced exactly by the kernel).
 constexpr uint64_t kMergeMax = 131072;
 constexpr uint64_t kDefaultStaging = 64ull << 20;
-// Host batches whose staged bytes (table + results + arena span) fit here run
-// zero-copy: the kernel reads the table and the bytes from mapped pinned host
-// memory over PCIe and writes the results there, so a small synchronous call
-// is one CPU copy, one launch and one wait instead of three DMA operations,
-// a launch and a wait (tools/latency.cc).
-constexpr uint64_t kZeroCopyMax = 1ull << 20;
+// Small host calls (bytes up to kStageBytes, below) run zero-copy: the kernel
+// reads the table and the bytes from mapped pinned host memory over PCIe and
+// writes the results there, so a small synchronous call is one CPU copy, one
+// launch and one wait instead of three DMA operations, a launch and a wait
+// (tools/latency.cc).
 
 thread_local hipError_t g_last_hip = hipSuccess;
 
@@ -107,6 +109,36 @@ struct PinBuf {
   }
 };
 
+// Mapped, coherent, all-device pinned memory: the kernel reads and writes it
+// over PCIe with ordinary loads and stores (zero-copy).
+using MappedPin = PinBuf<uint8_t, hipHostMallocMapped | hipHostMallocNonCoherent | hipHostMallocPortable>;
+
+// One small synchronous call's batch: `ndesc` descriptors over bytes
+// [lo, lo + nbytes) of the caller's arena, staged in mapped memory whose
+// device address is `dbytes` (= byte lo).
+struct SmallReq {
+  const uint8_t* dbytes = nullptr;
+  uint64_t nbytes = 0, lo = 0;
+  const ns_pkt_desc* desc = nullptr;
+  uint32_t ndesc = 0;
+  uint16_t* res = nullptr;
+  bool chained = false;  // NS_DESC_CONT runs are chains (else the flag is ignored)
+  int rc = NS_OK;
+  std::atomic<bool> done{false};  // set (release) once rc and the results are in
+  // bytes this request takes in a pass's table buffer (table + results)
+  uint64_t table_bytes() const { return (uint64_t)ndesc * (sizeof(ns_pkt_desc) + 2) + 16; }
+};
+
+// A small call's bytes live in one staging buffer of kStageBytes leased from
+// the context's pool for the duration of the call, so concurrent callers
+// gather in parallel straight into memory the kernel reads.
+constexpr uint64_t kStageBytes = 1ull << 20;
+// A pass's [table | results] buffer; a pass takes queued requests while they fit.
+constexpr uint64_t kPassTableBytes = 1ull << 20;
+// The "arena" of a zero-copy pass is the address space: descriptors hold
+// absolute device addresses (the kernel's per-tile windows take it from there).
+constexpr uint64_t kWholeSpace = 1ull << 60;
+
 }  // namespace
 
 struct ns_csum_ctx {
@@ -125,9 +157,16 @@ struct ns_csum_ctx {
   DevBuf<uint32_t> d_part[2];
   PinBuf<ns_pkt_desc> h_desc[2];
   PinBuf<uint16_t> h_out[2];
-  // zero-copy staging for small host batches: [table | results | arena],
-  // coherent so the kernel's loads and stores go straight to host memory
-  PinBuf<uint8_t, hipHostMallocMapped | hipHostMallocCoherent> z_buf;
+  // zero-copy pass buffer for small calls: [table | results]
+  MappedPin z_buf;
+  // flat combining of concurrent small calls (submit_small) and the pool of
+  // mapped staging buffers they gather into; guarded by qmu
+  std::mutex qmu;
+  std::condition_variable qcv;
+  std::vector<SmallReq*> pending;
+  bool combining = false;
+  std::vector<MappedPin*> stage_free;
+  std::vector<MappedPin*> stage_all;
   // gather staging for the VectorisedView entry points
   PinBuf<uint8_t> g_arena;
   std::vector<ns_pkt_desc> g_desc;
@@ -153,6 +192,178 @@ bool any_cont(const ns_pkt_desc* d, uint32_t n) {
   return false;
 }
 
+// Validates a host table against its arena and returns the byte span its
+// non-empty descriptors cover ([0, 0) if none).
+int table_span(const ns_pkt_desc* d, uint32_t n, uint64_t arena_bytes, uint64_t* lo, uint64_t* hi) {
+  uint64_t l = UINT64_MAX, h = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint64_t off = d[i].off, len = d[i].len;
+    if (off > arena_bytes || len > arena_bytes - off) return NS_ERANGE;
+    if (len) {
+      l = std::min(l, off);
+      h = std::max(h, off + len);
+    }
+  }
+  if (l == UINT64_MAX) l = h = 0;
+  *lo = l;
+  *hi = h;
+  return NS_OK;
+}
+
+bool zero_copy_enabled() {
+  // NS_CSUM_NO_ZERO_COPY=1 forces the DMA pipeline (A/B diagnostics only).
+  static const bool off = std::getenv("NS_CSUM_NO_ZERO_COPY") != nullptr;
+  return !off;
+}
+
+// Zero-copy pass over one or more small requests (caller holds ctx->mu and
+// the device guard): one table of all their descriptors with absolute device
+// addresses into their mapped staging, results beside it, one launch that
+// reads both over PCIe, one wait.  Requests never share a NS_DESC_CONT run: a
+// request's first descriptor is made a run head.
+int run_zero_copy(ns_csum_ctx* ctx, SmallReq* const* reqs, size_t nreq) {
+  uint64_t nd = 0, nb = 0;
+  bool chained = false;
+  for (size_t r = 0; r < nreq; ++r) {
+    nd += reqs[r]->ndesc;
+    nb += reqs[r]->nbytes;
+    chained = chained || reqs[r]->chained;
+  }
+  if (nd == 0) return NS_OK;
+  const uint64_t o_off = nd * sizeof(ns_pkt_desc);
+  int rc;
+  if ((rc = ctx->z_buf.ensure(std::max<uint64_t>(kPassTableBytes, o_off + nd * 2))) != NS_OK) return rc;
+  if (chained && (rc = ctx->d_part[0].ensure(nd)) != NS_OK) return rc;
+  uint8_t* z = ctx->z_buf.p;
+  ns_pkt_desc* zd = reinterpret_cast<ns_pkt_desc*>(z);
+  uint64_t k = 0;
+  for (size_t r = 0; r < nreq; ++r) {
+    const SmallReq& q = *reqs[r];
+    const uint64_t base = (uint64_t)(uintptr_t)q.dbytes;
+    for (uint32_t i = 0; i < q.ndesc; ++i, ++k) {
+      zd[k] = q.desc[i];
+      zd[k].off = zd[k].len ? base + (zd[k].off - q.lo) : 0;
+      if (!q.chained) {
+        zd[k].flags &= (uint16_t)~NS_DESC_CONT;  // independent in an unchained batch
+      } else if (i == 0 && (zd[k].flags & NS_DESC_CONT)) {
+        // A batch's first descriptor heads its run even when flagged CONT
+        // (with initial 0, csum_chain): keep that inside a combined pass.
+        zd[k].flags &= (uint16_t)~NS_DESC_CONT;
+        zd[k].initial = 0;
+      }
+    }
+  }
+  uint8_t* zdev = ctx->z_buf.dev;
+  hipStream_t s = ctx->stream[0];
+  HIP_TRY(nsk::launch_batch(nullptr, kWholeSpace, zdev, (uint32_t)nd, reinterpret_cast<uint16_t*>(zdev + o_off),
+                            chained ? ctx->d_part[0].p : nullptr, ctx->d_err, s, std::max<uint64_t>(nb, 1)));
+  HIP_TRY(hipStreamSynchronize(s));
+  const uint16_t* res = reinterpret_cast<const uint16_t*>(z + o_off);
+  for (size_t r = 0; r < nreq; ++r) {
+    std::memcpy(reqs[r]->res, res, (size_t)reqs[r]->ndesc * 2);
+    res += reqs[r]->ndesc;
+  }
+  return NS_OK;
+}
+
+// Lease / return a mapped staging buffer of kStageBytes from the context's pool.
+MappedPin* lease_stage(ns_csum_ctx* ctx, int* rc) {
+  {
+    std::lock_guard<std::mutex> ql(ctx->qmu);
+    if (!ctx->stage_free.empty()) {
+      MappedPin* b = ctx->stage_free.back();
+      ctx->stage_free.pop_back();
+      return b;
+    }
+  }
+  MappedPin* b = new (std::nothrow) MappedPin();
+  if (!b) {
+    *rc = NS_ENOMEM;
+    return nullptr;
+  }
+  {
+    DeviceGuard g(ctx->device);
+    if ((*rc = b->ensure(kStageBytes)) != NS_OK) {
+      delete b;
+      return nullptr;
+    }
+  }
+  std::lock_guard<std::mutex> ql(ctx->qmu);
+  ctx->stage_all.push_back(b);
+  return b;
+}
+
+void return_stage(ns_csum_ctx* ctx, MappedPin* b) {
+  if (!b) return;
+  std::lock_guard<std::mutex> ql(ctx->qmu);
+  ctx->stage_free.push_back(b);
+}
+
+// Flat combining of concurrent small synchronous calls.  netstack calls the
+// checksum from every endpoint's goroutine at once; one
+// launch + wait costs ~15-20 us whatever its size, so serialising calls on
+// the context would cap a context at ~50K calls/s.  Instead a caller queues
+// its request; if no pass is running it becomes the combiner: it takes every
+// queued request (while their tables fit kPassTableBytes), runs them as ONE
+// zero-copy pass, hands out the results and repeats while requests remain.
+// Each caller has already gathered its bytes into its own leased staging, so
+// the only serial host work per request is copying its descriptors.
+// Everyone else sleeps until its request is done.  Results are identical to
+// separate calls (descriptors are independent; chains never cross requests).
+int submit_small(ns_csum_ctx* ctx, SmallReq* req) {
+  // A combiner keeps serving queued requests after its own is done, up to
+  // kMaxPasses passes, so back-to-back passes do not wait for a sleeping
+  // thread to wake up and take the role over.
+  constexpr int kMaxPasses = 8;
+  std::unique_lock<std::mutex> ql(ctx->qmu);
+  ctx->pending.push_back(req);
+  while (!req->done.load(std::memory_order_acquire)) {
+    if (ctx->combining) {
+      // Spin briefly (a pass is ~20-60 us) before sleeping: a woken thread
+      // costs more than the spin.
+      ql.unlock();
+      const auto t0 = std::chrono::steady_clock::now();
+      while (!req->done.load(std::memory_order_acquire) &&
+             std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(50))
+        std::this_thread::yield();
+      ql.lock();
+      if (req->done.load(std::memory_order_acquire)) break;
+      if (ctx->combining) ctx->qcv.wait(ql);
+      continue;
+    }
+    ctx->combining = true;
+    for (int pass = 0; pass < kMaxPasses && !ctx->pending.empty(); ++pass) {
+      std::vector<SmallReq*> take;
+      uint64_t staged = 0;
+      size_t i = 0;
+      for (; i < ctx->pending.size(); ++i) {
+        const uint64_t sz = ctx->pending[i]->table_bytes();
+        if (!take.empty() && staged + sz > kPassTableBytes) break;
+        take.push_back(ctx->pending[i]);
+        staged += sz;
+      }
+      ctx->pending.erase(ctx->pending.begin(), ctx->pending.begin() + (long)i);
+      ql.unlock();
+      int rc;
+      {
+        std::lock_guard<std::mutex> lk(ctx->mu);
+        DeviceGuard g(ctx->device);
+        rc = run_zero_copy(ctx, take.data(), take.size());
+      }
+      for (SmallReq* t : take) {
+        t->rc = rc;
+        t->done.store(true, std::memory_order_release);
+      }
+      ql.lock();
+      ctx->qcv.notify_all();
+      if (req->done.load(std::memory_order_relaxed) && pass + 1 >= kMaxPasses) break;
+    }
+    ctx->combining = false;
+    ctx->qcv.notify_all();  // a waiter takes the role over if requests remain
+  }
+  return req->rc;
+}
+
 // Host batch core, caller holds ctx->mu and the device guard.  Pipelines
 // chunks of the descriptor table over the two slots/streams: H2D of chunk k+1
 // overlaps the kernel of chunk k.  Chunks never split a NS_DESC_CONT run.
@@ -163,39 +374,6 @@ int run_host_batch(ns_csum_ctx* ctx, const uint8_t* h_arena, uint64_t arena_byte
   for (uint32_t i = 0; i < n; ++i) {
     const uint64_t off = h_desc[i].off, len = h_desc[i].len;
     if (off > arena_bytes || len > arena_bytes - off) return NS_ERANGE;
-  }
-  {  // small batch: zero-copy through mapped pinned memory
-    uint64_t lo = UINT64_MAX, hi = 0;
-    for (uint32_t i = 0; i < n; ++i)
-      if (h_desc[i].len) {
-        lo = std::min(lo, h_desc[i].off);
-        hi = std::max(hi, h_desc[i].off + h_desc[i].len);
-      }
-    if (lo == UINT64_MAX) lo = hi = 0;
-    const uint64_t span = hi - lo;
-    const uint64_t t_bytes = (uint64_t)n * sizeof(ns_pkt_desc);
-    const uint64_t o_off = t_bytes, a_off = (o_off + (uint64_t)n * 2 + 15) & ~15ull;
-    // NS_CSUM_NO_ZERO_COPY=1 forces the DMA pipeline (A/B diagnostics only).
-    static const bool zc_off = std::getenv("NS_CSUM_NO_ZERO_COPY") != nullptr;
-    if (!zc_off && a_off + span <= kZeroCopyMax) {
-      int rc;
-      if ((rc = ctx->z_buf.ensure(kZeroCopyMax)) != NS_OK) return rc;
-      if (chained && (rc = ctx->d_part[0].ensure(n)) != NS_OK) return rc;
-      uint8_t* z = ctx->z_buf.p;
-      ns_pkt_desc* zd = reinterpret_cast<ns_pkt_desc*>(z);
-      for (uint32_t q = 0; q < n; ++q) {
-        zd[q] = h_desc[q];
-        zd[q].off = zd[q].len ? zd[q].off - lo : 0;
-      }
-      if (span) std::memcpy(z + a_off, h_arena + lo, span);
-      uint8_t* zdev = ctx->z_buf.dev;
-      hipStream_t s = ctx->stream[0];
-      HIP_TRY(nsk::launch_batch(zdev + a_off, span, zdev, n, reinterpret_cast<uint16_t*>(zdev + o_off),
-                                chained ? ctx->d_part[0].p : nullptr, ctx->d_err, s));
-      HIP_TRY(hipStreamSynchronize(s));
-      std::memcpy(h_out, z + o_off, (size_t)n * 2);
-      return NS_OK;
-    }
   }
   const uint64_t budget = ctx->staging;
   struct Pending {
@@ -277,12 +455,44 @@ int run_host_batch(ns_csum_ctx* ctx, const uint8_t* h_arena, uint64_t arena_byte
   return NS_OK;
 }
 
+// Where a gather assembles its bytes: a mapped staging buffer leased from the
+// context's pool (the kernel reads it in place), spilling to host memory once
+// the bytes outgrow it (those calls take the DMA pipeline).
+struct ByteSink {
+  ns_csum_ctx* ctx;
+  MappedPin* stage = nullptr;
+  std::vector<uint8_t> spill;
+  uint64_t n = 0;
+  bool spilled = false;
+  int rc = NS_OK;  // a failed lease: everything spills
+  explicit ByteSink(ns_csum_ctx* c) : ctx(c) {
+    if (zero_copy_enabled()) stage = lease_stage(ctx, &rc);
+    if (!stage) spilled = true;
+  }
+  ~ByteSink() { return_stage(ctx, stage); }
+  ByteSink(const ByteSink&) = delete;
+  ByteSink& operator=(const ByteSink&) = delete;
+  uint64_t size() const { return n; }
+  void append(const uint8_t* p, uint64_t len) {
+    if (!len) return;
+    if (!spilled && n + len > stage->cap) {
+      spill.assign(stage->p, stage->p + n);
+      spilled = true;
+    }
+    if (spilled) spill.insert(spill.end(), p, p + len);
+    else std::memcpy(stage->p + n, p, len);
+    n += len;
+  }
+  const uint8_t* data() const { return spilled ? spill.data() : stage->p; }
+};
+
 // ---- gather of VectorisedView pieces (tcpip/buffer -> staging arena) -----
 struct Gather {
   ns_csum_ctx* ctx;
-  std::vector<uint8_t> bytes;  // assembled here, then copied to pinned once
+  ByteSink bytes;  // assembled in mapped staging (or spilled host memory)
   std::vector<ns_pkt_desc> desc;
   std::vector<uint32_t> result_at;  // index of the descriptor holding each result
+  explicit Gather(ns_csum_ctx* c) : ctx(c), bytes(c) {}
 
   // Append one segment made of pieces (ptr,len) with Go VV semantics:
   // odd-carry across pieces, merged into runs of <= kMergeMax bytes.
@@ -309,7 +519,7 @@ struct Gather {
         first_desc = false;
         open = true;
       }
-      bytes.insert(bytes.end(), pc.first, pc.first + len);
+      bytes.append(pc.first, len);
       cur.len += (uint32_t)len;
       consumed += len;
       if (big) close();
@@ -336,7 +546,7 @@ struct Gather {
       d.len = (uint32_t)pc.second;
       d.initial = first ? initial : 0;
       d.flags = first ? 0 : NS_DESC_CONT;
-      if (pc.second) bytes.insert(bytes.end(), pc.first, pc.first + pc.second);
+      bytes.append(pc.first, pc.second);
       desc.push_back(d);
       first = false;
     }
@@ -383,7 +593,7 @@ struct Gather {
         first_desc = false;
         open = true;
       }
-      bytes.insert(bytes.end(), p[k].data, p[k].data + len);
+      bytes.append(p[k].data, len);
       cur.len += (uint32_t)len;
       parity ^= (uint32_t)(len & 1);
       if (big) close();
@@ -398,21 +608,28 @@ struct Gather {
   }
 
   int run(uint16_t* out) {
-    std::lock_guard<std::mutex> lk(ctx->mu);
-    DeviceGuard g(ctx->device);
-    // Small gathers go zero-copy straight from `bytes` (run_host_batch copies
-    // them into the mapped staging); large ones are staged in pinned memory
-    // for the DMA pipeline.
-    const uint8_t* src = bytes.data();
-    int rc = NS_OK;
-    if (std::getenv("NS_CSUM_NO_ZERO_COPY") || bytes.size() + desc.size() * (sizeof(ns_pkt_desc) + 2) + 16 > kZeroCopyMax) {
-      if ((rc = ctx->g_arena.ensure(std::max<size_t>(bytes.size(), 16))) != NS_OK) return rc;
-      if (!bytes.empty()) std::memcpy(ctx->g_arena.p, bytes.data(), bytes.size());
-      src = ctx->g_arena.p;
-    }
     std::vector<uint16_t> res(desc.size());
-    rc = run_host_batch(ctx, src, bytes.size(), desc.data(), (uint32_t)desc.size(), res.data(),
-                        any_cont(desc.data(), (uint32_t)desc.size()));
+    int rc;
+    if (!bytes.spilled) {
+      // Small: zero-copy from the leased staging, combined with concurrent calls.
+      SmallReq rq;
+      rq.dbytes = bytes.stage->dev;
+      rq.nbytes = bytes.size();
+      rq.desc = desc.data();
+      rq.ndesc = (uint32_t)desc.size();
+      rq.res = res.data();
+      rq.chained = any_cont(desc.data(), (uint32_t)desc.size());
+      rc = submit_small(ctx, &rq);
+    } else {
+      if (bytes.rc != NS_OK) return bytes.rc;
+      // Large gathers are staged in pinned memory for the DMA pipeline.
+      std::lock_guard<std::mutex> lk(ctx->mu);
+      DeviceGuard g(ctx->device);
+      if ((rc = ctx->g_arena.ensure(std::max<size_t>(bytes.size(), 16))) != NS_OK) return rc;
+      if (bytes.size()) std::memcpy(ctx->g_arena.p, bytes.data(), bytes.size());
+      rc = run_host_batch(ctx, ctx->g_arena.p, bytes.size(), desc.data(), (uint32_t)desc.size(), res.data(),
+                          any_cont(desc.data(), (uint32_t)desc.size()));
+    }
     if (rc != NS_OK) return rc;
     for (size_t q = 0; q < result_at.size(); ++q) out[q] = res[result_at[q]];
     return NS_OK;
@@ -514,6 +731,12 @@ void ns_csum_destroy(ns_csum_ctx* ctx) {
       if (ctx->stream[s]) (void)hipStreamSynchronize(ctx->stream[s]);
     ctx->partial.release();
     ctx->z_buf.release();
+    for (MappedPin* b : ctx->stage_all) {
+      b->release();
+      delete b;
+    }
+    ctx->stage_all.clear();
+    ctx->stage_free.clear();
     for (int s = 0; s < 2; ++s) {
       ctx->d_arena[s].release();
       ctx->d_desc[s].release();
@@ -570,6 +793,27 @@ int ns_csum_batch_host(ns_csum_ctx* ctx, const uint8_t* h_arena, uint64_t arena_
                        const ns_pkt_desc* h_desc, uint32_t n, uint16_t* h_out,
                        uint32_t batch_flags) {
   if (!ctx || (n && (!h_desc || !h_out)) || (arena_bytes && !h_arena)) return NS_EINVAL;
+  if (n == 0) return NS_OK;
+  uint64_t lo = 0, hi = 0;
+  const int vr = table_span(h_desc, n, arena_bytes, &lo, &hi);
+  if (vr != NS_OK) return vr;
+  if (zero_copy_enabled() && hi - lo <= kStageBytes) {
+    int rc = NS_OK;
+    MappedPin* st = lease_stage(ctx, &rc);
+    if (!st) return rc;
+    if (hi > lo) std::memcpy(st->p, h_arena + lo, hi - lo);
+    SmallReq rq;
+    rq.dbytes = st->dev;
+    rq.nbytes = hi - lo;
+    rq.lo = lo;
+    rq.desc = h_desc;
+    rq.ndesc = n;
+    rq.res = h_out;
+    rq.chained = (batch_flags & NS_BATCH_CHAINED) != 0;
+    rc = submit_small(ctx, &rq);
+    return_stage(ctx, st);
+    return rc;
+  }
   std::lock_guard<std::mutex> lk(ctx->mu);
   DeviceGuard g(ctx->device);
   return run_host_batch(ctx, h_arena, arena_bytes, h_desc, n, h_out,
@@ -579,7 +823,7 @@ int ns_csum_batch_host(ns_csum_ctx* ctx, const uint8_t* h_arena, uint64_t arena_
 int ns_csum_checksum(ns_csum_ctx* ctx, const uint8_t* buf, uint64_t len, uint16_t initial,
                      uint16_t* out) {
   if (!ctx || !out || (len && !buf) || len > 0xFFFFFFFFull) return NS_EINVAL;
-  Gather gt{ctx, {}, {}, {}};
+  Gather gt(ctx);
   std::vector<std::pair<const uint8_t*, uint64_t>> pieces;
   if (len) pieces.emplace_back(buf, len);
   gt.restart_chain(pieces, initial);  // one piece, odd = false: checksum.go:52-55
@@ -592,7 +836,7 @@ int ns_csum_vv_with_offset(ns_csum_ctx* ctx, const ns_view* views, uint32_t nvie
   std::vector<std::pair<const uint8_t*, uint64_t>> pieces;
   int rc = clip_views(views, nviews, off, size, &pieces);
   if (rc != NS_OK) return rc;
-  Gather gt{ctx, {}, {}, {}};
+  Gather gt(ctx);
   gt.segment(pieces, initial);
   return gt.run(out);
 }
@@ -601,7 +845,7 @@ int ns_csum_vv_batch(ns_csum_ctx* ctx, const ns_view* views, uint32_t nviews,
                      const ns_seg* segs, uint32_t nsegs, uint16_t* out) {
   if (!ctx || (nsegs && (!segs || !out)) || (nviews && !views)) return NS_EINVAL;
   if (nsegs == 0) return NS_OK;
-  Gather gt{ctx, {}, {}, {}};
+  Gather gt(ctx);
   std::vector<std::pair<const uint8_t*, uint64_t>> pieces;
   for (uint32_t q = 0; q < nsegs; ++q) {
     int rc = clip_views(views, nviews, segs[q].off, segs[q].size, &pieces);
@@ -620,7 +864,7 @@ int ns_csum_views_restart(ns_csum_ctx* ctx, const ns_view* views, uint32_t nview
     if (views[k].len > 0xFFFFFFFFull) return NS_EINVAL;
     pieces.emplace_back(views[k].data, views[k].len);
   }
-  Gather gt{ctx, {}, {}, {}};
+  Gather gt(ctx);
   gt.restart_chain(pieces, initial);
   return gt.run(out);
 }
@@ -637,7 +881,7 @@ int ns_csum_chains(ns_csum_ctx* ctx, const ns_piece* pieces, uint32_t npieces, u
   if (npieces && !(pieces[npieces - 1].flags & NS_PIECE_END)) return NS_EINVAL;  // unterminated
   if (chains > nout || (chains && !out)) return NS_EINVAL;
   if (chains == 0) return NS_OK;
-  Gather gt{ctx, {}, {}, {}};
+  Gather gt(ctx);
   uint32_t start = 0;
   for (uint32_t k = 0; k < npieces; ++k) {
     if (pieces[k].flags & NS_PIECE_END) {
@@ -657,7 +901,7 @@ int ns_csum_pseudo_header(ns_csum_ctx* ctx, uint32_t protocol, const uint8_t* sr
   const uint8_t proto[2] = {0, (uint8_t)protocol};
   std::vector<std::pair<const uint8_t*, uint64_t>> pieces = {
       {src, src_len}, {dst, dst_len}, {lenbe, 2}, {proto, 2}};
-  Gather gt{ctx, {}, {}, {}};
+  Gather gt(ctx);
   gt.restart_chain(pieces, 0);
   return gt.run(out);
 }

@@ -12,9 +12,12 @@ namespace nsk {
 // 32-bit partial sums go to `partial` and a chain fix-up pass resolves
 // NS_DESC_CONT runs into `out`; otherwise every descriptor is independent.
 // Out-of-range descriptors are summed as empty and counted in *err.
+// `sizing_bytes` (0: arena_bytes) is the byte count the launcher sizes tiles
+// by — the payload of a batch whose "arena" is the whole address space
+// (arena = nullptr, descriptors holding absolute addresses).
 hipError_t launch_batch(const uint8_t* arena, uint64_t arena_bytes,
                         const void* desc, uint32_t n, uint16_t* out,
                         uint32_t* partial, unsigned long long* err,
-                        hipStream_t stream);
+                        hipStream_t stream, uint64_t sizing_bytes = 0);
 
 }  // namespace nsk

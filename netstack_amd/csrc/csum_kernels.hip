@@ -657,8 +657,9 @@ static hipError_t launch_hyb_tp(const uint8_t* arena, uint64_t arena_bytes, cons
 template <int GB, int UB, int US, int AUXB, int UD = 0, bool LA = true, int SU = 1>
 static hipError_t launch_hyb(const uint8_t* arena, uint64_t arena_bytes, const void* desc,
                              uint32_t n, uint16_t* out, uint32_t* partial,
-                             unsigned long long* err, hipStream_t stream, uint32_t big_chunks) {
-  const uint64_t avg = std::max<uint64_t>(arena_bytes / n, 1);
+                             unsigned long long* err, hipStream_t stream, uint32_t big_chunks,
+                             uint64_t sizing_bytes = 0) {
+  const uint64_t avg = std::max<uint64_t>((sizing_bytes ? sizing_bytes : arena_bytes) / n, 1);
   const uint64_t want = (128u << 10) / avg;
 #define NSK_TP(tp) \
   if (want >= tp)              \
@@ -686,17 +687,19 @@ static hipError_t launch_hyb(const uint8_t* arena, uint64_t arena_bytes, const v
 hipError_t launch_batch(const uint8_t* arena, uint64_t arena_bytes,
                         const void* desc, uint32_t n, uint16_t* out,
                         uint32_t* partial, unsigned long long* err,
-                        hipStream_t stream) {
+                        hipStream_t stream, uint64_t sizing_bytes) {
   if (n == 0) return hipSuccess;
   hipError_t e;
-  if (arena_bytes / n >= 256) {
+  if (sizing_bytes == 0) sizing_bytes = arena_bytes;
+  if (sizing_bytes / n >= 256) {
     // Packets of >= 64 chunks (~1 KiB): their whole 128-B lines to 8-lane
     // groups (one full line per group per load instruction, 16 loads per lane
     // in flight) with nontemporal loads; their partial edge lines and all
     // smaller packets to per-lane runs of 4, two runs issued per lane per
     // iteration (tools/tune.py on MI355X: 220.6 us on 1M x 1500 B = 90.2% of
     // 8 TB/s, 107 us on the Zipf batch; profiles/r01/tune_*.json).
-    e = launch_hyb<8, 16, 4, 2, 0, true, 2>(arena, arena_bytes, desc, n, out, partial, err, stream, 64u);
+    e = launch_hyb<8, 16, 4, 2, 0, true, 2>(arena, arena_bytes, desc, n, out, partial, err, stream, 64u,
+                                            sizing_bytes);
   } else {
     // Small packets: the same kernel plus the direct path — a tile whose
     // packets all span <= 5 chunks (any <= 65-B packet) has each lane read its

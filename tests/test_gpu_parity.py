@@ -460,3 +460,58 @@ def test_w_only_threshold_and_zero_sums(engine, chained):
     assert np.array_equal(got, want), np.flatnonzero(got != want)[:10]
     if not chained:
         assert (want == 0).any() and (want == 0xFFFF).any()
+
+
+def test_concurrent_small_calls_are_combined_bit_exact(engine):
+    """Small synchronous calls from many threads on ONE context are
+    flat-combined into shared zero-copy launches (csum_api.cpp submit_small).
+    Mixed call shapes — VectorisedView batches, single buffers, chained and
+    unchained host batches whose CONT flags must be ignored when unchained —
+    each result against the oracle."""
+    import threading
+
+    import oracle as O
+    from netstack_amd import workloads as W
+
+    errors = []
+
+    def worker(t):
+        rng = np.random.default_rng(1000 + t)
+        try:
+            for it in range(30):
+                kind = (t + it) % 4
+                if kind == 0:
+                    buf = rng.integers(0, 256, int(rng.integers(1, 70000)), dtype=np.uint8)
+                    cuts = np.sort(rng.integers(0, buf.size, 3))
+                    views = [buf[:cuts[0]], buf[cuts[0]:cuts[1]], buf[cuts[1]:]]
+                    segs = [(int(o), int(rng.integers(0, 3000)), int(rng.integers(0, 65536)))
+                            for o in rng.integers(0, buf.size, 20)]
+                    got = engine.vv_batch(views, segs)
+                    want = [O.py_checksum_vv_with_offset([bytes(v) for v in views], i, o, s) for o, s, i in segs]
+                    if list(got) != want:
+                        errors.append((t, it, "vv_batch"))
+                elif kind == 1:
+                    buf = rng.integers(0, 256, int(rng.integers(0, 9000)), dtype=np.uint8)
+                    ini = int(rng.integers(0, 65536))
+                    if engine.checksum(buf, ini) != O.py_checksum(bytes(buf), ini):
+                        errors.append((t, it, "checksum"))
+                else:
+                    chained = kind == 3
+                    n = int(rng.integers(1, 400))
+                    lengths = rng.integers(0, 1600, n).astype(np.uint32)
+                    flags = (rng.integers(0, 2, n) | (2 * (rng.random(n) < 0.5))).astype(np.uint16)
+                    d, end = W.make_desc(lengths, rng.integers(0, 65536, n).astype(np.uint16), align=1,
+                                         base=int(rng.integers(0, 9)), flags=flags)
+                    arena = rng.integers(0, 256, end + 3, dtype=np.uint8)
+                    want, _ = O.c_batch(arena, d, chained=chained)
+                    if not np.array_equal(engine.batch_host(arena, d, chained=chained), want):
+                        errors.append((t, it, "batch_host", chained))
+        except Exception as e:  # surfaced below
+            errors.append((t, repr(e)))
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(8)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join(timeout=120)
+    assert not errors, errors[:5]

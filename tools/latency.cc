@@ -3,7 +3,9 @@
 //   ns_csum_checksum      one 1500-B segment            (header.Checksum)
 //   ns_csum_vv_batch      sendTCPBatch: 64 KiB GSO payload, MSS 1460 (45 segs)
 //   ns_csum_chains        45 TCP segments: pseudo-header + payload + header
-//   ns_csum_batch_host    1024 x 1500 B from pinned host memory
+//   ns_csum_batch_host    1024 x 1500 B from host memory
+//   concurrency           T threads issuing sendTCPBatch-shaped vv_batch calls
+//                         on one context (flat-combined into shared launches)
 // Median and p99 over many calls after warm-up; a scalar 2-B/iteration loop
 // (checksum.go:41-43) on the same bytes is timed beside each for scale.
 //   ./latency [iters]
@@ -14,6 +16,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <functional>
+#include <thread>
 #include <vector>
 
 #include "netstack_csum.h"
@@ -61,7 +64,7 @@ int main(int argc, char** argv) {
   const int iters = argc > 1 ? std::atoi(argv[1]) : 2000;
   ns_csum_ctx* ctx = nullptr;
   check(ns_csum_init(nullptr, &ctx), "init");
-  std::vector<uint8_t> payload(1 << 20);
+  std::vector<uint8_t> payload(4 << 20);
   for (size_t i = 0; i < payload.size(); ++i) payload[i] = (uint8_t)(i * 2654435761u >> 13);
   volatile uint32_t sink = 0;
   std::printf("{\n");
@@ -105,6 +108,22 @@ int main(int argc, char** argv) {
     });
     std::printf(" \"chains_45_tcp_segments\": {\"gpu_med_us\": %.2f, \"gpu_p99_us\": %.2f},\n", g.med, g.p99);
   }
+  {  // host batches of growing size: zero-copy below kStageBytes (1 MiB), DMA above
+    std::printf(" \"batch_host_sizes\": [");
+    const uint32_t ns[] = {43, 170, 680, 2720};
+    for (int qi = 0; qi < 4; ++qi) {
+      const uint32_t n = ns[qi];
+      std::vector<ns_pkt_desc> d(n);
+      for (uint32_t i = 0; i < n; ++i) d[i] = ns_pkt_desc{(uint64_t)i * 1504, 1500, (uint16_t)i, 0};
+      std::vector<uint16_t> out(n);
+      const Stat g = time_calls(std::max(20, iters / 8), [&] {
+        check(ns_csum_batch_host(ctx, payload.data(), (uint64_t)n * 1504, d.data(), n, out.data(), 0), "batch_host");
+      });
+      std::printf("%s{\"packets\": %u, \"bytes\": %u, \"gpu_med_us\": %.2f, \"GBps\": %.2f}", qi ? ", " : "", n,
+                  n * 1504, g.med, n * 1504 / g.med / 1e3);
+    }
+    std::printf("],\n");
+  }
   {  // 1024 x 1500 B from host memory
     const uint32_t n = 1024;
     std::vector<ns_pkt_desc> d(n);
@@ -116,8 +135,47 @@ int main(int argc, char** argv) {
     const Stat c = time_calls(iters / 4, [&] {
       for (uint32_t i = 0; i < n; ++i) sink += scalar(payload.data() + d[i].off, 1500, d[i].initial);
     });
-    std::printf(" \"batch_host_1024x1500B\": {\"gpu_med_us\": %.2f, \"gpu_p99_us\": %.2f, \"scalar_med_us\": %.3f}\n",
+    std::printf(" \"batch_host_1024x1500B\": {\"gpu_med_us\": %.2f, \"gpu_p99_us\": %.2f, \"scalar_med_us\": %.3f},\n",
                 g.med, g.p99, c.med);
+  }
+  {  // T threads x sendTCPBatch calls on one context
+    const int mss = 1460, total = 65536;
+    std::vector<ns_seg> segs;
+    for (int off = 0; off < total; off += mss) segs.push_back(ns_seg{off, std::min(mss, total - off), 0, 0, 0});
+    std::vector<uint16_t> want(segs.size());
+    ns_view v0{payload.data(), (uint64_t)total};
+    check(ns_csum_vv_batch(ctx, &v0, 1, segs.data(), (uint32_t)segs.size(), want.data()), "vv_batch");
+    std::printf(" \"concurrent_vv_batch_64KiB\": [");
+    const int threads[] = {1, 2, 4, 8, 16, 32};
+    for (int ti = 0; ti < 6; ++ti) {
+      const int T = threads[ti], per = std::max(20, iters / 8);
+      std::vector<std::thread> th;
+      std::vector<int> bad(T, 0);
+      const double a = now_us();
+      for (int t = 0; t < T; ++t)
+        th.emplace_back([&, t] {
+          // each thread its own payload window (distinct bytes, same shape)
+          ns_view v{payload.data() + 4096 * (t % 64), (uint64_t)total};
+          std::vector<ns_seg> sg = segs;
+          for (auto& x : sg) x.initial = (uint16_t)t;
+          std::vector<uint16_t> out(sg.size());
+          std::vector<uint16_t> ref(sg.size());
+          for (size_t k = 0; k < sg.size(); ++k)
+            ref[k] = scalar(payload.data() + 4096 * (t % 64) + sg[k].off, (size_t)sg[k].size, (uint16_t)t);
+          for (int i = 0; i < per; ++i) {
+            check(ns_csum_vv_batch(ctx, &v, 1, sg.data(), (uint32_t)sg.size(), out.data()), "vv_batch");
+            bad[t] += out != ref;  // every call checked (a vector compare, not a re-sum)
+          }
+        });
+      for (auto& x : th) x.join();
+      const double el = now_us() - a;
+      int nbad = 0;
+      for (int b : bad) nbad += b;
+      const double calls = (double)T * per;
+      std::printf("%s{\"threads\": %d, \"calls_per_s\": %.0f, \"payload_GiBps\": %.3f, \"us_per_call_per_thread\": %.2f, \"wrong\": %d}",
+                  ti ? ", " : "", T, calls / el * 1e6, calls * total / el * 1e6 / (1 << 30), el / per, nbad);
+    }
+    std::printf("]\n");
   }
   std::printf("}\n");
   ns_csum_destroy(ctx);
