@@ -189,7 +189,7 @@ def kernel_name(arena_bytes: int, n: int) -> str:
     launch_batch / launch_hyb / launch_hyb_tp), as rocprofv3 names it."""
     win = "true" if arena_bytes + 64 >= 0xFFFF0000 else "false"
     if arena_bytes // n >= 256:
-        want = (128 << 10) // max(arena_bytes // n, 1)
+        want = (64 << 10) // max(arena_bytes // n, 1)  # kTileBytes
         tp = next((t for t in (256, 128, 64, 32, 16, 8, 4, 2) if want >= t), 1)
         return f"nsk::csum_hyb<256,{tp},8,16,4,2,0,true,{win},2>"
     return f"nsk::csum_hyb<256,256,16,8,4,2,5,true,{win},1>"

@@ -650,17 +650,20 @@ static hipError_t launch_hyb_tp(const uint8_t* arena, uint64_t arena_bytes, cons
   return hipGetLastError();
 }
 
-// Descriptors per workgroup: the largest power of two <= 128 KiB of payload
-// per workgroup, clamped to [1, 256] (tools/tune.py on MI355X: 1M x 1500 B
-// best at 64 = 223 us vs 229 at 256; the Zipf batch at 128; 16K x 64 KiB
-// at 2-4 = 155 us vs 495 at 256 — profiles/r01/tune_tp*.log).
+// Descriptors per workgroup: the largest power of two <= kTileBytes of
+// payload per workgroup, clamped to [1, 256].  Tiles of 32-64 KiB balance the
+// tail best; below ~32 KiB per workgroup the prologue dominates (tools/tune.py
+// on MI355X, profiles/r01/tune_tile_bytes.log: 1M x 1500 B 218 us at 32
+// descriptors vs 221 at 64 and 244 at 16; the Zipf batch 103 us at 64 vs 107
+// at 128 and 114 at 32; 64 KiB GSO buffers flat).
+constexpr uint64_t kTileBytes = 64u << 10;
 template <int GB, int UB, int US, int AUXB, int UD = 0, bool LA = true, int SU = 1>
 static hipError_t launch_hyb(const uint8_t* arena, uint64_t arena_bytes, const void* desc,
                              uint32_t n, uint16_t* out, uint32_t* partial,
                              unsigned long long* err, hipStream_t stream, uint32_t big_chunks,
-                             uint64_t sizing_bytes = 0) {
+                             uint64_t sizing_bytes = 0, uint64_t tile_bytes = kTileBytes) {
   const uint64_t avg = std::max<uint64_t>((sizing_bytes ? sizing_bytes : arena_bytes) / n, 1);
-  const uint64_t want = (128u << 10) / avg;
+  const uint64_t want = tile_bytes / avg;
 #define NSK_TP(tp) \
   if (want >= tp)              \
   return launch_hyb_tp<tp, GB, UB, US, AUXB, UD, LA, SU>(arena, arena_bytes, desc, n, out, partial, err, stream, big_chunks)

@@ -222,6 +222,12 @@ hipError_t launch_floor(const uint8_t* arena, uint64_t arena_bytes, const void* 
   return hipGetLastError();
 }
 
+template <uint64_t TB>
+hipError_t launch_tb(const uint8_t* arena, uint64_t arena_bytes, const void* desc, uint32_t n,
+                     uint16_t* out, unsigned long long* err, hipStream_t s) {
+  return launch_hyb<8, 16, 4, 2, 0, true, 2>(arena, arena_bytes, desc, n, out, nullptr, err, s, 64u, 0, TB);
+}
+
 template <int TP, int GB, int UB>
 hipError_t launch_tp(const uint8_t* arena, uint64_t arena_bytes, const void* desc, uint32_t n,
                      uint16_t* out, unsigned long long* err, hipStream_t s) {
@@ -242,7 +248,21 @@ static const Variant kVariants[] = {
     {"g8u16_su1", launch_h<8, 16, 4, 2, 64>},
     {"prod_small_d5", launch_h<16, 8, 4, 2, 64, 5>},
     {"g8u16_b32", launch_h<8, 16, 4, 2, 32, 0, true, 2>},
-    {"g8u16_b48", launch_h<8, 16, 4, 2, 48, 0, true, 2>},
+    {"g8u8_b64", launch_h<8, 8, 4, 2, 64, 0, true, 2>},
+    {"g8u12_b64", launch_h<8, 12, 4, 2, 64, 0, true, 2>},
+    {"g8u24_b64", launch_h<8, 24, 4, 2, 64, 0, true, 2>},
+    {"g16u8_b64", launch_h<16, 8, 4, 2, 64, 0, true, 2>},
+    {"g4u16_b64", launch_h<4, 16, 4, 2, 64, 0, true, 2>},
+    {"tp32", launch_tp<32, 8, 16>},
+    {"tp64", launch_tp<64, 8, 16>},
+    {"tp128", launch_tp<128, 8, 16>},
+    {"tp256", launch_tp<256, 8, 16>},
+    {"tp16", launch_tp<16, 8, 16>},
+    {"tile32k", launch_tb<32u << 10>},
+    {"tile48k", launch_tb<48u << 10>},
+    {"tile64k", launch_tb<64u << 10>},
+    {"tile96k", launch_tb<96u << 10>},
+    {"tile128k", launch_tb<128u << 10>},
     {"floor_64B", launch_floor},
     {"quad_d4", launch_quad},
 };
