@@ -245,14 +245,11 @@ def main():
     bad = eng.sync()
     kern_avg_s = ev[0].elapsed_time(ev[1]) / 1e3 / args.steps
 
-    # parity of the measured kernel on this rank's batch (one more launch of
-    # the same instance over arenas[0], outside the timed region)
+    # one more launch of the same kernel instance over arenas[0], outside the
+    # timed region: its results are what the CPU leg checks against the oracle
     eng.batch_tensors(arenas[0], descs[0], out, stream=stream)
     torch.cuda.synchronize()
-    par = parity_sample(batch, out)
-    par_fail = dist.sum(0.0 if par["bit_exact"] else 1.0, dev)
 
-    # parity spot check of the last step's results against the oracle
     payload_rank = batch.payload_bytes
     total_payload = dist.sum(float(payload_rank), dev)
     algo_bytes = batch.algorithmic_bytes
@@ -300,16 +297,17 @@ def main():
             "avg_launch_us": kern_avg_s * 1e6,
         },
         "bad_descriptors": bad,
-        "parity_sample": dict(par, ranks_failed=int(par_fail)),
     }
 
     if dist.rank == 0 and not args.no_cpu:
+        # The CPU leg (rank 0): the oracle as the checker of the measured
+        # kernel's own results, then as the timed scalar baseline.
+        result["parity_sample"] = parity_sample(batch, out)
         cb, _ = cpu_baseline(batch, args.cpu_seconds, 1)
         result["cpu_baseline"] = cb
-        if args.cpu_threads or True:
-            th = args.cpu_threads or min(16, os.cpu_count() or 1)
-            cbm, _ = cpu_baseline(batch, max(2.0, args.cpu_seconds / 4), th)
-            result["cpu_baseline_multicore"] = cbm
+        th = args.cpu_threads or min(16, os.cpu_count() or 1)
+        cbm, _ = cpu_baseline(batch, max(2.0, args.cpu_seconds / 4), th)
+        result["cpu_baseline_multicore"] = cbm
 
     if dist.rank == 0:
         print(json.dumps(result), flush=True)
