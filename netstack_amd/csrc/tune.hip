@@ -215,6 +215,40 @@ hipError_t launch_quad(const uint8_t* arena, uint64_t arena_bytes, const void* d
   return hipGetLastError();
 }
 
+// The same floor with WG-thread workgroups and PER packets per lane (grid
+// shrinks accordingly): is a 14 us small-packet kernel limited by workgroup
+// dispatch?
+template <int WG, int PER>
+__global__ __launch_bounds__(WG) void small_floor_wg(const uint8_t* __restrict__ arena, const uint4* __restrict__ desc,
+                                                     uint32_t n, uint16_t* __restrict__ out) {
+  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)arena, (short)0, (int)0x7FFFFFF0, 0x00020000);
+  uint4 v[PER][4];
+  uint4 raw[PER];
+#pragma unroll
+  for (int p = 0; p < PER; ++p) {
+    const uint64_t i = ((uint64_t)blockIdx.x * PER + p) * WG + threadIdx.x;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[p][j] = bload(rsrc, i < n ? (uint32_t)(i * 64 + 16 * j) : 0x7FFFFFF0u);
+    raw[p] = i < n ? desc[i] : make_uint4(0, 0, 0, 0);
+  }
+#pragma unroll
+  for (int p = 0; p < PER; ++p) {
+    const uint64_t i = ((uint64_t)blockIdx.x * PER + p) * WG + threadIdx.x;
+    uint32_t T = 0, W = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) sad_chunk(v[p][j], T, W);
+    if (i < n) out[i] = (uint16_t)fold1((raw[p].w & 0xFFFFu) + s_of(T, W, (raw[p].w >> 16) & 1u));
+  }
+}
+
+template <int WG, int PER>
+hipError_t launch_floor_wg(const uint8_t* arena, uint64_t arena_bytes, const void* desc, uint32_t n,
+                           uint16_t* out, unsigned long long* err, hipStream_t s) {
+  hipLaunchKernelGGL((small_floor_wg<WG, PER>), dim3((n + WG * PER - 1) / (WG * PER)), dim3(WG), 0, s, arena,
+                     reinterpret_cast<const uint4*>(desc), n, out);
+  return hipGetLastError();
+}
+
 hipError_t launch_floor(const uint8_t* arena, uint64_t arena_bytes, const void* desc, uint32_t n,
                         uint16_t* out, unsigned long long* err, hipStream_t s) {
   hipLaunchKernelGGL(small_floor, dim3((n + 255) / 256), dim3(256), 0, s, arena, arena_bytes,
@@ -264,6 +298,13 @@ static const Variant kVariants[] = {
     {"tile96k", launch_tb<96u << 10>},
     {"tile128k", launch_tb<128u << 10>},
     {"floor_64B", launch_floor},
+    {"floor_wg256_p1", launch_floor_wg<256, 1>},
+    {"floor_wg512_p1", launch_floor_wg<512, 1>},
+    {"floor_wg1024_p1", launch_floor_wg<1024, 1>},
+    {"floor_wg256_p2", launch_floor_wg<256, 2>},
+    {"floor_wg256_p4", launch_floor_wg<256, 4>},
+    {"floor_wg128_p1", launch_floor_wg<128, 1>},
+    {"floor_wg64_p1", launch_floor_wg<64, 1>},
     {"quad_d4", launch_quad},
 };
 
