@@ -47,7 +47,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", type=int, default=2, choices=(2, 3, 4, 5))
+    ap.add_argument("--config", type=int, default=2, choices=(2, 3, 4, 5, 7),
+                    help="BASELINE.json configs[k-1]; 7 = device-resident RX verification (SURVEY §8(f) rank 2)")
     ap.add_argument("--mode", default="dev", choices=("dev", "host"))
     ap.add_argument("--rotate", type=int, default=0, help="distinct batches cycled per step (0 = auto)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline time budget")
@@ -184,15 +185,16 @@ def parity_sample(batch, out_dev, k: int = 65536) -> dict:
             "which": "first and last 65536 packets of the timed batch, results of the measured kernel"}
 
 
-def kernel_name(arena_bytes: int, n: int) -> str:
+def kernel_name(arena_bytes: int, n: int, chained: bool = False) -> str:
     """The csum_hyb instance launch_batch picks (csum_kernels.hip
     launch_batch / launch_hyb / launch_hyb_tp), as rocprofv3 names it."""
     win = "true" if arena_bytes + 64 >= 0xFFFF0000 else "false"
+    ch = "true" if chained else "false"
     if arena_bytes // n >= 256:
         want = (64 << 10) // max(arena_bytes // n, 1)  # kTileBytes
         tp = next((t for t in (256, 128, 64, 32, 16, 8, 4, 2) if want >= t), 1)
-        return f"nsk::csum_hyb<256,{tp},8,16,4,2,0,true,{win},2>"
-    return f"nsk::csum_hyb<256,256,16,8,4,2,5,true,{win},1>"
+        return f"nsk::csum_hyb<256,{tp},8,16,4,2,0,true,{win},2,{ch}>"
+    return f"nsk::csum_hyb<256,256,16,8,4,2,5,true,{win},1,{ch}>"
 
 
 def main():
@@ -209,6 +211,8 @@ def main():
     eng = Engine(dist.local)
 
     cfg = args.config
+    if cfg == 7:
+        return rx_mode(args, dist, eng, dev)
     batch = rank_batch(cfg, dist.rank, dist.world)
     rotate = args.rotate or (4 if cfg == 3 else 1)
     if cfg == 5 and rotate != 1:
@@ -309,6 +313,84 @@ def main():
         cbm, _ = cpu_baseline(batch, max(2.0, args.cpu_seconds / 4), th)
         result["cpu_baseline_multicore"] = cbm
 
+    if dist.rank == 0:
+        print(json.dumps(result), flush=True)
+    eng.close()
+    dist.close()
+
+
+RX_N = 1 << 20
+
+
+def rx_mode(args, dist, eng, dev):
+    """Device-resident RX verification: 1M received
+    1500-B IPv4/TCP packets per GPU in HBM, three chained descriptors per
+    packet (IPv4 header; pseudo-header addresses; TCP header + payload), one
+    ns_csum_batch_dev(NS_BATCH_CHAINED) per step = the checksum kernel (partial
+    sums and continuation flags) plus the csum_chain pass that folds the runs.  Every 1000th packet has a corrupted payload byte:
+    the check after the timed region requires exactly those TCP sums to fail
+    and every IPv4 header and every other TCP segment to sum to 0xffff
+    (segment.go:180, checker.go:51-53) — a size-independent property over
+    all 1M packets.  value = received packet bytes / s (GiB/s)."""
+    import torch
+
+    from netstack_amd import workloads as W
+
+    arena, d, bad_idx = W.rx_batch(RX_N, 7000 + dist.rank, dev, corrupt_every=1000)
+    desc = torch.from_numpy(d.view(np.uint8).copy()).to(dev)
+    out = torch.empty(len(d), dtype=torch.int16, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    ev = [torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)]
+    state = {"i": 0}
+
+    def step():
+        k = state["i"]
+        if k == args.warmup:
+            ev[0].record(stream)
+        eng.batch_tensors(arena, desc, out, chained=True, stream=stream)
+        state["i"] = k + 1
+        if state["i"] == args.warmup + args.steps:
+            ev[1].record(stream)
+
+    wall, _ = timed_region(step, torch.cuda.synchronize, dist, args.steps, args.warmup, dev)
+    bad = eng.sync()
+    kern_avg_s = ev[0].elapsed_time(ev[1]) / 1e3 / args.steps
+    res = out.cpu().numpy().view(np.uint16)
+    ip_ok = res[0::3] == 0xFFFF
+    tcp_fail = np.flatnonzero(res[2::3] != 0xFFFF)
+    prop_ok = bool(ip_ok.all()) and np.array_equal(tcp_fail, bad_idx)
+    fails = dist.sum(0.0 if prop_ok else 1.0, dev)
+    pkt_bytes = RX_N * W.RX_PKT
+    total = dist.sum(float(pkt_bytes), dev)
+    n_desc = len(d)
+    # packet bytes + the 8-B address re-read + per descriptor: 16-B read,
+    # u32 partial + flag byte written, then read back and a u16 result written
+    algo = pkt_bytes + 8 * RX_N + n_desc * (16 + 5 + 5 + 2)
+    achieved = algo / kern_avg_s / 1e9
+    result = {
+        "metric": "RX checksum verification GiB/s device-resident (IPv4 + TCP, 1500-B packets)",
+        "value": total * args.steps / wall / GIB, "unit": "GiB/s", "n_gpus": dist.world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": wall / args.steps * 1e3,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic received packets (valid IPv4/TCP checksums, 1 in 1000 corrupted), resident in HBM",
+        "config": {"workload": "rx: 1,048,576 x 1500-B IPv4/TCP packets per GPU, 3 chained descriptors each",
+                   "packets_per_gpu": RX_N, "descriptors_per_gpu": n_desc},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "kernel": kernel_name(arena.numel(), n_desc, chained=True) + " + nsk::csum_chain",
+                     "algorithmic_bytes_per_launch": algo, "avg_launch_us": kern_avg_s * 1e6},
+        "bad_descriptors": bad,
+        "property_check": {"ipv4_all_valid": bool(ip_ok.all()), "tcp_failures": int(tcp_fail.size),
+                           "expected_failures": int(bad_idx.size), "ok": prop_ok, "ranks_failed": int(fails)},
+    }
+    if dist.rank == 0 and not args.no_cpu:
+        import oracle as O
+
+        # CPU leg: the oracle on the first 65,536 packets' descriptors, same bytes
+        k = 3 * 65536
+        span = int(d["off"][k - 1] + d["len"][k - 1])
+        want, _ = O.c_batch(arena[:span].cpu().numpy(), d[:k], chained=True)
+        result["parity_sample"] = {"packets": k // 3, "bit_exact": bool(np.array_equal(res[:k], want))}
     if dist.rank == 0:
         print(json.dumps(result), flush=True)
     eng.close()

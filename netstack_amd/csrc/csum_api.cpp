@@ -186,6 +186,10 @@ struct DeviceGuard {
   }
 };
 
+// Chained-batch scratch for n descriptors: n u32 partials + n continuation
+// bytes (nsk::launch_batch).
+size_t chain_words(uint64_t n) { return (size_t)(n + (n + 3) / 4); }
+
 bool any_cont(const ns_pkt_desc* d, uint32_t n) {
   for (uint32_t i = 0; i < n; ++i)
     if (d[i].flags & NS_DESC_CONT) return true;
@@ -233,7 +237,7 @@ int run_zero_copy(ns_csum_ctx* ctx, SmallReq* const* reqs, size_t nreq) {
   const uint64_t o_off = nd * sizeof(ns_pkt_desc);
   int rc;
   if ((rc = ctx->z_buf.ensure(std::max<uint64_t>(kPassTableBytes, o_off + nd * 2))) != NS_OK) return rc;
-  if (chained && (rc = ctx->d_part[0].ensure(nd)) != NS_OK) return rc;
+  if (chained && (rc = ctx->d_part[0].ensure(chain_words(nd))) != NS_OK) return rc;
   uint8_t* z = ctx->z_buf.p;
   ns_pkt_desc* zd = reinterpret_cast<ns_pkt_desc*>(z);
   uint64_t k = 0;
@@ -425,7 +429,7 @@ int run_host_batch(ns_csum_ctx* ctx, const uint8_t* h_arena, uint64_t arena_byte
     if ((rc = ctx->d_out[slot].ensure(cnt)) != NS_OK) return rc;
     if ((rc = ctx->h_desc[slot].ensure(cnt)) != NS_OK) return rc;
     if ((rc = ctx->h_out[slot].ensure(cnt)) != NS_OK) return rc;
-    if (chained && (rc = ctx->d_part[slot].ensure(cnt)) != NS_OK) return rc;
+    if (chained && (rc = ctx->d_part[slot].ensure(chain_words(cnt))) != NS_OK) return rc;
     ns_pkt_desc* hd = ctx->h_desc[slot].p;
     for (uint32_t q = 0; q < cnt; ++q) {
       hd[q] = h_desc[k + q];
@@ -781,7 +785,7 @@ int ns_csum_batch_dev(ns_csum_ctx* ctx, const uint8_t* d_arena, uint64_t arena_b
   uint32_t* part = nullptr;
   if (batch_flags & NS_BATCH_CHAINED) {
     std::lock_guard<std::mutex> lk(ctx->mu);
-    int rc = ctx->partial.ensure(n);
+    int rc = ctx->partial.ensure(chain_words(n));
     if (rc != NS_OK) return rc;
     part = ctx->partial.p;
   }

@@ -8,9 +8,10 @@
 namespace nsk {
 
 // Enqueue the checksum of n descriptors (16-byte ns_pkt_desc, device memory)
-// over `arena` on `stream`.  With `partial` != nullptr the per-descriptor
-// 32-bit partial sums go to `partial` and a chain fix-up pass resolves
-// NS_DESC_CONT runs into `out`; otherwise every descriptor is independent.
+// over `arena` on `stream`.  With `partial` != nullptr (room for n u32 plus
+// n bytes) the per-descriptor partial sums and continuation flags go there
+// and a chain pass folds NS_DESC_CONT runs into `out`; otherwise every
+// descriptor is independent.
 // Out-of-range descriptors are summed as empty and counted in *err.
 // `sizing_bytes` (0: arena_bytes) is the byte count the launcher sizes tiles
 // by — the payload of a batch whose "arena" is the whole address space

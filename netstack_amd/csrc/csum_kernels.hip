@@ -147,17 +147,18 @@ __device__ __forceinline__ uint32_t group_sum(uint32_t s) {
 // One validated descriptor.
 struct Pkt {
   uint64_t A;  // absolute address of the first byte
-  uint32_t len, init, odd;
+  uint32_t len, init, odd, cont;
 };
 
 __device__ __forceinline__ Pkt decode(uint4 raw, bool mine, uint64_t arena_abs,
                                       uint64_t arena_bytes, unsigned long long* err) {
-  Pkt d{0ull, 0u, 0u, 0u};
+  Pkt d{0ull, 0u, 0u, 0u, 0u};
   if (!mine) return d;
   const uint64_t off = (uint64_t)raw.x | ((uint64_t)raw.y << 32);
   uint32_t len = raw.z;
   d.init = raw.w & 0xFFFFu;
   d.odd = (raw.w >> 16) & 1u;
+  d.cont = (raw.w >> 17) & 1u;
   if (off > arena_bytes || (uint64_t)len > arena_bytes - off) {
     len = 0;
     atomicAdd(err, 1ull);
@@ -199,12 +200,6 @@ __device__ __forceinline__ uint4 edge_mask(uint4 w, uint32_t ci, uint32_t lastc,
   return w;
 }
 
-__device__ __forceinline__ void put_result(uint32_t init, uint32_t s, uint64_t i,
-                                           uint16_t* out, uint32_t* partial) {
-  if (partial) partial[i] = s;
-  else out[i] = (uint16_t)fold1(init + s);
-}
-
 // W-only accumulation.  The result fold1(initial + S) depends on S only
 // through S mod 65535 and whether initial + S == 0, as long as Go's uint32
 // accumulator does not wrap (initial + S < 2^32, i.e. packets of at most
@@ -212,8 +207,8 @@ __device__ __forceinline__ void put_result(uint32_t init, uint32_t s, uint64_t i
 // word sum is S == 256*W (phase 0) or W (phase 1) (mod 65535), and S == 0 iff
 // every byte is 0 iff W == 0.  So those packets need only W — one v_sad_u16
 // per dword — and s_class() turns a packet's W total into a value with the
-// same fold1 behaviour as S (also as a chain partial: csum_chain adds it to a
-// u16).  Tiles holding a longer packet accumulate the exact S (EX = true).
+// same fold1 behaviour as S (also as a chain partial: a chained run adds it to
+// a u16).  Tiles holding a longer packet accumulate the exact S (EX = true).
 constexpr uint32_t kWOnlyMaxChunks = 8190;
 
 __device__ __forceinline__ uint32_t s_class(uint32_t W, uint32_t phase) {
@@ -378,10 +373,10 @@ __device__ __forceinline__ uint32_t direct_sum(const Srd& r, const PktInfo& p) {
 // One tile through the scan path (thread t holds packet p of global index i).
 // GL = 64-bit global loads (tile span >= 4 GiB) instead of the window SRD.
 // Every thread of the block must call it.
+// Returns this thread's packet sum (finish_tile turns it into the result).
 template <int WG, int TP, int GB, int UB, int US, int AUXB, bool LA, bool GL, int SU>
-__device__ __forceinline__ void hyb_scan_tile(HybLds<WG>& L, const Srd& r, const PktInfo& p,
-                                              bool mine, uint64_t i, uint16_t* __restrict__ out,
-                                              uint32_t* __restrict__ partial, uint32_t big_chunks) {
+__device__ __forceinline__ uint32_t hyb_scan_tile(HybLds<WG>& L, const Srd& r, const PktInfo& p,
+                                                  uint32_t big_chunks) {
   constexpr int P = WG;
   constexpr int NW = WG / 64;
   constexpr int NG = WG / GB;
@@ -554,10 +549,26 @@ __device__ __forceinline__ void hyb_scan_tile(HybLds<WG>& L, const Srd& r, const
   if (exact) loops(std::true_type{});
   else loops(std::false_type{});
   __syncthreads();
+  const uint32_t acc = L.acc[t];
+  return exact ? acc : s_class(acc, p.ew >> 31);
+}
 
-  if (mine) {
-    const uint32_t acc = L.acc[t];
-    put_result(p.init, exact ? acc : s_class(acc, p.ew >> 31), i, out, partial);
+// The tile's results.  Unchained: fold1(initial + s).  Chained (CH,
+// NS_DESC_CONT runs): a run head stores its folded value fold1(initial + s)
+// (descriptor 0 heads its run with initial 0), a continuation its s, each
+// with a one-byte continuation flag after the n partials; csum_chain folds
+// the runs from those alone (4 + 1 bytes per descriptor, no descriptor
+// re-read).
+template <bool CH>
+__device__ __forceinline__ void finish_tile(uint32_t s, const Pkt& d, bool mine, uint64_t i, uint64_t n,
+                                            uint16_t* __restrict__ out, uint32_t* __restrict__ partial) {
+  if (!mine) return;
+  if constexpr (CH) {
+    const bool head = !d.cont || i == 0;
+    partial[i] = head ? fold1((d.cont ? 0u : d.init) + s) : s;
+    reinterpret_cast<uint8_t*>(partial + n)[i] = head ? 0u : 1u;
+  } else {
+    out[i] = (uint16_t)fold1(d.init + s);
   }
 }
 
@@ -566,9 +577,10 @@ __device__ __forceinline__ void hyb_scan_tile(HybLds<WG>& L, const Srd& r, const
 // small-packet batches.
 // TP = descriptors per tile (<= WG): large packets get fewer per workgroup so
 // a batch of 64 KiB GSO buffers still spreads over every CU.
-// SU = small runs issued per lane per iteration.
+// SU = small runs issued per lane per iteration; CH = chained batch
+// (finish_tile writes partials and continuation flags for csum_chain).
 template <int WG, int TP, int GB, int UB, int US, int AUXB, int UD = 0, bool LA = true, bool WIN = false,
-          int SU = 1>
+          int SU = 1, bool CH = false>
 __global__ __launch_bounds__(WG) void csum_hyb(
     const uint8_t* __restrict__ arena, uint64_t arena_bytes,
     const uint4* __restrict__ desc, uint32_t n, uint16_t* __restrict__ out,
@@ -595,35 +607,43 @@ __global__ __launch_bounds__(WG) void csum_hyb(
     const PktInfo p = pkt_info(d, w.base);
     if (UD > 0 && w.small) {
       const uint32_t s = direct_sum<UD ? UD : 1>(r, p);
-      if (mine) put_result(p.init, s, i, out, partial);
+      finish_tile<CH>(s, d, mine, i, n, out, partial);
       return;
     }
-    hyb_scan_tile<WG, TP, GB, UB, US, AUXB, LA, false, SU>(L, r, p, mine, i, out, partial, big_chunks);
+    const uint32_t s = hyb_scan_tile<WG, TP, GB, UB, US, AUXB, LA, false, SU>(L, r, p, big_chunks);
+    finish_tile<CH>(s, d, mine, i, n, out, partial);
   } else if constexpr (WIN) {
     // The tile spans >= 4 GiB: 64-bit global loads, fewer in flight per lane
     // so this rarely taken path does not raise the kernel's register count.
     const Srd r = make_srd(0ull, 0ull);
     const PktInfo p = pkt_info(d, 0ull);
-    hyb_scan_tile<WG, TP, 16, 4, 4, AUXB, LA, true, 1>(L, r, p, mine, i, out, partial, big_chunks);
+    const uint32_t s = hyb_scan_tile<WG, TP, 16, 4, 4, AUXB, LA, true, 1>(L, r, p, big_chunks);
+    finish_tile<CH>(s, d, mine, i, n, out, partial);
   }
 }
 
-// Sequential chain fix-up for NS_DESC_CONT runs (checksum.go:89 / the
-// `xsum = Checksum(v, xsum)` loops): out[k] = fold1(out[k-1] + S_k).
-__global__ void csum_chain(const uint4* __restrict__ desc, uint32_t n,
-                           const uint32_t* __restrict__ partial,
-                           uint16_t* __restrict__ out) {
+// Sequential fold of NS_DESC_CONT runs (checksum.go:89 / the
+// `xsum = Checksum(v, xsum)` loops) over finish_tile's chained output: one
+// thread per run head, out[k] = fold1(out[k-1] + s_k).
+__global__ void csum_chain(const uint32_t* __restrict__ partial, uint32_t n, uint16_t* __restrict__ out) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint8_t* cont = reinterpret_cast<const uint8_t*>(partial + n);
   if (i >= n) return;
-  const uint32_t w = desc[i].w;
-  const bool cont = (w >> 16) & 2u;
-  if (cont && i > 0) return;  // not a run head
-  uint32_t s = fold1((cont ? 0u : (w & 0xFFFFu)) + partial[i]);
-  out[i] = (uint16_t)s;
-  for (uint64_t k = i + 1; k < n; ++k) {
-    if (!((desc[k].w >> 16) & 2u)) break;
-    s = fold1(s + partial[k]);
-    out[k] = (uint16_t)s;
+  // This descriptor and the next one are loaded together (most runs are one
+  // or two descriptors long: a header and its payload), so a short run costs
+  // one memory round trip.
+  const bool has1 = i + 1 < n;
+  const uint8_t c0 = cont[i], c1 = has1 ? cont[i + 1] : 0;
+  const uint32_t p0 = partial[i], p1 = has1 ? partial[i + 1] : 0u;
+  if (c0) return;
+  uint32_t v = p0;
+  out[i] = (uint16_t)v;
+  if (!c1) return;
+  v = fold1(v + p1);
+  out[i + 1] = (uint16_t)v;
+  for (uint64_t k = i + 2; k < n && cont[k]; ++k) {
+    v = fold1(v + partial[k]);
+    out[k] = (uint16_t)v;
   }
 }
 
@@ -641,12 +661,18 @@ static hipError_t launch_hyb_tp(const uint8_t* arena, uint64_t arena_bytes, cons
   const uint4* d = reinterpret_cast<const uint4*>(desc);
   // One SRD over the whole arena when it fits (arena base rounded down to 16 B
   // plus the arena), else per-tile windows.
-  if (((uintptr_t)arena & 15u) + arena_bytes + 64 < kMaxSrdBytes)
-    hipLaunchKernelGGL((csum_hyb<WG, TP, GB, UB, US, AUXB, UD, LA, false, SU>), dim3(grid), dim3(WG), 0,
-                       stream, arena, arena_bytes, d, n, out, partial, err, big_chunks);
-  else
-    hipLaunchKernelGGL((csum_hyb<WG, TP, GB, UB, US, AUXB, UD, LA, true, SU>), dim3(grid), dim3(WG), 0,
-                       stream, arena, arena_bytes, d, n, out, partial, err, big_chunks);
+  const bool win = ((uintptr_t)arena & 15u) + arena_bytes + 64 >= kMaxSrdBytes;
+#define NSK_LAUNCH(W, C)                                                                              \
+  hipLaunchKernelGGL((csum_hyb<WG, TP, GB, UB, US, AUXB, UD, LA, W, SU, C>), dim3(grid), dim3(WG), 0, \
+                     stream, arena, arena_bytes, d, n, out, partial, err, big_chunks)
+  if (partial) {
+    if (win) NSK_LAUNCH(true, true);
+    else NSK_LAUNCH(false, true);
+  } else {
+    if (win) NSK_LAUNCH(true, false);
+    else NSK_LAUNCH(false, false);
+  }
+#undef NSK_LAUNCH
   return hipGetLastError();
 }
 
@@ -711,9 +737,7 @@ hipError_t launch_batch(const uint8_t* arena, uint64_t arena_bytes,
     e = launch_hyb<16, 8, 4, 2, 5>(arena, arena_bytes, desc, n, out, partial, err, stream, 64u);
   }
   if (e != hipSuccess || partial == nullptr) return e;
-  const uint32_t blocks = (n + 255) / 256;
-  hipLaunchKernelGGL(csum_chain, dim3(blocks), dim3(256), 0, stream,
-                     reinterpret_cast<const uint4*>(desc), n, partial, out);
+  hipLaunchKernelGGL(csum_chain, dim3((n + 255) / 256), dim3(256), 0, stream, partial, n, out);
   return hipGetLastError();
 }
 

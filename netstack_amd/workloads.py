@@ -203,3 +203,77 @@ def config(k: int, n: int | None = None) -> Batch:
         # write, connect.go:668-702) in bulk — the large-packet tile sizing case.
         return uniform("gso_16Kx64KiB", 6, n or (16 << 10), 65536)
     raise ValueError(k)
+
+
+# ---------------------------------------------------------------------------
+# Received IPv4/TCP packets for device-resident RX verification (SURVEY.md
+# §8(f) rank 2: segment.parse's csumValid, transport/tcp/segment.go:166-181,
+# and the IPv4 header check of ipv4.go's IsValid/checker.go:51-53).
+# ---------------------------------------------------------------------------
+RX_PKT = 1500      # IPv4 total length
+RX_STRIDE = 1504   # 16-B-aligned packet starts
+RX_IHL = 20
+RX_TCP = RX_PKT - RX_IHL  # TCP header + payload bytes (1480)
+
+
+def _fold_np(s):
+    s = (s & 0xFFFF) + (s >> 16)
+    return (s & 0xFFFF) + (s >> 16)
+
+
+def rx_batch(n: int, seed: int, device, corrupt_every: int = 0):
+    """n received 1500-B IPv4/TCP packets packed at RX_STRIDE in HBM, with
+    valid IPv4 and TCP checksums (RFC 1071, computed here with torch integer
+    ops as plain data generation), and the descriptor table that verifies
+    them: per packet
+      3i    IPv4 header [0, 20), initial 0           -> must sum to 0xffff
+      3i+1  src+dst addresses [12, 20), initial = ChecksumCombine(1480, 6)
+            (PseudoHeaderChecksum, checksum.go:112-122: the length and
+            protocol words are host-known, the addresses are in the packet)
+      3i+2  TCP header + payload [20, 1500), NS_DESC_CONT (a restart over an
+            even-length piece: segment.go:177-179)  -> must sum to 0xffff
+    With corrupt_every = k > 0, one payload byte of every k-th packet is
+    flipped after its checksum was written (tcp_test.go:3246-3254): exactly
+    those TCP sums fail.  Returns (arena uint8 tensor, desc, bad indices)."""
+    import torch
+
+    arena = random_bytes_torch(seed, n * RX_STRIDE, device)
+    p = arena.view(n, RX_STRIDE)[:, :RX_PKT]
+    p[:, 0] = 0x45
+    p[:, 1] = 0
+    p[:, 2] = RX_PKT >> 8
+    p[:, 3] = RX_PKT & 0xFF
+    p[:, 6] = 0x40
+    p[:, 7] = 0
+    p[:, 8] = 64
+    p[:, 9] = 6
+    p[:, 10:12] = 0
+    p[:, 32] = 0x50  # data offset 5 words
+    p[:, 33] = 0x18  # PSH | ACK
+    p[:, 36:40] = 0  # checksum, urgent pointer
+
+    def be_sum(lo, hi):
+        w = p[:, lo:hi].to(torch.int64)
+        return (w[:, 0::2] * 256 + w[:, 1::2]).sum(dim=1)
+
+    ip = (~_fold_np(be_sum(0, RX_IHL))) & 0xFFFF
+    p[:, 10] = (ip >> 8).to(torch.uint8)
+    p[:, 11] = (ip & 0xFF).to(torch.uint8)
+    tcp = (~_fold_np(be_sum(RX_IHL, RX_PKT) + be_sum(12, 20) + RX_TCP + 6)) & 0xFFFF
+    p[:, 36] = (tcp >> 8).to(torch.uint8)
+    p[:, 37] = (tcp & 0xFF).to(torch.uint8)
+    bad = np.arange(0, n, corrupt_every, dtype=np.int64) if corrupt_every > 0 else np.zeros(0, np.int64)
+    if bad.size:
+        idx = torch.from_numpy(bad).to(device)
+        p[idx, 100] ^= 0x5A
+    base = np.arange(n, dtype=np.uint64) * np.uint64(RX_STRIDE)
+    d = np.zeros(3 * n, dtype=DESC_DTYPE)
+    d["off"][0::3] = base
+    d["len"][0::3] = RX_IHL
+    d["off"][1::3] = base + np.uint64(12)
+    d["len"][1::3] = 8
+    d["initial"][1::3] = RX_TCP + 6  # ChecksumCombine(1480, 6): no carry
+    d["off"][2::3] = base + np.uint64(RX_IHL)
+    d["len"][2::3] = RX_TCP
+    d["flags"][2::3] = 2  # NS_DESC_CONT
+    return arena, d, bad

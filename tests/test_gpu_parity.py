@@ -515,3 +515,23 @@ def test_concurrent_small_calls_are_combined_bit_exact(engine):
     for x in th:
         x.join(timeout=120)
     assert not errors, errors[:5]
+
+
+def test_rx_verification_batch_device_resident(engine):
+    """SURVEY §8(f) rank 2 on the device: received IPv4/TCP packets in HBM,
+    three chained descriptors per packet (workloads.rx_batch), one chained
+    batch_dev.  Every result bit-exact with the oracle, every IPv4 header and
+    every intact TCP segment sums to 0xffff, exactly the corrupted ones fail."""
+    import oracle as O
+    from netstack_amd import workloads as W
+
+    torch = _torch()
+    arena, d, bad_idx = W.rx_batch(20000, 77, "cuda", corrupt_every=97)
+    desc = torch.from_numpy(d.view(np.uint8).copy()).cuda()
+    out = engine.batch_tensors(arena, desc, chained=True)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy().view(np.uint16)
+    want, nbad = O.c_batch(arena.cpu().numpy(), d, chained=True)
+    assert nbad == 0 and np.array_equal(got, want)
+    assert (got[0::3] == 0xFFFF).all()
+    assert np.array_equal(np.flatnonzero(got[2::3] != 0xFFFF), bad_idx)

@@ -117,3 +117,27 @@ def test_batch_mt_matches(oracle_mod):
     assert bad == 0
     got = oracle_mod.c_batch_mt(arena, b.desc, 4)
     assert (got == want).all()
+
+
+def test_rx_batch_generator_valid_packets():
+    """workloads.rx_batch writes valid IPv4 and TCP checksums (checked by the
+    oracle composed as segment.parse and the IPv4 header check do) and breaks
+    exactly the packets it says it corrupts."""
+    import torch  # noqa: F401  (generator runs on the CPU device here)
+
+    import oracle as O
+    from netstack_amd import workloads as W
+
+    arena, d, bad = W.rx_batch(700, 3, "cpu", corrupt_every=11)
+    out, nbad = O.c_batch(arena.numpy(), d, chained=True)
+    assert nbad == 0
+    assert (out[0::3] == 0xFFFF).all()
+    assert np.array_equal(np.flatnonzero(out[2::3] != 0xFFFF), bad)
+    # the same TCP sums from the pure-Python chain of segment.parse (:176-180)
+    a = arena.numpy()
+    for i in (0, 1, 11, 699):
+        b = 1504 * i
+        xsum = O.py_pseudo_header(6, bytes(a[b + 12:b + 16]), bytes(a[b + 16:b + 20]), 1480)
+        xsum = O.py_checksum(bytes(a[b + 20:b + 40]), xsum)
+        xsum = O.py_checksum(bytes(a[b + 40:b + 1500]), xsum)
+        assert xsum == out[3 * i + 2]
