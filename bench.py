@@ -364,8 +364,8 @@ def rx_mode(args, dist, eng, dev):
     total = dist.sum(float(pkt_bytes), dev)
     n_desc = len(d)
     # packet bytes + the 8-B address re-read + per descriptor: 16-B read,
-    # u32 partial + flag byte written, then read back and a u16 result written
-    algo = pkt_bytes + 8 * RX_N + n_desc * (16 + 5 + 5 + 2)
+    # u32 partial + u16 flag written, then read back, and a u16 result written
+    algo = pkt_bytes + 8 * RX_N + n_desc * (16 + 6 + 6 + 2)
     achieved = algo / kern_avg_s / 1e9
     result = {
         "metric": "RX checksum verification GiB/s device-resident (IPv4 + TCP, 1500-B packets)",

@@ -186,9 +186,9 @@ struct DeviceGuard {
   }
 };
 
-// Chained-batch scratch for n descriptors: n u32 partials + n continuation
-// bytes (nsk::launch_batch).
-size_t chain_words(uint64_t n) { return (size_t)(n + (n + 3) / 4); }
+// Chained-batch scratch for n descriptors: n u32 partials + n u16
+// continuation flags (nsk::launch_batch).
+size_t chain_words(uint64_t n) { return (size_t)(n + (n + 1) / 2); }
 
 bool any_cont(const ns_pkt_desc* d, uint32_t n) {
   for (uint32_t i = 0; i < n; ++i)

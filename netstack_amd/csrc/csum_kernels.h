@@ -9,7 +9,7 @@ namespace nsk {
 
 // Enqueue the checksum of n descriptors (16-byte ns_pkt_desc, device memory)
 // over `arena` on `stream`.  With `partial` != nullptr (room for n u32 plus
-// n bytes) the per-descriptor partial sums and continuation flags go there
+// n u16) the per-descriptor partial sums and continuation flags go there
 // and a chain pass folds NS_DESC_CONT runs into `out`; otherwise every
 // descriptor is independent.
 // Out-of-range descriptors are summed as empty and counted in *err.

@@ -556,9 +556,10 @@ __device__ __forceinline__ uint32_t hyb_scan_tile(HybLds<WG>& L, const Srd& r, c
 // The tile's results.  Unchained: fold1(initial + s).  Chained (CH,
 // NS_DESC_CONT runs): a run head stores its folded value fold1(initial + s)
 // (descriptor 0 heads its run with initial 0), a continuation its s, each
-// with a one-byte continuation flag after the n partials; csum_chain folds
-// the runs from those alone (4 + 1 bytes per descriptor, no descriptor
-// re-read).
+// with a u16 continuation flag after the n partials (u16, not u8: a wave's
+// 64 flags then fill a whole 128-B line — byte flags cost 8.5 us more on 3M
+// descriptors, profiles/r01/tune_chained_b2b.log); csum_chain folds the runs
+// from those alone (6 bytes per descriptor, no descriptor re-read).
 template <bool CH>
 __device__ __forceinline__ void finish_tile(uint32_t s, const Pkt& d, bool mine, uint64_t i, uint64_t n,
                                             uint16_t* __restrict__ out, uint32_t* __restrict__ partial) {
@@ -566,7 +567,7 @@ __device__ __forceinline__ void finish_tile(uint32_t s, const Pkt& d, bool mine,
   if constexpr (CH) {
     const bool head = !d.cont || i == 0;
     partial[i] = head ? fold1((d.cont ? 0u : d.init) + s) : s;
-    reinterpret_cast<uint8_t*>(partial + n)[i] = head ? 0u : 1u;
+    reinterpret_cast<uint16_t*>(partial + n)[i] = head ? 0u : 1u;
   } else {
     out[i] = (uint16_t)fold1(d.init + s);
   }
@@ -627,13 +628,13 @@ __global__ __launch_bounds__(WG) void csum_hyb(
 // thread per run head, out[k] = fold1(out[k-1] + s_k).
 __global__ void csum_chain(const uint32_t* __restrict__ partial, uint32_t n, uint16_t* __restrict__ out) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint8_t* cont = reinterpret_cast<const uint8_t*>(partial + n);
+  const uint16_t* cont = reinterpret_cast<const uint16_t*>(partial + n);
   if (i >= n) return;
   // This descriptor and the next one are loaded together (most runs are one
   // or two descriptors long: a header and its payload), so a short run costs
   // one memory round trip.
   const bool has1 = i + 1 < n;
-  const uint8_t c0 = cont[i], c1 = has1 ? cont[i + 1] : 0;
+  const uint16_t c0 = cont[i], c1 = has1 ? cont[i + 1] : 0;
   const uint32_t p0 = partial[i], p1 = has1 ? partial[i + 1] : 0u;
   if (c0) return;
   uint32_t v = p0;

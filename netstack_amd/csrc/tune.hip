@@ -262,6 +262,28 @@ hipError_t launch_tb(const uint8_t* arena, uint64_t arena_bytes, const void* des
   return launch_hyb<8, 16, 4, 2, 0, true, 2>(arena, arena_bytes, desc, n, out, nullptr, err, s, 64u, 0, TB);
 }
 
+// Chained timing: the CH instance (partials + continuation flags) with or
+// without the csum_chain pass, over a scratch buffer owned here.
+static uint32_t* g_part = nullptr;
+static size_t g_part_n = 0;
+static uint32_t* part_for(uint32_t n) {
+  const size_t want = (size_t)n + (n + 1) / 2;
+  if (want > g_part_n) {
+    if (g_part) (void)hipFree(g_part);
+    if (hipMalloc(reinterpret_cast<void**>(&g_part), want * 4) != hipSuccess) return nullptr;
+    g_part_n = want;
+  }
+  return g_part;
+}
+template <bool FULL>
+hipError_t launch_chained(const uint8_t* arena, uint64_t arena_bytes, const void* desc, uint32_t n,
+                          uint16_t* out, unsigned long long* err, hipStream_t s) {
+  uint32_t* part = part_for(n);
+  if (!part) return hipErrorOutOfMemory;
+  if constexpr (FULL) return launch_batch(arena, arena_bytes, desc, n, out, part, err, s);
+  return launch_hyb<8, 16, 4, 2, 0, true, 2>(arena, arena_bytes, desc, n, out, part, err, s, 64u);
+}
+
 template <int TP, int GB, int UB>
 hipError_t launch_tp(const uint8_t* arena, uint64_t arena_bytes, const void* desc, uint32_t n,
                      uint16_t* out, unsigned long long* err, hipStream_t s) {
@@ -280,6 +302,8 @@ struct Variant {
 static const Variant kVariants[] = {
     {"prod_g8u16_b64", launch_h<8, 16, 4, 2, 64, 0, true, 2>},
     {"g8u16_su1", launch_h<8, 16, 4, 2, 64>},
+    {"chained_main", launch_chained<false>},
+    {"chained_full", launch_chained<true>},
     {"prod_small_d5", launch_h<16, 8, 4, 2, 64, 5>},
     {"g8u16_b32", launch_h<8, 16, 4, 2, 32, 0, true, 2>},
     {"g8u8_b64", launch_h<8, 8, 4, 2, 64, 0, true, 2>},
