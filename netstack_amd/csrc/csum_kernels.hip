@@ -120,7 +120,9 @@ __device__ __forceinline__ uint32_t group_sum(uint32_t s) {
 
 // ===========================================================================
 // csum_hyb — the checksum kernel.  One 256-thread workgroup owns a tile of
-// 256 descriptors.
+// TP <= 256 descriptors (about 64 KiB of payload, launch_hyb); packets of at
+// most 8190 chunks accumulate only the little-endian word sum W (see
+// kWOnlyMaxChunks), longer ones the exact (T, W) pair.
 //
 // Two lane shapes, chosen per packet.  Nontemporal loads stream at ~6.8 TB/s
 // on MI355X when every 128-B line is consumed by ONE wave instruction, and
