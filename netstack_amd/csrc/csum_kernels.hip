@@ -40,24 +40,6 @@ __device__ __forceinline__ uint32_t fold1(uint32_t v) {
   return (s + (s >> 16)) & 0xFFFFu;
 }
 
-// Byte mask of dword j (bytes 4j..4j+3) of a 16-byte chunk restricted to
-// bytes [lo, hi).
-__device__ __forceinline__ uint32_t dword_mask(int lo, int hi, int j) {
-  const int a = max(lo - 4 * j, 0);
-  const int b = min(hi - 4 * j, 4);
-  if (b <= a) return 0u;
-  const uint32_t below_b = (b >= 4) ? 0xFFFFFFFFu : ((1u << (8 * b)) - 1u);
-  return below_b & (0xFFFFFFFFu << (8 * a));
-}
-
-__device__ __forceinline__ uint4 mask_chunk(uint4 w, int lo, int hi) {
-  w.x &= dword_mask(lo, hi, 0);
-  w.y &= dword_mask(lo, hi, 1);
-  w.z &= dword_mask(lo, hi, 2);
-  w.w &= dword_mask(lo, hi, 3);
-  return w;
-}
-
 // Buffer resources cover < 4 GiB: a tile whose packets span more takes the
 // 64-bit-addressed path.
 constexpr uint64_t kMaxSrdBytes = 0xFFFF0000ull;
@@ -128,7 +110,7 @@ __device__ __forceinline__ uint32_t group_sum(uint32_t s) {
 // on MI355X when every 128-B line is consumed by ONE wave instruction, and
 // lose badly when a line is split across instructions (the evicted line is
 // fetched again).  So a packet of at least `big_chunks` chunks is split at
-// 128-B line boundaries (LA): its whole lines go to groups of GB lanes (runs
+// 128-B line boundaries: its whole lines go to groups of GB lanes (runs
 // of GB*UB chunks, lane li loads chunks li, li+GB, ...: one whole line per
 // group per load for GB = 8), and the partial lines it shares with its
 // neighbours — plus every smaller packet — go to single lanes (runs of US
@@ -196,12 +178,6 @@ __device__ __forceinline__ PktInfo pkt_info(const Pkt& d, uint64_t wbase) {
   return p;
 }
 
-__device__ __forceinline__ uint4 edge_mask(uint4 w, uint32_t ci, uint32_t lastc, uint32_t e) {
-  if (ci == 0u || ci == lastc)
-    w = mask_chunk(w, ci == 0u ? (int)(e & 31u) : 0, ci == lastc ? (int)((e >> 5) & 31u) : 16);
-  return w;
-}
-
 // W-only accumulation.  The result fold1(initial + S) depends on S only
 // through S mod 65535 and whether initial + S == 0, as long as Go's uint32
 // accumulator does not wrap (initial + S < 2^32, i.e. packets of at most
@@ -240,8 +216,8 @@ __device__ __forceinline__ uint32_t run_value(uint32_t T, uint32_t W, uint32_t p
 // first chunk and [hiex, 16) of its last (edge word e).  A run sums its chunks
 // unmasked and subtracts these (S is linear in T and W for a fixed phase):
 // one masked chunk per partial edge, in a branch taken only by lanes whose run
-// holds such an edge — a 16-B-aligned packet start never has one, so the
-// per-chunk mask work of edge_mask() is gone from every run.
+// holds such an edge — a 16-B-aligned packet start never has one, so no run
+// masks its chunks one by one.
 __device__ __forceinline__ uint32_t bytes_below(int c) {  // bytes [0, c) of a dword, c clamped to [0, 4]
   c = min(max(c, 0), 4);
   return c >= 4 ? 0xFFFFFFFFu : ((1u << (8 * c)) - 1u);
@@ -376,7 +352,7 @@ __device__ __forceinline__ uint32_t direct_sum(const Srd& r, const PktInfo& p) {
 // GL = 64-bit global loads (tile span >= 4 GiB) instead of the window SRD.
 // Every thread of the block must call it.
 // Returns this thread's packet sum (finish_tile turns it into the result).
-template <int WG, int TP, int GB, int UB, int US, int AUXB, bool LA, bool GL, int SU>
+template <int WG, int TP, int GB, int UB, int US, int AUXB, bool GL, int SU>
 __device__ __forceinline__ uint32_t hyb_scan_tile(HybLds<WG>& L, const Srd& r, const PktInfo& p,
                                                   uint32_t big_chunks) {
   constexpr int P = WG;
@@ -395,7 +371,7 @@ __device__ __forceinline__ uint32_t hyb_scan_tile(HybLds<WG>& L, const Srd& r, c
   // no byte masks: a partial first (last) chunk sends its whole line to the
   // lane runs — a line it shares with the neighbouring packet anyway.
   uint32_t h = nch, ts = nch;
-  const bool split = LA && nch >= big_chunks;
+  const bool split = nch >= big_chunks;
   if (split) {
     h = (8u - p.lp) & 7u;
     ts = ((p.lp + nch) & ~7u) - p.lp;
@@ -406,12 +382,9 @@ __device__ __forceinline__ uint32_t hyb_scan_tile(HybLds<WG>& L, const Srd& r, c
   // stays below 2^32 with RB >= 16; small runs per packet are bounded by
   // big_chunks / US + 4.
   const uint64_t nr = nch == 0 ? 0ull
-                      : !LA ? (nch >= big_chunks ? (uint64_t)((nch + RB - 1) / RB)
-                                                 : ((uint64_t)((nch + US - 1) / US) << 32))
-                      : split
-                          ? ((uint64_t)((ts - h + RB - 1) / RB) |
-                             ((uint64_t)((h + US - 1) / US + (nch - ts + US - 1) / US) << 32))
-                          : ((uint64_t)((nch + US - 1) / US) << 32);
+                      : split ? ((uint64_t)((ts - h + RB - 1) / RB) |
+                                 ((uint64_t)((h + US - 1) / US + (nch - ts + US - 1) / US) << 32))
+                              : ((uint64_t)((nch + US - 1) / US) << 32);
   uint64_t incl = nr;
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
@@ -481,7 +454,7 @@ __device__ __forceinline__ uint32_t hyb_scan_tile(HybLds<WG>& L, const Srd& r, c
         sr.lastc = inf.y - 1u;
         sr.ew = inf.z;
         cend = inf.y;
-        if (LA && (inf.z & kSplitBit)) {  // head runs cover [0, h), tail runs [ts, nch)
+        if (inf.z & kSplitBit) {  // head runs cover [0, h), tail runs [ts, nch)
           const uint32_t hh = (inf.z >> 10) & 15u, nh = (hh + US - 1) / US;
           if (k < nh) cend = hh;
           else sr.ci0 = inf.w + (k - nh) * US;
@@ -510,11 +483,8 @@ __device__ __forceinline__ uint32_t hyb_scan_tile(HybLds<WG>& L, const Srd& r, c
     for (uint32_t q = (uint32_t)(t / GB); q < RBt; q += NG) {
       const int pk = search(L.rb, q);
       const uint4 inf = L.info[pk];
-      uint32_t ci0 = (q - L.rb[pk]) * RB + li, cend = inf.y;
-      if constexpr (LA) {  // every big packet is split: body [h, ts)
-        ci0 += (inf.z >> 10) & 15u;
-        cend = inf.w;
-      }
+      // every big packet is split: the body [h, ts)
+      const uint32_t ci0 = (q - L.rb[pk]) * RB + li + ((inf.z >> 10) & 15u), cend = inf.w;
       uint4 v[UB];
       if constexpr (GL) {
         const uint64_t g0 = L.g[pk] + (uint64_t)ci0 * 16u;
@@ -530,7 +500,7 @@ __device__ __forceinline__ uint32_t hyb_scan_tile(HybLds<WG>& L, const Srd& r, c
       uint32_t T = 0, W = 0;
 #pragma unroll
       for (int j = 0; j < UB; ++j)
-        acc_chunk<EX>(LA ? v[j] : edge_mask(v[j], ci0 + (uint32_t)(GB * j), inf.y - 1u, inf.z), T, W);
+        acc_chunk<EX>(v[j], T, W);  // body chunks are whole chunks of the packet
       const uint32_t sg = group_sum<GB>(run_value<EX>(T, W, inf.z >> 31));
       if (li == 0) atomicAdd(&L.acc[pk], sg);
     }
@@ -582,7 +552,7 @@ __device__ __forceinline__ void finish_tile(uint32_t s, const Pkt& d, bool mine,
 // a batch of 64 KiB GSO buffers still spreads over every CU.
 // SU = small runs issued per lane per iteration; CH = chained batch
 // (finish_tile writes partials and continuation flags for csum_chain).
-template <int WG, int TP, int GB, int UB, int US, int AUXB, int UD = 0, bool LA = true, bool WIN = false,
+template <int WG, int TP, int GB, int UB, int US, int AUXB, int UD = 0, bool WIN = false,
           int SU = 1, bool CH = false>
 __global__ __launch_bounds__(WG) void csum_hyb(
     const uint8_t* __restrict__ arena, uint64_t arena_bytes,
@@ -613,14 +583,14 @@ __global__ __launch_bounds__(WG) void csum_hyb(
       finish_tile<CH>(s, d, mine, i, n, out, partial);
       return;
     }
-    const uint32_t s = hyb_scan_tile<WG, TP, GB, UB, US, AUXB, LA, false, SU>(L, r, p, big_chunks);
+    const uint32_t s = hyb_scan_tile<WG, TP, GB, UB, US, AUXB, false, SU>(L, r, p, big_chunks);
     finish_tile<CH>(s, d, mine, i, n, out, partial);
   } else if constexpr (WIN) {
     // The tile spans >= 4 GiB: 64-bit global loads, fewer in flight per lane
     // so this rarely taken path does not raise the kernel's register count.
     const Srd r = make_srd(0ull, 0ull);
     const PktInfo p = pkt_info(d, 0ull);
-    const uint32_t s = hyb_scan_tile<WG, TP, 16, 4, 4, AUXB, LA, true, 1>(L, r, p, big_chunks);
+    const uint32_t s = hyb_scan_tile<WG, TP, 16, 4, 4, AUXB, true, 1>(L, r, p, big_chunks);
     finish_tile<CH>(s, d, mine, i, n, out, partial);
   }
 }
@@ -655,7 +625,7 @@ __global__ void csum_chain(const uint32_t* __restrict__ partial, uint32_t n, uin
 // ---- launchers (C++ linkage, used by csum_api.cpp) ------------------------
 namespace nsk {
 
-template <int TP, int GB, int UB, int US, int AUXB, int UD, bool LA, int SU = 1>
+template <int TP, int GB, int UB, int US, int AUXB, int UD, int SU = 1>
 static hipError_t launch_hyb_tp(const uint8_t* arena, uint64_t arena_bytes, const void* desc,
                                 uint32_t n, uint16_t* out, uint32_t* partial,
                                 unsigned long long* err, hipStream_t stream, uint32_t big_chunks) {
@@ -666,7 +636,7 @@ static hipError_t launch_hyb_tp(const uint8_t* arena, uint64_t arena_bytes, cons
   // plus the arena), else per-tile windows.
   const bool win = ((uintptr_t)arena & 15u) + arena_bytes + 64 >= kMaxSrdBytes;
 #define NSK_LAUNCH(W, C)                                                                              \
-  hipLaunchKernelGGL((csum_hyb<WG, TP, GB, UB, US, AUXB, UD, LA, W, SU, C>), dim3(grid), dim3(WG), 0, \
+  hipLaunchKernelGGL((csum_hyb<WG, TP, GB, UB, US, AUXB, UD, W, SU, C>), dim3(grid), dim3(WG), 0, \
                      stream, arena, arena_bytes, d, n, out, partial, err, big_chunks)
   if (partial) {
     if (win) NSK_LAUNCH(true, true);
@@ -686,7 +656,7 @@ static hipError_t launch_hyb_tp(const uint8_t* arena, uint64_t arena_bytes, cons
 // descriptors vs 221 at 64 and 244 at 16; the Zipf batch 103 us at 64 vs 107
 // at 128 and 114 at 32; 64 KiB GSO buffers flat).
 constexpr uint64_t kTileBytes = 64u << 10;
-template <int GB, int UB, int US, int AUXB, int UD = 0, bool LA = true, int SU = 1>
+template <int GB, int UB, int US, int AUXB, int UD = 0, int SU = 1>
 static hipError_t launch_hyb(const uint8_t* arena, uint64_t arena_bytes, const void* desc,
                              uint32_t n, uint16_t* out, uint32_t* partial,
                              unsigned long long* err, hipStream_t stream, uint32_t big_chunks,
@@ -695,11 +665,11 @@ static hipError_t launch_hyb(const uint8_t* arena, uint64_t arena_bytes, const v
   const uint64_t want = tile_bytes / avg;
 #define NSK_TP(tp) \
   if (want >= tp)              \
-  return launch_hyb_tp<tp, GB, UB, US, AUXB, UD, LA, SU>(arena, arena_bytes, desc, n, out, partial, err, stream, big_chunks)
+  return launch_hyb_tp<tp, GB, UB, US, AUXB, UD, SU>(arena, arena_bytes, desc, n, out, partial, err, stream, big_chunks)
   if constexpr (UD > 0) {
     // The small-packet variant (launch_batch: < 256 B per descriptor) keeps
     // full tiles: its direct path is one packet per lane.
-    return launch_hyb_tp<256, GB, UB, US, AUXB, UD, LA, SU>(arena, arena_bytes, desc, n, out, partial, err,
+    return launch_hyb_tp<256, GB, UB, US, AUXB, UD, SU>(arena, arena_bytes, desc, n, out, partial, err,
                                                         stream, big_chunks);
   } else {
     NSK_TP(256);
@@ -710,7 +680,7 @@ static hipError_t launch_hyb(const uint8_t* arena, uint64_t arena_bytes, const v
     NSK_TP(8);
     NSK_TP(4);
     NSK_TP(2);
-    return launch_hyb_tp<1, GB, UB, US, AUXB, UD, LA, SU>(arena, arena_bytes, desc, n, out, partial, err, stream,
+    return launch_hyb_tp<1, GB, UB, US, AUXB, UD, SU>(arena, arena_bytes, desc, n, out, partial, err, stream,
                                                       big_chunks);
   }
 #undef NSK_TP
@@ -730,7 +700,7 @@ hipError_t launch_batch(const uint8_t* arena, uint64_t arena_bytes,
     // smaller packets to per-lane runs of 4, two runs issued per lane per
     // iteration (tools/tune.py on MI355X: 220.6 us on 1M x 1500 B = 90.2% of
     // 8 TB/s, 107 us on the Zipf batch; profiles/r01/tune_*.json).
-    e = launch_hyb<8, 16, 4, 2, 0, true, 2>(arena, arena_bytes, desc, n, out, partial, err, stream, 64u,
+    e = launch_hyb<8, 16, 4, 2, 0, 2>(arena, arena_bytes, desc, n, out, partial, err, stream, 64u,
                                             sizing_bytes);
   } else {
     // Small packets: the same kernel plus the direct path — a tile whose

@@ -7,6 +7,24 @@
 
 namespace nsk {
 
+// Byte mask of dword j (bytes 4j..4j+3) of a 16-byte chunk restricted to
+// bytes [lo, hi).
+__device__ __forceinline__ uint32_t dword_mask(int lo, int hi, int j) {
+  const int a = max(lo - 4 * j, 0);
+  const int b = min(hi - 4 * j, 4);
+  if (b <= a) return 0u;
+  const uint32_t below_b = (b >= 4) ? 0xFFFFFFFFu : ((1u << (8 * b)) - 1u);
+  return below_b & (0xFFFFFFFFu << (8 * a));
+}
+
+__device__ __forceinline__ uint4 mask_chunk(uint4 w, int lo, int hi) {
+  w.x &= dword_mask(lo, hi, 0);
+  w.y &= dword_mask(lo, hi, 1);
+  w.z &= dword_mask(lo, hi, 2);
+  w.w &= dword_mask(lo, hi, 3);
+  return w;
+}
+
 template <bool NT>
 __device__ __forceinline__ uint4 load16(const uint4* p) {
   if constexpr (NT) {
@@ -140,10 +158,10 @@ __global__ __launch_bounds__(256) void calib_grp(const uint4* __restrict__ p, ui
   if ((threadIdx.x & 63) == 0) atomicAdd(&out[blockIdx.x], acc);
 }
 
-template <int GB, int UB, int US, int AUXB, uint32_t BIG, int UD = 0, bool LA = true, int SU = 1>
+template <int GB, int UB, int US, int AUXB, uint32_t BIG, int UD = 0, int SU = 1>
 hipError_t launch_h(const uint8_t* arena, uint64_t arena_bytes, const void* desc, uint32_t n,
                     uint16_t* out, unsigned long long* err, hipStream_t s) {
-  return launch_hyb<GB, UB, US, AUXB, UD, LA, SU>(arena, arena_bytes, desc, n, out, nullptr, err, s, BIG);
+  return launch_hyb<GB, UB, US, AUXB, UD, SU>(arena, arena_bytes, desc, n, out, nullptr, err, s, BIG);
 }
 
 // Floor for the 1M x 64 B layout only (desc[i].off == 64 * i): the same
@@ -259,7 +277,7 @@ hipError_t launch_floor(const uint8_t* arena, uint64_t arena_bytes, const void* 
 template <uint64_t TB>
 hipError_t launch_tb(const uint8_t* arena, uint64_t arena_bytes, const void* desc, uint32_t n,
                      uint16_t* out, unsigned long long* err, hipStream_t s) {
-  return launch_hyb<8, 16, 4, 2, 0, true, 2>(arena, arena_bytes, desc, n, out, nullptr, err, s, 64u, 0, TB);
+  return launch_hyb<8, 16, 4, 2, 0, 2>(arena, arena_bytes, desc, n, out, nullptr, err, s, 64u, 0, TB);
 }
 
 // Chained timing: the CH instance (partials + continuation flags) with or
@@ -281,13 +299,13 @@ hipError_t launch_chained(const uint8_t* arena, uint64_t arena_bytes, const void
   uint32_t* part = part_for(n);
   if (!part) return hipErrorOutOfMemory;
   if constexpr (FULL) return launch_batch(arena, arena_bytes, desc, n, out, part, err, s);
-  return launch_hyb<8, 16, 4, 2, 0, true, 2>(arena, arena_bytes, desc, n, out, part, err, s, 64u);
+  return launch_hyb<8, 16, 4, 2, 0, 2>(arena, arena_bytes, desc, n, out, part, err, s, 64u);
 }
 
 template <int TP, int GB, int UB>
 hipError_t launch_tp(const uint8_t* arena, uint64_t arena_bytes, const void* desc, uint32_t n,
                      uint16_t* out, unsigned long long* err, hipStream_t s) {
-  return launch_hyb_tp<TP, GB, UB, 4, 2, 0, true, 2>(arena, arena_bytes, desc, n, out, nullptr, err, s, 64u);
+  return launch_hyb_tp<TP, GB, UB, 4, 2, 0, 2>(arena, arena_bytes, desc, n, out, nullptr, err, s, 64u);
 }
 
 typedef hipError_t (*launch_fn)(const uint8_t*, uint64_t, const void*, uint32_t, uint16_t*,
@@ -300,17 +318,17 @@ struct Variant {
 // against these and retired; their numbers are in profiles/r01/tune_*.json
 // and DESIGN.md §4.2.
 static const Variant kVariants[] = {
-    {"prod_g8u16_b64", launch_h<8, 16, 4, 2, 64, 0, true, 2>},
+    {"prod_g8u16_b64", launch_h<8, 16, 4, 2, 64, 0, 2>},
     {"g8u16_su1", launch_h<8, 16, 4, 2, 64>},
     {"chained_main", launch_chained<false>},
     {"chained_full", launch_chained<true>},
     {"prod_small_d5", launch_h<16, 8, 4, 2, 64, 5>},
-    {"g8u16_b32", launch_h<8, 16, 4, 2, 32, 0, true, 2>},
-    {"g8u8_b64", launch_h<8, 8, 4, 2, 64, 0, true, 2>},
-    {"g8u12_b64", launch_h<8, 12, 4, 2, 64, 0, true, 2>},
-    {"g8u24_b64", launch_h<8, 24, 4, 2, 64, 0, true, 2>},
-    {"g16u8_b64", launch_h<16, 8, 4, 2, 64, 0, true, 2>},
-    {"g4u16_b64", launch_h<4, 16, 4, 2, 64, 0, true, 2>},
+    {"g8u16_b32", launch_h<8, 16, 4, 2, 32, 0, 2>},
+    {"g8u8_b64", launch_h<8, 8, 4, 2, 64, 0, 2>},
+    {"g8u12_b64", launch_h<8, 12, 4, 2, 64, 0, 2>},
+    {"g8u24_b64", launch_h<8, 24, 4, 2, 64, 0, 2>},
+    {"g16u8_b64", launch_h<16, 8, 4, 2, 64, 0, 2>},
+    {"g4u16_b64", launch_h<4, 16, 4, 2, 64, 0, 2>},
     {"tp32", launch_tp<32, 8, 16>},
     {"tp64", launch_tp<64, 8, 16>},
     {"tp128", launch_tp<128, 8, 16>},

@@ -119,5 +119,5 @@ def test_cfg5_strong_scaling_shards_reproduce_the_whole_batch():
             assert not bench.parity_sample(s, torch.from_numpy(bad.view(np.int16)), k=100)["bit_exact"]
         assert np.array_equal(np.concatenate(got), want)
     assert "true" in bench.kernel_name(12_583_000_000, 8 << 20)
-    assert bench.kernel_name(1_577_058_304, 1 << 20) == "nsk::csum_hyb<256,32,8,16,4,2,0,true,false,2,false>"
-    assert bench.kernel_name(67_108_864, 1 << 20) == "nsk::csum_hyb<256,256,16,8,4,2,5,true,false,1,false>"
+    assert bench.kernel_name(1_577_058_304, 1 << 20) == "nsk::csum_hyb<256,32,8,16,4,2,0,false,2,false>"
+    assert bench.kernel_name(67_108_864, 1 << 20) == "nsk::csum_hyb<256,256,16,8,4,2,5,false,1,false>"
