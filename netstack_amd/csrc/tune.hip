@@ -302,6 +302,16 @@ hipError_t launch_chained(const uint8_t* arena, uint64_t arena_bytes, const void
   return launch_hyb<8, 16, 4, 2, 0, 2>(arena, arena_bytes, desc, n, out, part, err, s, 64u);
 }
 
+// Workgroup size with the tile: WG threads own TP descriptors.
+template <int WG, int TP>
+hipError_t launch_wg(const uint8_t* arena, uint64_t arena_bytes, const void* desc, uint32_t n,
+                     uint16_t* out, unsigned long long* err, hipStream_t s) {
+  const uint32_t grid = (uint32_t)(((uint64_t)n + TP - 1) / TP);
+  hipLaunchKernelGGL((csum_hyb<WG, TP, 8, 16, 4, 2, 0, false, 2, false>), dim3(grid), dim3(WG), 0, s, arena,
+                     arena_bytes, reinterpret_cast<const uint4*>(desc), n, out, nullptr, err, 64u);
+  return hipGetLastError();
+}
+
 template <int TP, int GB, int UB>
 hipError_t launch_tp(const uint8_t* arena, uint64_t arena_bytes, const void* desc, uint32_t n,
                      uint16_t* out, unsigned long long* err, hipStream_t s) {
@@ -330,6 +340,11 @@ static const Variant kVariants[] = {
     {"g16u8_b64", launch_h<16, 8, 4, 2, 64, 0, 2>},
     {"g4u16_b64", launch_h<4, 16, 4, 2, 64, 0, 2>},
     {"tp32", launch_tp<32, 8, 16>},
+    {"wg128_tp16", launch_wg<128, 16>},
+    {"wg128_tp32", launch_wg<128, 32>},
+    {"wg512_tp64", launch_wg<512, 64>},
+    {"wg512_tp32", launch_wg<512, 32>},
+    {"wg64_tp8", launch_wg<64, 8>},
     {"tp64", launch_tp<64, 8, 16>},
     {"tp128", launch_tp<128, 8, 16>},
     {"tp256", launch_tp<256, 8, 16>},
