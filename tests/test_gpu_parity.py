@@ -535,3 +535,37 @@ def test_rx_verification_batch_device_resident(engine):
     assert nbad == 0 and np.array_equal(got, want)
     assert (got[0::3] == 0xFFFF).all()
     assert np.array_equal(np.flatnonzero(got[2::3] != 0xFFFF), bad_idx)
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_randomized_layouts(engine, seed):
+    """Randomised batches mixing every packet class the kernel distinguishes —
+    empty, tiny (direct path), small runs, line-split big packets, jumbo, and
+    >128 KiB packets that switch a tile to the exact accumulator — at random
+    alignments, sorted or shuffled tables, random odd/CONT flags, chained or
+    not, device- and host-resident; every result against the oracle."""
+    import oracle as O
+    from netstack_amd import workloads as W
+
+    rng = np.random.default_rng(4242 + seed)
+    n = int(rng.integers(1, 6000))
+    kind = rng.choice(6, n, p=[0.05, 0.3, 0.3, 0.25, 0.09, 0.01])
+    lo = np.array([0, 1, 65, 1000, 9000, 131041])[kind]
+    hi = np.array([1, 65, 1000, 9000, 66000, 300000])[kind]
+    lengths = rng.integers(lo, hi).astype(np.uint32)
+    init = rng.integers(0, 65536, n).astype(np.uint16)
+    chained = bool(seed % 2)
+    flags = rng.integers(0, 2, n) | (2 * (rng.random(n) < (0.5 if chained else 0.3)))
+    d, end = W.make_desc(lengths, init, align=int(rng.choice([1, 2, 16])), base=int(rng.integers(0, 40)),
+                         flags=flags.astype(np.uint16))
+    if seed % 3 == 0:
+        d = d[rng.permutation(n)]
+    arena = rng.integers(0, 256, end + int(rng.integers(0, 64)), dtype=np.uint8)
+    if seed % 4 == 1:  # runs of 0xFF: largest sums
+        arena[rng.random(arena.size) < 0.3] = 0xFF
+    want, bad = O.c_batch(arena, d, chained=chained)
+    assert bad == 0
+    got = dev_batch(engine, arena, d, chained=chained, arena_offset=int(rng.integers(0, 16)))
+    assert np.array_equal(got, want), np.flatnonzero(got != want)[:8]
+    if seed % 3 == 1:
+        assert np.array_equal(engine.batch_host(arena, d, chained=chained), want)
