@@ -136,3 +136,23 @@ def test_product_kernels_never_spill_and_keep_occupancy():
         windowed = "Li5ELb1E" in k or "Li0ELb1E" in k  # WIN = true: carries the 64-bit-address fallback too
         chained = k.endswith("Lb1EEEvPKhmPK15HIP_vector_typeIjLj4EEjPtPjPyj")  # CH = true
         assert v["Occupancy"] >= (8 if small else 4 if (windowed or chained) else 6), (k, v)
+
+
+def test_go_shim_keeps_reference_signatures_and_binds_declared_symbols():
+    """No Go toolchain here, so the cgo shim (go/header/checksum_hip.go) is
+    checked statically: it declares netstack's exported checksum functions
+    with the reference's exact signatures (tcpip/header/checksum.go:52, 61,
+    69, 104, 112) and calls only functions include/netstack_csum.h declares."""
+    src = open(os.path.join(ROOT, "go", "header", "checksum_hip.go")).read()
+    for sig in (
+        "func Checksum(buf []byte, initial uint16) uint16",
+        "func ChecksumVV(vv buffer.VectorisedView, initial uint16) uint16",
+        "func ChecksumVVWithOffset(vv buffer.VectorisedView, initial uint16, off int, size int) uint16",
+        "func ChecksumCombine(a, b uint16) uint16",
+        "func PseudoHeaderChecksum(protocol tcpip.TransportProtocolNumber, srcAddr tcpip.Address, "
+        "dstAddr tcpip.Address, totalLen uint16) uint16",
+    ):
+        assert sig in src, sig
+    assert "// +build hipcsum" in src and "package header" in src
+    called = set(re.findall(r"C\.(ns_csum_\w+)\(", src))
+    assert called and called <= declared_symbols(), called - declared_symbols()
