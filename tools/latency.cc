@@ -138,6 +138,24 @@ int main(int argc, char** argv) {
     std::printf(" \"batch_host_1024x1500B\": {\"gpu_med_us\": %.2f, \"gpu_p99_us\": %.2f, \"scalar_med_us\": %.3f},\n",
                 g.med, g.p99, c.med);
   }
+  {  // large gathers: one VectorisedView batch of 64 MiB in 1 MiB views, 64 KiB segments
+    const uint64_t total = 64ull << 20, vsz = 1ull << 20;
+    std::vector<uint8_t> big(total);
+    for (size_t i = 0; i < big.size(); ++i) big[i] = (uint8_t)(i * 2654435761u >> 11);
+    std::vector<ns_view> views;
+    for (uint64_t o = 0; o < total; o += vsz) views.push_back(ns_view{big.data() + o, vsz});
+    std::vector<ns_seg> segs;
+    for (uint64_t o = 0; o < total; o += 65536) segs.push_back(ns_seg{(int64_t)o, 65536, 0x77, 0, 0});
+    std::vector<uint16_t> out(segs.size());
+    const Stat g = time_calls(20, [&] {
+      check(ns_csum_vv_batch(ctx, views.data(), (uint32_t)views.size(), segs.data(), (uint32_t)segs.size(),
+                             out.data()), "vv_batch");
+    });
+    bool ok = true;
+    for (size_t k = 0; k < segs.size(); k += 97) ok = ok && out[k] == scalar(big.data() + segs[k].off, 65536, 0x77);
+    std::printf(" \"vv_batch_64MiB_1024segs\": {\"gpu_med_us\": %.1f, \"GBps\": %.2f, \"ok\": %s},\n", g.med,
+                total / g.med / 1e3, ok ? "true" : "false");
+  }
   {  // T threads x sendTCPBatch calls on one context
     const int mss = 1460, total = 65536;
     std::vector<ns_seg> segs;
