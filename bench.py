@@ -47,8 +47,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", type=int, default=2, choices=(2, 3, 4, 5, 7),
-                    help="BASELINE.json configs[k-1]; 7 = device-resident RX verification (SURVEY §8(f) rank 2)")
+    ap.add_argument("--config", type=int, default=2, choices=(2, 3, 4, 5, 7, 8),
+                    help="BASELINE.json configs[k-1]; 7 = device-resident RX verification, "
+                         "8 = device-resident TX checksum fill (SURVEY §8(f) ranks 2 and 1)")
     ap.add_argument("--mode", default="dev", choices=("dev", "host"))
     ap.add_argument("--rotate", type=int, default=0, help="distinct batches cycled per step (0 = auto)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline time budget")
@@ -211,8 +212,8 @@ def main():
     eng = Engine(dist.local)
 
     cfg = args.config
-    if cfg == 7:
-        return rx_mode(args, dist, eng, dev)
+    if cfg in (7, 8):
+        return packet_mode(args, dist, eng, dev, tx=cfg == 8)
     batch = rank_batch(cfg, dist.rank, dist.world)
     rotate = args.rotate or (4 if cfg == 3 else 1)
     if cfg == 5 and rotate != 1:
@@ -322,21 +323,38 @@ def main():
 RX_N = 1 << 20
 
 
-def rx_mode(args, dist, eng, dev):
-    """Device-resident RX verification: 1M received
-    1500-B IPv4/TCP packets per GPU in HBM, three chained descriptors per
-    packet (IPv4 header; pseudo-header addresses; TCP header + payload), one
-    ns_csum_batch_dev(NS_BATCH_CHAINED) per step = the checksum kernel (partial
-    sums and continuation flags) plus the csum_chain pass that folds the runs.  Every 1000th packet has a corrupted payload byte:
-    the check after the timed region requires exactly those TCP sums to fail
-    and every IPv4 header and every other TCP segment to sum to 0xffff
-    (segment.go:180, checker.go:51-53) — a size-independent property over
-    all 1M packets.  value = received packet bytes / s (GiB/s)."""
+def packet_mode(args, dist, eng, dev, tx: bool):
+    """Device-resident IPv4/TCP packet batches: 1M 1500-B
+    packets per GPU in HBM, three chained descriptors per packet (IPv4 header;
+    pseudo-header addresses; TCP header + payload), one
+    ns_csum_batch_dev(NS_BATCH_CHAINED) per step = the checksum kernel
+    (partial sums and continuation flags) plus the csum_chain pass that folds
+    the runs.
+
+    RX (config 7, rank 2: segment.parse / the IPv4 header check): every
+    1000th packet has a corrupted payload byte; the check after the timed
+    region requires exactly those TCP sums to fail and every IPv4 header and
+    every other TCP segment to sum to 0xffff (segment.go:180,
+    checker.go:51-53) — a size-independent property over all 1M packets.
+
+    TX (config 8, rank 1: buildTCPHdr + addIPHeader for a whole batch): the
+    same packets with zeroed checksum fields, ns_csum_batch_dev_store writes
+    ^sum into both fields of every packet (connect.go:662-663, ipv4.go:236).
+    The fields are re-zeroed after the timed region and filled by one more
+    launch; the check requires the whole arena to equal rx_batch's, whose
+    checksums torch integer ops computed independently.
+
+    value = packet bytes / s (GiB/s)."""
     import torch
 
     from netstack_amd import workloads as W
 
-    arena, d, bad_idx = W.rx_batch(RX_N, 7000 + dist.rank, dev, corrupt_every=1000)
+    seed = 7000 + dist.rank
+    if tx:
+        arena, d = W.tx_batch(RX_N, seed, dev)
+        bad_idx = np.zeros(0, np.int64)
+    else:
+        arena, d, bad_idx = W.rx_batch(RX_N, seed, dev, corrupt_every=1000)
     desc = torch.from_numpy(d.view(np.uint8).copy()).to(dev)
     out = torch.empty(len(d), dtype=torch.int16, device=dev)
     stream = torch.cuda.current_stream(dev)
@@ -347,7 +365,7 @@ def rx_mode(args, dist, eng, dev):
         k = state["i"]
         if k == args.warmup:
             ev[0].record(stream)
-        eng.batch_tensors(arena, desc, out, chained=True, stream=stream)
+        eng.batch_tensors(arena, desc, out, chained=True, stream=stream, store=tx)
         state["i"] = k + 1
         if state["i"] == args.warmup + args.steps:
             ev[1].record(stream)
@@ -355,42 +373,75 @@ def rx_mode(args, dist, eng, dev):
     wall, _ = timed_region(step, torch.cuda.synchronize, dist, args.steps, args.warmup, dev)
     bad = eng.sync()
     kern_avg_s = ev[0].elapsed_time(ev[1]) / 1e3 / args.steps
-    res = out.cpu().numpy().view(np.uint16)
-    ip_ok = res[0::3] == 0xFFFF
-    tcp_fail = np.flatnonzero(res[2::3] != 0xFFFF)
-    prop_ok = bool(ip_ok.all()) and np.array_equal(tcp_fail, bad_idx)
+    k_cpu = 3 * 65536
+    span = int(d["off"][k_cpu - 1] + d["len"][k_cpu - 1])
+    if tx:
+        # untimed: re-zero both fields, fill them with one launch, check
+        p = arena.view(RX_N, W.RX_STRIDE)
+        p[:, 10:12] = 0
+        p[:, 36:38] = 0
+        before = arena[:span].cpu().numpy() if dist.rank == 0 and not args.no_cpu else None
+        eng.batch_tensors(arena, desc, out, chained=True, stream=stream, store=True)
+        torch.cuda.synchronize()
+        bad += eng.sync()
+        rx, _, _ = W.rx_batch(RX_N, seed, dev)
+        arena_ok = bool(torch.equal(arena, rx))
+        del rx
+        chk = torch.from_numpy(W._tcp_desc(RX_N).view(np.uint8).copy()).to(dev)
+        vres = eng.batch_tensors(arena, chk, chained=True, stream=stream).cpu().numpy().view(np.uint16)
+        res = out.cpu().numpy().view(np.uint16)
+        ip_ok = vres[0::3] == 0xFFFF
+        tcp_fail = np.flatnonzero(vres[2::3] != 0xFFFF)
+        prop_ok = arena_ok and bool(ip_ok.all()) and tcp_fail.size == 0
+    else:
+        before = None
+        res = out.cpu().numpy().view(np.uint16)
+        ip_ok = res[0::3] == 0xFFFF
+        tcp_fail = np.flatnonzero(res[2::3] != 0xFFFF)
+        prop_ok = bool(ip_ok.all()) and np.array_equal(tcp_fail, bad_idx)
     fails = dist.sum(0.0 if prop_ok else 1.0, dev)
     pkt_bytes = RX_N * W.RX_PKT
     total = dist.sum(float(pkt_bytes), dev)
     n_desc = len(d)
     # packet bytes + the 8-B address re-read + per descriptor: 16-B read,
-    # u32 partial + u16 flag written, then read back, and a u16 result written
-    algo = pkt_bytes + 8 * RX_N + n_desc * (16 + 6 + 6 + 2)
+    # u32 partial + u16 flag written, then read back, and a u16 result
+    # written; TX adds the two 2-B field stores per packet
+    algo = pkt_bytes + 8 * RX_N + n_desc * (16 + 6 + 6 + 2) + (4 * RX_N if tx else 0)
     achieved = algo / kern_avg_s / 1e9
+    check = {"ipv4_all_valid": bool(ip_ok.all()), "tcp_failures": int(tcp_fail.size),
+             "expected_failures": int(bad_idx.size), "ok": prop_ok, "ranks_failed": int(fails)}
+    if tx:
+        check["arena_equals_rx_batch"] = arena_ok
     result = {
-        "metric": "RX checksum verification GiB/s device-resident (IPv4 + TCP, 1500-B packets)",
+        "metric": ("TX checksum fill" if tx else "RX checksum verification")
+        + " GiB/s device-resident (IPv4 + TCP, 1500-B packets)",
         "value": total * args.steps / wall / GIB, "unit": "GiB/s", "n_gpus": dist.world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": wall / args.steps * 1e3,
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
-        "data": "synthetic received packets (valid IPv4/TCP checksums, 1 in 1000 corrupted), resident in HBM",
-        "config": {"workload": "rx: 1,048,576 x 1500-B IPv4/TCP packets per GPU, 3 chained descriptors each",
+        "data": ("synthetic packets to send (checksum fields zero), resident in HBM" if tx else
+                 "synthetic received packets (valid IPv4/TCP checksums, 1 in 1000 corrupted), resident in HBM"),
+        "config": {"workload": ("tx" if tx else "rx") + ": 1,048,576 x 1500-B IPv4/TCP packets per GPU, "
+                   "3 chained descriptors each" + (", 2 checksum stores" if tx else ""),
                    "packets_per_gpu": RX_N, "descriptors_per_gpu": n_desc},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                      "kernel": kernel_name(arena.numel(), n_desc, chained=True) + " + nsk::csum_chain",
                      "algorithmic_bytes_per_launch": algo, "avg_launch_us": kern_avg_s * 1e6},
         "bad_descriptors": bad,
-        "property_check": {"ipv4_all_valid": bool(ip_ok.all()), "tcp_failures": int(tcp_fail.size),
-                           "expected_failures": int(bad_idx.size), "ok": prop_ok, "ranks_failed": int(fails)},
+        "property_check": check,
     }
     if dist.rank == 0 and not args.no_cpu:
         import oracle as O
 
-        # CPU leg: the oracle on the first 65,536 packets' descriptors, same bytes
-        k = 3 * 65536
-        span = int(d["off"][k - 1] + d["len"][k - 1])
-        want, _ = O.c_batch(arena[:span].cpu().numpy(), d[:k], chained=True)
-        result["parity_sample"] = {"packets": k // 3, "bit_exact": bool(np.array_equal(res[:k], want))}
+        # CPU leg: the oracle on the first 65,536 packets' descriptors, same
+        # bytes (TX: the bytes before the checked launch, and its stores)
+        src = before if tx else arena[:span].cpu().numpy()
+        want, _ = O.c_batch(src, d[:k_cpu], chained=True)
+        ps = {"packets": k_cpu // 3, "bit_exact": bool(np.array_equal(res[:k_cpu], want))}
+        if tx:
+            stored, _ = O.apply_stores(src, d[:k_cpu], want)
+            ps["stores_bit_exact"] = bool(np.array_equal(arena[:span].cpu().numpy(), stored))
+        result["parity_sample"] = ps
     if dist.rank == 0:
         print(json.dumps(result), flush=True)
     eng.close()

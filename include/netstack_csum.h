@@ -61,6 +61,23 @@ extern "C" {
 #define NS_DESC_ODD 0x1u
 /* bit 1: chain: initial := result of the previous descriptor (checksum.go:89). */
 #define NS_DESC_CONT 0x2u
+/* bit 2: store: once this descriptor's result r is final (after its chain),
+ *        write ^r big-endian at arena[off + NS_DESC_STORE_AT(flags)], i.e.
+ *        the header's SetChecksum(^CalculateChecksum(xsum)) (tcp.go:252,
+ *        connect.go:663; ipv4.go:223, :236).  Honoured only by
+ *        ns_csum_batch_dev_store (a writable arena); ignored elsewhere.
+ * bit 3: with bit 2, store r itself, not ^r: the CHECKSUM_PARTIAL
+ *        pseudo-header sum of a GSO segment (connect.go:655-660).
+ * bits 4-15: the store offset from `off` (0..4095); the 2 bytes must lie in
+ *        the arena (else the store is dropped and counted by ns_csum_sync).
+ *        Every sum of the batch sees the arena as it was before the call
+ *        provided no descriptor reads stored bytes other than the storing
+ *        descriptor itself (unchained) or any descriptor (NS_BATCH_CHAINED:
+ *        stores happen after all reads, in the run-folding pass).          */
+#define NS_DESC_STORE 0x4u
+#define NS_DESC_STORE_RAW 0x8u
+#define NS_DESC_STORE_SHIFT 4
+#define NS_DESC_STORE_AT(flags) ((uint32_t)(flags) >> NS_DESC_STORE_SHIFT)
 
 /* One packet (or one piece of a chained packet).  16 bytes, little-endian,
  * naturally aligned: maps 1:1 onto stack.PacketDescriptor{Off,Size}
@@ -126,6 +143,15 @@ int ns_csum_batch_dev(ns_csum_ctx* ctx, const uint8_t* d_arena,
                       uint64_t arena_bytes, const ns_pkt_desc* d_desc,
                       uint32_t n, uint16_t* d_out, uint32_t batch_flags,
                       void* stream);
+
+/* ns_csum_batch_dev over a writable arena, honouring NS_DESC_STORE: the
+ * device-resident transmit path writes every checksum field in place
+ * (buildTCPHdr connect.go:653-663 and addIPHeader ipv4.go:217-238 for a whole
+ * batch, without the packets leaving HBM).  Results also go to d_out.       */
+int ns_csum_batch_dev_store(ns_csum_ctx* ctx, uint8_t* d_arena,
+                            uint64_t arena_bytes, const ns_pkt_desc* d_desc,
+                            uint32_t n, uint16_t* d_out, uint32_t batch_flags,
+                            void* stream);
 
 /* Host-memory batch: H2D of arena and table, kernels, D2H of results,
  * pipelined over two streams in chunks; synchronous.  Pageable host memory is

@@ -24,12 +24,15 @@ NS_EHIP = -5
 
 NS_DESC_ODD = 0x1
 NS_DESC_CONT = 0x2
+NS_DESC_STORE = 0x4
+NS_DESC_STORE_RAW = 0x8
+NS_DESC_STORE_SHIFT = 4
 NS_BATCH_CHAINED = 0x1
 
 # Every symbol include/netstack_csum.h declares (checked by the CPU tests).
 EXPORTED = (
     "ns_csum_abi_version", "ns_csum_last_hip_error", "ns_csum_strerror", "ns_csum_device_count",
-    "ns_csum_init", "ns_csum_destroy", "ns_csum_sync", "ns_csum_batch_dev",
+    "ns_csum_init", "ns_csum_destroy", "ns_csum_sync", "ns_csum_batch_dev", "ns_csum_batch_dev_store",
     "ns_csum_batch_host", "ns_csum_checksum", "ns_csum_vv_with_offset",
     "ns_csum_vv_batch", "ns_csum_views_restart", "ns_csum_pseudo_header",
     "ns_csum_combine", "ns_csum_shard_plan", "ns_csum_batch_multi", "ns_csum_chains",
@@ -98,6 +101,7 @@ def _declare(lib):
         "ns_csum_destroy": (None, [vp]),
         "ns_csum_sync": (c.c_int, [vp, vp, c.POINTER(c.c_uint64)]),
         "ns_csum_batch_dev": (c.c_int, [vp, u8p, c.c_uint64, vp, c.c_uint32, vp, c.c_uint32, vp]),
+        "ns_csum_batch_dev_store": (c.c_int, [vp, u8p, c.c_uint64, vp, c.c_uint32, vp, c.c_uint32, vp]),
         "ns_csum_batch_host": (c.c_int, [vp, u8p, c.c_uint64, vp, c.c_uint32, vp, c.c_uint32]),
         "ns_csum_checksum": (c.c_int, [vp, u8p, c.c_uint64, c.c_uint16, u16p]),
         "ns_csum_vv_with_offset": (c.c_int, [vp, c.POINTER(NsView), c.c_uint32, c.c_uint16,

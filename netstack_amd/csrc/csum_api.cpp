@@ -794,9 +794,9 @@ int ns_csum_sync(ns_csum_ctx* ctx, void* stream, uint64_t* bad) {
   return NS_OK;
 }
 
-int ns_csum_batch_dev(ns_csum_ctx* ctx, const uint8_t* d_arena, uint64_t arena_bytes,
-                      const ns_pkt_desc* d_desc, uint32_t n, uint16_t* d_out,
-                      uint32_t batch_flags, void* stream) {
+namespace {
+int batch_dev(ns_csum_ctx* ctx, const uint8_t* d_arena, uint64_t arena_bytes, const ns_pkt_desc* d_desc,
+              uint32_t n, uint16_t* d_out, uint32_t batch_flags, void* stream, bool store) {
   if (!ctx || (n && (!d_desc || !d_out)) || (arena_bytes && !d_arena)) return NS_EINVAL;
   if (n == 0) return NS_OK;
   DeviceGuard g(ctx->device);
@@ -808,8 +808,21 @@ int ns_csum_batch_dev(ns_csum_ctx* ctx, const uint8_t* d_arena, uint64_t arena_b
     if (rc != NS_OK) return rc;
     part = ctx->partial.p;
   }
-  HIP_TRY(nsk::launch_batch(d_arena, arena_bytes, d_desc, n, d_out, part, ctx->d_err, s));
+  HIP_TRY(nsk::launch_batch(d_arena, arena_bytes, d_desc, n, d_out, part, ctx->d_err, s, 0, store));
   return NS_OK;
+}
+}  // namespace
+
+int ns_csum_batch_dev(ns_csum_ctx* ctx, const uint8_t* d_arena, uint64_t arena_bytes,
+                      const ns_pkt_desc* d_desc, uint32_t n, uint16_t* d_out,
+                      uint32_t batch_flags, void* stream) {
+  return batch_dev(ctx, d_arena, arena_bytes, d_desc, n, d_out, batch_flags, stream, false);
+}
+
+int ns_csum_batch_dev_store(ns_csum_ctx* ctx, uint8_t* d_arena, uint64_t arena_bytes,
+                            const ns_pkt_desc* d_desc, uint32_t n, uint16_t* d_out,
+                            uint32_t batch_flags, void* stream) {
+  return batch_dev(ctx, d_arena, arena_bytes, d_desc, n, d_out, batch_flags, stream, true);
 }
 
 int ns_csum_batch_host(ns_csum_ctx* ctx, const uint8_t* h_arena, uint64_t arena_bytes,

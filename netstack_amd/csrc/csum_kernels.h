@@ -16,9 +16,11 @@ namespace nsk {
 // `sizing_bytes` (0: arena_bytes) is the byte count the launcher sizes tiles
 // by — the payload of a batch whose "arena" is the whole address space
 // (arena = nullptr, descriptors holding absolute addresses).
+// `store`: descriptors flagged NS_DESC_STORE write their final result into
+// the (then writable) arena.
 hipError_t launch_batch(const uint8_t* arena, uint64_t arena_bytes,
                         const void* desc, uint32_t n, uint16_t* out,
                         uint32_t* partial, unsigned long long* err,
-                        hipStream_t stream, uint64_t sizing_bytes = 0);
+                        hipStream_t stream, uint64_t sizing_bytes = 0, bool store = false);
 
 }  // namespace nsk

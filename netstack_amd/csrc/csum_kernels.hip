@@ -532,16 +532,54 @@ __device__ __forceinline__ uint32_t hyb_scan_tile(HybLds<WG>& L, const Srd& r, c
 // 64 flags then fill a whole 128-B line — byte flags cost 8.5 us more on 3M
 // descriptors, profiles/r01/tune_chained_b2b.log); csum_chain folds the runs
 // from those alone (6 bytes per descriptor, no descriptor re-read).
+// NS_DESC_STORE: a run's final result r goes into the packet, big-endian,
+// as ^r (SetChecksum(^xsum): connect.go:663, ipv4.go:236) or, with
+// NS_DESC_STORE_RAW, as r (the CHECKSUM_PARTIAL pseudo-header sum,
+// connect.go:660).  Two byte stores: the field need not be 2-byte aligned.
+__device__ __forceinline__ void store_result(uint64_t addr, uint32_t r, uint32_t stw) {
+  const uint32_t v = (stw & 2u) ? r : (~r & 0xFFFFu);
+  uint8_t* p = reinterpret_cast<uint8_t*>((uintptr_t)addr);
+  p[0] = (uint8_t)(v >> 8);
+  p[1] = (uint8_t)v;
+}
+
+// The store word (flags bits 2-15: NS_DESC_STORE | STORE_RAW | offset << 2)
+// is decoded here from a re-read of the (L2-resident) descriptor, and only
+// when the launch asked for stores: carrying it through the scan loops cost
+// every kernel 10-20 VGPRs and a wave per SIMD.  A store that would land
+// past the arena is dropped and counted as an error.
+__device__ __forceinline__ uint32_t store_word(uint32_t store, const uint4* __restrict__ desc, uint64_t i,
+                                               uint64_t arena_bytes, unsigned long long* err,
+                                               uint64_t* off) {
+  if (!store) return 0u;
+  const uint4 raw = desc[i];
+  const uint32_t stw = (raw.w >> 18) & 0x3FFFu;
+  if (!(stw & 3u)) return 0u;
+  *off = ((uint64_t)raw.x | ((uint64_t)raw.y << 32)) + (stw >> 2);
+  if (*off > arena_bytes || arena_bytes - *off < 2) {
+    atomicAdd(err, 1ull);
+    return 0u;
+  }
+  return stw;
+}
+
 template <bool CH>
 __device__ __forceinline__ void finish_tile(uint32_t s, const Pkt& d, bool mine, uint64_t i, uint64_t n,
-                                            uint16_t* __restrict__ out, uint32_t* __restrict__ partial) {
+                                            uint16_t* __restrict__ out, uint32_t* __restrict__ partial,
+                                            uint32_t store, const uint4* __restrict__ desc,
+                                            uint64_t arena_abs, uint64_t arena_bytes,
+                                            unsigned long long* err) {
   if (!mine) return;
+  uint64_t at = 0;
+  const uint32_t stw = store_word(store, desc, i, arena_bytes, err, &at);
   if constexpr (CH) {
     const bool head = !d.cont || i == 0;
     partial[i] = head ? fold1((d.cont ? 0u : d.init) + s) : s;
-    reinterpret_cast<uint16_t*>(partial + n)[i] = head ? 0u : 1u;
+    reinterpret_cast<uint16_t*>(partial + n)[i] = (uint16_t)((head ? 0u : 1u) | (stw << 1));
   } else {
-    out[i] = (uint16_t)fold1(d.init + s);
+    const uint32_t r = fold1(d.init + s);
+    out[i] = (uint16_t)r;
+    if (stw) store_result(arena_abs + at, r, stw);
   }
 }
 
@@ -557,7 +595,8 @@ template <int WG, int TP, int GB, int UB, int US, int AUXB, int UD = 0, bool WIN
 __global__ __launch_bounds__(WG) void csum_hyb(
     const uint8_t* __restrict__ arena, uint64_t arena_bytes,
     const uint4* __restrict__ desc, uint32_t n, uint16_t* __restrict__ out,
-    uint32_t* __restrict__ partial, unsigned long long* __restrict__ err, uint32_t big_chunks) {
+    uint32_t* __restrict__ partial, unsigned long long* __restrict__ err, uint32_t big_chunks,
+    uint32_t store) {
   static_assert((WG & (WG - 1)) == 0, "tile must be a power of two");
   __shared__ HybLds<WG> L;
   const int t = threadIdx.x;
@@ -580,43 +619,54 @@ __global__ __launch_bounds__(WG) void csum_hyb(
     const PktInfo p = pkt_info(d, w.base);
     if (UD > 0 && w.small) {
       const uint32_t s = direct_sum<UD ? UD : 1>(r, p);
-      finish_tile<CH>(s, d, mine, i, n, out, partial);
+      finish_tile<CH>(s, d, mine, i, n, out, partial, store, desc, arena_abs, arena_bytes, err);
       return;
     }
     const uint32_t s = hyb_scan_tile<WG, TP, GB, UB, US, AUXB, false, SU>(L, r, p, big_chunks);
-    finish_tile<CH>(s, d, mine, i, n, out, partial);
+    finish_tile<CH>(s, d, mine, i, n, out, partial, store, desc, arena_abs, arena_bytes, err);
   } else if constexpr (WIN) {
     // The tile spans >= 4 GiB: 64-bit global loads, fewer in flight per lane
     // so this rarely taken path does not raise the kernel's register count.
     const Srd r = make_srd(0ull, 0ull);
     const PktInfo p = pkt_info(d, 0ull);
     const uint32_t s = hyb_scan_tile<WG, TP, 16, 4, 4, AUXB, true, 1>(L, r, p, big_chunks);
-    finish_tile<CH>(s, d, mine, i, n, out, partial);
+    finish_tile<CH>(s, d, mine, i, n, out, partial, store, desc, arena_abs, arena_bytes, err);
   }
 }
 
 // Sequential fold of NS_DESC_CONT runs (checksum.go:89 / the
 // `xsum = Checksum(v, xsum)` loops) over finish_tile's chained output: one
-// thread per run head, out[k] = fold1(out[k-1] + s_k).
-__global__ void csum_chain(const uint32_t* __restrict__ partial, uint32_t n, uint16_t* __restrict__ out) {
+// thread per run head, out[k] = fold1(out[k-1] + s_k).  A descriptor whose
+// flag word carries a store (bits 1-15) writes its result into the packet at
+// arena + desc.off + offset.
+__global__ void csum_chain(const uint32_t* __restrict__ partial, uint32_t n, uint16_t* __restrict__ out,
+                           const uint4* __restrict__ desc, const uint8_t* __restrict__ arena) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint16_t* cont = reinterpret_cast<const uint16_t*>(partial + n);
+  const uint16_t* flag = reinterpret_cast<const uint16_t*>(partial + n);
   if (i >= n) return;
+  auto put = [&](uint64_t k, uint32_t v, uint16_t f) {
+    out[k] = (uint16_t)v;
+    const uint32_t stw = (uint32_t)f >> 1;
+    if (stw & 3u) {
+      const uint4 dk = desc[k];
+      store_result((uint64_t)(uintptr_t)arena + ((uint64_t)dk.x | ((uint64_t)dk.y << 32)) + (stw >> 2), v, stw);
+    }
+  };
   // This descriptor and the next one are loaded together (most runs are one
   // or two descriptors long: a header and its payload), so a short run costs
   // one memory round trip.
   const bool has1 = i + 1 < n;
-  const uint16_t c0 = cont[i], c1 = has1 ? cont[i + 1] : 0;
+  const uint16_t c0 = flag[i], c1 = has1 ? flag[i + 1] : 0;
   const uint32_t p0 = partial[i], p1 = has1 ? partial[i + 1] : 0u;
-  if (c0) return;
+  if (c0 & 1u) return;
   uint32_t v = p0;
-  out[i] = (uint16_t)v;
-  if (!c1) return;
+  put(i, v, c0);
+  if (!(c1 & 1u)) return;
   v = fold1(v + p1);
-  out[i + 1] = (uint16_t)v;
-  for (uint64_t k = i + 2; k < n && cont[k]; ++k) {
+  put(i + 1, v, c1);
+  for (uint64_t k = i + 2; k < n && (flag[k] & 1u); ++k) {
     v = fold1(v + partial[k]);
-    out[k] = (uint16_t)v;
+    put(k, v, flag[k]);
   }
 }
 
@@ -628,7 +678,8 @@ namespace nsk {
 template <int TP, int GB, int UB, int US, int AUXB, int UD, int SU = 1>
 static hipError_t launch_hyb_tp(const uint8_t* arena, uint64_t arena_bytes, const void* desc,
                                 uint32_t n, uint16_t* out, uint32_t* partial,
-                                unsigned long long* err, hipStream_t stream, uint32_t big_chunks) {
+                                unsigned long long* err, hipStream_t stream, uint32_t big_chunks,
+                                uint32_t store = 0) {
   constexpr int WG = 256;
   const uint32_t grid = (uint32_t)(((uint64_t)n + TP - 1) / TP);
   const uint4* d = reinterpret_cast<const uint4*>(desc);
@@ -637,7 +688,7 @@ static hipError_t launch_hyb_tp(const uint8_t* arena, uint64_t arena_bytes, cons
   const bool win = ((uintptr_t)arena & 15u) + arena_bytes + 64 >= kMaxSrdBytes;
 #define NSK_LAUNCH(W, C)                                                                              \
   hipLaunchKernelGGL((csum_hyb<WG, TP, GB, UB, US, AUXB, UD, W, SU, C>), dim3(grid), dim3(WG), 0, \
-                     stream, arena, arena_bytes, d, n, out, partial, err, big_chunks)
+                     stream, arena, arena_bytes, d, n, out, partial, err, big_chunks, store)
   if (partial) {
     if (win) NSK_LAUNCH(true, true);
     else NSK_LAUNCH(false, true);
@@ -660,17 +711,17 @@ template <int GB, int UB, int US, int AUXB, int UD = 0, int SU = 1>
 static hipError_t launch_hyb(const uint8_t* arena, uint64_t arena_bytes, const void* desc,
                              uint32_t n, uint16_t* out, uint32_t* partial,
                              unsigned long long* err, hipStream_t stream, uint32_t big_chunks,
-                             uint64_t sizing_bytes = 0, uint64_t tile_bytes = kTileBytes) {
+                             uint64_t sizing_bytes = 0, uint64_t tile_bytes = kTileBytes, uint32_t store = 0) {
   const uint64_t avg = std::max<uint64_t>((sizing_bytes ? sizing_bytes : arena_bytes) / n, 1);
   const uint64_t want = tile_bytes / avg;
 #define NSK_TP(tp) \
   if (want >= tp)              \
-  return launch_hyb_tp<tp, GB, UB, US, AUXB, UD, SU>(arena, arena_bytes, desc, n, out, partial, err, stream, big_chunks)
+  return launch_hyb_tp<tp, GB, UB, US, AUXB, UD, SU>(arena, arena_bytes, desc, n, out, partial, err, stream, big_chunks, store)
   if constexpr (UD > 0) {
     // The small-packet variant (launch_batch: < 256 B per descriptor) keeps
     // full tiles: its direct path is one packet per lane.
     return launch_hyb_tp<256, GB, UB, US, AUXB, UD, SU>(arena, arena_bytes, desc, n, out, partial, err,
-                                                        stream, big_chunks);
+                                                        stream, big_chunks, store);
   } else {
     NSK_TP(256);
     NSK_TP(128);
@@ -681,7 +732,7 @@ static hipError_t launch_hyb(const uint8_t* arena, uint64_t arena_bytes, const v
     NSK_TP(4);
     NSK_TP(2);
     return launch_hyb_tp<1, GB, UB, US, AUXB, UD, SU>(arena, arena_bytes, desc, n, out, partial, err, stream,
-                                                      big_chunks);
+                                                      big_chunks, store);
   }
 #undef NSK_TP
 }
@@ -689,7 +740,7 @@ static hipError_t launch_hyb(const uint8_t* arena, uint64_t arena_bytes, const v
 hipError_t launch_batch(const uint8_t* arena, uint64_t arena_bytes,
                         const void* desc, uint32_t n, uint16_t* out,
                         uint32_t* partial, unsigned long long* err,
-                        hipStream_t stream, uint64_t sizing_bytes) {
+                        hipStream_t stream, uint64_t sizing_bytes, bool store) {
   if (n == 0) return hipSuccess;
   hipError_t e;
   if (sizing_bytes == 0) sizing_bytes = arena_bytes;
@@ -701,16 +752,18 @@ hipError_t launch_batch(const uint8_t* arena, uint64_t arena_bytes,
     // iteration (tools/tune.py on MI355X: 220.6 us on 1M x 1500 B = 90.2% of
     // 8 TB/s, 107 us on the Zipf batch; profiles/r01/tune_*.json).
     e = launch_hyb<8, 16, 4, 2, 0, 2>(arena, arena_bytes, desc, n, out, partial, err, stream, 64u,
-                                            sizing_bytes);
+                                      sizing_bytes, kTileBytes, store);
   } else {
     // Small packets: the same kernel plus the direct path — a tile whose
     // packets all span <= 5 chunks (any <= 65-B packet) has each lane read its
     // own packet with no scan; 16 x 8 groups keep the register count (and the
     // occupancy this latency-bound case needs) lower.
-    e = launch_hyb<16, 8, 4, 2, 5>(arena, arena_bytes, desc, n, out, partial, err, stream, 64u);
+    e = launch_hyb<16, 8, 4, 2, 5>(arena, arena_bytes, desc, n, out, partial, err, stream, 64u, 0, kTileBytes,
+                                   store);
   }
   if (e != hipSuccess || partial == nullptr) return e;
-  hipLaunchKernelGGL(csum_chain, dim3((n + 255) / 256), dim3(256), 0, stream, partial, n, out);
+  hipLaunchKernelGGL(csum_chain, dim3((n + 255) / 256), dim3(256), 0, stream, partial, n, out,
+                     reinterpret_cast<const uint4*>(desc), arena);
   return hipGetLastError();
 }
 

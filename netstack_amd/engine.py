@@ -79,13 +79,17 @@ class Engine:
 
     # -- device-resident batch (the hot path) ------------------------------
     def batch_dev(self, arena_ptr: int, arena_bytes: int, desc_ptr: int, n: int,
-                  out_ptr: int, chained: bool = False, stream: int | None = None) -> None:
-        """Enqueue (asynchronously) the batch on `stream` (hipStream_t as int)."""
-        check(lib().ns_csum_batch_dev(self._h, arena_ptr, arena_bytes, desc_ptr, n, out_ptr,
-                                      _lib.NS_BATCH_CHAINED if chained else 0, stream),
-              "ns_csum_batch_dev")
+                  out_ptr: int, chained: bool = False, stream: int | None = None,
+                  store: bool = False) -> None:
+        """Enqueue (asynchronously) the batch on `stream` (hipStream_t as int).
+        With store=True (ns_csum_batch_dev_store) descriptors flagged
+        NS_DESC_STORE also write their result into the arena."""
+        fn, name = (lib().ns_csum_batch_dev_store, "ns_csum_batch_dev_store") if store else \
+            (lib().ns_csum_batch_dev, "ns_csum_batch_dev")
+        check(fn(self._h, arena_ptr, arena_bytes, desc_ptr, n, out_ptr,
+                 _lib.NS_BATCH_CHAINED if chained else 0, stream), name)
 
-    def batch_tensors(self, arena, desc, out=None, chained: bool = False, stream=None):
+    def batch_tensors(self, arena, desc, out=None, chained: bool = False, stream=None, store: bool = False):
         """torch front end: `arena` uint8 CUDA tensor, `desc` CUDA tensor whose
         bytes are the 16-byte ns_pkt_desc table, `out` int16/uint16 CUDA tensor
         of n elements (allocated if None).  Launches on `stream` (a
@@ -105,7 +109,7 @@ class Engine:
         if stream is None:
             stream = torch.cuda.current_stream(arena.device)
         self.batch_dev(arena.data_ptr(), arena.numel() * arena.element_size(), desc.data_ptr(), n,
-                       out.data_ptr(), chained, stream.cuda_stream)
+                       out.data_ptr(), chained, stream.cuda_stream, store)
         return out
 
     def sync(self, stream: int | None = None) -> int:

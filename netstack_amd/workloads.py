@@ -221,6 +221,41 @@ def _fold_np(s):
     return (s & 0xFFFF) + (s >> 16)
 
 
+def _tcp_packets(n: int, seed: int, device):
+    """n 1500-B IPv4/TCP packets at RX_STRIDE (splitmix64 bytes with fixed
+    header fields), both checksum fields zero.  Returns (arena, packet view)."""
+    arena = random_bytes_torch(seed, n * RX_STRIDE, device)
+    p = arena.view(n, RX_STRIDE)[:, :RX_PKT]
+    p[:, 0] = 0x45
+    p[:, 1] = 0
+    p[:, 2] = RX_PKT >> 8
+    p[:, 3] = RX_PKT & 0xFF
+    p[:, 6] = 0x40
+    p[:, 7] = 0
+    p[:, 8] = 64
+    p[:, 9] = 6
+    p[:, 10:12] = 0
+    p[:, 32] = 0x50  # data offset 5 words
+    p[:, 33] = 0x18  # PSH | ACK
+    p[:, 36:40] = 0  # checksum, urgent pointer
+    return arena, p
+
+
+def _tcp_desc(n: int) -> np.ndarray:
+    """The three-descriptor table over _tcp_packets (see rx_batch)."""
+    base = np.arange(n, dtype=np.uint64) * np.uint64(RX_STRIDE)
+    d = np.zeros(3 * n, dtype=DESC_DTYPE)
+    d["off"][0::3] = base
+    d["len"][0::3] = RX_IHL
+    d["off"][1::3] = base + np.uint64(12)
+    d["len"][1::3] = 8
+    d["initial"][1::3] = RX_TCP + 6  # ChecksumCombine(1480, 6): no carry
+    d["off"][2::3] = base + np.uint64(RX_IHL)
+    d["len"][2::3] = RX_TCP
+    d["flags"][2::3] = 2  # NS_DESC_CONT
+    return d
+
+
 def rx_batch(n: int, seed: int, device, corrupt_every: int = 0):
     """n received 1500-B IPv4/TCP packets packed at RX_STRIDE in HBM, with
     valid IPv4 and TCP checksums (RFC 1071, computed here with torch integer
@@ -237,20 +272,7 @@ def rx_batch(n: int, seed: int, device, corrupt_every: int = 0):
     those TCP sums fail.  Returns (arena uint8 tensor, desc, bad indices)."""
     import torch
 
-    arena = random_bytes_torch(seed, n * RX_STRIDE, device)
-    p = arena.view(n, RX_STRIDE)[:, :RX_PKT]
-    p[:, 0] = 0x45
-    p[:, 1] = 0
-    p[:, 2] = RX_PKT >> 8
-    p[:, 3] = RX_PKT & 0xFF
-    p[:, 6] = 0x40
-    p[:, 7] = 0
-    p[:, 8] = 64
-    p[:, 9] = 6
-    p[:, 10:12] = 0
-    p[:, 32] = 0x50  # data offset 5 words
-    p[:, 33] = 0x18  # PSH | ACK
-    p[:, 36:40] = 0  # checksum, urgent pointer
+    arena, p = _tcp_packets(n, seed, device)
 
     def be_sum(lo, hi):
         w = p[:, lo:hi].to(torch.int64)
@@ -266,14 +288,29 @@ def rx_batch(n: int, seed: int, device, corrupt_every: int = 0):
     if bad.size:
         idx = torch.from_numpy(bad).to(device)
         p[idx, 100] ^= 0x5A
-    base = np.arange(n, dtype=np.uint64) * np.uint64(RX_STRIDE)
-    d = np.zeros(3 * n, dtype=DESC_DTYPE)
-    d["off"][0::3] = base
-    d["len"][0::3] = RX_IHL
-    d["off"][1::3] = base + np.uint64(12)
-    d["len"][1::3] = 8
-    d["initial"][1::3] = RX_TCP + 6  # ChecksumCombine(1480, 6): no carry
-    d["off"][2::3] = base + np.uint64(RX_IHL)
-    d["len"][2::3] = RX_TCP
-    d["flags"][2::3] = 2  # NS_DESC_CONT
-    return arena, d, bad
+    return arena, _tcp_desc(n), bad
+
+
+TX_IP_CSUM = 10   # header.IPv4 checksum field (ipv4.go:35 checksum offset)
+TX_TCP_CSUM = 16  # header.TCP checksum field, from the TCP header start
+
+
+def tx_desc(n: int) -> np.ndarray:
+    """rx_batch's table with the stores of the transmit side (flags for
+    ns_csum_batch_dev_store): the IPv4 run stores ^sum at byte 10
+    (addIPHeader: ip.SetChecksum(^ip.CalculateChecksum()), ipv4.go:236) and
+    the pseudo-header + TCP run stores ^sum at TCP byte 16 (buildTCPHdr:
+    tcp.SetChecksum(^tcp.CalculateChecksum(xsum)), connect.go:662-663)."""
+    d = _tcp_desc(n)
+    d["flags"][0::3] |= 0x4 | (TX_IP_CSUM << 4)
+    d["flags"][2::3] |= 0x4 | (TX_TCP_CSUM << 4)
+    return d
+
+
+def tx_batch(n: int, seed: int, device):
+    """The transmit side of rx_batch: the same n packets with both checksum
+    fields zero, and tx_desc(n).  One ns_csum_batch_dev_store(CHAINED) launch
+    fills the fields in place; afterwards the arena equals
+    rx_batch(n, seed)'s byte for byte.  Returns (arena, desc)."""
+    arena, _ = _tcp_packets(n, seed, device)
+    return arena, tx_desc(n)

@@ -128,6 +128,35 @@ def py_batch(arena: bytes, desc: np.ndarray, chained: bool = False) -> np.ndarra
     return out
 
 
+STORE = 0x4
+STORE_RAW = 0x8
+STORE_SHIFT = 4
+
+
+def apply_stores(arena: np.ndarray, desc: np.ndarray, results: np.ndarray) -> tuple[np.ndarray, int]:
+    """The NS_DESC_STORE contract of ns_csum_batch_dev_store: every sum is
+    taken over the arena as it was before the call (`results` = py_batch /
+    c_batch of it), then each flagged descriptor writes its result r
+    big-endian at off + (flags >> 4): ^r, as header SetChecksum(^xsum)
+    (ipv4.go:223 via ipv4.go:236; tcp.go:252 via connect.go:663), or r itself
+    with STORE_RAW (the CHECKSUM_PARTIAL pseudo-header sum, connect.go:660).
+    A store whose 2 bytes leave the arena is dropped and counted.
+    Returns (new arena copy, dropped stores)."""
+    a = np.array(arena, dtype=np.uint8, copy=True)
+    dropped = 0
+    for i in np.flatnonzero(desc["flags"] & STORE):
+        f = int(desc["flags"][i])
+        at = int(desc["off"][i]) + (f >> STORE_SHIFT)
+        if at + 2 > len(a):
+            dropped += 1
+            continue
+        r = int(results[i])
+        v = r if f & STORE_RAW else (~r & 0xFFFF)
+        a[at] = v >> 8
+        a[at + 1] = v & 0xFF
+    return a, dropped
+
+
 # --------------------------------------------------------------------------
 # C restatement (oracle/csum_oracle.c)
 # --------------------------------------------------------------------------

@@ -569,3 +569,120 @@ def test_randomized_layouts(engine, seed):
     assert np.array_equal(got, want), np.flatnonzero(got != want)[:8]
     if seed % 3 == 1:
         assert np.array_equal(engine.batch_host(arena, d, chained=chained), want)
+
+
+def test_tx_store_device_resident(engine):
+    """The transmit side on the device (ns_csum_batch_dev_store): tx_batch's
+    packets with zeroed IPv4/TCP checksum fields, one chained launch computes
+    and stores both fields in place (ipv4.go:236, connect.go:662-663).  The
+    arena afterwards equals rx_batch's (checksums made independently by torch
+    integer ops), the results match the oracle over the pre-store bytes, and
+    the RX table over the stored packets sums every run to 0xffff."""
+    import oracle as O
+    from netstack_amd import workloads as W
+
+    torch = _torch()
+    n = 20000
+    arena, d = W.tx_batch(n, 77, "cuda")
+    before = arena.cpu().numpy()
+    want, nbad = O.c_batch(before, d, chained=True)
+    assert nbad == 0
+    desc = torch.from_numpy(d.view(np.uint8).copy()).cuda()
+    out = engine.batch_tensors(arena, desc, chained=True, store=True)
+    torch.cuda.synchronize()
+    assert engine.sync() == 0
+    assert np.array_equal(out.cpu().numpy().view(np.uint16), want)
+    after = arena.cpu().numpy()
+    expect, dropped = O.apply_stores(before, d, want)
+    assert dropped == 0 and np.array_equal(after, expect)
+    rx, _, _ = W.rx_batch(n, 77, "cuda")
+    assert torch.equal(arena, rx)
+    rd = torch.from_numpy(W._tcp_desc(n).view(np.uint8).copy()).cuda()
+    chk = engine.batch_tensors(arena, rd, chained=True)
+    torch.cuda.synchronize()
+    assert (chk.cpu().numpy().view(np.uint16)[0::3] == 0xFFFF).all()
+    assert (chk.cpu().numpy().view(np.uint16)[2::3] == 0xFFFF).all()
+
+
+def _store_batch(rng, n, chained, big):
+    """Random packets, each followed by a 4-byte unread gap; about half the
+    descriptors store (^r or raw r) at a random, often odd, offset inside
+    their own bytes or into their gap."""
+    from netstack_amd import workloads as W
+
+    lengths = (rng.integers(1000, 70000, n) if big else rng.integers(0, 300, n)).astype(np.uint32)
+    init = rng.integers(0, 65536, n).astype(np.uint16)
+    flags = rng.integers(0, 2, n).astype(np.uint16)
+    if chained:
+        flags |= (2 * (rng.random(n) < 0.5)).astype(np.uint16)
+    d, end = W.make_desc(lengths + 4, init, align=int(rng.choice([1, 2, 16])), base=int(rng.integers(0, 40)),
+                         flags=flags)
+    d["len"] = lengths
+    st = np.flatnonzero(rng.random(n) < 0.5)
+    own = (rng.random(st.size) < 0.5) & (lengths[st] >= 2)
+    at = np.where(own, (rng.random(st.size) * np.maximum(lengths[st].astype(np.int64) - 1, 1)).astype(np.int64),
+                  lengths[st].astype(np.int64) + rng.integers(0, 3, st.size))
+    raw = (rng.random(st.size) < 0.25).astype(np.uint16)
+    at = np.minimum(at, 4095)  # the 12-bit offset field
+    keep = at + 2 <= np.where(own, lengths[st], lengths[st] + 4)
+    st, at, raw = st[keep], at[keep], raw[keep]
+    d["flags"][st] |= (0x4 | (raw << 3) | (at.astype(np.uint16) << 4)).astype(np.uint16)
+    arena = rng.integers(0, 256, end + 8, dtype=np.uint8)
+    return arena, d
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_store_randomized(engine, seed):
+    """NS_DESC_STORE over random layouts: small (direct path) and big
+    packets, chained or not, stores inside the descriptor's own bytes (read
+    before the store) or into an unread gap, ^r and raw r, odd addresses.
+    The arena afterwards equals oracle.apply_stores over the oracle's results;
+    ns_csum_batch_dev (no store) leaves the same flags unapplied."""
+    import oracle as O
+
+    torch = _torch()
+    rng = np.random.default_rng(900 + seed)
+    chained, big = bool(seed % 2), seed >= 3
+    arena, d = _store_batch(rng, int(rng.integers(1, 3000)), chained, big)
+    want, bad = O.c_batch(arena, d, chained=chained)
+    assert bad == 0
+    expect, dropped = O.apply_stores(arena, d, want)
+    assert dropped == 0
+    # without store: results identical, arena untouched
+    dt = torch.from_numpy(arena).cuda()
+    desc = torch.from_numpy(d.view(np.uint8).copy()).cuda()
+    out = engine.batch_tensors(dt, desc, chained=chained)
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy().view(np.uint16), want)
+    assert np.array_equal(dt.cpu().numpy(), arena)
+    out = engine.batch_tensors(dt, desc, chained=chained, store=True)
+    torch.cuda.synchronize()
+    assert engine.sync() == 0
+    assert np.array_equal(out.cpu().numpy().view(np.uint16), want)
+    got = dt.cpu().numpy()
+    assert np.array_equal(got, expect), np.flatnonzero(got != expect)[:8]
+
+
+@pytest.mark.parametrize("chained", [False, True])
+def test_store_past_arena_dropped_and_counted(engine, chained):
+    """A store whose 2 bytes would leave the arena is dropped and counted in
+    ns_csum_sync's bad-descriptor count; the result is still written."""
+    import oracle as O
+
+    torch = _torch()
+    arena = np.arange(64, dtype=np.uint8)
+    d = np.zeros(3, dtype=O.DESC_DTYPE)
+    d["off"] = [0, 40, 10]
+    d["len"] = [20, 24, 6]
+    d["flags"] = [0x4 | (63 << 4), 0x4 | (23 << 4), 0x4 | (2 << 4)]  # at 63 (1 byte left), 63, 12
+    want, _ = O.c_batch(arena, d, chained=chained)
+    expect, dropped = O.apply_stores(arena, d, want)
+    assert dropped == 2
+    dt = torch.from_numpy(arena).cuda()
+    desc = torch.from_numpy(d.view(np.uint8).copy()).cuda()
+    engine.sync()
+    out = engine.batch_tensors(dt, desc, chained=chained, store=True)
+    torch.cuda.synchronize()
+    assert engine.sync() == 2
+    assert np.array_equal(out.cpu().numpy().view(np.uint16), want)
+    assert np.array_equal(dt.cpu().numpy(), expect)

@@ -141,3 +141,38 @@ def test_rx_batch_generator_valid_packets():
         xsum = O.py_checksum(bytes(a[b + 20:b + 40]), xsum)
         xsum = O.py_checksum(bytes(a[b + 40:b + 1500]), xsum)
         assert xsum == out[3 * i + 2]
+
+
+def test_tx_stores_reproduce_rx_packets():
+    """oracle.apply_stores over tx_batch (zeroed checksum fields, the store
+    flags of ns_csum_batch_dev_store) yields exactly rx_batch's packets, whose
+    checksums torch integer ops wrote independently; the IPv4 store matches
+    Go's ip.SetChecksum(^ip.CalculateChecksum()) (ipv4.go:236) restated in
+    pure Python."""
+    import oracle as O
+    from netstack_amd import workloads as W
+
+    tx, d = W.tx_batch(300, 9, "cpu")
+    rx, _, _ = W.rx_batch(300, 9, "cpu")
+    before = tx.numpy()
+    res, nbad = O.c_batch(before, d, chained=True)
+    assert nbad == 0
+    after, dropped = O.apply_stores(before, d, res)
+    assert dropped == 0 and np.array_equal(after, rx.numpy())
+    for i in (0, 299):
+        b = W.RX_STRIDE * i
+        x = ~O.py_checksum(bytes(before[b:b + 20]), 0) & 0xFFFF
+        assert after[b + 10] == x >> 8 and after[b + 11] == x & 0xFF
+
+
+def test_apply_stores_raw_odd_and_dropped():
+    """STORE_RAW writes r itself, offsets may be odd, and a store past the
+    arena end is dropped and counted."""
+    import oracle as O
+
+    a = np.zeros(10, dtype=np.uint8)
+    d = np.zeros(3, dtype=O.DESC_DTYPE)
+    d["flags"] = [O.STORE | (3 << 4), O.STORE | O.STORE_RAW | (6 << 4), O.STORE | (9 << 4)]
+    out, dropped = O.apply_stores(a, d, np.array([0x1234, 0xABCD, 1], dtype=np.uint16))
+    assert dropped == 1
+    assert list(out) == [0, 0, 0, 0xED, 0xCB, 0, 0xAB, 0xCD, 0, 0]
