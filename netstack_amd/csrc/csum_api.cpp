@@ -808,7 +808,7 @@ int batch_dev(ns_csum_ctx* ctx, const uint8_t* d_arena, uint64_t arena_bytes, co
     if (rc != NS_OK) return rc;
     part = ctx->partial.p;
   }
-  HIP_TRY(nsk::launch_batch(d_arena, arena_bytes, d_desc, n, d_out, part, ctx->d_err, s, 0, store));
+  HIP_TRY(nsk::launch_batch(d_arena, arena_bytes, d_desc, n, d_out, part, ctx->d_err, s, 0, store ? 1u : 0u));
   return NS_OK;
 }
 }  // namespace

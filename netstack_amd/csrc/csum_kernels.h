@@ -21,6 +21,6 @@ namespace nsk {
 hipError_t launch_batch(const uint8_t* arena, uint64_t arena_bytes,
                         const void* desc, uint32_t n, uint16_t* out,
                         uint32_t* partial, unsigned long long* err,
-                        hipStream_t stream, uint64_t sizing_bytes = 0, bool store = false);
+                        hipStream_t stream, uint64_t sizing_bytes = 0, uint32_t store = 0);
 
 }  // namespace nsk

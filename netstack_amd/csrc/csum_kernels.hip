@@ -269,6 +269,10 @@ struct HybLds {
   uint32_t acc[P];
   uint32_t wsmall[P / 64];
   uint32_t wex[P / 64];
+  // NS_DESC_STORE launches only: each lane's validated store word and
+  // address (written at decode, read back by the same lane after the scan).
+  uint64_t sat[P];
+  uint32_t stw[P];
 };
 
 struct Srd {
@@ -535,51 +539,68 @@ __device__ __forceinline__ uint32_t hyb_scan_tile(HybLds<WG>& L, const Srd& r, c
 // NS_DESC_STORE: a run's final result r goes into the packet, big-endian,
 // as ^r (SetChecksum(^xsum): connect.go:663, ipv4.go:236) or, with
 // NS_DESC_STORE_RAW, as r (the CHECKSUM_PARTIAL pseudo-header sum,
-// connect.go:660).  Two byte stores: the field need not be 2-byte aligned.
+// connect.go:660).  One u16 store, or two byte stores at an odd address.
 __device__ __forceinline__ void store_result(uint64_t addr, uint32_t r, uint32_t stw) {
   const uint32_t v = (stw & 2u) ? r : (~r & 0xFFFFu);
   uint8_t* p = reinterpret_cast<uint8_t*>((uintptr_t)addr);
-  p[0] = (uint8_t)(v >> 8);
-  p[1] = (uint8_t)v;
+  if (!(addr & 1u)) {
+    *reinterpret_cast<uint16_t*>(p) = (uint16_t)(((v & 0xFFu) << 8) | (v >> 8));
+  } else {
+    p[0] = (uint8_t)(v >> 8);
+    p[1] = (uint8_t)v;
+  }
 }
 
 // The store word (flags bits 2-15: NS_DESC_STORE | STORE_RAW | offset << 2)
-// is decoded here from a re-read of the (L2-resident) descriptor, and only
-// when the launch asked for stores: carrying it through the scan loops cost
-// every kernel 10-20 VGPRs and a wave per SIMD.  A store that would land
-// past the arena is dropped and counted as an error.
-__device__ __forceinline__ uint32_t store_word(uint32_t store, const uint4* __restrict__ desc, uint64_t i,
-                                               uint64_t arena_bytes, unsigned long long* err,
-                                               uint64_t* off) {
-  if (!store) return 0u;
-  const uint4 raw = desc[i];
-  const uint32_t stw = (raw.w >> 18) & 0x3FFFu;
-  if (!(stw & 3u)) return 0u;
-  *off = ((uint64_t)raw.x | ((uint64_t)raw.y << 32)) + (stw >> 2);
-  if (*off > arena_bytes || arena_bytes - *off < 2) {
+// and its absolute address are validated at decode and parked in LDS for
+// the lane's finish: carrying them through the scan loops in registers cost
+// every kernel 10-20 VGPRs and a wave per SIMD, and re-reading the
+// descriptor after the scan put a dependent global load at the end of every
+// tile (+25 us on 3M descriptors).  A store that would land past the arena
+// is dropped and counted as an error.
+template <int P>
+__device__ __forceinline__ void park_store(HybLds<P>& L, uint32_t store, uint4 raw, bool mine,
+                                           uint64_t arena_abs, uint64_t arena_bytes,
+                                           unsigned long long* err) {
+  if (!store) return;
+  uint32_t stw = mine ? (raw.w >> 18) & 0x3FFFu : 0u;
+  const uint64_t at = ((uint64_t)raw.x | ((uint64_t)raw.y << 32)) + (stw >> 2);
+  if (!(stw & 3u)) {
+    stw = 0;
+  } else if (at > arena_bytes || arena_bytes - at < 2) {
     atomicAdd(err, 1ull);
-    return 0u;
+    stw = 0;
   }
-  return stw;
+  L.stw[threadIdx.x] = stw;
+  L.sat[threadIdx.x] = arena_abs + at;
 }
 
-template <bool CH>
-__device__ __forceinline__ void finish_tile(uint32_t s, const Pkt& d, bool mine, uint64_t i, uint64_t n,
-                                            uint16_t* __restrict__ out, uint32_t* __restrict__ partial,
-                                            uint32_t store, const uint4* __restrict__ desc,
-                                            uint64_t arena_abs, uint64_t arena_bytes,
-                                            unsigned long long* err) {
-  if (!mine) return;
-  uint64_t at = 0;
-  const uint32_t stw = store_word(store, desc, i, arena_bytes, err, &at);
+template <int P, bool CH>
+__device__ __forceinline__ void finish_tile(HybLds<P>& L, uint32_t s, const Pkt& d, bool mine, uint64_t i,
+                                            uint64_t n, uint16_t* __restrict__ out,
+                                            uint32_t* __restrict__ partial, uint32_t store) {
+  const int t = threadIdx.x;
   if constexpr (CH) {
     const bool head = !d.cont || i == 0;
-    partial[i] = head ? fold1((d.cont ? 0u : d.init) + s) : s;
+    const uint32_t v = head ? fold1((d.cont ? 0u : d.init) + s) : s;
+    // Chained stores wait for csum_chain, which knows the final run value:
+    // the flag word carries the store word.  (An in-tile fold that stored
+    // runs lying inside the tile from this kernel measured 4-6 us slower on
+    // the TX batch: 2M scattered 2-byte stores cost the same ~50 us of HBM
+    // read-modify-write wherever they are issued, and issuing them here
+    // holds every workgroup until its stores drain.)
+    const uint32_t stw = (store && mine) ? L.stw[t] : 0u;
+    if (!mine) return;
+    partial[i] = v;
     reinterpret_cast<uint16_t*>(partial + n)[i] = (uint16_t)((head ? 0u : 1u) | (stw << 1));
   } else {
+    if (!mine) return;
     const uint32_t r = fold1(d.init + s);
     out[i] = (uint16_t)r;
-    if (stw) store_result(arena_abs + at, r, stw);
+    if (store) {
+      const uint32_t stw = L.stw[t];
+      if (stw) store_result(L.sat[t], r, stw);
+    }
   }
 }
 
@@ -605,6 +626,7 @@ __global__ __launch_bounds__(WG) void csum_hyb(
   const uint4 raw = mine ? desc[i] : make_uint4(0, 0, 0, 0);
   const uint64_t arena_abs = (uint64_t)(uintptr_t)arena;
   const Pkt d = decode(raw, mine, arena_abs, arena_bytes, err);
+  park_store(L, store, raw, mine, arena_abs, arena_bytes, err);
   Win w;
   if constexpr (WIN) {
     w = tile_window<WG>(L, d, chunks_of(d), (uint32_t)UD);
@@ -619,18 +641,18 @@ __global__ __launch_bounds__(WG) void csum_hyb(
     const PktInfo p = pkt_info(d, w.base);
     if (UD > 0 && w.small) {
       const uint32_t s = direct_sum<UD ? UD : 1>(r, p);
-      finish_tile<CH>(s, d, mine, i, n, out, partial, store, desc, arena_abs, arena_bytes, err);
+      finish_tile<WG, CH>(L, s, d, mine, i, n, out, partial, store);
       return;
     }
     const uint32_t s = hyb_scan_tile<WG, TP, GB, UB, US, AUXB, false, SU>(L, r, p, big_chunks);
-    finish_tile<CH>(s, d, mine, i, n, out, partial, store, desc, arena_abs, arena_bytes, err);
+    finish_tile<WG, CH>(L, s, d, mine, i, n, out, partial, store);
   } else if constexpr (WIN) {
     // The tile spans >= 4 GiB: 64-bit global loads, fewer in flight per lane
     // so this rarely taken path does not raise the kernel's register count.
     const Srd r = make_srd(0ull, 0ull);
     const PktInfo p = pkt_info(d, 0ull);
     const uint32_t s = hyb_scan_tile<WG, TP, 16, 4, 4, AUXB, true, 1>(L, r, p, big_chunks);
-    finish_tile<CH>(s, d, mine, i, n, out, partial, store, desc, arena_abs, arena_bytes, err);
+    finish_tile<WG, CH>(L, s, d, mine, i, n, out, partial, store);
   }
 }
 
@@ -740,7 +762,7 @@ static hipError_t launch_hyb(const uint8_t* arena, uint64_t arena_bytes, const v
 hipError_t launch_batch(const uint8_t* arena, uint64_t arena_bytes,
                         const void* desc, uint32_t n, uint16_t* out,
                         uint32_t* partial, unsigned long long* err,
-                        hipStream_t stream, uint64_t sizing_bytes, bool store) {
+                        hipStream_t stream, uint64_t sizing_bytes, uint32_t store) {
   if (n == 0) return hipSuccess;
   hipError_t e;
   if (sizing_bytes == 0) sizing_bytes = arena_bytes;
