@@ -122,6 +122,57 @@ def timed_region(step, sync, dist: Dist, steps: int, warmup: int, device=None):
     return dist.max(local, device), local
 
 
+CALIB_MODE, CALIB_BLOCKS = 2164, 16384  # calib_grp<16,4,nt>: the best pure read
+
+
+def launch_stats(launch, stream, reps: int = 20):
+    """SURVEY §8(d)'s per-launch view, measured after the timed region: `reps`
+    launches each bracketed by its own HIP event pair on the launch stream
+    (3 warm-ups first); returns sorted per-launch microseconds."""
+    import torch
+
+    for _ in range(3):
+        launch()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    for a, b in ev:
+        a.record(stream)
+        launch()
+        b.record(stream)
+    torch.cuda.synchronize()
+    return sorted(a.elapsed_time(b) * 1e3 for a, b in ev)
+
+
+def stream_calibration(arena, stream):
+    """Same-run read-stream calibration: the best pure-read
+    kernel of tools/tune.py (calib_grp<16,4,nt>, libns_tune.so, not product
+    code) over the same arena bytes; median of 20 launches.  None when the
+    tuning library is absent."""
+    import ctypes
+
+    path = os.path.join(ROOT, "netstack_amd", "lib", "libns_tune.so")
+    if not os.path.exists(path):
+        return None
+    import torch
+
+    L = ctypes.CDLL(path)
+    L.nsk_calib_launch.restype = ctypes.c_int
+    L.nsk_calib_launch.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                   ctypes.c_uint32, ctypes.c_void_p]
+    nbytes = min(arena.numel(), 0x7FFFFFF0) & ~15  # the kernel's SRD covers < 2 GiB
+    outb = torch.zeros(CALIB_BLOCKS, dtype=torch.int32, device=arena.device)  # one word per block
+
+    def launch():
+        rc = L.nsk_calib_launch(CALIB_MODE, arena.data_ptr(), nbytes, outb.data_ptr(), CALIB_BLOCKS,
+                                stream.cuda_stream)
+        if rc != 0:
+            raise RuntimeError(f"nsk_calib_launch failed: {rc}")
+
+    us = launch_stats(launch, stream)
+    med = us[len(us) // 2]
+    return {"kernel": "nsk::calib_grp<16,4,2> (pure nt read, 16-lane groups)", "bytes": nbytes,
+            "median_us": med, "GBps": nbytes / med / 1e3}
+
+
 def rank_batch(cfg: int, rank: int, world: int = 1):
     """This rank's batch.  cfg 2-4 (weak scaling): the config's layout, a
     distinct seed per rank.  cfg 5 (strong scaling): shard `rank` of `world`
@@ -250,8 +301,11 @@ def main():
     bad = eng.sync()
     kern_avg_s = ev[0].elapsed_time(ev[1]) / 1e3 / args.steps
 
-    # one more launch of the same kernel instance over arenas[0], outside the
-    # timed region: its results are what the CPU leg checks against the oracle
+    # per-launch statistics and the same-run read calibration (untimed), then
+    # one more launch of the same kernel instance over arenas[0]: its results
+    # are what the CPU leg checks against the oracle
+    per_launch = launch_stats(lambda: eng.batch_tensors(arenas[0], descs[0], out, stream=stream), stream)
+    calib = stream_calibration(arenas[0], stream)
     eng.batch_tensors(arenas[0], descs[0], out, stream=stream)
     torch.cuda.synchronize()
 
@@ -300,6 +354,11 @@ def main():
             "kernel": kernel_name(batch.arena_bytes, batch.n),
             "algorithmic_bytes_per_launch": algo_bytes,
             "avg_launch_us": kern_avg_s * 1e6,
+            "per_launch_us": {"median": per_launch[len(per_launch) // 2], "min": per_launch[0],
+                              "max": per_launch[-1], "launches": len(per_launch),
+                              "note": "own event pair per launch, after the timed region (rotation 0)"},
+            "stream_calibration": calib,
+            "frac_of_calibration": (achieved_gbs / calib["GBps"]) if calib else None,
         },
         "bad_descriptors": bad,
     }
