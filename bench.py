@@ -387,7 +387,7 @@ def packet_mode(args, dist, eng, dev, tx: bool):
     packets per GPU in HBM, three chained descriptors per packet (IPv4 header;
     pseudo-header addresses; TCP header + payload), one
     ns_csum_batch_dev(NS_BATCH_CHAINED) per step = the checksum kernel
-    (partial sums and continuation flags) plus the csum_chain pass that folds
+    (partial sums and continuation flags) plus the fold_scan pass that folds
     the runs.
 
     RX (config 7, rank 2: segment.parse / the IPv4 header check): every
@@ -484,7 +484,7 @@ def packet_mode(args, dist, eng, dev, tx: bool):
                    "packets_per_gpu": RX_N, "descriptors_per_gpu": n_desc},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "kernel": kernel_name(arena.numel(), n_desc, chained=True) + " + nsk::csum_chain",
+                     "kernel": kernel_name(arena.numel(), n_desc, chained=True) + " + nsk::fold_scan",
                      "algorithmic_bytes_per_launch": algo, "avg_launch_us": kern_avg_s * 1e6},
         "bad_descriptors": bad,
         "property_check": check,

@@ -69,13 +69,16 @@ template <typename T>
 struct DevBuf {
   T* p = nullptr;
   size_t cap = 0;  // elements
-  int ensure(size_t n) {
+  // zero = clear a fresh allocation (the chained-batch scratch: see
+  // csum_kernels.h).
+  int ensure(size_t n, bool zero = false) {
     if (n <= cap) return NS_OK;
     if (p) (void)hipFree(p);
     p = nullptr;
     cap = 0;
     size_t want = std::max<size_t>(n, 1);
     HIP_TRY(hipMalloc(reinterpret_cast<void**>(&p), want * sizeof(T)));
+    if (zero) HIP_TRY(hipMemset(p, 0, want * sizeof(T)));
     cap = want;
     return NS_OK;
   }
@@ -186,9 +189,9 @@ struct DeviceGuard {
   }
 };
 
-// Chained-batch scratch for n descriptors: n u32 partials + n u16
-// continuation flags (nsk::launch_batch).
-size_t chain_words(uint64_t n) { return (size_t)(n + (n + 1) / 2); }
+// Chained-batch scratch for n descriptors (nsk::launch_batch): partials,
+// continuation flags and the run-fold aggregates.
+size_t chain_words(uint64_t n) { return (size_t)nsk::chain_scratch_words(n); }
 
 bool any_cont(const ns_pkt_desc* d, uint32_t n) {
   for (uint32_t i = 0; i < n; ++i)
@@ -237,7 +240,7 @@ int run_zero_copy(ns_csum_ctx* ctx, SmallReq* const* reqs, size_t nreq) {
   const uint64_t o_off = nd * sizeof(ns_pkt_desc);
   int rc;
   if ((rc = ctx->z_buf.ensure(std::max<uint64_t>(kPassTableBytes, o_off + nd * 2))) != NS_OK) return rc;
-  if (chained && (rc = ctx->d_part[0].ensure(chain_words(nd))) != NS_OK) return rc;
+  if (chained && (rc = ctx->d_part[0].ensure(chain_words(nd), true)) != NS_OK) return rc;
   uint8_t* z = ctx->z_buf.p;
   ns_pkt_desc* zd = reinterpret_cast<ns_pkt_desc*>(z);
   uint64_t k = 0;
@@ -251,7 +254,7 @@ int run_zero_copy(ns_csum_ctx* ctx, SmallReq* const* reqs, size_t nreq) {
         zd[k].flags &= (uint16_t)~NS_DESC_CONT;  // independent in an unchained batch
       } else if (i == 0 && (zd[k].flags & NS_DESC_CONT)) {
         // A batch's first descriptor heads its run even when flagged CONT
-        // (with initial 0, csum_chain): keep that inside a combined pass.
+        // (with initial 0, fold_scan): keep that inside a combined pass.
         zd[k].flags &= (uint16_t)~NS_DESC_CONT;
         zd[k].initial = 0;
       }
@@ -429,7 +432,7 @@ int run_host_batch(ns_csum_ctx* ctx, const uint8_t* h_arena, uint64_t arena_byte
     if ((rc = ctx->d_out[slot].ensure(cnt)) != NS_OK) return rc;
     if ((rc = ctx->h_desc[slot].ensure(cnt)) != NS_OK) return rc;
     if ((rc = ctx->h_out[slot].ensure(cnt)) != NS_OK) return rc;
-    if (chained && (rc = ctx->d_part[slot].ensure(chain_words(cnt))) != NS_OK) return rc;
+    if (chained && (rc = ctx->d_part[slot].ensure(chain_words(cnt), true)) != NS_OK) return rc;
     ns_pkt_desc* hd = ctx->h_desc[slot].p;
     for (uint32_t q = 0; q < cnt; ++q) {
       hd[q] = h_desc[k + q];
@@ -804,7 +807,7 @@ int batch_dev(ns_csum_ctx* ctx, const uint8_t* d_arena, uint64_t arena_bytes, co
   uint32_t* part = nullptr;
   if (batch_flags & NS_BATCH_CHAINED) {
     std::lock_guard<std::mutex> lk(ctx->mu);
-    int rc = ctx->partial.ensure(chain_words(n));
+    int rc = ctx->partial.ensure(chain_words(n), true);
     if (rc != NS_OK) return rc;
     part = ctx->partial.p;
   }

@@ -28,6 +28,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <atomic>
 #include <type_traits>
 
 #include "csum_kernels.h"
@@ -534,7 +535,7 @@ __device__ __forceinline__ uint32_t hyb_scan_tile(HybLds<WG>& L, const Srd& r, c
 // (descriptor 0 heads its run with initial 0), a continuation its s, each
 // with a u16 continuation flag after the n partials (u16, not u8: a wave's
 // 64 flags then fill a whole 128-B line — byte flags cost 8.5 us more on 3M
-// descriptors, profiles/r01/tune_chained_b2b.log); csum_chain folds the runs
+// descriptors, profiles/r01/tune_chained_b2b.log); fold_scan folds the runs
 // from those alone (6 bytes per descriptor, no descriptor re-read).
 // NS_DESC_STORE: a run's final result r goes into the packet, big-endian,
 // as ^r (SetChecksum(^xsum): connect.go:663, ipv4.go:236) or, with
@@ -583,7 +584,7 @@ __device__ __forceinline__ void finish_tile(HybLds<P>& L, uint32_t s, const Pkt&
   if constexpr (CH) {
     const bool head = !d.cont || i == 0;
     const uint32_t v = head ? fold1((d.cont ? 0u : d.init) + s) : s;
-    // Chained stores wait for csum_chain, which knows the final run value:
+    // Chained stores wait for fold_scan, which knows the final run value:
     // the flag word carries the store word.  (An in-tile fold that stored
     // runs lying inside the tile from this kernel measured 4-6 us slower on
     // the TX batch: 2M scattered 2-byte stores cost the same ~50 us of HBM
@@ -592,7 +593,7 @@ __device__ __forceinline__ void finish_tile(HybLds<P>& L, uint32_t s, const Pkt&
     const uint32_t stw = (store && mine) ? L.stw[t] : 0u;
     if (!mine) return;
     partial[i] = v;
-    reinterpret_cast<uint16_t*>(partial + n)[i] = (uint16_t)((head ? 0u : 1u) | (stw << 1));
+    reinterpret_cast<uint16_t*>(partial + chain_flag_word(n))[i] = (uint16_t)((head ? 0u : 1u) | (stw << 1));
   } else {
     if (!mine) return;
     const uint32_t r = fold1(d.init + s);
@@ -610,7 +611,7 @@ __device__ __forceinline__ void finish_tile(HybLds<P>& L, uint32_t s, const Pkt&
 // TP = descriptors per tile (<= WG): large packets get fewer per workgroup so
 // a batch of 64 KiB GSO buffers still spreads over every CU.
 // SU = small runs issued per lane per iteration; CH = chained batch
-// (finish_tile writes partials and continuation flags for csum_chain).
+// (finish_tile writes partials and continuation flags for fold_scan).
 template <int WG, int TP, int GB, int UB, int US, int AUXB, int UD = 0, bool WIN = false,
           int SU = 1, bool CH = false>
 __global__ __launch_bounds__(WG) void csum_hyb(
@@ -656,39 +657,239 @@ __global__ __launch_bounds__(WG) void csum_hyb(
   }
 }
 
-// Sequential fold of NS_DESC_CONT runs (checksum.go:89 / the
-// `xsum = Checksum(v, xsum)` loops) over finish_tile's chained output: one
-// thread per run head, out[k] = fold1(out[k-1] + s_k).  A descriptor whose
-// flag word carries a store (bits 1-15) writes its result into the packet at
-// arena + desc.off + offset.
-__global__ void csum_chain(const uint32_t* __restrict__ partial, uint32_t n, uint16_t* __restrict__ out,
-                           const uint4* __restrict__ desc, const uint8_t* __restrict__ arena) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint16_t* flag = reinterpret_cast<const uint16_t*>(partial + n);
-  if (i >= n) return;
-  auto put = [&](uint64_t k, uint32_t v, uint16_t f) {
-    out[k] = (uint16_t)v;
-    const uint32_t stw = (uint32_t)f >> 1;
-    if (stw & 3u) {
-      const uint4 dk = desc[k];
-      store_result((uint64_t)(uintptr_t)arena + ((uint64_t)dk.x | ((uint64_t)dk.y << 32)) + (stw >> 2), v, stw);
+// ---- run folding (NS_DESC_CONT chains) -------------------------------------
+// After the CH kernel, descriptor k holds partial p_k and flag f_k (bit 0:
+// continuation; bits 1-15: the store word).  Go's chaining (checksum.go:89,
+// the `xsum = Checksum(v, xsum)` loops) is x_k = fold1(x_{k-1} + p_k) along a
+// run, x_head = p_head (already folded with its initial).
+//
+// As a scan.  While x + p cannot wrap 2^32 (x <= 0xFFFF, so only p >=
+// 0xFFFF0001 can), fold1(x + p) == x + p (mod 65535), and it is 0 iff x == 0
+// and p == 0, else in [1, 0xFFFF].  So x is exactly described by
+// (r = x mod 65535, z = x is 0), and a continuation acts as
+// (r, z) -> (r + p mod 65535, z && p == 0): an associative segmented scan in
+// which a head resets the state.  fold_scan is one pass (decoupled look-back):
+// each workgroup scans kFoldBlock descriptors, publishes its aggregate (or,
+// holding a head, its inclusive state) and takes its carry-in from its
+// predecessors' statuses.  O(n) for any run length: one thread per head
+// walking its run cost 183 ms on a 1M-descriptor run
+// (profiles/r01/chain_fold.txt).  A block holding a continuation that could
+// wrap folds its descriptors sequentially from the exact carry-in, as Go does,
+// and publishes only its (exact) inclusive state.
+//
+// State word: bits 0-15 r, bit 16 z, bit 17 "a run head inside".
+constexpr uint32_t kFZ = 1u << 16, kFH = 1u << 17, kFIdent = kFZ, kFMask = (1u << 18) - 1;
+constexpr uint32_t kFAgg = 1u, kFIncl = 2u;  // status kinds
+
+__device__ __forceinline__ uint32_t mod65535(uint32_t v) {
+  v = (v & 0xFFFFu) + (v >> 16);
+  v = (v & 0xFFFFu) + (v >> 16);
+  return v == 0xFFFFu ? 0u : v;
+}
+
+__device__ __forceinline__ uint32_t fold_state(uint32_t x) {  // a head with value x
+  return (x == 0xFFFFu ? 0u : x) | (x == 0 ? kFZ : 0u) | kFH;
+}
+
+__device__ __forceinline__ uint32_t fold_elem(uint32_t p, uint32_t f) {
+  return (f & 1u) ? (mod65535(p) | (p == 0 ? kFZ : 0u)) : fold_state(p);
+}
+
+__device__ __forceinline__ uint32_t fold_combine(uint32_t a, uint32_t b) {  // a, then b
+  if (b & kFH) return b;
+  uint32_t r = (a & 0xFFFFu) + (b & 0xFFFFu);
+  r = r >= 65535u ? r - 65535u : r;
+  return r | (a & b & kFZ) | (a & kFH);
+}
+
+__device__ __forceinline__ uint32_t fold_value(uint32_t st) {
+  return (st & kFZ) ? 0u : ((st & 0xFFFFu) == 0 ? 0xFFFFu : (st & 0xFFFFu));
+}
+
+__device__ __forceinline__ void fold_publish(uint64_t* st, uint32_t gen, uint32_t kind, uint32_t state) {
+  // Relaxed: a status word carries all it says (no other data is published
+  // through it), and a release/acquire pair at agent scope would write back /
+  // invalidate the XCD's whole L2 per block.
+  __hip_atomic_store(st, ((uint64_t)gen << 32) | ((uint64_t)kind << 30) | state, __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+
+constexpr uint32_t kFoldSpins = 4096;
+
+// The state just before descriptor k0 > 0, by Go's own sequential fold from
+// the head of the run k0 falls in (exact; the look-back's fallback).
+__device__ __noinline__ uint32_t fold_carry_walk(const uint32_t* __restrict__ partial,
+                                                 const uint16_t* __restrict__ flags, uint64_t k0) {
+  uint64_t h = k0 - 1;
+  while (h > 0 && (flags[h] & 1u)) --h;
+  uint32_t x = partial[h];
+  for (uint64_t k = h + 1; k < k0; ++k) x = fold1(x + partial[k]);
+  return fold_state(x);
+}
+
+__global__ __launch_bounds__(256) void fold_scan(const uint32_t* __restrict__ partial,
+                                                 const uint16_t* __restrict__ flags, uint32_t n,
+                                                 uint64_t* __restrict__ status, uint32_t gen,
+                                                 uint16_t* __restrict__ out, const uint4* __restrict__ desc,
+                                                 const uint8_t* __restrict__ arena) {
+  __shared__ uint32_t sh[4];
+  __shared__ uint32_t s_carry;
+  __shared__ uint32_t lx[kFoldBlock];  // results + flags (wrap path; store transposition)
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  // The look-back below waits only on lower-numbered blocks, which the
+  // dispatcher starts first; should one not be running (or be slow), the
+  // waiter stops after kFoldSpins polls and derives its carry-in itself
+  // (fold_carry_walk), so no schedule can deadlock.  (An atomic ticket for
+  // the block order instead cost 17 us on 1,536 blocks: one contended
+  // device-scope atomic per block.)
+  const uint32_t blk = blockIdx.x;
+  const uint64_t b0 = (uint64_t)blk * kFoldBlock;
+  const uint64_t base = b0 + (uint64_t)t * kFoldPer;
+
+  // Scan phase: each thread owns 8 consecutive descriptors (3 vector loads).
+  uint32_t p[kFoldPer], f[kFoldPer];
+  if (base + kFoldPer <= n) {
+    const uint4 a = *reinterpret_cast<const uint4*>(partial + base);
+    const uint4 b = *reinterpret_cast<const uint4*>(partial + base + 4);
+    const uint4 c = *reinterpret_cast<const uint4*>(flags + base);
+    p[0] = a.x; p[1] = a.y; p[2] = a.z; p[3] = a.w;
+    p[4] = b.x; p[5] = b.y; p[6] = b.z; p[7] = b.w;
+    f[0] = c.x & 0xFFFFu; f[1] = c.x >> 16; f[2] = c.y & 0xFFFFu; f[3] = c.y >> 16;
+    f[4] = c.z & 0xFFFFu; f[5] = c.z >> 16; f[6] = c.w & 0xFFFFu; f[7] = c.w >> 16;
+  } else {
+#pragma unroll
+    for (uint32_t j = 0; j < kFoldPer; ++j) {
+      const bool in = base + j < n;
+      p[j] = in ? partial[base + j] : 0u;
+      f[j] = in ? flags[base + j] : 1u;  // past the end: an empty continuation
     }
-  };
-  // This descriptor and the next one are loaded together (most runs are one
-  // or two descriptors long: a header and its payload), so a short run costs
-  // one memory round trip.
-  const bool has1 = i + 1 < n;
-  const uint16_t c0 = flag[i], c1 = has1 ? flag[i + 1] : 0;
-  const uint32_t p0 = partial[i], p1 = has1 ? partial[i + 1] : 0u;
-  if (c0 & 1u) return;
-  uint32_t v = p0;
-  put(i, v, c0);
-  if (!(c1 & 1u)) return;
-  v = fold1(v + p1);
-  put(i + 1, v, c1);
-  for (uint64_t k = i + 2; k < n && (flag[k] & 1u); ++k) {
-    v = fold1(v + partial[k]);
-    put(k, v, flag[k]);
+  }
+  uint32_t e[kFoldPer];
+  uint32_t a = kFIdent;
+  bool wraps = false;
+#pragma unroll
+  for (uint32_t j = 0; j < kFoldPer; ++j) {
+    e[j] = fold_elem(p[j], f[j]);
+    a = fold_combine(a, e[j]);
+    wraps |= (f[j] & 1u) && p[j] >= 0xFFFF0001u;
+  }
+  // ordered inclusive scan of the thread totals: within the wave, then the waves
+  uint32_t v = a;
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t o = __shfl_up(v, d, 64);
+    if (lane >= d) v = fold_combine(o, v);
+  }
+  if (lane == 63) sh[w] = v;
+  const bool seq = __syncthreads_or(wraps) != 0;
+  const uint32_t total = fold_combine(fold_combine(sh[0], sh[1]), fold_combine(sh[2], sh[3]));
+
+  if (t == 0) {
+    const bool incl = blk == 0 || (total & kFH);
+    if (!seq) fold_publish(&status[blk], gen, incl ? kFIncl : kFAgg, total);
+    uint32_t carry = kFIdent;
+    if (blk > 0) {
+      // Walk back to the nearest inclusive status; the aggregates passed on
+      // the way hold no head and no wrap, so they combine as residue adds.
+      uint32_t run = kFIdent;
+      for (uint32_t j = blk - 1;; --j) {
+        uint64_t sw = 0;
+        bool ready = false;
+        for (uint32_t spins = 0; spins < kFoldSpins; ++spins) {
+          sw = __hip_atomic_load(&status[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if ((uint32_t)(sw >> 32) == gen && ((sw >> 30) & 3u)) {
+            ready = true;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(2);
+        }
+        if (!ready) {
+          carry = fold_carry_walk(partial, flags, b0);
+          break;
+        }
+        const uint32_t val = (uint32_t)sw & kFMask;
+        if (((sw >> 30) & 3u) == kFIncl) {
+          carry = fold_combine(val, run);
+          break;
+        }
+        run = fold_combine(val, run);
+      }
+      if (!seq && !incl) fold_publish(&status[blk], gen, kFIncl, fold_combine(carry, total));
+    }
+    s_carry = carry;
+  }
+  __syncthreads();
+  const uint32_t carry = s_carry;
+
+  uint32_t x[kFoldPer];
+  if (!seq) {
+    uint32_t st = carry;
+    for (int q = 0; q < w; ++q) st = fold_combine(st, sh[q]);
+    const uint32_t before = __shfl_up(v, 1, 64);
+    if (lane > 0) st = fold_combine(st, before);
+#pragma unroll
+    for (uint32_t j = 0; j < kFoldPer; ++j) {
+      st = fold_combine(st, e[j]);
+      x[j] = fold_value(st);
+    }
+  } else {
+    // Go's own sequential fold over the block, from the exact carry-in (a
+    // head-holding state, or nothing before descriptor 0).
+    if (t == 0) {
+      uint32_t xv = fold_value(carry);
+      const uint64_t cnt = min<uint64_t>(kFoldBlock, n - b0);
+      for (uint32_t k = 0; k < cnt; ++k) {
+        const uint32_t pk = partial[b0 + k];
+        const uint32_t fk = flags[b0 + k];
+        xv = (fk & 1u) ? fold1(xv + pk) : pk;
+        lx[k] = xv | (fk << 16);
+      }
+      fold_publish(&status[blk], gen, kFIncl, fold_state(xv));
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t j = 0; j < kFoldPer; ++j) x[j] = lx[t * kFoldPer + j] & 0xFFFFu;
+  }
+  uint32_t mine_st = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < kFoldPer; ++j) mine_st |= (f[j] >> 1) & 3u;
+  const bool stores = __syncthreads_or(mine_st) != 0;
+
+  if (base + kFoldPer <= n && ((uintptr_t)(out + base) & 15u) == 0) {
+    uint4 o;
+    o.x = x[0] | (x[1] << 16); o.y = x[2] | (x[3] << 16);
+    o.z = x[4] | (x[5] << 16); o.w = x[6] | (x[7] << 16);
+    *reinterpret_cast<uint4*>(out + base) = o;
+  } else {
+#pragma unroll
+    for (uint32_t j = 0; j < kFoldPer; ++j)
+      if (base + j < n) out[base + j] = (uint16_t)x[j];
+  }
+  if (!stores) return;
+
+  // In-packet stores (NS_DESC_STORE), transposed through LDS: round j covers
+  // descriptors b0 + 256 j + t, so each store instruction of a round writes
+  // neighbouring packets (the partial-sector read-modify-writes then stay in
+  // nearby HBM rows: 11 us less per 2M stores than descriptors 8 apart per
+  // instruction).
+  if (!seq) {
+#pragma unroll
+    for (uint32_t j = 0; j < kFoldPer; ++j) lx[t * kFoldPer + j] = x[j] | (f[j] << 16);
+  }
+  __syncthreads();
+  uint32_t xf[kFoldPer];
+  uint4 dk[kFoldPer];
+#pragma unroll
+  for (uint32_t j = 0; j < kFoldPer; ++j) {
+    const uint64_t k = b0 + 256u * j + t;
+    xf[j] = k < n ? lx[256u * j + t] : 0u;
+    dk[j] = ((xf[j] >> 17) & 3u) ? desc[k] : make_uint4(0, 0, 0, 0);
+  }
+#pragma unroll
+  for (uint32_t j = 0; j < kFoldPer; ++j) {
+    const uint32_t stw = xf[j] >> 17;
+    if (stw & 3u)
+      store_result((uint64_t)(uintptr_t)arena + ((uint64_t)dk[j].x | ((uint64_t)dk[j].y << 32)) + (stw >> 2),
+                   xf[j] & 0xFFFFu, stw);
   }
 }
 
@@ -763,6 +964,7 @@ hipError_t launch_batch(const uint8_t* arena, uint64_t arena_bytes,
                         const void* desc, uint32_t n, uint16_t* out,
                         uint32_t* partial, unsigned long long* err,
                         hipStream_t stream, uint64_t sizing_bytes, uint32_t store) {
+  uint32_t* part = partial;  // the chained scratch (layout: csum_kernels.h)
   if (n == 0) return hipSuccess;
   hipError_t e;
   if (sizing_bytes == 0) sizing_bytes = arena_bytes;
@@ -773,18 +975,25 @@ hipError_t launch_batch(const uint8_t* arena, uint64_t arena_bytes,
     // smaller packets to per-lane runs of 4, two runs issued per lane per
     // iteration (tools/tune.py on MI355X: 220.6 us on 1M x 1500 B = 90.2% of
     // 8 TB/s, 107 us on the Zipf batch; profiles/r01/tune_*.json).
-    e = launch_hyb<8, 16, 4, 2, 0, 2>(arena, arena_bytes, desc, n, out, partial, err, stream, 64u,
+    e = launch_hyb<8, 16, 4, 2, 0, 2>(arena, arena_bytes, desc, n, out, part, err, stream, 64u,
                                       sizing_bytes, kTileBytes, store);
   } else {
     // Small packets: the same kernel plus the direct path — a tile whose
     // packets all span <= 5 chunks (any <= 65-B packet) has each lane read its
     // own packet with no scan; 16 x 8 groups keep the register count (and the
     // occupancy this latency-bound case needs) lower.
-    e = launch_hyb<16, 8, 4, 2, 5>(arena, arena_bytes, desc, n, out, partial, err, stream, 64u, 0, kTileBytes,
+    e = launch_hyb<16, 8, 4, 2, 5>(arena, arena_bytes, desc, n, out, part, err, stream, 64u, 0, kTileBytes,
                                    store);
   }
-  if (e != hipSuccess || partial == nullptr) return e;
-  hipLaunchKernelGGL(csum_chain, dim3((n + 255) / 256), dim3(256), 0, stream, partial, n, out,
+  if (e != hipSuccess || part == nullptr) return e;
+  // run folding: one pass over 6 B per descriptor, any run length
+  static std::atomic<uint32_t> gen_counter{0};
+  uint32_t gen = ++gen_counter;
+  if (gen == 0) gen = ++gen_counter;  // 0 never tags a status
+  const uint32_t nb = (uint32_t)chain_blocks(n);
+  const uint16_t* flags = reinterpret_cast<const uint16_t*>(part + chain_flag_word(n));
+  uint64_t* status = reinterpret_cast<uint64_t*>(part + chain_status_word(n));
+  hipLaunchKernelGGL(fold_scan, dim3(nb), dim3(256), 0, stream, part, flags, n, status, gen, out,
                      reinterpret_cast<const uint4*>(desc), arena);
   return hipGetLastError();
 }

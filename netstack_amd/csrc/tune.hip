@@ -281,14 +281,15 @@ hipError_t launch_tb(const uint8_t* arena, uint64_t arena_bytes, const void* des
 }
 
 // Chained timing: the CH instance (partials + continuation flags) with or
-// without the csum_chain pass, over a scratch buffer owned here.
+// without the run-fold passes, over a scratch buffer owned here.
 static uint32_t* g_part = nullptr;
 static size_t g_part_n = 0;
 static uint32_t* part_for(uint32_t n) {
-  const size_t want = (size_t)n + (n + 1) / 2;
+  const size_t want = (size_t)chain_scratch_words(n);
   if (want > g_part_n) {
     if (g_part) (void)hipFree(g_part);
     if (hipMalloc(reinterpret_cast<void**>(&g_part), want * 4) != hipSuccess) return nullptr;
+    if (hipMemset(g_part, 0, want * 4) != hipSuccess) return nullptr;  // see chain_scratch_words
     g_part_n = want;
   }
   return g_part;

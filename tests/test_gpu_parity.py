@@ -428,7 +428,7 @@ def test_w_only_threshold_and_zero_sums(engine, chained):
     both sides of the threshold at odd starts, all-0xFF bytes (largest sums),
     all-zero bytes (S == 0 must stay distinguishable from S == 65535), initial
     0 / 1 / 0xFFFF, odd flags, mixed into the same tiles as small packets —
-    plain and chained (the W-only class value as a csum_chain partial)."""
+    plain and chained (the W-only class value as a chained partial)."""
     import oracle as O
     from netstack_amd import workloads as W
 
@@ -686,3 +686,70 @@ def test_store_past_arena_dropped_and_counted(engine, chained):
     assert engine.sync() == 2
     assert np.array_equal(out.cpu().numpy().view(np.uint16), want)
     assert np.array_equal(dt.cpu().numpy(), expect)
+
+
+@pytest.mark.parametrize("layout", ["one_run", "mixed", "zeros"])
+def test_long_chained_runs(engine, layout):
+    """Run folding at any run length (the segmented scan of fold_reduce /
+    fold_apply): one run over 300K descriptors, runs of random length up to
+    50K crossing many 2048-descriptor blocks, and all-zero runs whose results
+    hinge on 0 vs 0xFFFF; every result against the oracle."""
+    import oracle as O
+    from netstack_amd import workloads as W
+
+    rng = np.random.default_rng({"one_run": 1, "mixed": 2, "zeros": 3}[layout])
+    n = 300_000
+    lengths = rng.integers(0, 40, n).astype(np.uint32)
+    init = rng.integers(0, 65536, n).astype(np.uint16)
+    if layout == "one_run":
+        flags = np.full(n, 2, np.uint16)
+    else:
+        flags = np.full(n, 2, np.uint16)
+        heads = np.cumsum(rng.integers(1, 50_000, 40))
+        heads = heads[heads < n]
+        flags[heads] = 0
+        flags[rng.random(n) < 0.001] = 0
+    flags[0] = 0
+    flags |= rng.integers(0, 2, n).astype(np.uint16)  # odd carry-ins
+    d, end = W.make_desc(lengths, init, align=int(rng.choice([1, 2])), flags=flags)
+    arena = rng.integers(0, 256, end + 16, dtype=np.uint8)
+    if layout == "zeros":
+        arena[:] = 0
+        d["initial"][rng.random(n) < 0.9] = 0
+    want, bad = O.c_batch(arena, d, chained=True)
+    assert bad == 0
+    got = dev_batch(engine, arena, d, chained=True)
+    assert np.array_equal(got, want), np.flatnonzero(got != want)[:8]
+
+
+def test_chain_wrap_fallback(engine):
+    """A continuation whose 32-bit sum is 0xFFFFFFFF (65,537 words of 0xFFFF,
+    above the W-only limit, so summed exactly) makes x + s wrap 2^32 for any
+    x >= 1: the launch falls back to Go's sequential fold and stays bit-exact,
+    including runs elsewhere in the batch and long runs."""
+    import oracle as O
+    from netstack_amd import workloads as W
+
+    rng = np.random.default_rng(77)
+    n = 20_000
+    lengths = rng.integers(0, 60, n).astype(np.uint32)
+    lengths[[5, 9000, 15000]] = 131_074
+    flags = (2 * (rng.random(n) < 0.7)).astype(np.uint16)
+    flags[[5, 9000, 15000]] = 2
+    flags[[4, 8999]] = 0
+    flags[0] = 0
+    init = rng.integers(0, 65536, n).astype(np.uint16)
+    d, end = W.make_desc(lengths, init, align=2, flags=flags)
+    arena = rng.integers(0, 256, end, dtype=np.uint8)
+    for k in (5, 9000, 15000):
+        o = int(d["off"][k])
+        arena[o:o + 131_074] = 0xFF
+    want, bad = O.c_batch(arena, d, chained=True)
+    assert bad == 0
+    got = dev_batch(engine, arena, d, chained=True)
+    assert np.array_equal(got, want), np.flatnonzero(got != want)[:8]
+    # and the same batch without the wrapping pieces takes the scan
+    d2 = d.copy()
+    d2["len"][[5, 9000, 15000]] = 7
+    want2, _ = O.c_batch(arena, d2, chained=True)
+    assert np.array_equal(dev_batch(engine, arena, d2, chained=True), want2)

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Workload for --pmc passes comparing the device-resident RX check (chained,
 no stores) with the TX fill (the same table plus two checksum stores per
-packet): REPS launches each, in that order, then csum_hyb / csum_chain
+packet): REPS launches each, in that order, then csum_hyb / fold_scan
 counter values per dispatch are printed by `--parse DIR`.
 
   rocprofv3 --pmc WRITE_SIZE -d OUT -o run --output-format csv -- python3 tools/pmc_tx.py
@@ -52,7 +52,7 @@ def parse(outdir):
                 continue
             k = int(r["Dispatch_Id"])
             per[k][r["Counter_Name"]] += float(r["Counter_Value"])
-            names[k] = "csum_chain" if "csum_chain" in r["Kernel_Name"] else "csum_hyb"
+            names[k] = "fold_scan" if "fold_scan" in r["Kernel_Name"] else "csum_hyb"
     for k in sorted(per):
         print(k, names[k], dict(per[k]))
 
