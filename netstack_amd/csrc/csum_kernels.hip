@@ -727,6 +727,9 @@ __device__ __noinline__ uint32_t fold_carry_walk(const uint32_t* __restrict__ pa
   return fold_state(x);
 }
 
+// SPINS: polls of a predecessor's status before deriving the carry-in
+// directly (the tuning library builds SPINS = 0 to test that path).
+template <uint32_t SPINS = kFoldSpins>
 __global__ __launch_bounds__(256) void fold_scan(const uint32_t* __restrict__ partial,
                                                  const uint16_t* __restrict__ flags, uint32_t n,
                                                  uint64_t* __restrict__ status, uint32_t gen,
@@ -794,7 +797,7 @@ __global__ __launch_bounds__(256) void fold_scan(const uint32_t* __restrict__ pa
       for (uint32_t j = blk - 1;; --j) {
         uint64_t sw = 0;
         bool ready = false;
-        for (uint32_t spins = 0; spins < kFoldSpins; ++spins) {
+        for (uint32_t spins = 0; spins < SPINS; ++spins) {
           sw = __hip_atomic_load(&status[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           if ((uint32_t)(sw >> 32) == gen && ((sw >> 30) & 3u)) {
             ready = true;
@@ -898,6 +901,19 @@ __global__ __launch_bounds__(256) void fold_scan(const uint32_t* __restrict__ pa
 // ---- launchers (C++ linkage, used by csum_api.cpp) ------------------------
 namespace nsk {
 
+template <uint32_t SPINS = kFoldSpins>
+static void launch_fold(uint32_t* part, uint32_t n, uint16_t* out, const void* desc, const uint8_t* arena,
+                        hipStream_t stream) {
+  static std::atomic<uint32_t> gen_counter{0};
+  uint32_t gen = ++gen_counter;
+  if (gen == 0) gen = ++gen_counter;  // 0 never tags a status
+  const uint32_t nb = (uint32_t)chain_blocks(n);
+  const uint16_t* flags = reinterpret_cast<const uint16_t*>(part + chain_flag_word(n));
+  uint64_t* status = reinterpret_cast<uint64_t*>(part + chain_status_word(n));
+  hipLaunchKernelGGL(fold_scan<SPINS>, dim3(nb), dim3(256), 0, stream, part, flags, n, status, gen, out,
+                     reinterpret_cast<const uint4*>(desc), arena);
+}
+
 template <int TP, int GB, int UB, int US, int AUXB, int UD, int SU = 1>
 static hipError_t launch_hyb_tp(const uint8_t* arena, uint64_t arena_bytes, const void* desc,
                                 uint32_t n, uint16_t* out, uint32_t* partial,
@@ -987,14 +1003,7 @@ hipError_t launch_batch(const uint8_t* arena, uint64_t arena_bytes,
   }
   if (e != hipSuccess || part == nullptr) return e;
   // run folding: one pass over 6 B per descriptor, any run length
-  static std::atomic<uint32_t> gen_counter{0};
-  uint32_t gen = ++gen_counter;
-  if (gen == 0) gen = ++gen_counter;  // 0 never tags a status
-  const uint32_t nb = (uint32_t)chain_blocks(n);
-  const uint16_t* flags = reinterpret_cast<const uint16_t*>(part + chain_flag_word(n));
-  uint64_t* status = reinterpret_cast<uint64_t*>(part + chain_status_word(n));
-  hipLaunchKernelGGL(fold_scan, dim3(nb), dim3(256), 0, stream, part, flags, n, status, gen, out,
-                     reinterpret_cast<const uint4*>(desc), arena);
+  launch_fold<>(part, n, out, desc, arena, stream);
   return hipGetLastError();
 }
 

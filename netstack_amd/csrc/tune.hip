@@ -303,6 +303,19 @@ hipError_t launch_chained(const uint8_t* arena, uint64_t arena_bytes, const void
   return launch_hyb<8, 16, 4, 2, 0, 2>(arena, arena_bytes, desc, n, out, part, err, s, 64u);
 }
 
+// The chained batch with the fold's look-back disabled: every fold block
+// derives its carry-in by walking its run (fold_carry_walk), the path a
+// block takes when a predecessor is not running; tests/test_gpu_parity.py.
+hipError_t launch_fold_walk(const uint8_t* arena, uint64_t arena_bytes, const void* desc, uint32_t n,
+                            uint16_t* out, unsigned long long* err, hipStream_t s) {
+  uint32_t* part = part_for(n);
+  if (!part) return hipErrorOutOfMemory;
+  const hipError_t e = launch_hyb<8, 16, 4, 2, 0, 2>(arena, arena_bytes, desc, n, out, part, err, s, 64u);
+  if (e != hipSuccess) return e;
+  launch_fold<0>(part, n, out, desc, arena, s);
+  return hipGetLastError();
+}
+
 // Workgroup size with the tile: WG threads own TP descriptors.
 template <int WG, int TP>
 hipError_t launch_wg(const uint8_t* arena, uint64_t arena_bytes, const void* desc, uint32_t n,
@@ -333,6 +346,7 @@ static const Variant kVariants[] = {
     {"g8u16_su1", launch_h<8, 16, 4, 2, 64>},
     {"chained_main", launch_chained<false>},
     {"chained_full", launch_chained<true>},
+    {"chained_fold_walk", launch_fold_walk},
     {"prod_small_d5", launch_h<16, 8, 4, 2, 64, 5>},
     {"g8u16_b32", launch_h<8, 16, 4, 2, 32, 0, 2>},
     {"g8u8_b64", launch_h<8, 8, 4, 2, 64, 0, 2>},

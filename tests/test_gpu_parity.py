@@ -753,3 +753,48 @@ def test_chain_wrap_fallback(engine):
     d2["len"][[5, 9000, 15000]] = 7
     want2, _ = O.c_batch(arena, d2, chained=True)
     assert np.array_equal(dev_batch(engine, arena, d2, chained=True), want2)
+
+
+def test_fold_carry_walk_path(engine):
+    """fold_scan's no-wait path: with the look-back disabled (the tuning
+    library's `chained_fold_walk`, SPINS = 0) every block derives its carry-in
+    by walking its run, as a block does when a predecessor is not running.
+    Long runs, short runs and wrapping pieces, against the oracle."""
+    import ctypes
+    import os
+
+    import oracle as O
+    from netstack_amd import workloads as W
+
+    torch = _torch()
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    L = ctypes.CDLL(os.path.join(root, "netstack_amd", "lib", "libns_tune.so"))
+    L.nsk_tune_name.restype = ctypes.c_char_p
+    v = [i for i in range(L.nsk_tune_count()) if L.nsk_tune_name(i) == b"chained_fold_walk"]
+    assert v, "libns_tune.so lacks chained_fold_walk"
+    L.nsk_tune_launch.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                  ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    rng = np.random.default_rng(31)
+    n = 60_000
+    lengths = rng.integers(256, 400, n).astype(np.uint32)  # the big-packet kernel instance
+    flags = (2 * (rng.random(n) < 0.999)).astype(np.uint16) | rng.integers(0, 2, n).astype(np.uint16)
+    flags[0] &= 1
+    lengths[[100, 30_000]] = 131_074
+    flags[[100, 30_000]] = 2
+    d, end = W.make_desc(lengths, rng.integers(0, 65536, n).astype(np.uint16), align=2, flags=flags)
+    arena = rng.integers(0, 256, end, dtype=np.uint8)
+    for k in (100, 30_000):
+        o = int(d["off"][k])
+        arena[o:o + 131_074] = 0xFF
+    want, bad = O.c_batch(arena, d, chained=True)
+    assert bad == 0
+    a = torch.from_numpy(arena).cuda()
+    dd = torch.from_numpy(d.view(np.uint8).copy()).cuda()
+    out = torch.empty(n, dtype=torch.int16, device="cuda")
+    err = torch.zeros(1, dtype=torch.int64, device="cuda")
+    assert L.nsk_tune_launch(v[0], a.data_ptr(), a.numel(), dd.data_ptr(), n, out.data_ptr(), err.data_ptr(),
+                             None) == 0
+    torch.cuda.synchronize()
+    assert int(err.item()) == 0
+    got = out.cpu().numpy().view(np.uint16)
+    assert np.array_equal(got, want), np.flatnonzero(got != want)[:8]
