@@ -137,8 +137,9 @@ int ns_csum_sync(ns_csum_ctx* ctx, void* stream, uint64_t* bad);
 /* ---- device-resident batch (the hot path) --------------------------------
  * d_arena/d_desc/d_out are device pointers on ctx's device; the call only
  * enqueues kernels on `stream` and returns (asynchronous).  With
- * NS_BATCH_CHAINED the context's scratch is used: calls with that flag on one
- * context must be serialised by the caller's stream order.                  */
+ * NS_BATCH_CHAINED, or when descriptors average >= 1 MiB (arena_bytes / n:
+ * then each is spread over many workgroups), the context's scratch is used:
+ * such calls on one context must be serialised by the caller's stream order. */
 int ns_csum_batch_dev(ns_csum_ctx* ctx, const uint8_t* d_arena,
                       uint64_t arena_bytes, const ns_pkt_desc* d_desc,
                       uint32_t n, uint16_t* d_out, uint32_t batch_flags,

@@ -153,6 +153,7 @@ struct ns_csum_ctx {
   std::mutex mu;  // guards everything below
 
   DevBuf<uint32_t> partial;  // chained-batch scratch (device-resident API)
+  DevBuf<uint32_t> split;    // csum_split scratch (device-resident API, huge descriptors)
   // host-path slots (double-buffered)
   DevBuf<uint8_t> d_arena[2];
   DevBuf<ns_pkt_desc> d_desc[2];
@@ -756,6 +757,7 @@ void ns_csum_destroy(ns_csum_ctx* ctx) {
     for (int s = 0; s < 2; ++s)
       if (ctx->stream[s]) (void)hipStreamSynchronize(ctx->stream[s]);
     ctx->partial.release();
+    ctx->split.release();
     ctx->z_buf.release();
     for (MappedPin* b : ctx->stage_all) {
       b->release();
@@ -805,13 +807,22 @@ int batch_dev(ns_csum_ctx* ctx, const uint8_t* d_arena, uint64_t arena_bytes, co
   DeviceGuard g(ctx->device);
   hipStream_t s = (hipStream_t)stream;  // NULL = the HIP null stream
   uint32_t* part = nullptr;
-  if (batch_flags & NS_BATCH_CHAINED) {
+  uint32_t* split = nullptr;
+  if ((batch_flags & NS_BATCH_CHAINED) || arena_bytes / n >= nsk::split_min_avg()) {
     std::lock_guard<std::mutex> lk(ctx->mu);
-    int rc = ctx->partial.ensure(chain_words(n), true);
-    if (rc != NS_OK) return rc;
-    part = ctx->partial.p;
+    if (batch_flags & NS_BATCH_CHAINED) {
+      int rc = ctx->partial.ensure(chain_words(n), true);
+      if (rc != NS_OK) return rc;
+      part = ctx->partial.p;
+    }
+    if (arena_bytes / n >= nsk::split_min_avg()) {
+      int rc = ctx->split.ensure(nsk::split_words(n), true);  // zero once; the kernel keeps it so
+      if (rc != NS_OK) return rc;
+      split = ctx->split.p;
+    }
   }
-  HIP_TRY(nsk::launch_batch(d_arena, arena_bytes, d_desc, n, d_out, part, ctx->d_err, s, 0, store ? 1u : 0u));
+  HIP_TRY(nsk::launch_batch(d_arena, arena_bytes, d_desc, n, d_out, part, ctx->d_err, s, 0, store ? 1u : 0u,
+                            split));
   return NS_OK;
 }
 }  // namespace

@@ -19,6 +19,7 @@ namespace nsk {
 // (arena = nullptr, descriptors holding absolute addresses).
 // `store`: descriptors flagged NS_DESC_STORE write their final result into
 // the (then writable) arena.
+// `split`: scratch for csum_split (see below), or nullptr.
 // Chained-batch scratch layout, in u32 words: the n partial sums, their u16
 // flags from chain_flag_word(n) (16-B aligned), then one 8-B fold status per
 // kFoldBlock descriptors from chain_status_word(n) (csum_kernels.hip, run
@@ -35,6 +36,13 @@ constexpr uint64_t chain_scratch_words(uint64_t n) { return chain_status_word(n)
 hipError_t launch_batch(const uint8_t* arena, uint64_t arena_bytes,
                         const void* desc, uint32_t n, uint16_t* out,
                         uint32_t* partial, unsigned long long* err,
-                        hipStream_t stream, uint64_t sizing_bytes = 0, uint32_t store = 0);
+                        hipStream_t stream, uint64_t sizing_bytes = 0, uint32_t store = 0,
+                        uint32_t* split = nullptr);
+
+// Batches of few descriptors averaging >= split_min_avg() bytes take the
+// split kernel when launch_batch gets `split`: a scratch of split_words(n)
+// u32, zeroed once at allocation (every launch leaves it zero).
+constexpr uint64_t split_min_avg() { return 1u << 20; }
+constexpr uint64_t split_words(uint64_t n) { return 2 * n; }
 
 }  // namespace nsk

@@ -357,7 +357,9 @@ __device__ __forceinline__ uint32_t direct_sum(const Srd& r, const PktInfo& p) {
 // GL = 64-bit global loads (tile span >= 4 GiB) instead of the window SRD.
 // Every thread of the block must call it.
 // Returns this thread's packet sum (finish_tile turns it into the result).
-template <int WG, int TP, int GB, int UB, int US, int AUXB, bool GL, int SU>
+// FX = always the exact (T, W) accumulator (csum_split: its pieces' sums are
+// added, so they must be exact mod 2^32, not W-only class values).
+template <int WG, int TP, int GB, int UB, int US, int AUXB, bool GL, int SU, bool FX = false>
 __device__ __forceinline__ uint32_t hyb_scan_tile(HybLds<WG>& L, const Srd& r, const PktInfo& p,
                                                   uint32_t big_chunks) {
   constexpr int P = WG;
@@ -396,7 +398,7 @@ __device__ __forceinline__ uint32_t hyb_scan_tile(HybLds<WG>& L, const Srd& r, c
     const uint64_t y = __shfl_up(incl, d, 64);
     if (lane >= d) incl += y;
   }
-  const int wex = __any(nch > kWOnlyMaxChunks);
+  const int wex = FX || __any(nch > kWOnlyMaxChunks);
   if (lane == 63) {
     L.wtot[wv] = incl;
     L.wex[wv] = (uint32_t)wex;
@@ -654,6 +656,80 @@ __global__ __launch_bounds__(WG) void csum_hyb(
     const PktInfo p = pkt_info(d, 0ull);
     const uint32_t s = hyb_scan_tile<WG, TP, 16, 4, 4, AUXB, true, 1>(L, r, p, big_chunks);
     finish_tile<WG, CH>(L, s, d, mine, i, n, out, partial, store);
+  }
+}
+
+// ---- descriptors far larger than a tile: csum_split -----------------------
+// The tile kernel gives one workgroup to each descriptor of >= 64 KiB, which
+// leaves most of the chip idle on a batch of a few huge descriptors (one
+// 1 GiB buffer: one workgroup, 41 GB/s).  csum_split cuts each descriptor
+// into `per` pieces of whole 128-B lines (even offsets from the packet
+// start, so every piece keeps the packet's byte phase) and runs each piece
+// through the tile kernel's own scan as a one-packet tile, always with the
+// exact accumulator.  A piece adds its sum mod 2^32 — Go's uint32
+// accumulator wraps the same way — to the descriptor's accumulator; the
+// last piece to finish folds and writes the result (unchained) or the
+// partial and flag (chained), as finish_tile does.  (A plain grid-stride
+// streaming kernel in its place reached only 3.0-4.1 TB/s.)
+constexpr uint64_t kSplitAvg = split_min_avg();  // launch_batch: the average size that selects it
+constexpr uint32_t kSplitMaxN = 160;  // ... for fewer descriptors than this (more fill the chip as tiles)
+constexpr uint32_t kSplitWGs = 256;   // pieces over the whole batch: one per CU (tools/split_probe.py)
+
+template <int GB, int UB, int US, int AUXB, int SU>
+__global__ __launch_bounds__(256) void csum_split(const uint8_t* __restrict__ arena, uint64_t arena_bytes,
+                                                  const uint4* __restrict__ desc, uint32_t n, uint32_t per,
+                                                  uint16_t* __restrict__ out, uint32_t* __restrict__ partial,
+                                                  uint32_t* __restrict__ acc, unsigned long long* __restrict__ err,
+                                                  uint32_t store, uint32_t big_chunks) {
+  __shared__ HybLds<256> L;
+  const uint32_t i = blockIdx.x / per, y = blockIdx.x % per;
+  const int t = threadIdx.x;
+  const uint4 raw = desc[i];
+  const uint64_t off = (uint64_t)raw.x | ((uint64_t)raw.y << 32);
+  uint64_t len = raw.z;
+  const bool bad = off > arena_bytes || len > arena_bytes - off;
+  if (bad) len = 0;
+  if (bad && y == 0 && t == 0) atomicAdd(err, 1ull);
+  const uint64_t arena_abs = (uint64_t)(uintptr_t)arena;
+  const uint64_t piece = (((len + per - 1) / per) + 127) & ~127ull;
+  const uint64_t r0 = min(len, (uint64_t)y * piece), r1 = min(len, r0 + piece);
+  Pkt d{0ull, 0u, 0u, 0u, 0u};
+  if (t == 0 && r1 > r0) {
+    d.A = arena_abs + off + r0;
+    d.len = (uint32_t)(r1 - r0);
+    d.odd = (raw.w >> 16) & 1u;
+  }
+  const uint64_t base = arena_abs & ~15ull;
+  const Srd r = make_srd(base, arena_abs + arena_bytes - base);
+  const PktInfo p = pkt_info(d, base);
+  const uint32_t s = hyb_scan_tile<256, 1, GB, UB, US, AUXB, false, SU, true>(L, r, p, big_chunks);
+  if (t != 0) return;
+  atomicAdd(&acc[i], s);
+  __threadfence();
+  if (atomicAdd(&acc[n + i], 1u) != per - 1) return;
+  // the last piece: finish descriptor i
+  __threadfence();
+  // (and leave its accumulator and counter zero for the next launch: the
+  // scratch is zeroed once, at allocation, instead of per launch)
+  const uint32_t sum = __hip_atomic_exchange(&acc[i], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(&acc[n + i], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t init = raw.w & 0xFFFFu, cont = (raw.w >> 17) & 1u;
+  uint32_t stw = store ? (raw.w >> 18) & 0x3FFFu : 0u;
+  const uint64_t at = off + (stw >> 2);
+  if (!(stw & 3u)) {
+    stw = 0;
+  } else if (at > arena_bytes || arena_bytes - at < 2) {
+    atomicAdd(err, 1ull);
+    stw = 0;
+  }
+  if (partial) {
+    const bool head = !cont || i == 0;
+    partial[i] = head ? fold1((cont ? 0u : init) + sum) : sum;
+    reinterpret_cast<uint16_t*>(partial + chain_flag_word(n))[i] = (uint16_t)((head ? 0u : 1u) | (stw << 1));
+  } else {
+    const uint32_t res = fold1(init + sum);
+    out[i] = (uint16_t)res;
+    if (stw) store_result(arena_abs + at, res, stw);
   }
 }
 
@@ -979,12 +1055,21 @@ static hipError_t launch_hyb(const uint8_t* arena, uint64_t arena_bytes, const v
 hipError_t launch_batch(const uint8_t* arena, uint64_t arena_bytes,
                         const void* desc, uint32_t n, uint16_t* out,
                         uint32_t* partial, unsigned long long* err,
-                        hipStream_t stream, uint64_t sizing_bytes, uint32_t store) {
+                        hipStream_t stream, uint64_t sizing_bytes, uint32_t store,
+                        uint32_t* split) {
   uint32_t* part = partial;  // the chained scratch (layout: csum_kernels.h)
   if (n == 0) return hipSuccess;
   hipError_t e;
   if (sizing_bytes == 0) sizing_bytes = arena_bytes;
-  if (sizing_bytes / n >= 256) {
+  if (split && sizing_bytes / n >= kSplitAvg && n < kSplitMaxN &&
+      ((uintptr_t)arena & 15u) + arena_bytes + 64 < kMaxSrdBytes) {
+    // A few huge descriptors: spread each over many workgroups.  (`split`
+    // holds zeros between launches: csum_split leaves it so.)
+    const uint32_t per = std::max<uint32_t>(1, kSplitWGs / n);
+    hipLaunchKernelGGL((csum_split<8, 16, 4, 2, 2>), dim3(n * per), dim3(256), 0, stream, arena, arena_bytes,
+                       reinterpret_cast<const uint4*>(desc), n, per, out, part, split, err, store, 64u);
+    e = hipGetLastError();
+  } else if (sizing_bytes / n >= 256) {
     // Packets of >= 64 chunks (~1 KiB): their whole 128-B lines to 8-lane
     // groups (one full line per group per load instruction, 16 loads per lane
     // in flight) with nontemporal loads; their partial edge lines and all

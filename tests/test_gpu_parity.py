@@ -798,3 +798,45 @@ def test_fold_carry_walk_path(engine):
     assert int(err.item()) == 0
     got = out.cpu().numpy().view(np.uint16)
     assert np.array_equal(got, want), np.flatnonzero(got != want)[:8]
+
+
+@pytest.mark.parametrize("chained", [False, True])
+def test_huge_descriptors_split(engine, chained):
+    """A batch of a few descriptors of many MiB (average >= 1 MiB selects
+    csum_split: 512-KiB slices over many workgroups): odd offsets and lengths,
+    odd carry-ins, an empty and an out-of-range descriptor, runs of 0xFF (the
+    uint32 wrap), stores; results and stored bytes against the oracle."""
+    import oracle as O
+
+    torch = _torch()
+    rng = np.random.default_rng(5 + chained)
+    lengths = [40 << 20, 3 << 20, 0, 17 << 20, 1, (9 << 20) + 3, 64 << 20, 12345]
+    n = len(lengths)
+    d = np.zeros(n, dtype=O.DESC_DTYPE)
+    pos = 7
+    for k, L in enumerate(lengths):
+        d["off"][k] = pos
+        d["len"][k] = L
+        pos += L + int(rng.integers(0, 40))
+    arena = rng.integers(0, 256, pos + 64, dtype=np.uint8)
+    arena[int(d["off"][6]):int(d["off"][6]) + (8 << 20)] = 0xFF
+    d["initial"] = rng.integers(0, 65536, n)
+    d["flags"] = rng.integers(0, 2, n)
+    if chained:
+        d["flags"][[1, 4, 5, 7]] |= 2
+    d["flags"][3] |= 0x4 | (3 << 4)       # store ^r at off + 3 (odd address)
+    d["flags"][0] |= 0x4 | 0x8 | (0 << 4)  # raw r at off
+    d = np.concatenate([d, np.array([(pos + 100, 5, 0, 0)], dtype=O.DESC_DTYPE)])  # out of range
+    want, bad = O.c_batch(arena, d, chained=chained)
+    assert bad == 1
+    expect, dropped = O.apply_stores(arena, d, want)
+    assert dropped == 0
+    dt = torch.from_numpy(arena).cuda()
+    desc = torch.from_numpy(d.view(np.uint8).copy()).cuda()
+    engine.sync()
+    out = engine.batch_tensors(dt, desc, chained=chained, store=True)
+    torch.cuda.synchronize()
+    assert engine.sync() == 1
+    got = out.cpu().numpy().view(np.uint16)
+    assert np.array_equal(got, want), (got, want)
+    assert np.array_equal(dt.cpu().numpy(), expect)
