@@ -349,6 +349,9 @@ static const Variant kVariants[] = {
     {"chained_fold_walk", launch_fold_walk},
     {"prod_small_d5", launch_h<16, 8, 4, 2, 64, 5>},
     {"g8u16_b32", launch_h<8, 16, 4, 2, 32, 0, 2>},
+    {"g8u16_b16", launch_h<8, 16, 4, 2, 16, 0, 2>},
+    {"g8u16_b24", launch_h<8, 16, 4, 2, 24, 0, 2>},
+    {"g8u16_b48", launch_h<8, 16, 4, 2, 48, 0, 2>},
     {"g8u8_b64", launch_h<8, 8, 4, 2, 64, 0, 2>},
     {"g8u12_b64", launch_h<8, 12, 4, 2, 64, 0, 2>},
     {"g8u24_b64", launch_h<8, 24, 4, 2, 64, 0, 2>},
