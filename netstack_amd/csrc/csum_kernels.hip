@@ -24,6 +24,13 @@
 // An aligned chunk never crosses a page and holds at least one byte of the
 // packet, so no read can fault.  No MFMA: this is a byte sum, HBM-bound
 // (DESIGN.md §4).
+//
+// Kernels.  csum_hyb: tiles of TP descriptors per workgroup, the hot path
+// (DESIGN.md §4.1-4.3).  fold_scan: NS_DESC_CONT runs of a chained batch,
+// a one-pass segmented scan (§4.4).  csum_split: batches of a few huge
+// descriptors, each cut into pieces over many workgroups (§4.6).  Stores of
+// NS_DESC_STORE results into the packets happen in csum_hyb (unchained),
+// fold_scan (chained) or csum_split (§4.5).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
