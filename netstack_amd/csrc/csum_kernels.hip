@@ -873,7 +873,9 @@ __global__ __launch_bounds__(256) void fold_scan(const uint32_t* __restrict__ pa
     const bool incl = blk == 0 || (total & kFH);
     if (!seq) fold_publish(&status[blk], gen, incl ? kFIncl : kFAgg, total);
     uint32_t carry = kFIdent;
-    if (blk > 0) {
+    // A block whose first descriptor heads a run needs no carry-in (every
+    // state in it starts at or after that head): only its statuses matter.
+    if (blk > 0 && (f[0] & 1u)) {
       // Walk back to the nearest inclusive status; the aggregates passed on
       // the way hold no head and no wrap, so they combine as residue adds.
       uint32_t run = kFIdent;
@@ -899,8 +901,8 @@ __global__ __launch_bounds__(256) void fold_scan(const uint32_t* __restrict__ pa
         }
         run = fold_combine(val, run);
       }
-      if (!seq && !incl) fold_publish(&status[blk], gen, kFIncl, fold_combine(carry, total));
     }
+    if (blk > 0 && !seq && !incl) fold_publish(&status[blk], gen, kFIncl, fold_combine(carry, total));
     s_carry = carry;
   }
   __syncthreads();
