@@ -20,6 +20,10 @@
  *   (stack/route.go:174-188)                                      -> ns_csum_vv_batch
  *   the per-packet calculateChecksum (checksum.go:26-46) over a
  *   device-resident batch                                         -> ns_csum_batch_dev / _host
+ *   ... and the header write that follows it, SetChecksum(^xsum)
+ *   (connect.go:663, ipv4.go:236; tcp.go:252, ipv4.go:223)        -> ns_csum_batch_dev_store
+ *   any composition of Checksum(v, xsum) / view chaining (a whole
+ *   TCP/UDP/ICMP/IPv4 checksum per chain)                         -> ns_csum_chains
  *
  * Semantics (bit-exact with checksum.go, including its un-folded uint32 wrap for
  * buffers > 128 KiB): every descriptor d is one calculateChecksum call over
