@@ -840,3 +840,27 @@ def test_huge_descriptors_split(engine, chained):
     got = out.cpu().numpy().view(np.uint16)
     assert np.array_equal(got, want), (got, want)
     assert np.array_equal(dt.cpu().numpy(), expect)
+
+
+@pytest.mark.parametrize("bad_at", [5, 300_000])
+def test_host_batch_out_of_range_is_erange_and_pipeline_recovers(engine, bad_at):
+    """ns_csum_batch_host over a multi-chunk DMA pipeline (an arena above one
+    staging buffer, 128K-descriptor chunks): a descriptor past the arena, in
+    the first or a later chunk, fails the call with NS_ERANGE after the
+    chunks in flight drained; the next call on the same context is exact."""
+    import oracle as O
+    from netstack_amd import workloads as W
+    from netstack_amd._lib import NS_ERANGE, ChecksumError
+
+    rng = np.random.default_rng(bad_at)
+    n = 400_000
+    d, end = W.make_desc(rng.integers(0, 64, n).astype(np.uint32), rng.integers(0, 65536, n).astype(np.uint16))
+    arena = rng.integers(0, 256, end, dtype=np.uint8)
+    bad = d.copy()
+    bad["off"][bad_at] = end + 1
+    bad["len"][bad_at] = 1
+    with pytest.raises(ChecksumError) as ei:
+        engine.batch_host(arena, bad)
+    assert ei.value.status == NS_ERANGE
+    want, _ = O.c_batch(arena, d)
+    assert np.array_equal(engine.batch_host(arena, d), want)
