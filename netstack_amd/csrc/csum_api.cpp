@@ -375,7 +375,9 @@ int submit_small(ns_csum_ctx* ctx, SmallReq* req) {
 // Host batch core, caller holds ctx->mu and the device guard.  Pipelines
 // chunks of the descriptor table over the two slots/streams: H2D of chunk k+1
 // overlaps the kernel of chunk k.  Chunks never split a NS_DESC_CONT run.
-constexpr uint32_t kHostChunkDesc = 1u << 17;  // descriptors per host-pipeline chunk
+// Descriptors per host-pipeline chunk (cfg3, 1M x 64 B: 64K 3.11 ms, 128K
+// 2.18, 256K 2.16, 512K 2.52 ms per call).
+constexpr uint32_t kHostChunkDesc = 1u << 17;
 
 int run_host_batch(ns_csum_ctx* ctx, const uint8_t* h_arena, uint64_t arena_bytes,
                    const ns_pkt_desc* h_desc, uint32_t n, uint16_t* h_out,
@@ -405,8 +407,9 @@ int run_host_batch(ns_csum_ctx* ctx, const uint8_t* h_arena, uint64_t arena_byte
     // Grow the chunk while its byte span stays within budget and it holds at
     // most kHostChunkDesc descriptors (so that the CPU's table copy of one
     // chunk overlaps the other chunk's transfers).  Descriptors are
-    // range-checked on the way.  1M x 64 B: 4.27 ms -> 2.21 ms per call
-    // with this and the skipped span pass (profiles/r01/bench_host3.json).
+    // range-checked on the way.  1M x 64 B: 4.27 ms -> 2.15 ms per call
+    // with this, the skipped span pass and the device-side table rebase
+    // (profiles/r01/bench_host3.json).
     uint64_t lo = UINT64_MAX, hi = 0;
     uint32_t j = k;
     uint32_t cut = k;  // last index (exclusive) at which we may cut
@@ -454,14 +457,15 @@ int run_host_batch(ns_csum_ctx* ctx, const uint8_t* h_arena, uint64_t arena_byte
     if ((rc = ctx->h_desc[slot].ensure(cnt)) != NS_OK) return rc;
     if ((rc = ctx->h_out[slot].ensure(cnt)) != NS_OK) return rc;
     if (chained && (rc = ctx->d_part[slot].ensure(chain_words(cnt), true)) != NS_OK) return rc;
+    // The table goes over verbatim (one memcpy into pinned memory) and is
+    // rebased to the chunk on the device: a per-descriptor rewrite on the CPU
+    // was the limit of small-packet batches.
     ns_pkt_desc* hd = ctx->h_desc[slot].p;
-    for (uint32_t q = 0; q < cnt; ++q) {
-      hd[q] = h_desc[k + q];
-      hd[q].off = hd[q].len ? hd[q].off - cut_lo : 0;
-    }
+    std::memcpy(hd, h_desc + k, (size_t)cnt * sizeof(ns_pkt_desc));
     hipStream_t s = ctx->stream[slot];
     if (span) HIP_TRY(hipMemcpyAsync(ctx->d_arena[slot].p, h_arena + cut_lo, span, hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemcpyAsync(ctx->d_desc[slot].p, hd, cnt * sizeof(ns_pkt_desc), hipMemcpyHostToDevice, s));
+    HIP_TRY(nsk::launch_rebase(ctx->d_desc[slot].p, cnt, cut_lo, s));
     HIP_TRY(nsk::launch_batch(ctx->d_arena[slot].p, span, ctx->d_desc[slot].p, cnt, ctx->d_out[slot].p,
                               chained ? ctx->d_part[slot].p : nullptr, ctx->d_err, s));
     HIP_TRY(hipMemcpyAsync(ctx->h_out[slot].p, ctx->d_out[slot].p, cnt * sizeof(uint16_t), hipMemcpyDeviceToHost, s));

@@ -39,6 +39,10 @@ hipError_t launch_batch(const uint8_t* arena, uint64_t arena_bytes,
                         hipStream_t stream, uint64_t sizing_bytes = 0, uint32_t store = 0,
                         uint32_t* split = nullptr);
 
+// Rewrite n device-resident descriptors' offsets relative to `bias` (empty
+// descriptors get 0): the host pipeline's per-chunk table rebase.
+hipError_t launch_rebase(void* desc, uint32_t n, uint64_t bias, hipStream_t stream);
+
 // Batches of few descriptors averaging >= split_min_avg() bytes take the
 // split kernel when launch_batch gets `split`: a scratch of split_words(n)
 // u32, zeroed once at allocation (every launch leaves it zero).

@@ -981,6 +981,19 @@ __global__ __launch_bounds__(256) void fold_scan(const uint32_t* __restrict__ pa
   }
 }
 
+// Rebase a host-pipeline chunk's descriptor table on the device: offsets
+// relative to the chunk's first byte (and 0 for empty descriptors), so the
+// host copies the caller's table verbatim instead of rewriting it.
+__global__ __launch_bounds__(256) void rebase_desc(uint4* __restrict__ d, uint32_t n, uint64_t bias) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  uint4 v = d[i];
+  const uint64_t off = v.z ? (((uint64_t)v.x | ((uint64_t)v.y << 32)) - bias) : 0ull;
+  v.x = (uint32_t)off;
+  v.y = (uint32_t)(off >> 32);
+  d[i] = v;
+}
+
 }  // namespace nsk
 
 // ---- launchers (C++ linkage, used by csum_api.cpp) ------------------------
@@ -1059,6 +1072,13 @@ static hipError_t launch_hyb(const uint8_t* arena, uint64_t arena_bytes, const v
                                                       big_chunks, store);
   }
 #undef NSK_TP
+}
+
+hipError_t launch_rebase(void* desc, uint32_t n, uint64_t bias, hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(rebase_desc, dim3((n + 255) / 256), dim3(256), 0, stream, reinterpret_cast<uint4*>(desc), n,
+                     bias);
+  return hipGetLastError();
 }
 
 hipError_t launch_batch(const uint8_t* arena, uint64_t arena_bytes,
