@@ -1044,6 +1044,7 @@ static hipError_t launch_hyb_tp(const uint8_t* arena, uint64_t arena_bytes, cons
 // descriptors vs 221 at 64 and 244 at 16; the Zipf batch 103 us at 64 vs 107
 // at 128 and 114 at 32; 64 KiB GSO buffers flat).
 constexpr uint64_t kTileBytes = 64u << 10;
+constexpr uint32_t kBigChunks = 40;  // packets of >= this many 16-B chunks take the 8-lane groups
 template <int GB, int UB, int US, int AUXB, int UD = 0, int SU = 1>
 static hipError_t launch_hyb(const uint8_t* arena, uint64_t arena_bytes, const void* desc,
                              uint32_t n, uint16_t* out, uint32_t* partial,
@@ -1099,13 +1100,18 @@ hipError_t launch_batch(const uint8_t* arena, uint64_t arena_bytes,
                        reinterpret_cast<const uint4*>(desc), n, per, out, part, split, err, store, 64u);
     e = hipGetLastError();
   } else if (sizing_bytes / n >= 256) {
-    // Packets of >= 64 chunks (~1 KiB): their whole 128-B lines to 8-lane
+    // Packets of >= 40 chunks (~640 B): their whole 128-B lines to 8-lane
     // groups (one full line per group per load instruction, 16 loads per lane
     // in flight) with nontemporal loads; their partial edge lines and all
     // smaller packets to per-lane runs of 4, two runs issued per lane per
     // iteration (tools/tune.py on MI355X: 220.6 us on 1M x 1500 B = 90.2% of
-    // 8 TB/s, 107 us on the Zipf batch; profiles/r01/tune_*.json).
-    e = launch_hyb<8, 16, 4, 2, 0, 2>(arena, arena_bytes, desc, n, out, part, err, stream, 64u,
+    // 8 TB/s, 107 us on the Zipf batch; profiles/r01/tune_*.json).  The
+    // group threshold, swept over uniform 576-960-B packets
+    // (profiles/r01/tune_bc_*.log): 40 chunks beats 64 by up to 15% on
+    // 704-960-B packets (960 B: 219.8 vs 253.5 us per 1.5 GB) and ties it
+    // elsewhere; at 36 chunks and below the groups lose (576 B: 277.7 vs
+    // 253.4 us).
+    e = launch_hyb<8, 16, 4, 2, 0, 2>(arena, arena_bytes, desc, n, out, part, err, stream, kBigChunks,
                                       sizing_bytes, kTileBytes, store);
   } else {
     // Small packets: the same kernel plus the direct path — a tile whose

@@ -352,6 +352,9 @@ static const Variant kVariants[] = {
     {"g8u16_b16", launch_h<8, 16, 4, 2, 16, 0, 2>},
     {"g8u16_b24", launch_h<8, 16, 4, 2, 24, 0, 2>},
     {"g8u16_b48", launch_h<8, 16, 4, 2, 48, 0, 2>},
+    {"g8u16_b40", launch_h<8, 16, 4, 2, 40, 0, 2>},
+    {"g8u16_b36", launch_h<8, 16, 4, 2, 36, 0, 2>},
+    {"g8u16_b44", launch_h<8, 16, 4, 2, 44, 0, 2>},
     {"g8u8_b64", launch_h<8, 8, 4, 2, 64, 0, 2>},
     {"g8u12_b64", launch_h<8, 12, 4, 2, 64, 0, 2>},
     {"g8u24_b64", launch_h<8, 24, 4, 2, 64, 0, 2>},

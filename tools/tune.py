@@ -98,6 +98,9 @@ def main():
             a7, d7, _ = W.rx_batch(nover.get(7, 1 << 20), 7000, dev)
             b = W.Batch("rx_1Mx1500_3desc", 7000, d7, a7.numel())
             arenas = [a7]
+        elif cfg >= 100:  # uniform packets of `cfg` bytes, 1.5 GB of payload (TP-rule sweeps)
+            b = W.uniform(f"uniform_{cfg}B", 9000 + cfg, nover.get(cfg, (1_572_864_000 // cfg)), cfg)
+            arenas = [b.arena_device(dev)]
         else:
             b = W.config(cfg, nover.get(cfg))
             arenas = [b.arena_device(dev)] + [W.random_bytes_torch(b.seed + 77 * r, b.arena_bytes, dev)
