@@ -519,6 +519,7 @@ __device__ __forceinline__ uint32_t hyb_scan_tile(HybLds<WG>& L, const Srd& r, c
       if (li == 0) atomicAdd(&L.acc[pk], sg);
     }
 
+    static_assert(SU == 1 || SU == 2, "the small loop issues one or two runs per iteration");
     for (uint32_t q = (uint32_t)t; q < RSt; q += SU * WG) {
       uint4 va[US];
       const SRun ra = small_issue(q, va);
