@@ -329,7 +329,7 @@ hipError_t launch_wg(const uint8_t* arena, uint64_t arena_bytes, const void* des
 template <int TP, int GB, int UB>
 hipError_t launch_tp(const uint8_t* arena, uint64_t arena_bytes, const void* desc, uint32_t n,
                      uint16_t* out, unsigned long long* err, hipStream_t s) {
-  return launch_hyb_tp<TP, GB, UB, 4, 2, 0, 2>(arena, arena_bytes, desc, n, out, nullptr, err, s, 64u);
+  return launch_hyb_tp<TP, GB, UB, 4, 2, 0, 2>(arena, arena_bytes, desc, n, out, nullptr, err, s, kBigChunks);
 }
 
 typedef hipError_t (*launch_fn)(const uint8_t*, uint64_t, const void*, uint32_t, uint16_t*,
@@ -342,6 +342,7 @@ struct Variant {
 // against these and retired; their numbers are in profiles/r01/tune_*.json
 // and DESIGN.md §4.2.
 static const Variant kVariants[] = {
+    {"prod", launch_h<8, 16, 4, 2, kBigChunks, 0, 2>},  // the production big-packet launch
     {"prod_g8u16_b64", launch_h<8, 16, 4, 2, 64, 0, 2>},
     {"g8u16_su1", launch_h<8, 16, 4, 2, 64>},
     {"chained_main", launch_chained<false>},
