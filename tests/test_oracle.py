@@ -176,3 +176,63 @@ def test_apply_stores_raw_odd_and_dropped():
     out, dropped = O.apply_stores(a, d, np.array([0x1234, 0xABCD, 1], dtype=np.uint16))
     assert dropped == 1
     assert list(out) == [0, 0, 0, 0xED, 0xCB, 0, 0xAB, 0xCD, 0, 0]
+
+
+def _fold1(v: int) -> int:
+    s = (v & 0xFFFF) + (v >> 16)
+    return (s + (s >> 16)) & 0xFFFF
+
+
+def test_run_fold_scan_algebra():
+    """The algebra fold_scan relies on, checked in plain
+    Python: with x <= 0xFFFF and a continuation partial p <= 0xFFFF0000,
+    Go's chaining x' = fold1(x + p) (checksum.go:89 and :44-45) equals the
+    state map (r, z) -> (r + p mod 65535, z and p == 0) read back as
+    z ? 0 : (r or 0xFFFF); and that map composes associatively, so a
+    segmented scan in any grouping gives Go's sequential results.  Edge
+    values: 0, 0xFFFF, multiples of 65535, partials near the wrap bound."""
+    rng = np.random.default_rng(17)
+    edge = [0, 1, 0xFFFE, 0xFFFF, 0x10000, 65535 * 3, 65535 * 65537, 0xFFFF0000, 0xFFFEFFFF]
+
+    def elem(p, head):
+        if head:
+            return ((0 if p == 0xFFFF else p), p == 0, True)
+        return (p % 65535, p == 0, False)
+
+    def comb(a, b):
+        if b[2]:
+            return b
+        return ((a[0] + b[0]) % 65535, a[1] and b[1], a[2])
+
+    def value(st):
+        return 0 if st[1] else (st[0] if st[0] else 0xFFFF)
+
+    for trial in range(300):
+        n = int(rng.integers(1, 60))
+        heads = rng.random(n) < 0.2
+        heads[0] = True
+        parts = []
+        for k in range(n):
+            if heads[k]:
+                parts.append(int(rng.choice([0, 0xFFFF, int(rng.integers(0, 0x10000))])))
+            else:
+                parts.append(int(rng.choice(edge)) if rng.random() < 0.5 else int(rng.integers(0, 0xFFFF0001)))
+        # Go's sequential fold
+        want, x = [], 0
+        for k in range(n):
+            x = parts[k] if heads[k] else _fold1(x + parts[k])
+            want.append(x)
+        # the scan, grouped at random split points (associativity)
+        es = [elem(parts[k], heads[k]) for k in range(n)]
+        cuts = sorted(set(rng.integers(0, n + 1, 3).tolist()) | {0, n})
+        got, carry = [], (0, True, False)
+        for a, b in zip(cuts[:-1], cuts[1:]):
+            agg = (0, True, False)
+            for e in es[a:b]:
+                agg = comb(agg, e)
+            st = carry
+            for e in es[a:b]:
+                st = comb(st, e)
+                got.append(value(st))
+            carry = comb(carry, agg)
+        assert got == want, (trial, parts, heads.tolist())
