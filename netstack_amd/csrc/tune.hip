@@ -355,6 +355,8 @@ static const Variant kVariants[] = {
     {"g8u16_b48", launch_h<8, 16, 4, 2, 48, 0, 2>},
     {"g8u16_b40", launch_h<8, 16, 4, 2, 40, 0, 2>},
     {"b40_us8_su1", launch_h<8, 16, 8, 2, 40, 0, 1>},
+    {"b40_us8_su2", launch_h<8, 16, 8, 2, 40, 0, 2>},
+    {"b40_us2_su2", launch_h<8, 16, 2, 2, 40, 0, 2>},
     {"g8u16_b36", launch_h<8, 16, 4, 2, 36, 0, 2>},
     {"g8u16_b44", launch_h<8, 16, 4, 2, 44, 0, 2>},
     {"g8u8_b64", launch_h<8, 8, 4, 2, 64, 0, 2>},
