@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define NS_CSUM_ABI_VERSION 1
+#define NS_CSUM_ABI_VERSION 2  /* 2: ns_csum_batch_dev_store, NS_DESC_STORE* */
 
 /* ---- status codes ------------------------------------------------------- */
 #define NS_OK 0
