@@ -3,7 +3,7 @@
 path on MI355X, against the HBM roofline, with the scalar CPU port timed
 beside it.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4] [--mode dev|host]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config 1|2|3|4|5|7|8] [--mode dev|host]
 
 One step = one pass of the checksum engine (ns_csum_batch_dev) over one batch
 already resident in HBM.  Default workload = BASELINE.json configs[1]:
@@ -34,6 +34,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 GIB = float(1 << 30)
 
 WORKLOADS = {
+    1: "cfg1: one 65,536-B buffer, seed 1, initial 0: header.Checksum (BASELINE.json configs[0])",
     2: "cfg2: 1,048,576 x 1500 B TCP payloads per GPU, 16-B-aligned starts (BASELINE.json configs[1])",
     3: "cfg3: 1,048,576 x 64 B min-size packets per GPU, 4 rotating batches (BASELINE.json configs[2])",
     4: "cfg4: 1,048,576 Zipf(1.1) 64-9000 B packets per GPU (BASELINE.json configs[3])",
@@ -47,11 +48,12 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", type=int, default=2, choices=(2, 3, 4, 5, 7, 8),
+    ap.add_argument("--config", type=int, default=2, choices=(1, 2, 3, 4, 5, 7, 8),
                     help="BASELINE.json configs[k-1]; 7 = device-resident RX verification, "
                          "8 = device-resident TX checksum fill (SURVEY §8(f) ranks 2 and 1)")
     ap.add_argument("--mode", default="dev", choices=("dev", "host"))
-    ap.add_argument("--rotate", type=int, default=0, help="distinct batches cycled per step (0 = auto)")
+    ap.add_argument("--rotate", type=int, default=0,
+                    help="distinct batches cycled per step (0 = auto: enough to exceed the 256 MiB MALL)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline time budget")
     ap.add_argument("--cpu-threads", type=int, default=0, help="threads for the multi-core CPU figure")
     ap.add_argument("--no-cpu", action="store_true")
@@ -122,7 +124,24 @@ def timed_region(step, sync, dist: Dist, steps: int, warmup: int, device=None):
     return dist.max(local, device), local
 
 
-CALIB_MODE, CALIB_BLOCKS = 2164, 16384  # calib_grp<16,4,nt>: the best pure read
+CALIB_BLOCKS = 16384
+
+
+def b2b_us(launch, stream, reps: int = 20, warm: int = 3) -> float:
+    """Average microseconds per launch over `reps` back-to-back launches
+    (launch(k) for k = 0..reps-1), timed by one HIP event pair on the launch
+    stream — the method of the timed region."""
+    import torch
+
+    for k in range(warm):
+        launch(k)
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record(stream)
+    for k in range(reps):
+        launch(k)
+    b.record(stream)
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) * 1e3 / reps
 
 
 def launch_stats(launch, stream, reps: int = 20):
@@ -142,11 +161,21 @@ def launch_stats(launch, stream, reps: int = 20):
     return sorted(a.elapsed_time(b) * 1e3 for a, b in ev)
 
 
-def stream_calibration(arena, stream):
-    """Same-run read-stream calibration: the best pure-read
-    kernel of tools/tune.py (calib_grp<16,4,nt>, libns_tune.so, not product
-    code) over the same arena bytes; median of 20 launches.  None when the
-    tuning library is absent."""
+# Pure-read calibrations (libns_tune.so, not product code), each cycled over
+# the same rotated arenas as the timed region.  "tile" kernels have the
+# checksum kernel's own big-packet access shape (nsk::calib_tile: 8-lane
+# groups, 16 nontemporal buffer_load_dwordx4 per lane in flight, one run of
+# `lpr` whole lines per group, a non-persistent grid of contiguous tiles);
+# "grp16x4" is round 1's best persistent grid-stride read.
+CALIB_TILE = (("tile_g8u16_lpr11", 1, 11), ("tile_g8u16_lpr16", 1, 16), ("tile_g8u16x2_lpr11", 2, 11),
+              ("tile_g8u16x2_lpr16", 2, 16), ("tile_g16u8_lpr16", 3, 16))
+
+
+def stream_calibration(arenas, stream):
+    """Same-run read-stream calibration: pure-read kernels over
+    the same arena bytes, rotated like the timed region, back-to-back
+    average of 20 launches each.  Returns {"variants": {...}, "best": ...};
+    None when the tuning library is absent."""
     import ctypes
 
     path = os.path.join(ROOT, "netstack_amd", "lib", "libns_tune.so")
@@ -158,19 +187,37 @@ def stream_calibration(arena, stream):
     L.nsk_calib_launch.restype = ctypes.c_int
     L.nsk_calib_launch.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
                                    ctypes.c_uint32, ctypes.c_void_p]
-    nbytes = min(arena.numel(), 0x7FFFFFF0) & ~15  # the kernel's SRD covers < 2 GiB
-    outb = torch.zeros(CALIB_BLOCKS, dtype=torch.int32, device=arena.device)  # one word per block
+    L.nsk_calib_tile_launch.restype = ctypes.c_int
+    L.nsk_calib_tile_launch.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
+                                        ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64), ctypes.c_void_p]
+    outb = torch.zeros(CALIB_BLOCKS, dtype=torch.int32, device=arenas[0].device)  # one word per block
+    R = len(arenas)
+    variants = {}
 
-    def launch():
-        rc = L.nsk_calib_launch(CALIB_MODE, arena.data_ptr(), nbytes, outb.data_ptr(), CALIB_BLOCKS,
-                                stream.cuda_stream)
-        if rc != 0:
-            raise RuntimeError(f"nsk_calib_launch failed: {rc}")
+    def run(name, fn):
+        rb = ctypes.c_uint64(0)
 
-    us = launch_stats(launch, stream)
-    med = us[len(us) // 2]
-    return {"kernel": "nsk::calib_grp<16,4,2> (pure nt read, 16-lane groups)", "bytes": nbytes,
-            "median_us": med, "GBps": nbytes / med / 1e3}
+        def launch(k):
+            a = arenas[k % R]
+            rc = fn(a, rb)
+            if rc != 0:
+                raise RuntimeError(f"calibration {name} failed: {rc}")
+
+        us = b2b_us(launch, stream, reps=10 * R if R > 1 else 20)
+        variants[name] = {"bytes": int(rb.value), "avg_us": us, "GBps": rb.value / us / 1e3}
+
+    def grp(a, rb):
+        nbytes = min(a.numel(), 0x7FFFFFF0) & ~15  # that kernel's SRD covers < 2 GiB
+        rb.value = nbytes
+        return L.nsk_calib_launch(2164, a.data_ptr(), nbytes, outb.data_ptr(), CALIB_BLOCKS, stream.cuda_stream)
+
+    run("grp16x4_persistent", grp)
+    for name, mode, lpr in CALIB_TILE:
+        run(name, lambda a, rb, mode=mode, lpr=lpr: L.nsk_calib_tile_launch(
+            mode, a.data_ptr(), a.numel(), lpr, outb.data_ptr(), ctypes.byref(rb), stream.cuda_stream))
+    best = max(variants, key=lambda k: variants[k]["GBps"])
+    return {"what": "pure nontemporal reads of the same rotated arenas (libns_tune.so), back-to-back average",
+            "variants": variants, "best": best, "GBps": variants[best]["GBps"]}
 
 
 def rank_batch(cfg: int, rank: int, world: int = 1):
@@ -265,8 +312,13 @@ def main():
     cfg = args.config
     if cfg in (7, 8):
         return packet_mode(args, dist, eng, dev, tx=cfg == 8)
+    if cfg == 1:
+        return single_buffer_mode(args, dist, eng, dev)
     batch = rank_batch(cfg, dist.rank, dist.world)
-    rotate = args.rotate or (4 if cfg == 3 else 1)
+    # Enough distinct batches per rank that one rotation exceeds the 256 MiB
+    # MALL (cfg2: 2 x 1.5 GB, cfg3: 4 x 82 MB, cfg4: 2 x 0.67 GB); cfg5's
+    # 12.6 GB batch is re-read as is.
+    rotate = args.rotate or {2: 2, 3: 4, 4: 2, 5: 1}[cfg]
     if cfg == 5 and rotate != 1:
         raise SystemExit("--rotate applies to cfg 2-4 only")
     if args.mode == "host":
@@ -305,7 +357,10 @@ def main():
     # one more launch of the same kernel instance over arenas[0]: its results
     # are what the CPU leg checks against the oracle
     per_launch = launch_stats(lambda: eng.batch_tensors(arenas[0], descs[0], out, stream=stream), stream)
-    calib = stream_calibration(arenas[0], stream)
+    # the same batch re-read back to back (no rotation: part of it may be
+    # served by the MALL) — reported beside the rotated headline
+    unrot_us = b2b_us(lambda k: eng.batch_tensors(arenas[0], descs[0], out, stream=stream), stream)
+    calib = stream_calibration(arenas, stream)
     eng.batch_tensors(arenas[0], descs[0], out, stream=stream)
     torch.cuda.synchronize()
 
@@ -354,9 +409,15 @@ def main():
             "kernel": kernel_name(batch.arena_bytes, batch.n),
             "algorithmic_bytes_per_launch": algo_bytes,
             "avg_launch_us": kern_avg_s * 1e6,
+            "rotating_batches": rotate,
+            "basis": (f"avg_launch_us over the timed region's back-to-back launches cycling {rotate} distinct "
+                      f"batches ({rotate * batch.arena_bytes / 2**20:.0f} MiB > the 256 MiB MALL)"
+                      if rotate > 1 else "avg_launch_us over the timed region's back-to-back launches"),
+            "unrotated": {"avg_launch_us": unrot_us, "frac": algo_bytes / unrot_us / 1e3 / HBM_PEAK_GBS,
+                          "note": "batch 0 re-read back to back, 20 launches: may hit the MALL"},
             "per_launch_us": {"median": per_launch[len(per_launch) // 2], "min": per_launch[0],
                               "max": per_launch[-1], "launches": len(per_launch),
-                              "note": "own event pair per launch, after the timed region (rotation 0)"},
+                              "note": "own event pair per launch, after the timed region (batch 0)"},
             "stream_calibration": calib,
             "frac_of_calibration": (achieved_gbs / calib["GBps"]) if calib else None,
         },
@@ -367,6 +428,8 @@ def main():
         # The CPU leg (rank 0): the oracle as the checker of the measured
         # kernel's own results, then as the timed scalar baseline.
         result["parity_sample"] = parity_sample(batch, out)
+        result["parity_sample"]["scope"] = ("sampled: 131,072 results of the measured launch; "
+                                            "every result is checked at full size by pytest -m gpu")
         cb, _ = cpu_baseline(batch, args.cpu_seconds, 1)
         result["cpu_baseline"] = cb
         th = args.cpu_threads or min(16, os.cpu_count() or 1)
@@ -501,6 +564,89 @@ def packet_mode(args, dist, eng, dev, tx: bool):
             stored, _ = O.apply_stores(src, d[:k_cpu], want)
             ps["stores_bit_exact"] = bool(np.array_equal(arena[:span].cpu().numpy(), stored))
         result["parity_sample"] = ps
+    if dist.rank == 0:
+        print(json.dumps(result), flush=True)
+    eng.close()
+    dist.close()
+
+
+def single_buffer_mode(args, dist, eng, dev):
+    """BASELINE.json configs[0]: one 65,536-B buffer (splitmix64 seed 1),
+    header.Checksum(buf, 0) (checksum.go:52-55).  The reference times this on
+    the host CPU; here three things are timed on the same buffer, each
+    checked bit for bit against the oracle:
+      - the scalar CPU port of checksum.go:41-43 (oracle/csum_oracle.c, one
+        core) — the reference's own path, restated (cpu_baseline);
+      - the synchronous C-ABI call ns_csum_checksum (what the Go shim calls:
+        copy into mapped staging, one launch, one wait), median latency over
+        `steps` calls through ctypes — `value`;
+      - the kernel alone on the buffer resident in HBM (ns_csum_batch_dev,
+        one descriptor), back-to-back average.
+    One buffer per call is latency-bound, not bandwidth-bound: this config is
+    plumbing, as BASELINE.json says, not the headline."""
+    import torch
+
+    import oracle as O
+    from netstack_amd import workloads as W
+
+    b = W.config(1)
+    buf = b.arena_host()[:65536].copy()
+    d1 = b.desc.copy()
+    want = int(O.c_batch(buf, d1)[0][0])
+    # warm-up + timed synchronous calls
+    for _ in range(args.warmup + 3):
+        got = eng.checksum(buf, 0)
+    dist.barrier()
+    lat = []
+    ok = got == want
+    t0 = time.perf_counter()
+    for _ in range(max(args.steps, 20)):
+        a = time.perf_counter()
+        r = eng.checksum(buf, 0)
+        lat.append(time.perf_counter() - a)
+        ok = ok and r == want
+    wall = time.perf_counter() - t0
+    dist.barrier()
+    lat.sort()
+    med = lat[len(lat) // 2]
+    # the kernel alone, buffer and descriptor resident in HBM
+    arena = torch.from_numpy(buf).to(dev)
+    desc = torch.from_numpy(d1.view(np.uint8).copy()).to(dev)
+    out = torch.empty(1, dtype=torch.int16, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    kern_us = b2b_us(lambda k: eng.batch_tensors(arena, desc, out, stream=stream), stream, reps=200)
+    ok = ok and (int(out.cpu().numpy().view(np.uint16)[0]) == want)
+    result = {
+        "metric": "header.Checksum GiB/s on one 64 KiB buffer (BASELINE configs[0], plumbing)",
+        "value": 65536 / med / GIB, "unit": "GiB/s", "n_gpus": dist.world,
+        "steps": len(lat), "warmup": args.warmup, "ms_per_step": wall / len(lat) * 1e3,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic (splitmix64 seed 1), initial 0",
+        "config": {"workload": WORKLOADS[1], "call": "ns_csum_checksum (synchronous, ctypes)"},
+        "sync_call_us": {"median": med * 1e6, "min": lat[0] * 1e6, "max": lat[-1] * 1e6},
+        "kernel_only_us": kern_us,
+        "result": {"got": got, "want": want, "bit_exact": bool(ok)},
+    }
+    if dist.rank == 0 and not args.no_cpu:
+        # 1 core, the scalar port: many descriptors over the one buffer, so
+        # the per-call Python overhead is not what is timed
+        reps_per = 2048
+        dd = np.repeat(d1, reps_per)
+        outc = np.zeros(reps_per, dtype=np.uint16)
+        O.c_batch_mt(buf, dd, 1, outc)
+        reps, t0 = 0, time.perf_counter()
+        while True:
+            O.c_batch_mt(buf, dd, 1, outc)
+            reps += 1
+            el = time.perf_counter() - t0
+            if el >= args.cpu_seconds:
+                break
+        calls = reps * reps_per
+        result["cpu_baseline"] = {
+            "value": 65536 * calls / el / GIB, "unit": "GiB/s", "cores": 1, "kind": "port",
+            "per_call_us": el / calls * 1e6, "bit_exact": bool((outc == want).all()),
+            "sample": f"{calls} Checksum(buf, 0) calls over the one 64 KiB buffer in {el:.1f} s; "
+                      "oracle/csum_oracle.c scalar 2-B/iteration loop (checksum.go:41-43), single thread"}
     if dist.rank == 0:
         print(json.dumps(result), flush=True)
     eng.close()

@@ -134,16 +134,19 @@ int ns_csum_init(const ns_csum_opts* opts, ns_csum_ctx** out);
 void ns_csum_destroy(ns_csum_ctx* ctx);
 
 /* Blocks until `stream` is idle (NULL: the whole device); returns the
- * number of out-of-range descriptors seen since the last call in *bad
- * (descriptors past `arena_bytes` are summed as empty and counted).          */
+ * number of out-of-range descriptors (and dropped stores) counted since the
+ * last call in *bad (descriptors past `arena_bytes` are summed as empty and
+ * counted).  The count is read and reset in one device atomic: counts from
+ * kernels still running on other streams are reported by a later call.      */
 int ns_csum_sync(ns_csum_ctx* ctx, void* stream, uint64_t* bad);
 
 /* ---- device-resident batch (the hot path) --------------------------------
  * d_arena/d_desc/d_out are device pointers on ctx's device; the call only
  * enqueues kernels on `stream` and returns (asynchronous).  With
  * NS_BATCH_CHAINED, or when descriptors average >= 1 MiB (arena_bytes / n:
- * then each is spread over many workgroups), the context's scratch is used:
- * such calls on one context must be serialised by the caller's stream order. */
+ * then each is spread over many workgroups), the call uses device scratch
+ * that the context keeps per stream: calls on different streams of one
+ * context run concurrently, calls on one stream are ordered by it.          */
 int ns_csum_batch_dev(ns_csum_ctx* ctx, const uint8_t* d_arena,
                       uint64_t arena_bytes, const ns_pkt_desc* d_desc,
                       uint32_t n, uint16_t* d_out, uint32_t batch_flags,

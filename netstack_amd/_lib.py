@@ -15,6 +15,10 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libnetstack_csum.so")
 CSRC = os.path.join(_HERE, "csrc")
 
+# The NS_CSUM_ABI_VERSION this binding is written against; lib() refuses a
+# library that reports another (a stale build).
+ABI_VERSION = 2
+
 NS_OK = 0
 NS_EINVAL = -1
 NS_ERANGE = -2
@@ -144,6 +148,17 @@ def lib():
                 l = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
             except OSError as e:
                 raise NativeLibraryError(f"cannot load {LIB_PATH}: {e}") from e
+            try:
+                ver_fn = l.ns_csum_abi_version
+            except AttributeError as e:
+                raise NativeLibraryError(f"{LIB_PATH} exports no ns_csum_abi_version") from e
+            ver_fn.restype = ctypes.c_int
+            ver_fn.argtypes = []
+            ver = int(ver_fn())
+            if ver != ABI_VERSION:
+                raise NativeLibraryError(
+                    f"{LIB_PATH} has C ABI version {ver}, this binding needs {ABI_VERSION}: "
+                    f"rebuild it with `make -C {CSRC}`")
             _declare(l)
             _lib = l
     return _lib

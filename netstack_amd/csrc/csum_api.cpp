@@ -112,9 +112,40 @@ struct PinBuf {
   }
 };
 
-// Mapped, coherent, all-device pinned memory: the kernel reads and writes it
-// over PCIe with ordinary loads and stores (zero-copy).
+// Mapped, all-device pinned memory that the kernel reads and writes over PCIe
+// with ordinary loads and stores (zero-copy).  It is coarse-grained
+// (hipHostMallocNonCoherent): device writes become visible to the host at
+// kernel completion, and host writes to a kernel at its dispatch.  That is
+// all the zero-copy path needs — the host fills the table and bytes before
+// the launch and reads results only after hipStreamSynchronize — but it is
+// not safe for polling a buffer while a kernel runs.
 using MappedPin = PinBuf<uint8_t, hipHostMallocMapped | hipHostMallocNonCoherent | hipHostMallocPortable>;
+
+// Chained-batch scratch (csum_kernels.h ChainScratch): partials + flags, and
+// the fold statuses in a buffer of their own, zeroed once at allocation.
+struct ChainBuf {
+  DevBuf<uint32_t> part;
+  DevBuf<uint64_t> status;
+  int ensure(uint64_t n) {
+    int rc = part.ensure((size_t)nsk::chain_scratch_words(n));
+    if (rc == NS_OK) rc = status.ensure((size_t)nsk::chain_blocks(n), true);
+    return rc;
+  }
+  nsk::ChainScratch get() const { return nsk::ChainScratch{part.p, status.p}; }
+  void release() {
+    part.release();
+    status.release();
+  }
+};
+
+// Scratch of the device-resident API for one caller stream: chained batches
+// and huge-descriptor splits on different streams of one context run
+// concurrently, each on its own scratch (the same stream orders its own).
+struct StreamScratch {
+  hipStream_t stream = nullptr;
+  ChainBuf chain;
+  DevBuf<uint32_t> split;  // csum_split accumulators (zero between launches)
+};
 
 // One small synchronous call's batch: `ndesc` descriptors over bytes
 // [lo, lo + nbytes) of the caller's arena, staged in mapped memory whose
@@ -152,13 +183,15 @@ struct ns_csum_ctx {
   unsigned long long* d_err = nullptr;
   std::mutex mu;  // guards everything below
 
-  DevBuf<uint32_t> partial;  // chained-batch scratch (device-resident API)
-  DevBuf<uint32_t> split;    // csum_split scratch (device-resident API, huge descriptors)
+  // device-resident API scratch, one per caller stream (allocated on first use)
+  std::vector<StreamScratch*> scratch;
+  // ns_csum_sync's exchanged error count (mapped: written by take_err)
+  MappedPin err_taken;
   // host-path slots (double-buffered)
   DevBuf<uint8_t> d_arena[2];
   DevBuf<ns_pkt_desc> d_desc[2];
   DevBuf<uint16_t> d_out[2];
-  DevBuf<uint32_t> d_part[2];
+  ChainBuf d_chain[2];
   PinBuf<ns_pkt_desc> h_desc[2];
   PinBuf<uint16_t> h_out[2];
   // zero-copy pass buffer for small calls: [table | results]
@@ -189,10 +222,6 @@ struct DeviceGuard {
     if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
   }
 };
-
-// Chained-batch scratch for n descriptors (nsk::launch_batch): partials,
-// continuation flags and the run-fold aggregates.
-size_t chain_words(uint64_t n) { return (size_t)nsk::chain_scratch_words(n); }
 
 bool any_cont(const ns_pkt_desc* d, uint32_t n) {
   for (uint32_t i = 0; i < n; ++i)
@@ -241,7 +270,7 @@ int run_zero_copy(ns_csum_ctx* ctx, SmallReq* const* reqs, size_t nreq) {
   const uint64_t o_off = nd * sizeof(ns_pkt_desc);
   int rc;
   if ((rc = ctx->z_buf.ensure(std::max<uint64_t>(kPassTableBytes, o_off + nd * 2))) != NS_OK) return rc;
-  if (chained && (rc = ctx->d_part[0].ensure(chain_words(nd), true)) != NS_OK) return rc;
+  if (chained && (rc = ctx->d_chain[0].ensure(nd)) != NS_OK) return rc;
   uint8_t* z = ctx->z_buf.p;
   ns_pkt_desc* zd = reinterpret_cast<ns_pkt_desc*>(z);
   uint64_t k = 0;
@@ -264,7 +293,8 @@ int run_zero_copy(ns_csum_ctx* ctx, SmallReq* const* reqs, size_t nreq) {
   uint8_t* zdev = ctx->z_buf.dev;
   hipStream_t s = ctx->stream[0];
   HIP_TRY(nsk::launch_batch(nullptr, kWholeSpace, zdev, (uint32_t)nd, reinterpret_cast<uint16_t*>(zdev + o_off),
-                            chained ? ctx->d_part[0].p : nullptr, ctx->d_err, s, std::max<uint64_t>(nb, 1)));
+                            chained ? ctx->d_chain[0].get() : nsk::ChainScratch{}, ctx->d_err, s,
+                            std::max<uint64_t>(nb, 1)));
   HIP_TRY(hipStreamSynchronize(s));
   const uint16_t* res = reinterpret_cast<const uint16_t*>(z + o_off);
   for (size_t r = 0; r < nreq; ++r) {
@@ -450,26 +480,38 @@ int run_host_batch(ns_csum_ctx* ctx, const uint8_t* h_arena, uint64_t arena_byte
       std::memcpy(h_out + pend[slot].first, ctx->h_out[slot].p, pend[slot].count * sizeof(uint16_t));
       pend[slot].live = false;
     }
-    int rc;
-    if ((rc = ctx->d_arena[slot].ensure(std::max<uint64_t>(span, 16))) != NS_OK) return rc;
-    if ((rc = ctx->d_desc[slot].ensure(cnt)) != NS_OK) return rc;
-    if ((rc = ctx->d_out[slot].ensure(cnt)) != NS_OK) return rc;
-    if ((rc = ctx->h_desc[slot].ensure(cnt)) != NS_OK) return rc;
-    if ((rc = ctx->h_out[slot].ensure(cnt)) != NS_OK) return rc;
-    if (chained && (rc = ctx->d_part[slot].ensure(chain_words(cnt), true)) != NS_OK) return rc;
-    // The table goes over verbatim (one memcpy into pinned memory) and is
-    // rebased to the chunk on the device: a per-descriptor rewrite on the CPU
-    // was the limit of small-packet batches.
-    ns_pkt_desc* hd = ctx->h_desc[slot].p;
-    std::memcpy(hd, h_desc + k, (size_t)cnt * sizeof(ns_pkt_desc));
-    hipStream_t s = ctx->stream[slot];
-    if (span) HIP_TRY(hipMemcpyAsync(ctx->d_arena[slot].p, h_arena + cut_lo, span, hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemcpyAsync(ctx->d_desc[slot].p, hd, cnt * sizeof(ns_pkt_desc), hipMemcpyHostToDevice, s));
-    HIP_TRY(nsk::launch_rebase(ctx->d_desc[slot].p, cnt, cut_lo, s));
-    HIP_TRY(nsk::launch_batch(ctx->d_arena[slot].p, span, ctx->d_desc[slot].p, cnt, ctx->d_out[slot].p,
-                              chained ? ctx->d_part[slot].p : nullptr, ctx->d_err, s));
-    HIP_TRY(hipMemcpyAsync(ctx->h_out[slot].p, ctx->d_out[slot].p, cnt * sizeof(uint16_t), hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipEventRecord(ctx->done[slot], s));
+    // Everything that can fail for this chunk; on failure the other slot's
+    // transfers are drained before returning (the next call reuses the
+    // pinned buffers they read and write).
+    auto enqueue = [&]() -> int {
+      int rc;
+      if ((rc = ctx->d_arena[slot].ensure(std::max<uint64_t>(span, 16))) != NS_OK) return rc;
+      if ((rc = ctx->d_desc[slot].ensure(cnt)) != NS_OK) return rc;
+      if ((rc = ctx->d_out[slot].ensure(cnt)) != NS_OK) return rc;
+      if ((rc = ctx->h_desc[slot].ensure(cnt)) != NS_OK) return rc;
+      if ((rc = ctx->h_out[slot].ensure(cnt)) != NS_OK) return rc;
+      if (chained && (rc = ctx->d_chain[slot].ensure(cnt)) != NS_OK) return rc;
+      // The table goes over verbatim (one memcpy into pinned memory) and is
+      // rebased to the chunk on the device: a per-descriptor rewrite on the
+      // CPU was the limit of small-packet batches.
+      ns_pkt_desc* hd = ctx->h_desc[slot].p;
+      std::memcpy(hd, h_desc + k, (size_t)cnt * sizeof(ns_pkt_desc));
+      hipStream_t s = ctx->stream[slot];
+      if (span) HIP_TRY(hipMemcpyAsync(ctx->d_arena[slot].p, h_arena + cut_lo, span, hipMemcpyHostToDevice, s));
+      HIP_TRY(hipMemcpyAsync(ctx->d_desc[slot].p, hd, cnt * sizeof(ns_pkt_desc), hipMemcpyHostToDevice, s));
+      HIP_TRY(nsk::launch_rebase(ctx->d_desc[slot].p, cnt, cut_lo, s));
+      HIP_TRY(nsk::launch_batch(ctx->d_arena[slot].p, span, ctx->d_desc[slot].p, cnt, ctx->d_out[slot].p,
+                                chained ? ctx->d_chain[slot].get() : nsk::ChainScratch{}, ctx->d_err, s));
+      HIP_TRY(hipMemcpyAsync(ctx->h_out[slot].p, ctx->d_out[slot].p, cnt * sizeof(uint16_t), hipMemcpyDeviceToHost,
+                             s));
+      HIP_TRY(hipEventRecord(ctx->done[slot], s));
+      return NS_OK;
+    };
+    const int rc = enqueue();
+    if (rc != NS_OK) {
+      (void)drain(slot);
+      return rc;
+    }
     pend[slot].live = true;
     pend[slot].first = k;
     pend[slot].count = cnt;
@@ -762,6 +804,10 @@ int ns_csum_init(const ns_csum_opts* opts, ns_csum_ctx** out) {
     ns_csum_destroy(ctx);
     return report_hip(e, "ns_csum_init", __FILE__, __LINE__);
   }
+  if ((rc = ctx->err_taken.ensure(sizeof(unsigned long long))) != NS_OK) {
+    ns_csum_destroy(ctx);
+    return rc;
+  }
   *out = ctx;
   return NS_OK;
 }
@@ -772,8 +818,13 @@ void ns_csum_destroy(ns_csum_ctx* ctx) {
     DeviceGuard g(ctx->device);
     for (int s = 0; s < 2; ++s)
       if (ctx->stream[s]) (void)hipStreamSynchronize(ctx->stream[s]);
-    ctx->partial.release();
-    ctx->split.release();
+    for (StreamScratch* sc : ctx->scratch) {
+      sc->chain.release();
+      sc->split.release();
+      delete sc;
+    }
+    ctx->scratch.clear();
+    ctx->err_taken.release();
     ctx->z_buf.release();
     for (MappedPin* b : ctx->stage_all) {
       b->release();
@@ -785,7 +836,7 @@ void ns_csum_destroy(ns_csum_ctx* ctx) {
       ctx->d_arena[s].release();
       ctx->d_desc[s].release();
       ctx->d_out[s].release();
-      ctx->d_part[s].release();
+      ctx->d_chain[s].release();
       ctx->h_desc[s].release();
       ctx->h_out[s].release();
       if (ctx->done[s]) (void)hipEventDestroy(ctx->done[s]);
@@ -807,37 +858,56 @@ int ns_csum_sync(ns_csum_ctx* ctx, void* stream, uint64_t* bad) {
   }
   unsigned long long v = 0;
   {
+    // Read and reset in one device atomic (take_err): a separate copy and
+    // memset would lose counts that kernels on other streams add in between.
     std::lock_guard<std::mutex> lk(ctx->mu);
-    HIP_TRY(hipMemcpy(&v, ctx->d_err, sizeof(v), hipMemcpyDeviceToHost));
-    if (v) HIP_TRY(hipMemset(ctx->d_err, 0, sizeof(v)));
+    unsigned long long* taken = reinterpret_cast<unsigned long long*>(ctx->err_taken.p);
+    HIP_TRY(nsk::launch_take_err(ctx->d_err, reinterpret_cast<unsigned long long*>(ctx->err_taken.dev),
+                                 ctx->stream[0]));
+    HIP_TRY(hipStreamSynchronize(ctx->stream[0]));
+    v = *reinterpret_cast<volatile unsigned long long*>(taken);
   }
   if (bad) *bad = v;
   return NS_OK;
 }
 
 namespace {
+// The scratch of `s` (caller holds ctx->mu).  Growing a buffer frees the old
+// one with hipFree, which waits for the device, so no launch still uses it.
+StreamScratch* stream_scratch(ns_csum_ctx* ctx, hipStream_t s) {
+  for (StreamScratch* sc : ctx->scratch)
+    if (sc->stream == s) return sc;
+  StreamScratch* sc = new (std::nothrow) StreamScratch();
+  if (!sc) return nullptr;
+  sc->stream = s;
+  ctx->scratch.push_back(sc);
+  return sc;
+}
+
 int batch_dev(ns_csum_ctx* ctx, const uint8_t* d_arena, uint64_t arena_bytes, const ns_pkt_desc* d_desc,
               uint32_t n, uint16_t* d_out, uint32_t batch_flags, void* stream, bool store) {
   if (!ctx || (n && (!d_desc || !d_out)) || (arena_bytes && !d_arena)) return NS_EINVAL;
   if (n == 0) return NS_OK;
   DeviceGuard g(ctx->device);
   hipStream_t s = (hipStream_t)stream;  // NULL = the HIP null stream
-  uint32_t* part = nullptr;
+  nsk::ChainScratch chain{};
   uint32_t* split = nullptr;
   if ((batch_flags & NS_BATCH_CHAINED) || arena_bytes / n >= nsk::split_min_avg()) {
     std::lock_guard<std::mutex> lk(ctx->mu);
+    StreamScratch* sc = stream_scratch(ctx, s);
+    if (!sc) return NS_ENOMEM;
     if (batch_flags & NS_BATCH_CHAINED) {
-      int rc = ctx->partial.ensure(chain_words(n), true);
+      int rc = sc->chain.ensure(n);
       if (rc != NS_OK) return rc;
-      part = ctx->partial.p;
+      chain = sc->chain.get();
     }
     if (arena_bytes / n >= nsk::split_min_avg()) {
-      int rc = ctx->split.ensure(nsk::split_words(n), true);  // zero once; the kernel keeps it so
+      int rc = sc->split.ensure(nsk::split_words(n), true);  // zero once; the kernel keeps it so
       if (rc != NS_OK) return rc;
-      split = ctx->split.p;
+      split = sc->split.p;
     }
   }
-  HIP_TRY(nsk::launch_batch(d_arena, arena_bytes, d_desc, n, d_out, part, ctx->d_err, s, 0, store ? 1u : 0u,
+  HIP_TRY(nsk::launch_batch(d_arena, arena_bytes, d_desc, n, d_out, chain, ctx->d_err, s, 0, store ? 1u : 0u,
                             split));
   return NS_OK;
 }

@@ -8,11 +8,10 @@
 namespace nsk {
 
 // Enqueue the checksum of n descriptors (16-byte ns_pkt_desc, device memory)
-// over `arena` on `stream`.  With `partial` != nullptr (a chained-batch
-// scratch of chain_scratch_words(n) u32, layout below) the per-descriptor
-// partial sums and continuation flags go there and a fold pass folds
-// NS_DESC_CONT runs into `out`; otherwise every
-// descriptor is independent.
+// over `arena` on `stream`.  With `chain` set (a chained-batch scratch, layout
+// below) the per-descriptor partial sums and continuation flags go there and
+// a fold pass folds NS_DESC_CONT runs into `out`; otherwise every descriptor
+// is independent.
 // Out-of-range descriptors are summed as empty and counted in *err.
 // `sizing_bytes` (0: arena_bytes) is the byte count the launcher sizes tiles
 // by — the payload of a batch whose "arena" is the whole address space
@@ -20,24 +19,39 @@ namespace nsk {
 // `store`: descriptors flagged NS_DESC_STORE write their final result into
 // the (then writable) arena.
 // `split`: scratch for csum_split (see below), or nullptr.
-// Chained-batch scratch layout, in u32 words: the n partial sums, their u16
-// flags from chain_flag_word(n) (16-B aligned), then one 8-B fold status per
-// kFoldBlock descriptors from chain_status_word(n) (csum_kernels.hip, run
-// folding).  Statuses are tagged with a launch generation, so stale ones are
-// ignored; a fresh scratch is zeroed so that no garbage word can carry a
-// live generation.
+//
+// Chained-batch scratch: `partial`, chain_scratch_words(n) u32 — the n
+// partial sums, then their u16 flags from chain_flag_word(n) (16-B aligned);
+// and `status`, chain_blocks(n) u64 fold statuses (one per kFoldBlock
+// descriptors, csum_kernels.hip run folding) in a buffer of their own that
+// holds nothing but status words.  Statuses are tagged with a process-wide
+// launch generation, so stale ones are ignored; the status buffer is zeroed
+// when it is allocated, so no word in it can carry a live generation (a
+// status array that shared its buffer with the partials could land on a
+// previous launch's partials).  Neither needs clearing between launches.
+// Concurrent chained launches need distinct scratch (csum_api.cpp keys it by
+// stream).
 constexpr uint32_t kFoldPer = 8;                 // descriptors per thread
 constexpr uint32_t kFoldBlock = 256 * kFoldPer;  // descriptors per workgroup
 constexpr uint64_t chain_flag_word(uint64_t n) { return (n + 3) & ~3ull; }
-constexpr uint64_t chain_status_word(uint64_t n) { return (chain_flag_word(n) + ((n + 7) & ~7ull) / 2 + 1) & ~1ull; }
 constexpr uint64_t chain_blocks(uint64_t n) { return (n + kFoldBlock - 1) / kFoldBlock; }
-constexpr uint64_t chain_scratch_words(uint64_t n) { return chain_status_word(n) + 2 * chain_blocks(n); }
+constexpr uint64_t chain_scratch_words(uint64_t n) { return (chain_flag_word(n) + ((n + 7) & ~7ull) / 2 + 3) & ~3ull; }
+
+struct ChainScratch {
+  uint32_t* partial = nullptr;  // chain_scratch_words(n) u32
+  uint64_t* status = nullptr;   // chain_blocks(n) u64, zeroed at allocation
+};
 
 hipError_t launch_batch(const uint8_t* arena, uint64_t arena_bytes,
                         const void* desc, uint32_t n, uint16_t* out,
-                        uint32_t* partial, unsigned long long* err,
+                        ChainScratch chain, unsigned long long* err,
                         hipStream_t stream, uint64_t sizing_bytes = 0, uint32_t store = 0,
                         uint32_t* split = nullptr);
+
+// *taken = the error count, which is reset to 0 in the same atomic exchange
+// (counts added by kernels still running on other streams are never lost).
+// `taken` must be device-visible (mapped host memory).
+hipError_t launch_take_err(unsigned long long* err, unsigned long long* taken, hipStream_t stream);
 
 // Rewrite n device-resident descriptors' offsets relative to `bias` (empty
 // descriptors get 0): the host pipeline's per-chunk table rebase.

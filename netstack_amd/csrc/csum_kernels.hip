@@ -576,7 +576,7 @@ __device__ __forceinline__ void park_store(HybLds<P>& L, uint32_t store, uint4 r
   if (!store) return;
   uint32_t stw = mine ? (raw.w >> 18) & 0x3FFFu : 0u;
   const uint64_t at = ((uint64_t)raw.x | ((uint64_t)raw.y << 32)) + (stw >> 2);
-  if (!(stw & 3u)) {
+  if (!(stw & 1u)) {  // NS_DESC_STORE_RAW counts only with NS_DESC_STORE
     stw = 0;
   } else if (at > arena_bytes || arena_bytes - at < 2) {
     atomicAdd(err, 1ull);
@@ -724,7 +724,7 @@ __global__ __launch_bounds__(256) void csum_split(const uint8_t* __restrict__ ar
   const uint32_t init = raw.w & 0xFFFFu, cont = (raw.w >> 17) & 1u;
   uint32_t stw = store ? (raw.w >> 18) & 0x3FFFu : 0u;
   const uint64_t at = off + (stw >> 2);
-  if (!(stw & 3u)) {
+  if (!(stw & 1u)) {  // NS_DESC_STORE_RAW counts only with NS_DESC_STORE
     stw = 0;
   } else if (at > arena_bytes || arena_bytes - at < 2) {
     atomicAdd(err, 1ull);
@@ -940,7 +940,7 @@ __global__ __launch_bounds__(256) void fold_scan(const uint32_t* __restrict__ pa
   }
   uint32_t mine_st = 0;
 #pragma unroll
-  for (uint32_t j = 0; j < kFoldPer; ++j) mine_st |= (f[j] >> 1) & 3u;
+  for (uint32_t j = 0; j < kFoldPer; ++j) mine_st |= (f[j] >> 1) & 1u;
   const bool stores = __syncthreads_or(mine_st) != 0;
 
   if (base + kFoldPer <= n && ((uintptr_t)(out + base) & 15u) == 0) {
@@ -971,12 +971,12 @@ __global__ __launch_bounds__(256) void fold_scan(const uint32_t* __restrict__ pa
   for (uint32_t j = 0; j < kFoldPer; ++j) {
     const uint64_t k = b0 + 256u * j + t;
     xf[j] = k < n ? lx[256u * j + t] : 0u;
-    dk[j] = ((xf[j] >> 17) & 3u) ? desc[k] : make_uint4(0, 0, 0, 0);
+    dk[j] = ((xf[j] >> 17) & 1u) ? desc[k] : make_uint4(0, 0, 0, 0);
   }
 #pragma unroll
   for (uint32_t j = 0; j < kFoldPer; ++j) {
     const uint32_t stw = xf[j] >> 17;
-    if (stw & 3u)
+    if (stw & 1u)
       store_result((uint64_t)(uintptr_t)arena + ((uint64_t)dk[j].x | ((uint64_t)dk[j].y << 32)) + (stw >> 2),
                    xf[j] & 0xFFFFu, stw);
   }
@@ -1001,15 +1001,14 @@ __global__ __launch_bounds__(256) void rebase_desc(uint4* __restrict__ d, uint32
 namespace nsk {
 
 template <uint32_t SPINS = kFoldSpins>
-static void launch_fold(uint32_t* part, uint32_t n, uint16_t* out, const void* desc, const uint8_t* arena,
+static void launch_fold(ChainScratch ch, uint32_t n, uint16_t* out, const void* desc, const uint8_t* arena,
                         hipStream_t stream) {
   static std::atomic<uint32_t> gen_counter{0};
   uint32_t gen = ++gen_counter;
   if (gen == 0) gen = ++gen_counter;  // 0 never tags a status
   const uint32_t nb = (uint32_t)chain_blocks(n);
-  const uint16_t* flags = reinterpret_cast<const uint16_t*>(part + chain_flag_word(n));
-  uint64_t* status = reinterpret_cast<uint64_t*>(part + chain_status_word(n));
-  hipLaunchKernelGGL(fold_scan<SPINS>, dim3(nb), dim3(256), 0, stream, part, flags, n, status, gen, out,
+  const uint16_t* flags = reinterpret_cast<const uint16_t*>(ch.partial + chain_flag_word(n));
+  hipLaunchKernelGGL(fold_scan<SPINS>, dim3(nb), dim3(256), 0, stream, ch.partial, flags, n, ch.status, gen, out,
                      reinterpret_cast<const uint4*>(desc), arena);
 }
 
@@ -1083,12 +1082,23 @@ hipError_t launch_rebase(void* desc, uint32_t n, uint64_t bias, hipStream_t stre
   return hipGetLastError();
 }
 
+// The error-count exchange of ns_csum_sync: one atomic, so a kernel still
+// running on another stream never has its count wiped by a separate reset.
+__global__ void take_err(unsigned long long* __restrict__ err, unsigned long long* __restrict__ taken) {
+  if (threadIdx.x == 0) *taken = atomicExch(err, 0ull);
+}
+
+hipError_t launch_take_err(unsigned long long* err, unsigned long long* taken, hipStream_t stream) {
+  hipLaunchKernelGGL(take_err, dim3(1), dim3(64), 0, stream, err, taken);
+  return hipGetLastError();
+}
+
 hipError_t launch_batch(const uint8_t* arena, uint64_t arena_bytes,
                         const void* desc, uint32_t n, uint16_t* out,
-                        uint32_t* partial, unsigned long long* err,
+                        ChainScratch chain, unsigned long long* err,
                         hipStream_t stream, uint64_t sizing_bytes, uint32_t store,
                         uint32_t* split) {
-  uint32_t* part = partial;  // the chained scratch (layout: csum_kernels.h)
+  uint32_t* part = chain.partial;  // the chained scratch (layout: csum_kernels.h)
   if (n == 0) return hipSuccess;
   hipError_t e;
   if (sizing_bytes == 0) sizing_bytes = arena_bytes;
@@ -1124,7 +1134,7 @@ hipError_t launch_batch(const uint8_t* arena, uint64_t arena_bytes,
   }
   if (e != hipSuccess || part == nullptr) return e;
   // run folding: one pass over 6 B per descriptor, any run length
-  launch_fold<>(part, n, out, desc, arena, stream);
+  launch_fold<>(chain, n, out, desc, arena, stream);
   return hipGetLastError();
 }
 

@@ -688,6 +688,98 @@ def test_store_past_arena_dropped_and_counted(engine, chained):
     assert np.array_equal(dt.cpu().numpy(), expect)
 
 
+@pytest.mark.parametrize("chained,huge", [(False, False), (True, False), (False, True)])
+def test_store_raw_bit_alone_stores_nothing(engine, chained, huge):
+    """NS_DESC_STORE_RAW (bit 3) means something only with NS_DESC_STORE
+    (bit 2): descriptors flagged RAW alone, with an offset in range or past
+    the arena, leave the arena unchanged and count nothing, in the tile
+    kernel, the chained fold pass and the huge-descriptor split kernel."""
+    import oracle as O
+
+    torch = _torch()
+    rng = np.random.default_rng(41 + chained + 2 * huge)
+    n = 4 if huge else 3000
+    lengths = rng.integers(2 << 20, 3 << 20, n) if huge else rng.integers(2, 2000, n)
+    d = np.zeros(n, dtype=O.DESC_DTYPE)
+    d["len"] = lengths
+    d["off"] = np.concatenate([[0], np.cumsum(lengths + 3)[:-1]])
+    d["initial"] = rng.integers(0, 65536, n)
+    at = np.minimum(rng.integers(0, 4096, n), 4095).astype(np.uint16)
+    d["flags"] = (0x8 | (at << 4) | rng.integers(0, 2, n)).astype(np.uint16)
+    if chained:
+        d["flags"][1::2] |= 2
+    end = int(d["off"][-1] + d["len"][-1])
+    d["flags"][-1] = 0x8 | (4095 << 4)  # past the arena too
+    arena = rng.integers(0, 256, end, dtype=np.uint8)
+    want, bad = O.c_batch(arena, d, chained=chained)
+    expect, dropped = O.apply_stores(arena, d, want)
+    assert bad == 0 and dropped == 0 and np.array_equal(expect, arena)
+    dt = torch.from_numpy(arena).cuda()
+    desc = torch.from_numpy(d.view(np.uint8).copy()).cuda()
+    engine.sync()
+    out = engine.batch_tensors(dt, desc, chained=chained, store=True)
+    torch.cuda.synchronize()
+    assert engine.sync() == 0
+    assert np.array_equal(out.cpu().numpy().view(np.uint16), want)
+    assert np.array_equal(dt.cpu().numpy(), arena)
+
+
+def test_concurrent_chained_batches_on_two_streams_of_one_context(engine):
+    """Chained batches (fold scratch) and huge-descriptor batches (split
+    scratch) issued on two streams of ONE context without waiting: the
+    context keeps scratch per stream, so both streams' results are
+    bit-exact.  Out-of-range descriptors on both streams are counted exactly
+    once across a sync of one stream (taken while the other may still run)
+    and a sync of the device: ns_csum_sync reads and resets the count in one
+    device atomic."""
+    import oracle as O
+    from netstack_amd import workloads as W
+
+    torch = _torch()
+    batches = []
+    for k, (n, nbad) in enumerate([(250_000, 3), (180_000, 5)]):
+        rng = np.random.default_rng(600 + k)
+        flags = (2 * (rng.random(n) < 0.8)).astype(np.uint16) | rng.integers(0, 2, n).astype(np.uint16)
+        flags[0] = 0
+        d, end = W.make_desc(rng.integers(0, 300, n).astype(np.uint32),
+                             rng.integers(0, 65536, n).astype(np.uint16), align=2, flags=flags)
+        arena = rng.integers(0, 256, end, dtype=np.uint8)
+        badi = rng.choice(n, nbad, replace=False)
+        d["off"][badi] = end + 10
+        d["len"][badi] = 4
+        want, bad = O.c_batch(arena, d, chained=True)
+        assert bad == nbad
+        batches.append((torch.from_numpy(arena).cuda(), torch.from_numpy(d.view(np.uint8).copy()).cuda(), want))
+    # two huge-descriptor batches (csum_split) as well
+    huge = []
+    for k in range(2):
+        rng = np.random.default_rng(700 + k)
+        d = np.zeros(3, dtype=O.DESC_DTYPE)
+        d["len"] = rng.integers(4 << 20, 6 << 20, 3)
+        d["off"] = np.concatenate([[1], 1 + np.cumsum(d["len"][:-1].astype(np.uint64))])
+        d["initial"] = rng.integers(0, 65536, 3)
+        arena = rng.integers(0, 256, int(d["off"][-1] + d["len"][-1]) + 1, dtype=np.uint8)
+        want, _ = O.c_batch(arena, d)
+        huge.append((torch.from_numpy(arena).cuda(), torch.from_numpy(d.view(np.uint8).copy()).cuda(), want))
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    torch.cuda.synchronize()
+    engine.sync()
+    for rep in range(3):
+        outs = []
+        for k in range(2):
+            a, dd, _ = batches[k]
+            outs.append(engine.batch_tensors(a, dd, chained=True, stream=streams[k]))
+        houts = [engine.batch_tensors(huge[k][0], huge[k][1], stream=streams[k]) for k in range(2)]
+        first = engine.sync(streams[0].cuda_stream)
+        torch.cuda.synchronize()
+        rest = engine.sync()
+        assert first + rest == 8, (rep, first, rest)
+        for k in range(2):
+            got = outs[k].cpu().numpy().view(np.uint16)
+            assert np.array_equal(got, batches[k][2]), (rep, k, np.flatnonzero(got != batches[k][2])[:8])
+            assert np.array_equal(houts[k].cpu().numpy().view(np.uint16), huge[k][2]), (rep, k)
+
+
 @pytest.mark.parametrize("layout", ["one_run", "mixed", "zeros"])
 def test_long_chained_runs(engine, layout):
     """Run folding at any run length (the segmented scan of fold_reduce /
