@@ -1,6 +1,7 @@
-// netstack/buffer.hpp — C++ mirror of google/netstack tcpip/buffer/view.go,
-// the checksum's input layout.  Same type and method names as the Go package
-// (View, VectorisedView, TrimFront, CapLength, ToView, ...), same semantics;
+// netstack/buffer.hpp — C++ mirror of google/netstack tcpip/buffer (view.go,
+// prependable.go), the checksum's input layout.  Same type and method names
+// as the Go package (View, VectorisedView, Prependable, TrimFront, CapLength,
+// ToView, Prepend, ...), same semantics;
 // views alias their backing bytes exactly like Go slices (no copies on trim).
 // Out-of-range slicing throws std::out_of_range where Go panics.
 #pragma once
@@ -122,6 +123,62 @@ class VectorisedView {
 // NewVectorisedView (view.go:64-66)
 inline VectorisedView NewVectorisedView(size_t size, std::vector<View> views) {
   return VectorisedView(size, std::move(views));
+}
+
+// Prependable (prependable.go:22-28): a buffer that grows backwards; each
+// protocol prepends its header in front of the one above.  The bytes are
+// shared by copies of the value, as a Go slice's backing array is.
+class Prependable {
+ public:
+  Prependable() = default;
+  Prependable(std::shared_ptr<std::vector<uint8_t>> buf, size_t used_idx)
+      : buf_(std::move(buf)), end_(buf_ ? buf_->size() : 0), used_(used_idx) {}
+
+  // prependable.go:56-58: the used part (aliases the bytes).
+  buffer::View View() const { return buffer::View(base() + used_, end_ - used_); }
+  // The used part, writable (header fields are set through it).
+  uint8_t* Data() { return base() + used_; }
+  // prependable.go:61-63, 66-68
+  size_t UsedLength() const { return end_ - used_; }
+  size_t AvailableLength() const { return used_; }
+  // prependable.go:71-73
+  void TrimBack(size_t size) {
+    if (size > end_ - used_) throw std::out_of_range("Prependable.TrimBack: slice bounds out of range");
+    end_ -= size;
+  }
+  // prependable.go:77-84: the reserved bytes in front, or nullptr if they do
+  // not fit (Go returns nil).
+  uint8_t* Prepend(size_t size) {
+    if (size > used_) return nullptr;
+    used_ -= size;
+    return base() + used_;
+  }
+  // prependable.go:87-90
+  Prependable DeepCopy() const {
+    auto b = std::make_shared<std::vector<uint8_t>>(base(), base() + end_);
+    Prependable p(std::move(b), used_);
+    return p;
+  }
+
+ private:
+  uint8_t* base() const { return buf_ ? buf_->data() : nullptr; }
+  std::shared_ptr<std::vector<uint8_t>> buf_;
+  size_t end_ = 0;
+  size_t used_ = 0;
+};
+
+// prependable.go:31-33
+inline Prependable NewPrependable(size_t size) {
+  return Prependable(std::make_shared<std::vector<uint8_t>>(size, 0), size);
+}
+// prependable.go:40-42 (takes ownership of the bytes)
+inline Prependable NewPrependableFromView(std::vector<uint8_t> v) {
+  return Prependable(std::make_shared<std::vector<uint8_t>>(std::move(v)), 0);
+}
+// prependable.go:45-47
+inline Prependable NewEmptyPrependableFromView(std::vector<uint8_t> v) {
+  const size_t n = v.size();
+  return Prependable(std::make_shared<std::vector<uint8_t>>(std::move(v)), n);
 }
 
 }  // namespace buffer

@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "netstack/buffer.hpp"
+#include "netstack/packet_buffer.hpp"
 #include "netstack_csum.h"
 
 namespace netstack {
@@ -61,6 +62,23 @@ std::vector<uint16_t> ChecksumVVBatch(const buffer::VectorisedView& vv,
 // xsum = initial; for v in views: xsum = Checksum(v, xsum)
 // (transport/udp/endpoint.go:811-813, header/icmpv4.go:158-160).
 uint16_t ChecksumViews(const std::vector<buffer::View>& views, uint16_t initial);
+
+// Batched checksum steps over tcpip.PacketBuffer (ns_csum_packet_buffers),
+// one device pass per call.  Receive (a recvmmsg batch, Data = the IP
+// packet): the verdict per packet — TCP segment.parse (segment.go:174-180),
+// ICMPv4 echo (network/ipv4/icmp.go:72-80), ICMPv6 (network/ipv6/icmp.go:
+// 76-84) — one of the constants below.  Transmit (Header = IP + transport
+// headers, Data = payload): the transport checksum (buildTCPHdr, sendUDP,
+// the ICMP echo reply, ICMPv6Checksum) and the IPv4 header checksum
+// (addIPHeader) are written into each Header.
+enum PacketVerdict : uint8_t {
+  PacketChecksumInvalid = NS_PKB_INVALID,
+  PacketChecksumValid = NS_PKB_VALID,
+  PacketChecksumUnchecked = NS_PKB_UNCHECKED,
+  PacketMalformed = NS_PKB_MALFORMED,
+};
+std::vector<uint8_t> VerifyPacketBuffers(const std::vector<tcpip::PacketBuffer>& pkts);
+void FillPacketBuffers(std::vector<tcpip::PacketBuffer>& pkts);
 
 }  // namespace header
 }  // namespace netstack

@@ -24,6 +24,14 @@
  *   (connect.go:663, ipv4.go:236; tcp.go:252, ipv4.go:223)        -> ns_csum_batch_dev_store
  *   any composition of Checksum(v, xsum) / view chaining (a whole
  *   TCP/UDP/ICMP/IPv4 checksum per chain)                         -> ns_csum_chains
+ *   the checksum steps of a batch of tcpip.PacketBuffer
+ *   (tcpip/packet_buffer.go:25-50): receive — segment.parse
+ *   (tcp/segment.go:166-181), ICMPv4/v6 handleICMP
+ *   (network/ipv4/icmp.go:60-80, network/ipv6/icmp.go:62-84);
+ *   transmit — buildTCPHdr (tcp/connect.go:653-663), sendUDP
+ *   (udp/endpoint.go:808-815), the ICMP echo reply
+ *   (network/ipv4/icmp.go:96-100), ICMPv6Checksum (icmpv6.go:202-221),
+ *   addIPHeader (network/ipv4/ipv4.go:217-238)                  -> ns_csum_packet_buffers
  *
  * Semantics (bit-exact with checksum.go, including its un-folded uint32 wrap for
  * buffers > 128 KiB): every descriptor d is one calculateChecksum call over
@@ -48,7 +56,8 @@
 extern "C" {
 #endif
 
-#define NS_CSUM_ABI_VERSION 2  /* 2: ns_csum_batch_dev_store, NS_DESC_STORE* */
+#define NS_CSUM_ABI_VERSION 3  /* 2: ns_csum_batch_dev_store, NS_DESC_STORE*;
+                                  3: ns_csum_stage_*, ns_csum_packet_buffers */
 
 /* ---- status codes ------------------------------------------------------- */
 #define NS_OK 0
@@ -214,6 +223,62 @@ typedef struct ns_piece {
 } ns_piece;
 int ns_csum_chains(ns_csum_ctx* ctx, const ns_piece* pieces, uint32_t npieces,
                    uint16_t* out, uint32_t nout);
+
+/* ---- caller-filled staging ----------------------------------------------
+ * A pinned, device-mapped host buffer of at least `bytes` bytes leased from
+ * the context (released with ns_csum_stage_release).  Every entry point that
+ * takes host byte pointers (ns_csum_checksum, _vv_with_offset, _vv_batch,
+ * _views_restart, _chains, _packet_buffers) reads them IN PLACE, without a
+ * copy, when all of a call's bytes lie inside one acquired stage: a host that
+ * must not hand the library pointers into its own heap (Go: cgo forbids C
+ * memory holding Go pointers) copies its views into a stage once and passes
+ * pointers into it.  One call at a time per stage.                          */
+int ns_csum_stage_acquire(ns_csum_ctx* ctx, uint64_t bytes, uint8_t** base);
+int ns_csum_stage_release(ns_csum_ctx* ctx, uint8_t* base);
+
+/* ---- tcpip.PacketBuffer batches --------------------------------------------
+ * One tcpip.PacketBuffer (tcpip/packet_buffer.go:25-50): the packet's bytes
+ * are its Header's used part (buffer.Prependable View(), prependable.go:
+ * 55-58) followed by its Data views clipped to Data.Size().  The network
+ * header (IPv4 or IPv6, no extension headers) is the packet's first byte.  */
+typedef struct ns_pkt_buf {
+  uint8_t* hdr;        /* Header.View(); NS_PKB_FILL writes checksum fields here */
+  uint64_t hdr_len;
+  const ns_view* data; /* Data.Views()                                        */
+  uint32_t ndata;
+  uint32_t flags;      /* reserved, 0                                         */
+  uint64_t data_size;  /* Data.Size() (<= the views' total: CapLength)       */
+} ns_pkt_buf;
+
+/* NS_PKB_VERIFY — a received batch (a recvmmsg batch as the link layer
+ * delivers it: Data holds the IP packet, Header is empty), the checksum steps
+ * of the receive path after IPv4/IPv6 HandlePacket's checks and trims:
+ *   TCP: segment.parse (segment.go:174-180), valid iff the sum is 0xffff;
+ *   ICMPv4 echo request: handleICMP's ^ChecksumVV(Data with the field
+ *     zeroed) == the field (network/ipv4/icmp.go:72-80);
+ *   ICMPv6: ICMPv6Checksum(first view, src, dst, the other views) == the
+ *     field (network/ipv6/icmp.go:76-84).
+ * verdict[i]: NS_PKB_VALID / NS_PKB_INVALID; NS_PKB_UNCHECKED where the
+ * reference verifies nothing on receive (UDP, other protocols, IPv4
+ * fragments before reassembly, ICMPv4 other than echo); NS_PKB_MALFORMED
+ * where IsValid or the transport's length checks drop the packet first.
+ * NS_PKB_FILL — a batch to transmit: Header holds the IP header and the
+ * transport header (Data the payload); writes ^sum into the transport
+ * checksum field — TCP buildTCPHdr (connect.go:653-663), UDP sendUDP
+ * (udp/endpoint.go:808-815), ICMPv4 echo reply (icmp.go:96-100), ICMPv6
+ * ICMPv6Checksum — and into the IPv4 header checksum (addIPHeader,
+ * ipv4.go:236).  NS_EINVAL if a field to write lies outside Header.
+ * sums (2n, or NULL): [2i] the IPv4 header sum (0 for IPv6), [2i+1] the
+ * transport chain's un-complemented sum (0 when there is none).
+ * All sums of the batch are one device pass.                                */
+#define NS_PKB_VERIFY 1u
+#define NS_PKB_FILL 2u
+#define NS_PKB_INVALID 0u
+#define NS_PKB_VALID 1u
+#define NS_PKB_UNCHECKED 2u
+#define NS_PKB_MALFORMED 3u
+int ns_csum_packet_buffers(ns_csum_ctx* ctx, const ns_pkt_buf* pkts, uint32_t n,
+                           uint32_t op, uint16_t* sums, uint8_t* verdict);
 
 /* header.ChecksumCombine(a, b)                     checksum.go:104-107      */
 uint16_t ns_csum_combine(uint16_t a, uint16_t b);

@@ -17,7 +17,7 @@ CSRC = os.path.join(_HERE, "csrc")
 
 # The NS_CSUM_ABI_VERSION this binding is written against; lib() refuses a
 # library that reports another (a stale build).
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 NS_OK = 0
 NS_EINVAL = -1
@@ -40,9 +40,16 @@ EXPORTED = (
     "ns_csum_batch_host", "ns_csum_checksum", "ns_csum_vv_with_offset",
     "ns_csum_vv_batch", "ns_csum_views_restart", "ns_csum_pseudo_header",
     "ns_csum_combine", "ns_csum_shard_plan", "ns_csum_batch_multi", "ns_csum_chains",
+    "ns_csum_stage_acquire", "ns_csum_stage_release", "ns_csum_packet_buffers",
 )
 NS_PIECE_RESTART = 0x1
 NS_PIECE_END = 0x2
+NS_PKB_VERIFY = 1
+NS_PKB_FILL = 2
+NS_PKB_INVALID = 0
+NS_PKB_VALID = 1
+NS_PKB_UNCHECKED = 2
+NS_PKB_MALFORMED = 3
 
 
 class NativeLibraryError(RuntimeError):
@@ -81,12 +88,18 @@ class NsPiece(ctypes.Structure):
                 ("flags", ctypes.c_uint16), ("pad", ctypes.c_uint32)]
 
 
+class NsPktBuf(ctypes.Structure):
+    _fields_ = [("hdr", ctypes.c_void_p), ("hdr_len", ctypes.c_uint64), ("data", ctypes.c_void_p),
+                ("ndata", ctypes.c_uint32), ("flags", ctypes.c_uint32), ("data_size", ctypes.c_uint64)]
+
+
 class NsOpts(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int32), ("flags", ctypes.c_uint32),
                 ("staging_bytes", ctypes.c_uint64)]
 
 
 assert ctypes.sizeof(NsPktDesc) == 16 and ctypes.sizeof(NsSeg) == 24 and ctypes.sizeof(NsPiece) == 24
+assert ctypes.sizeof(NsPktBuf) == 40
 
 _lock = threading.Lock()
 _lib = None
@@ -120,6 +133,10 @@ def _declare(lib):
         "ns_csum_chains": (c.c_int, [vp, c.POINTER(NsPiece), c.c_uint32, u16p, c.c_uint32]),
         "ns_csum_batch_multi": (c.c_int, [c.POINTER(vp), c.c_uint32, u8p, c.c_uint64, vp, c.c_uint32,
                                           vp, c.c_uint32]),
+        "ns_csum_stage_acquire": (c.c_int, [vp, c.c_uint64, c.POINTER(vp)]),
+        "ns_csum_stage_release": (c.c_int, [vp, vp]),
+        "ns_csum_packet_buffers": (c.c_int, [vp, c.POINTER(NsPktBuf), c.c_uint32, c.c_uint32, u16p,
+                                             c.POINTER(c.c_uint8)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

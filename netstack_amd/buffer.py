@@ -1,8 +1,10 @@
-"""Mirror of google/netstack ``tcpip/buffer`` (view.go) — the checksum's input
-layout.
+"""Mirror of google/netstack ``tcpip/buffer`` (view.go, prependable.go) — the
+checksum's input layout.
 
-``View`` is a byte slice with ``TrimFront``/``CapLength`` (view.go:18-51) and
-``VectorisedView`` a list of views plus a size (view.go:53-158).  The methods
+``View`` is a byte slice with ``TrimFront``/``CapLength`` (view.go:18-51),
+``VectorisedView`` a list of views plus a size (view.go:53-158) and
+``Prependable`` the outbound header buffer that grows backwards
+(prependable.go:17-85).  The methods
 keep the Go names and semantics so tests read like the reference's own
 (tcpip/buffer/view_test.go, tcpip/header/checksum_test.go).  No copies are made
 when trimming: views are memoryviews over the caller's bytes, exactly as Go
@@ -131,3 +133,51 @@ class VectorisedView:
 
 def NewVectorisedView(size: int, views) -> VectorisedView:  # view.go:64-66
     return VectorisedView([v if isinstance(v, View) else View(v) for v in views], size)
+
+
+class Prependable:
+    """buffer.Prependable (prependable.go:22-28): a buffer that grows
+    backwards; each layer prepends its header in front of the one above.
+    ``View()`` aliases the backing bytes, as the Go slice does."""
+
+    __slots__ = ("buf", "usedIdx")
+
+    def __init__(self, buf: View | None = None, usedIdx: int = 0):
+        self.buf = buf if buf is not None else View(bytearray())
+        self.usedIdx = usedIdx
+
+    def View(self) -> View:  # prependable.go:56-58
+        return self.buf[self.usedIdx:]
+
+    def UsedLength(self) -> int:  # prependable.go:61-63
+        return len(self.buf) - self.usedIdx
+
+    def AvailableLength(self) -> int:  # prependable.go:66-68
+        return self.usedIdx
+
+    def TrimBack(self, size: int) -> None:  # prependable.go:71-73
+        self.buf = self.buf[: len(self.buf) - size]
+
+    def Prepend(self, size: int):  # prependable.go:77-84
+        """The reserved `size` bytes in front (a writable memoryview), or
+        None if they do not fit."""
+        if size > self.usedIdx:
+            return None
+        self.usedIdx -= size
+        return self.View().memory[:size]
+
+    def DeepCopy(self) -> "Prependable":  # prependable.go:87-90
+        return Prependable(View(bytearray(bytes(self.buf))), self.usedIdx)
+
+
+def NewPrependable(size: int) -> Prependable:  # prependable.go:31-33
+    return Prependable(NewView(size), size)
+
+
+def NewPrependableFromView(v: View) -> Prependable:  # prependable.go:40-42
+    return Prependable(v if isinstance(v, View) else View(v), 0)
+
+
+def NewEmptyPrependableFromView(v: View) -> Prependable:  # prependable.go:45-47
+    v = v if isinstance(v, View) else View(v)
+    return Prependable(v, len(v))

@@ -24,6 +24,7 @@
 static_assert(sizeof(ns_pkt_desc) == 16, "ns_pkt_desc must be 16 bytes");
 static_assert(sizeof(ns_seg) == 24, "ns_seg layout");
 static_assert(sizeof(ns_piece) == 24, "ns_piece layout");
+static_assert(sizeof(ns_pkt_buf) == 40, "ns_pkt_buf layout");
 
 namespace {
 
@@ -204,6 +205,8 @@ struct ns_csum_ctx {
   bool combining = false;
   std::vector<MappedPin*> stage_free;
   std::vector<MappedPin*> stage_all;
+  std::vector<MappedPin*> big_free;  // pooled caller stages above kStageBytes
+  std::vector<MappedPin*> leased;    // stages a caller holds (ns_csum_stage_acquire)
   // gather staging for the VectorisedView entry points
   PinBuf<uint8_t> g_arena;
   std::vector<ns_pkt_desc> g_desc;
@@ -521,29 +524,89 @@ int run_host_batch(ns_csum_ctx* ctx, const uint8_t* h_arena, uint64_t arena_byte
   return drain(slot);
 }
 
+// Caller-acquired staging (ns_csum_stage_acquire): mapped pinned buffers a
+// caller fills itself — the Go shim, which may not hand C memory holding Go
+// pointers to the library, copies its views there once.  Gathers whose bytes
+// all lie in one acquired stage read them in place (ByteSink adopt mode).
+// Buffers above kStageBytes come from a second pool (big_free).
+MappedPin* lease_big(ns_csum_ctx* ctx, uint64_t bytes, int* rc) {
+  {
+    std::lock_guard<std::mutex> ql(ctx->qmu);
+    for (size_t i = 0; i < ctx->big_free.size(); ++i) {
+      if (ctx->big_free[i]->cap >= bytes) {
+        MappedPin* b = ctx->big_free[i];
+        ctx->big_free.erase(ctx->big_free.begin() + (long)i);
+        return b;
+      }
+    }
+  }
+  MappedPin* b = new (std::nothrow) MappedPin();
+  if (!b) {
+    *rc = NS_ENOMEM;
+    return nullptr;
+  }
+  {
+    DeviceGuard g(ctx->device);
+    // whole MiB, so a pooled buffer fits the next call of a similar size
+    if ((*rc = b->ensure((bytes + (1ull << 20) - 1) & ~((1ull << 20) - 1))) != NS_OK) {
+      delete b;
+      return nullptr;
+    }
+  }
+  std::lock_guard<std::mutex> ql(ctx->qmu);
+  ctx->stage_all.push_back(b);
+  return b;
+}
+
+// The acquired stage holding every byte of [lo, hi), or nullptr.
+MappedPin* find_acquired(ns_csum_ctx* ctx, uintptr_t lo, uintptr_t hi) {
+  std::lock_guard<std::mutex> ql(ctx->qmu);
+  for (MappedPin* b : ctx->leased) {
+    const uintptr_t a = (uintptr_t)b->p;
+    if (lo >= a && hi <= a + b->cap) return b;
+  }
+  return nullptr;
+}
+
+// The byte span of a call's inputs, to decide whether they all lie in one
+// acquired stage.
+struct SpanProbe {
+  uintptr_t lo = UINTPTR_MAX, hi = 0;
+  void add(const uint8_t* p, uint64_t len) {
+    if (!len || !p) return;
+    lo = std::min(lo, (uintptr_t)p);
+    hi = std::max(hi, (uintptr_t)p + (uintptr_t)len);
+  }
+  MappedPin* stage(ns_csum_ctx* ctx) const { return hi ? find_acquired(ctx, lo, hi) : nullptr; }
+};
+
 // Where a gather assembles its bytes.  Small gathers go to a mapped staging
 // buffer leased from the context's pool (the kernel reads it in place).  A
 // gather that outgrows it moves, under the context lock it then keeps until
 // the call ends, into the context's pinned arena `g_arena` (grown by doubling
 // and kept between calls) and takes the DMA pipeline: one CPU copy per byte
 // either way (a 64 MiB VectorisedView batch went from 31 ms through a
-// growing std::vector to a few ms; tools/latency.cc).
+// growing std::vector to a few ms; tools/latency.cc).  A gather whose bytes
+// already lie in a caller's acquired stage copies nothing: its descriptors
+// address that stage (adopt mode).
 struct ByteSink {
   ns_csum_ctx* ctx;
-  MappedPin* stage = nullptr;
+  MappedPin* stage = nullptr;    // leased from the pool (copy mode)
+  MappedPin* adopted = nullptr;  // the caller's acquired stage (adopt mode)
   std::unique_lock<std::mutex> big;  // held once the bytes live in ctx->g_arena
-  uint64_t n = 0;
+  uint64_t n = 0;  // copy: bytes appended; adopt: end of the highest byte used
   int rc = NS_OK;
-  explicit ByteSink(ns_csum_ctx* c) : ctx(c) {
+  explicit ByteSink(ns_csum_ctx* c, MappedPin* adopt = nullptr) : ctx(c), adopted(adopt) {
+    if (adopted) return;
     if (zero_copy_enabled()) stage = lease_stage(ctx, &rc);
     if (!stage) rc = to_big(0);
   }
   ~ByteSink() { return_stage(ctx, stage); }
   ByteSink(const ByteSink&) = delete;
   ByteSink& operator=(const ByteSink&) = delete;
-  bool in_stage() const { return !big.owns_lock(); }
+  bool in_big() const { return big.owns_lock(); }
   uint64_t size() const { return n; }
-  uint8_t* base() const { return in_stage() ? stage->p : ctx->g_arena.p; }
+  uint8_t* base() const { return adopted ? adopted->p : in_big() ? ctx->g_arena.p : stage->p; }
   // g_arena with room for `need` bytes, keeping its first `keep` bytes.
   int reserve_big(uint64_t need, uint64_t keep) {
     PinBuf<uint8_t>& g = ctx->g_arena;
@@ -564,14 +627,32 @@ struct ByteSink {
     if (r == NS_OK && n) std::memcpy(ctx->g_arena.p, stage->p, n);
     return r;
   }
-  void append(const uint8_t* p, uint64_t len) {
-    if (!len || rc != NS_OK) return;
-    if (in_stage() && n + len > stage->cap) rc = to_big(n + len);
-    else if (!in_stage()) rc = reserve_big(n + len, n);
-    if (rc != NS_OK) return;
+  // Makes bytes [p, p + len) part of the arena; returns their arena offset.
+  uint64_t append(const uint8_t* p, uint64_t len) {
+    if (adopted) {
+      const uint64_t at = len ? (uint64_t)(p - adopted->p) : n;
+      n = std::max(n, at + len);
+      return at;
+    }
+    const uint64_t at = n;
+    if (!len || rc != NS_OK) return at;
+    if (!in_big() && n + len > stage->cap) rc = to_big(n + len);
+    else if (in_big()) rc = reserve_big(n + len, n);
+    if (rc != NS_OK) return at;
     std::memcpy(base() + n, p, len);
     n += len;
+    return at;
   }
+};
+
+// One piece of a checksum chain: `restart` = a fresh Checksum(piece, xsum)
+// (alignment restarts, checksum.go:52-55); otherwise the piece continues the
+// previous piece's byte stream with its odd-byte carry (the view chaining of
+// ChecksumVVWithOffset, checksum.go:89).
+struct Piece {
+  const uint8_t* p;
+  uint64_t len;
+  bool restart;
 };
 
 // ---- gather of VectorisedView pieces (tcpip/buffer -> staging arena) -----
@@ -580,114 +661,50 @@ struct Gather {
   ByteSink bytes;  // assembled in mapped staging (or spilled host memory)
   std::vector<ns_pkt_desc> desc;
   std::vector<uint32_t> result_at;  // index of the descriptor holding each result
-  explicit Gather(ns_csum_ctx* c) : ctx(c), bytes(c) {}
+  explicit Gather(ns_csum_ctx* c, MappedPin* adopt = nullptr) : ctx(c), bytes(c, adopt) {}
 
-  // Append one segment made of pieces (ptr,len) with Go VV semantics:
-  // odd-carry across pieces, merged into runs of <= kMergeMax bytes.
-  void segment(const std::vector<std::pair<const uint8_t*, uint64_t>>& pieces, uint16_t initial) {
-    bool first_desc = true;
-    uint64_t consumed = 0;  // bytes of this segment already described
-    ns_pkt_desc cur{};
-    bool open = false;
-    auto close = [&]() {
-      if (!open) return;
-      desc.push_back(cur);
-      open = false;
-    };
-    for (const auto& pc : pieces) {
-      const uint64_t len = pc.second;
-      if (len == 0) continue;
-      const bool big = len > kMergeMax;
-      if (open && (big || cur.len + len > kMergeMax)) close();
-      if (!open) {
-        cur.off = bytes.size();
-        cur.len = 0;
-        cur.initial = first_desc ? initial : 0;
-        cur.flags = (uint16_t)((first_desc ? 0u : NS_DESC_CONT) | ((consumed & 1) ? NS_DESC_ODD : 0u));
-        first_desc = false;
-        open = true;
-      }
-      bytes.append(pc.first, len);
-      cur.len += (uint32_t)len;
-      consumed += len;
-      if (big) close();
-    }
-    close();
-    if (first_desc) {  // no bytes: result = initial (checksum.go:97)
-      ns_pkt_desc z{};
-      z.off = 0;
-      z.len = 0;
-      z.initial = initial;
-      z.flags = 0;
-      desc.push_back(z);
-    }
-    result_at.push_back((uint32_t)desc.size() - 1);
-  }
-
-  // Each view its own calculateChecksum with odd=false, chained
-  // (xsum = Checksum(v, xsum): udp/endpoint.go:811-813).
-  void restart_chain(const std::vector<std::pair<const uint8_t*, uint64_t>>& pieces, uint16_t initial) {
-    bool first = true;
-    for (const auto& pc : pieces) {
-      ns_pkt_desc d{};
-      d.off = bytes.size();
-      d.len = (uint32_t)pc.second;
-      d.initial = first ? initial : 0;
-      d.flags = first ? 0 : NS_DESC_CONT;
-      bytes.append(pc.first, pc.second);
-      desc.push_back(d);
-      first = false;
-    }
-    if (first) {
-      ns_pkt_desc z{};
-      z.initial = initial;
-      desc.push_back(z);
-    }
-    result_at.push_back((uint32_t)desc.size() - 1);
-  }
-
-  // A chain of pieces with per-piece restart/continue semantics
-  // (include/netstack_csum.h, ns_csum_chains).  Continue pieces merge into the
-  // open descriptor up to kMergeMax bytes (exact, see kMergeMax); a restart
-  // piece always opens a new descriptor with odd = 0.
-  void chain(const ns_piece* p, uint32_t np) {
+  // One chain (include/netstack_csum.h, ns_csum_chains): sum = initial,
+  // odd = false; per piece (sum, odd) = calculateChecksum(piece, odd', sum)
+  // with odd' = false on a restart piece.  Continue pieces that follow each
+  // other in the arena merge into the open descriptor up to kMergeMax bytes
+  // (exact, see kMergeMax); a restart piece opens a new descriptor with
+  // odd = 0; empty pieces are skipped (checksum.go:73-75; Checksum(empty, x)
+  // == x).  A piece is never split: its own > 128 KiB wrap is reproduced
+  // exactly by the kernel.
+  void chain(const Piece* p, size_t np, uint16_t initial) {
     bool first_desc = true;
     uint32_t parity = 0;  // odd flag carried to the next continue piece
     ns_pkt_desc cur{};
     bool open = false;
-    uint16_t initial = np ? p[0].initial : 0;
     auto close = [&]() {
       if (!open) return;
       desc.push_back(cur);
       open = false;
     };
-    for (uint32_t k = 0; k < np; ++k) {
-      const bool restart = (p[k].flags & NS_PIECE_RESTART) != 0;
+    for (size_t k = 0; k < np; ++k) {
       const uint64_t len = p[k].len;
-      if (restart) {
+      if (p[k].restart) {
         close();
         parity = 0;
-        if (len == 0) continue;  // Checksum(empty, x) == x, odd = false
-      } else if (len == 0) {
-        continue;  // empty views are skipped (checksum.go:73-75)
       }
+      if (len == 0) continue;
       const bool big = len > kMergeMax;
-      if (open && (big || cur.len + len > kMergeMax)) close();
+      const uint64_t at = bytes.append(p[k].p, len);
+      if (open && (big || cur.len + len > kMergeMax || at != cur.off + cur.len)) close();
       if (!open) {
-        cur.off = bytes.size();
+        cur.off = at;
         cur.len = 0;
         cur.initial = first_desc ? initial : 0;
         cur.flags = (uint16_t)((first_desc ? 0u : NS_DESC_CONT) | (parity ? NS_DESC_ODD : 0u));
         first_desc = false;
         open = true;
       }
-      bytes.append(p[k].data, len);
       cur.len += (uint32_t)len;
       parity ^= (uint32_t)(len & 1);
       if (big) close();
     }
     close();
-    if (first_desc) {  // no bytes at all: result = initial
+    if (first_desc) {  // no bytes at all: result = initial (checksum.go:97)
       ns_pkt_desc z{};
       z.initial = initial;
       desc.push_back(z);
@@ -695,25 +712,51 @@ struct Gather {
     result_at.push_back((uint32_t)desc.size() - 1);
   }
 
+  // ChecksumVVWithOffset's view walk over already clipped pieces: the first
+  // restarts, the rest continue (checksum.go:69-98).
+  void segment(const std::vector<std::pair<const uint8_t*, uint64_t>>& pieces, uint16_t initial) {
+    std::vector<Piece> ps;
+    ps.reserve(pieces.size());
+    for (size_t k = 0; k < pieces.size(); ++k) ps.push_back(Piece{pieces[k].first, pieces[k].second, k == 0});
+    chain(ps.data(), ps.size(), initial);
+  }
+
+  // Each view its own calculateChecksum with odd=false, chained
+  // (xsum = Checksum(v, xsum): udp/endpoint.go:811-813).
+  void restart_chain(const std::vector<std::pair<const uint8_t*, uint64_t>>& pieces, uint16_t initial) {
+    std::vector<Piece> ps;
+    ps.reserve(pieces.size());
+    for (const auto& pc : pieces) ps.push_back(Piece{pc.first, pc.second, true});
+    chain(ps.data(), ps.size(), initial);
+  }
+
   int run(uint16_t* out) {
     if (bytes.rc != NS_OK) return bytes.rc;
     std::vector<uint16_t> res(desc.size());
     int rc;
-    if (bytes.in_stage()) {
-      // Small: zero-copy from the leased staging, combined with concurrent calls.
+    const bool chained = any_cont(desc.data(), (uint32_t)desc.size());
+    if (bytes.adopted && !(zero_copy_enabled() && bytes.size() <= kStageBytes)) {
+      // A large caller stage: pinned already, so the DMA pipeline reads it.
+      std::lock_guard<std::mutex> lk(ctx->mu);
+      DeviceGuard g(ctx->device);
+      rc = run_host_batch(ctx, bytes.base(), bytes.size(), desc.data(), (uint32_t)desc.size(), res.data(),
+                          chained);
+    } else if (!bytes.in_big()) {
+      // Small: zero-copy from the leased (or the caller's) staging, combined
+      // with concurrent calls.
       SmallReq rq;
-      rq.dbytes = bytes.stage->dev;
+      rq.dbytes = bytes.adopted ? bytes.adopted->dev : bytes.stage->dev;
       rq.nbytes = bytes.size();
       rq.desc = desc.data();
       rq.ndesc = (uint32_t)desc.size();
       rq.res = res.data();
-      rq.chained = any_cont(desc.data(), (uint32_t)desc.size());
+      rq.chained = chained;
       rc = submit_small(ctx, &rq);
     } else {
       // Large: the bytes are in the pinned g_arena and ctx->mu is held.
       DeviceGuard g(ctx->device);
       rc = run_host_batch(ctx, ctx->g_arena.p, bytes.size(), desc.data(), (uint32_t)desc.size(), res.data(),
-                          any_cont(desc.data(), (uint32_t)desc.size()));
+                          chained);
     }
     if (rc != NS_OK) return rc;
     for (size_t q = 0; q < result_at.size(); ++q) out[q] = res[result_at[q]];
@@ -741,6 +784,297 @@ int clip_views(const ns_view* views, uint32_t nviews, int64_t off, int64_t size,
     s -= l;  // :91-94
     if (s == 0) break;
     o = 0;
+  }
+  return NS_OK;
+}
+
+// ---- tcpip.PacketBuffer batches (ns_csum_packet_buffers) -------------------
+// A packet as one byte stream: its Header bytes, then its Data views clipped
+// to Data.Size() (packet_buffer.go:25-50).  The host reads header fields from
+// it (plumbing: lengths, addresses' positions, protocol numbers) and cuts it
+// into the pieces of each reference call sequence; every sum is computed by
+// the kernel.
+struct PacketBytes {
+  std::vector<std::pair<const uint8_t*, uint64_t>> seg;  // non-empty segments in order
+  std::vector<uint64_t> at;                             // byte offset of each segment
+  uint64_t size = 0;
+  uint64_t hdr_len = 0;  // bytes [0, hdr_len) are the Header's (writable)
+
+  int init(const ns_pkt_buf& pk) {
+    if (pk.hdr_len && !pk.hdr) return NS_EINVAL;
+    hdr_len = pk.hdr_len;
+    if (pk.ndata && !pk.data) return NS_EINVAL;
+    add(pk.hdr, pk.hdr_len);
+    uint64_t left = pk.data_size;
+    for (uint32_t k = 0; k < pk.ndata && left; ++k) {
+      const uint64_t l = std::min<uint64_t>(pk.data[k].len, left);
+      if (l && !pk.data[k].data) return NS_EINVAL;
+      add(pk.data[k].data, l);
+      left -= l;
+    }
+    return NS_OK;
+  }
+  void add(const uint8_t* p, uint64_t l) {
+    if (!l) return;
+    seg.emplace_back(p, l);
+    at.push_back(size);
+    size += l;
+  }
+  // Segment holding byte k (k < size).
+  size_t seg_of(uint64_t k) const {
+    size_t lo = 0, hi = seg.size();
+    while (hi - lo > 1) {
+      const size_t mid = (lo + hi) / 2;
+      if (at[mid] <= k) lo = mid;
+      else hi = mid;
+    }
+    return lo;
+  }
+  // End of the segment (view) holding byte k: "Data.First()" after a trim to k.
+  uint64_t seg_end(uint64_t k) const {
+    if (k >= size) return size;
+    const size_t s = seg_of(k);
+    return at[s] + seg[s].second;
+  }
+  bool read(uint64_t k, uint8_t* out, uint64_t n) const {
+    if (k + n > size) return false;
+    while (n) {
+      const size_t s = seg_of(k);
+      const uint64_t o = k - at[s], l = std::min<uint64_t>(n, seg[s].second - o);
+      std::memcpy(out, seg[s].first + o, l);
+      out += l;
+      k += l;
+      n -= l;
+    }
+    return true;
+  }
+  uint8_t* mut(uint64_t k) const {  // address of byte k (a Header byte for stores)
+    const size_t s = seg_of(k);
+    return const_cast<uint8_t*>(seg[s].first) + (k - at[s]);
+  }
+  // Pieces covering [a, b), cut at view boundaries: the first `first_restart`,
+  // then each next view restarting (`per_view`, the `xsum = Checksum(v, xsum)`
+  // loops) or continuing (ChecksumVV's view walk).
+  void pieces(uint64_t a, uint64_t b, bool first_restart, bool per_view, std::vector<Piece>* out) const {
+    bool first = true;
+    while (a < b) {
+      const size_t s = seg_of(a);
+      const uint64_t o = a - at[s], l = std::min<uint64_t>(b - a, seg[s].second - o);
+      out->push_back(Piece{seg[s].first + o, l, first ? first_restart : per_view});
+      first = false;
+      a += l;
+    }
+  }
+};
+
+constexpr uint8_t kProtoICMPv4 = 1, kProtoTCP = 6, kProtoUDP = 17, kProtoICMPv6 = 58;
+
+// One packet's plan: up to two chains (network header, transport) and where
+// their results go.
+struct PacketPlan {
+  int net_chain = -1, tr_chain = -1;  // result indices in the Gather
+  uint8_t verdict = NS_PKB_UNCHECKED;
+  uint8_t kind = 0;                   // transport protocol for the verdict
+  uint64_t net_store = UINT64_MAX, tr_store = UINT64_MAX;  // FILL: field offsets
+  uint16_t field = 0;                 // VERIFY (ICMP): the received checksum field
+};
+
+// ChecksumCombine (checksum.go:104-107): folds the pseudo-header's length and
+// protocol words into the initial of the address piece.  The pseudo-header
+// pieces are all even-length restarts, so any grouping of them gives Go's
+// value (both are fold1 of the same total, and 0 only when all
+// pieces are 0).
+uint16_t combine(uint16_t a, uint16_t b) { return ns_csum_combine(a, b); }
+
+// The IP layer of a packet: header length, transport range and protocol, the
+// pseudo-header address bytes.  Returns false for what IPv4/IPv6 IsValid
+// (header/ipv4.go:280-296, ipv6.go:207-222) and HandlePacket reject.
+struct IpInfo {
+  bool v4 = false;
+  uint64_t hlen = 0, tbeg = 0, tend = 0, addr = 0, addr_len = 0;
+  uint8_t proto = 0;
+  bool fragment = false;
+};
+
+bool parse_ip(const PacketBytes& pb, bool rx, IpInfo* ip) {
+  uint8_t h[40];
+  if (pb.size < 1 || !pb.read(0, h, 1)) return false;
+  const uint8_t ver = h[0] >> 4;
+  // RX: the network header lies in Data.First() (packet_buffer.go:27-29);
+  // IsValid looks at that view alone.
+  const uint64_t first = pb.seg_end(0);
+  if (ver == 4) {
+    if ((rx && first < 20) || !pb.read(0, h, 20)) return false;
+    ip->v4 = true;
+    ip->hlen = (uint64_t)(h[0] & 0xF) * 4;
+    const uint64_t tlen = ((uint64_t)h[2] << 8) | h[3];
+    if (rx) {
+      if (ip->hlen < 20 || ip->hlen > tlen || tlen > pb.size || ip->hlen > first) return false;
+      ip->tend = tlen;  // Data.CapLength(tlen - hlen), ipv4.go:353
+    } else {
+      if (ip->hlen < 20 || ip->hlen > pb.size) return false;
+      ip->tend = pb.size;
+    }
+    ip->proto = h[9];
+    ip->addr = 12;
+    ip->addr_len = 8;
+    ip->fragment = (h[6] & 0x20) || (((h[6] & 0x1F) << 8) | h[7]);  // MF or a fragment offset
+  } else if (ver == 6) {
+    if ((rx && first < 40) || !pb.read(0, h, 40)) return false;
+    ip->hlen = 40;
+    const uint64_t plen = ((uint64_t)h[4] << 8) | h[5];
+    if (rx) {
+      if (plen > pb.size - 40) return false;
+      ip->tend = 40 + plen;  // Data.CapLength(PayloadLength), ipv6.go:177
+    } else {
+      ip->tend = pb.size;
+    }
+    ip->proto = h[6];
+    ip->addr = 8;
+    ip->addr_len = 32;
+  } else {
+    return false;
+  }
+  ip->tbeg = ip->hlen;
+  return true;
+}
+
+// Builds one packet's chains into g.  RX (NS_PKB_VERIFY) mirrors the receive
+// path's checks; TX (NS_PKB_FILL) the transmit path's sums (see the header).
+int plan_packet(Gather& g, const PacketBytes& pb, uint32_t op, PacketPlan* pp) {
+  IpInfo ip;
+  const bool rx = op == NS_PKB_VERIFY;
+  if (!parse_ip(pb, rx, &ip)) {
+    if (rx) {
+      pp->verdict = NS_PKB_MALFORMED;
+      return NS_OK;
+    }
+    return NS_EINVAL;
+  }
+  std::vector<Piece> ps;
+  const int nres = (int)g.result_at.size();
+  auto add_chain = [&](uint16_t init) {
+    g.chain(ps.data(), ps.size(), init);
+    ps.clear();
+    return (int)g.result_at.size() - 1;
+  };
+  if (ip.v4 && !rx) {
+    // addIPHeader: ip.SetChecksum(^ip.CalculateChecksum()) (ipv4.go:236),
+    // CalculateChecksum = Checksum(b[:HeaderLength()], 0) (ipv4.go:251-253)
+    pb.pieces(0, ip.hlen, true, false, &ps);
+    pp->net_chain = add_chain(0);
+    pp->net_store = 10;
+  } else if (ip.v4) {
+    // not verified on receive in the reference; reported for the caller
+    pb.pieces(0, ip.hlen, true, false, &ps);
+    pp->net_chain = add_chain(0);
+  }
+  (void)nres;
+  const uint64_t t0 = ip.tbeg, te = ip.tend, tl = te - t0;
+  const uint64_t first_end = std::min(pb.seg_end(t0), te);  // Data.First() after the IP trim
+  pp->kind = ip.proto;
+  auto pseudo = [&](uint8_t proto, uint64_t len, bool icmpv6) -> uint16_t {
+    // PseudoHeaderChecksum (checksum.go:112-122) / ICMPv6Checksum's
+    // pseudo-header (icmpv6.go:204-210): the addresses in place, the length
+    // and protocol words as the initial.
+    pb.pieces(ip.addr, ip.addr + ip.addr_len, true, false, &ps);
+    if (icmpv6) return combine(combine((uint16_t)(len >> 16), (uint16_t)len), proto);
+    return combine((uint16_t)len, proto);
+  };
+  if (rx) {
+    if (ip.fragment) return NS_OK;  // reassembled before the transport layer sees it
+    if (ip.proto == kProtoTCP) {
+      // stack.DeliverTransportPacket: First() >= TCPMinimumSize; segment.parse
+      // (segment.go:145-181): offset in [20, len(First())]
+      uint8_t h[13];
+      if (first_end - t0 < 20 || !pb.read(t0, h, 13)) {
+        pp->verdict = NS_PKB_MALFORMED;
+        return NS_OK;
+      }
+      const uint64_t off = (uint64_t)(h[12] >> 4) * 4;
+      if (off < 20 || off > first_end - t0) {
+        pp->verdict = NS_PKB_MALFORMED;
+        return NS_OK;
+      }
+      const uint16_t init = pseudo(kProtoTCP, (uint16_t)tl, false);  // :176 PseudoHeaderChecksum(data.Size())
+      pb.pieces(t0, t0 + off, true, false, &ps);                     // :177 h.CalculateChecksum(xsum)
+      pb.pieces(t0 + off, te, true, false, &ps);                     // :179 ChecksumVV(s.data, xsum)
+      pp->tr_chain = add_chain(init);
+      pp->verdict = NS_PKB_INVALID;  // decided from the result (:180)
+    } else if (ip.proto == kProtoICMPv4 && ip.v4) {
+      // handleICMP (network/ipv4/icmp.go:60-80): echo requests only
+      uint8_t h[4];
+      if (first_end - t0 < 8 || !pb.read(t0, h, 4)) {
+        pp->verdict = NS_PKB_MALFORMED;
+        return NS_OK;
+      }
+      if (h[0] != 8) return NS_OK;
+      pp->field = (uint16_t)((h[2] << 8) | h[3]);
+      // h.SetChecksum(0); ^ChecksumVV(pkt.Data, 0): bytes [2, 4) as zeros
+      pb.pieces(t0, t0 + 2, true, false, &ps);
+      pb.pieces(t0 + 4, te, false, false, &ps);
+      pp->tr_chain = add_chain(0);
+      pp->verdict = NS_PKB_INVALID;
+    } else if (ip.proto == kProtoICMPv6 && !ip.v4) {
+      // handleICMP (network/ipv6/icmp.go:62-84): h = the first view, payload
+      // = the other views, ICMPv6Checksum (header/icmpv6.go:202-221)
+      uint8_t h[4];
+      if (first_end - t0 < 4 || !pb.read(t0, h, 4)) {
+        pp->verdict = NS_PKB_MALFORMED;
+        return NS_OK;
+      }
+      pp->field = (uint16_t)((h[2] << 8) | h[3]);
+      const uint16_t init = pseudo(kProtoICMPv6, tl, true);
+      pb.pieces(first_end, te, true, true, &ps);        // for v in vv.Views(): Checksum(v, xsum)
+      pb.pieces(t0, t0 + 2, true, false, &ps);          // Checksum(h with h[2:4] = 0, xsum)
+      pb.pieces(t0 + 4, first_end, false, false, &ps);
+      pp->tr_chain = add_chain(init);
+      pp->verdict = NS_PKB_INVALID;
+    }
+    return NS_OK;
+  }
+  // TX: the transport header follows the IP header in Header; its checksum
+  // field must lie in Header (it is written there).
+  const uint64_t hdr_end = pb.hdr_len;
+  auto need = [&](uint64_t field_end) { return field_end <= hdr_end; };
+  if (ip.proto == kProtoTCP) {
+    uint8_t h[13];
+    if (!pb.read(t0, h, 13)) return NS_EINVAL;
+    const uint64_t thl = (uint64_t)(h[12] >> 4) * 4;
+    if (thl < 20 || t0 + thl > te || !need(t0 + 18)) return NS_EINVAL;
+    // buildTCPHdr (connect.go:653-663): PseudoHeaderChecksum(length),
+    // ChecksumVVWithOffset(payload), tcp.CalculateChecksum(xsum) = Checksum(tcp[:DataOffset])
+    const uint16_t init = pseudo(kProtoTCP, (uint16_t)tl, false);
+    pb.pieces(t0 + thl, te, true, false, &ps);
+    pb.pieces(t0, t0 + thl, true, false, &ps);
+    pp->tr_chain = add_chain(init);
+    pp->tr_store = t0 + 16;
+  } else if (ip.proto == kProtoUDP) {
+    if (t0 + 8 > te || !need(t0 + 8)) return NS_EINVAL;
+    // sendUDP (udp/endpoint.go:808-815): per-view restart, then the header
+    const uint16_t init = pseudo(kProtoUDP, (uint16_t)tl, false);
+    pb.pieces(t0 + 8, te, true, true, &ps);
+    pb.pieces(t0, t0 + 8, true, false, &ps);
+    pp->tr_chain = add_chain(init);
+    pp->tr_store = t0 + 6;
+  } else if (ip.proto == kProtoICMPv4 && ip.v4) {
+    // the echo reply (network/ipv4/icmp.go:96-100): pkt = the ICMP bytes in
+    // Header, SetChecksum(0), ^Checksum(pkt, ChecksumVV(vv, 0))
+    if (!need(t0 + 4)) return NS_EINVAL;
+    pb.pieces(hdr_end, te, true, false, &ps);
+    pb.pieces(t0, t0 + 2, true, false, &ps);
+    pb.pieces(t0 + 4, hdr_end, false, false, &ps);
+    pp->tr_chain = add_chain(0);
+    pp->tr_store = t0 + 2;
+  } else if (ip.proto == kProtoICMPv6 && !ip.v4) {
+    // ICMPv6Checksum(h = the ICMP bytes in Header, src, dst, Data) (icmpv6.go:202-221)
+    if (!need(t0 + 4)) return NS_EINVAL;
+    const uint16_t init = pseudo(kProtoICMPv6, tl, true);
+    pb.pieces(hdr_end, te, true, true, &ps);
+    pb.pieces(t0, t0 + 2, true, false, &ps);
+    pb.pieces(t0 + 4, hdr_end, false, false, &ps);
+    pp->tr_chain = add_chain(init);
+    pp->tr_store = t0 + 2;
   }
   return NS_OK;
 }
@@ -966,10 +1300,11 @@ int ns_csum_batch_host(ns_csum_ctx* ctx, const uint8_t* h_arena, uint64_t arena_
 int ns_csum_checksum(ns_csum_ctx* ctx, const uint8_t* buf, uint64_t len, uint16_t initial,
                      uint16_t* out) {
   if (!ctx || !out || (len && !buf) || len > 0xFFFFFFFFull) return NS_EINVAL;
-  Gather gt(ctx);
-  std::vector<std::pair<const uint8_t*, uint64_t>> pieces;
-  if (len) pieces.emplace_back(buf, len);
-  gt.restart_chain(pieces, initial);  // one piece, odd = false: checksum.go:52-55
+  SpanProbe pr;
+  pr.add(buf, len);
+  Gather gt(ctx, pr.stage(ctx));
+  const Piece pc{buf, len, true};  // one piece, odd = false: checksum.go:52-55
+  gt.chain(&pc, 1, initial);
   return gt.run(out);
 }
 
@@ -979,7 +1314,9 @@ int ns_csum_vv_with_offset(ns_csum_ctx* ctx, const ns_view* views, uint32_t nvie
   std::vector<std::pair<const uint8_t*, uint64_t>> pieces;
   int rc = clip_views(views, nviews, off, size, &pieces);
   if (rc != NS_OK) return rc;
-  Gather gt(ctx);
+  SpanProbe pr;
+  for (const auto& pc : pieces) pr.add(pc.first, pc.second);
+  Gather gt(ctx, pr.stage(ctx));
   gt.segment(pieces, initial);
   return gt.run(out);
 }
@@ -988,13 +1325,15 @@ int ns_csum_vv_batch(ns_csum_ctx* ctx, const ns_view* views, uint32_t nviews,
                      const ns_seg* segs, uint32_t nsegs, uint16_t* out) {
   if (!ctx || (nsegs && (!segs || !out)) || (nviews && !views)) return NS_EINVAL;
   if (nsegs == 0) return NS_OK;
-  Gather gt(ctx);
-  std::vector<std::pair<const uint8_t*, uint64_t>> pieces;
+  std::vector<std::vector<std::pair<const uint8_t*, uint64_t>>> clipped(nsegs);
+  SpanProbe pr;
   for (uint32_t q = 0; q < nsegs; ++q) {
-    int rc = clip_views(views, nviews, segs[q].off, segs[q].size, &pieces);
+    int rc = clip_views(views, nviews, segs[q].off, segs[q].size, &clipped[q]);
     if (rc != NS_OK) return rc;
-    gt.segment(pieces, segs[q].initial);
+    for (const auto& pc : clipped[q]) pr.add(pc.first, pc.second);
   }
+  Gather gt(ctx, pr.stage(ctx));
+  for (uint32_t q = 0; q < nsegs; ++q) gt.segment(clipped[q], segs[q].initial);
   return gt.run(out);
 }
 
@@ -1002,12 +1341,14 @@ int ns_csum_views_restart(ns_csum_ctx* ctx, const ns_view* views, uint32_t nview
                           uint16_t initial, uint16_t* out) {
   if (!ctx || !out || (nviews && !views)) return NS_EINVAL;
   std::vector<std::pair<const uint8_t*, uint64_t>> pieces;
+  SpanProbe pr;
   for (uint32_t k = 0; k < nviews; ++k) {
     if (views[k].len && !views[k].data) return NS_EINVAL;
     if (views[k].len > 0xFFFFFFFFull) return NS_EINVAL;
     pieces.emplace_back(views[k].data, views[k].len);
+    pr.add(views[k].data, views[k].len);
   }
-  Gather gt(ctx);
+  Gather gt(ctx, pr.stage(ctx));
   gt.restart_chain(pieces, initial);
   return gt.run(out);
 }
@@ -1016,19 +1357,25 @@ int ns_csum_chains(ns_csum_ctx* ctx, const ns_piece* pieces, uint32_t npieces, u
                    uint32_t nout) {
   if (!ctx || (npieces && !pieces)) return NS_EINVAL;
   uint32_t chains = 0;
+  SpanProbe pr;
   for (uint32_t k = 0; k < npieces; ++k) {
     if (pieces[k].len && !pieces[k].data) return NS_EINVAL;
     if (pieces[k].len > 0xFFFFFFFFull) return NS_EINVAL;
     if (pieces[k].flags & NS_PIECE_END) ++chains;
+    pr.add(pieces[k].data, pieces[k].len);
   }
   if (npieces && !(pieces[npieces - 1].flags & NS_PIECE_END)) return NS_EINVAL;  // unterminated
   if (chains > nout || (chains && !out)) return NS_EINVAL;
   if (chains == 0) return NS_OK;
-  Gather gt(ctx);
+  Gather gt(ctx, pr.stage(ctx));
+  std::vector<Piece> ps;
   uint32_t start = 0;
   for (uint32_t k = 0; k < npieces; ++k) {
+    ps.push_back(Piece{pieces[k].data, pieces[k].len, (pieces[k].flags & NS_PIECE_RESTART) != 0});
     if (pieces[k].flags & NS_PIECE_END) {
-      gt.chain(pieces + start, k + 1 - start);
+      ps[0].restart = true;  // a chain starts fresh: sum = initial, odd = false
+      gt.chain(ps.data(), ps.size(), pieces[start].initial);
+      ps.clear();
       start = k + 1;
     }
   }
@@ -1047,6 +1394,85 @@ int ns_csum_pseudo_header(ns_csum_ctx* ctx, uint32_t protocol, const uint8_t* sr
   Gather gt(ctx);
   gt.restart_chain(pieces, 0);
   return gt.run(out);
+}
+
+int ns_csum_stage_acquire(ns_csum_ctx* ctx, uint64_t bytes, uint8_t** base) {
+  if (!ctx || !base) return NS_EINVAL;
+  *base = nullptr;
+  int rc = NS_OK;
+  MappedPin* b = bytes <= kStageBytes ? lease_stage(ctx, &rc) : lease_big(ctx, bytes, &rc);
+  if (!b) return rc != NS_OK ? rc : NS_ENOMEM;
+  {
+    std::lock_guard<std::mutex> ql(ctx->qmu);
+    ctx->leased.push_back(b);
+  }
+  *base = b->p;
+  return NS_OK;
+}
+
+int ns_csum_stage_release(ns_csum_ctx* ctx, uint8_t* base) {
+  if (!ctx || !base) return NS_EINVAL;
+  std::lock_guard<std::mutex> ql(ctx->qmu);
+  for (size_t i = 0; i < ctx->leased.size(); ++i) {
+    MappedPin* b = ctx->leased[i];
+    if (b->p != base) continue;
+    ctx->leased.erase(ctx->leased.begin() + (long)i);
+    if (b->cap == kStageBytes) ctx->stage_free.push_back(b);
+    else ctx->big_free.push_back(b);
+    return NS_OK;
+  }
+  return NS_EINVAL;
+}
+
+int ns_csum_packet_buffers(ns_csum_ctx* ctx, const ns_pkt_buf* pkts, uint32_t n, uint32_t op,
+                           uint16_t* sums, uint8_t* verdict) {
+  if (!ctx || (n && !pkts) || (op != NS_PKB_VERIFY && op != NS_PKB_FILL)) return NS_EINVAL;
+  if (n == 0) return NS_OK;
+  std::vector<PacketBytes> pb(n);
+  SpanProbe pr;
+  for (uint32_t i = 0; i < n; ++i) {
+    const int rc = pb[i].init(pkts[i]);
+    if (rc != NS_OK) return rc;
+    for (const auto& sg : pb[i].seg) pr.add(sg.first, sg.second);
+  }
+  Gather gt(ctx, pr.stage(ctx));
+  std::vector<PacketPlan> plan(n);
+  for (uint32_t i = 0; i < n; ++i) {
+    const int rc = plan_packet(gt, pb[i], op, &plan[i]);
+    if (rc != NS_OK) return rc;
+  }
+  std::vector<uint16_t> res(gt.result_at.size());
+  if (!res.empty()) {
+    const int rc = gt.run(res.data());
+    if (rc != NS_OK) return rc;
+  }
+  for (uint32_t i = 0; i < n; ++i) {
+    PacketPlan& p = plan[i];
+    const uint16_t net = p.net_chain >= 0 ? res[(size_t)p.net_chain] : 0;
+    const uint16_t tr = p.tr_chain >= 0 ? res[(size_t)p.tr_chain] : 0;
+    if (sums) {
+      sums[2 * i] = net;
+      sums[2 * i + 1] = tr;
+    }
+    if (op == NS_PKB_FILL) {
+      // SetChecksum(^sum), big-endian, into the packet's Header
+      auto put = [&](uint64_t at, uint16_t v) {
+        uint8_t* q = pb[i].mut(at);
+        q[0] = (uint8_t)(v >> 8);
+        q[1] = (uint8_t)v;
+      };
+      if (p.net_store != UINT64_MAX) put(p.net_store, (uint16_t)~net);
+      if (p.tr_store != UINT64_MAX) put(p.tr_store, (uint16_t)~tr);
+    } else if (verdict) {
+      if (p.tr_chain >= 0) {
+        // TCP: xsum == 0xffff (segment.go:180); ICMP: ^sum == the received field
+        const bool ok = p.kind == kProtoTCP ? tr == 0xFFFF : (uint16_t)~tr == p.field;
+        p.verdict = ok ? NS_PKB_VALID : NS_PKB_INVALID;
+      }
+      verdict[i] = p.verdict;
+    }
+  }
+  return NS_OK;
 }
 
 int ns_csum_batch_multi(ns_csum_ctx* const* ctxs, uint32_t nctx, const uint8_t* h_arena,

@@ -160,51 +160,22 @@ __global__ __launch_bounds__(256) void calib_grp(const uint4* __restrict__ p, ui
 
 // The checksum kernel's own big-packet access shape with nothing else: a
 // non-persistent grid of 256-thread workgroups, each streaming one
-// contiguous tile of (256 / GB) * RPG runs; a run is `lpr` whole 128-B lines,
-// owned by a group of GB lanes, lane li loading chunks li, li + GB, ... with
-// UB nontemporal buffer_load_dwordx4 in flight (out-of-range slots read the
-// SRD size: zeros, no memory touched).  At GB = 8, UB = 16, lpr = 11 this is
-// csum_hyb's group loop on 1500-B packets (one 11-line body per group,
-// 32 groups per workgroup) minus the descriptors, the scan, the edge runs
-// and the sums: the read ceiling for that shape (bench.py
-// stream_calibration).  Reads bytes [0, tiles * tile) of p, < 4 GiB.
-template <int GB, int UB, int RPG>
-__global__ __launch_bounds__(256) void calib_tile(const uint4* __restrict__ p, uint64_t bytes, uint32_t lpr,
-                                                  uint32_t* __restrict__ out) {
-  constexpr int NG = 256 / GB;
-  const uint32_t nrec = (uint32_t)min<uint64_t>(bytes & ~15ull, 0xFFFF0000ull);
-  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, (int)nrec, 0x00020000);
-  const uint32_t g = threadIdx.x / GB, li = threadIdx.x % GB;
-  const uint32_t run_chunks = lpr * 8u;
-  const uint64_t tile = (uint64_t)NG * RPG * run_chunks * 16u;
-  uint32_t acc = 0;
-#pragma unroll
-  for (int r = 0; r < RPG; ++r) {
-    const uint64_t start = (uint64_t)blockIdx.x * tile + ((uint64_t)r * NG + g) * run_chunks * 16u;
-    uint4 v[UB];
-#pragma unroll
-    for (int j = 0; j < UB; ++j) {
-      const uint32_t c = li + (uint32_t)(GB * j);
-      const uint64_t o = start + 16u * c;
-      const uint32_t off = (c < run_chunks && o + 16 <= nrec) ? (uint32_t)o : nrec;
-      auto x = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (int)off, 0, 2);
-      v[j] = *reinterpret_cast<uint4*>(&x);
-    }
-#pragma unroll
-    for (int j = 0; j < UB; ++j) acc += v[j].x ^ v[j].y ^ v[j].z ^ v[j].w;
-  }
-  for (int d = 32; d > 0; d >>= 1) acc += __shfl_xor(acc, d, 64);
-  if ((threadIdx.x & 63) == 0) atomicAdd(&out[blockIdx.x % 16384u], acc);
-}
-
-// calib_tile with the knobs that could explain why the checksum kernel
-// outruns it: `sleep` s_sleep(8) rounds before the loads (the checksum
+// contiguous tile of 256 / GB runs; a run is `lpr` whole 128-B lines, owned
+// by a group of GB lanes, lane li loading chunks li, li + GB, ... with UB
+// nontemporal buffer_load_dwordx4 in flight (out-of-range slots read the SRD
+// size: zeros, no memory touched).  At GB = 8, UB = 16, lpr = 11 this is
+// csum_hyb's group loop on 1500-B packets (one 11-line body per group, 32
+// groups per workgroup) minus the descriptors, the scan, the edge runs and
+// the sums: the read ceiling for that shape (bench.py stream_calibration,
+// tools/calib_sweep.py).  Knobs that could explain a gap to the checksum
+// kernel: `sleep` s_sleep(8) rounds before the loads (the checksum
 // kernel's prologue staggers its workgroups), dynamic LDS per workgroup
 // (launch parameter: caps residency like the checksum kernel's 9.4 KB tile
 // state), EDGE = the first and last line of each run loaded with the default
 // policy instead of nt (the checksum kernel reads a packet's edge lines in
-// its lane runs), and a result store only on an impossible value instead of
-// per-wave atomics.
+// its lane runs).  The result is stored only on an impossible value: a first
+// version that ended every wave with a global atomicAdd streamed 4% slower
+// (6.85-6.88 vs 7.13-7.22 TB/s on cfg2's arenas, profiles/r02/calib_sweep.txt).
 template <int GB, int UB, bool EDGE>
 __global__ __launch_bounds__(256) void calib_tile_x(const uint4* __restrict__ p, uint64_t bytes, uint32_t lpr,
                                                     uint32_t sleep, uint32_t* __restrict__ out) {
@@ -508,34 +479,6 @@ int nsk_tune_launch(int v, const uint8_t* arena, uint64_t arena_bytes, const voi
 }
 
 // mode 0: coalesced grid-stride read; mode 4/8/16: per-lane runs of U chunks.
-// calib_tile over the first `bytes` of p (< 4 GiB) with runs of `lpr` lines:
-// mode 1 = <8, 16, 1 run per group>, 2 = <8, 16, 2>, 3 = <16, 8, 1>.  The
-// grid covers whole tiles only; *read_bytes = the bytes it reads.
-int nsk_calib_tile_launch(int mode, const void* p, uint64_t bytes, uint32_t lpr, uint32_t* out,
-                          uint64_t* read_bytes, void* stream) {
-  if (lpr == 0 || lpr > 16) return -1;
-  bytes = std::min<uint64_t>(bytes, 0xFFFF0000ull);
-  const auto* q = reinterpret_cast<const uint4*>(p);
-  hipStream_t s = (hipStream_t)stream;
-  const uint64_t run = (uint64_t)lpr * 128u;
-  uint64_t tile = 0;
-  switch (mode) {
-    case 1: tile = 32 * run; break;
-    case 2: tile = 64 * run; break;
-    case 3: tile = 16 * run; break;
-    default: return -1;
-  }
-  const uint32_t grid = (uint32_t)(bytes / tile);
-  if (grid == 0) return -1;
-  if (read_bytes) *read_bytes = (uint64_t)grid * tile;
-  switch (mode) {
-    case 1: hipLaunchKernelGGL((nsk::calib_tile<8, 16, 1>), dim3(grid), dim3(256), 0, s, q, bytes, lpr, out); break;
-    case 2: hipLaunchKernelGGL((nsk::calib_tile<8, 16, 2>), dim3(grid), dim3(256), 0, s, q, bytes, lpr, out); break;
-    case 3: hipLaunchKernelGGL((nsk::calib_tile<16, 8, 1>), dim3(grid), dim3(256), 0, s, q, bytes, lpr, out); break;
-  }
-  return hipGetLastError() == hipSuccess ? 0 : -5;
-}
-
 // calib_tile_x: mode 0 = <8, 16>, 1 = <8, 16, EDGE>, 2 = <8, 8>, 3 = <16, 8>.
 int nsk_calib_tile_x_launch(int mode, const void* p, uint64_t bytes, uint32_t lpr, uint32_t sleep,
                             uint32_t lds_bytes, uint32_t* out, uint64_t* read_bytes, void* stream) {

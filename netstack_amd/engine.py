@@ -186,6 +186,19 @@ class Engine:
               "ns_csum_chains")
         return out
 
+    # -- caller-filled staging (ns_csum_stage_acquire) -----------------------
+    def stage_acquire(self, nbytes: int) -> np.ndarray:
+        """A leased, pinned, device-mapped host buffer of >= nbytes as a
+        writable numpy array.  Pointers into it passed to the gather entry
+        points are read in place.  Return it with stage_release."""
+        base = ctypes.c_void_p()
+        check(lib().ns_csum_stage_acquire(self._h, nbytes, ctypes.byref(base)), "ns_csum_stage_acquire")
+        buf = (ctypes.c_uint8 * max(nbytes, 1)).from_address(base.value)
+        return np.frombuffer(buf, dtype=np.uint8)[:nbytes]
+
+    def stage_release(self, arr: np.ndarray) -> None:
+        check(lib().ns_csum_stage_release(self._h, arr.ctypes.data), "ns_csum_stage_release")
+
     def pseudo_header(self, protocol: int, src: bytes, dst: bytes, total_len: int) -> int:
         s, d = _u8(bytes(src)), _u8(bytes(dst))
         r = ctypes.c_uint16(0)

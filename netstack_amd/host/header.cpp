@@ -92,5 +92,45 @@ uint16_t ChecksumViews(const std::vector<buffer::View>& views, uint16_t initial)
   return r;
 }
 
+namespace {
+// ns_pkt_buf table over the packets' own bytes (Header's used part, Data's
+// views); `views` keeps each packet's ns_view array alive.
+std::vector<ns_pkt_buf> to_pkt_bufs(const std::vector<tcpip::PacketBuffer>& pkts,
+                                    std::vector<std::vector<ns_view>>* views) {
+  std::vector<ns_pkt_buf> t(pkts.size());
+  views->resize(pkts.size());
+  for (size_t i = 0; i < pkts.size(); ++i) {
+    const tcpip::PacketBuffer& p = pkts[i];
+    (*views)[i] = to_views(p.Data.Views());
+    const buffer::View hv = p.Header.View();
+    t[i].hdr = const_cast<uint8_t*>(hv.data());
+    t[i].hdr_len = hv.size();
+    t[i].data = (*views)[i].data();
+    t[i].ndata = (uint32_t)(*views)[i].size();
+    t[i].flags = 0;
+    t[i].data_size = p.Data.Size();
+  }
+  return t;
+}
+}  // namespace
+
+std::vector<uint8_t> VerifyPacketBuffers(const std::vector<tcpip::PacketBuffer>& pkts) {
+  std::vector<std::vector<ns_view>> keep;
+  std::vector<ns_pkt_buf> t = to_pkt_bufs(pkts, &keep);
+  std::vector<uint8_t> verdict(pkts.size());
+  if (!pkts.empty())
+    check(ns_csum_packet_buffers(Engine(), t.data(), (uint32_t)t.size(), NS_PKB_VERIFY, nullptr, verdict.data()),
+          "VerifyPacketBuffers");
+  return verdict;
+}
+
+void FillPacketBuffers(std::vector<tcpip::PacketBuffer>& pkts) {
+  std::vector<std::vector<ns_view>> keep;
+  std::vector<ns_pkt_buf> t = to_pkt_bufs(pkts, &keep);
+  if (!pkts.empty())
+    check(ns_csum_packet_buffers(Engine(), t.data(), (uint32_t)t.size(), NS_PKB_FILL, nullptr, nullptr),
+          "FillPacketBuffers");
+}
+
 }  // namespace header
 }  // namespace netstack

@@ -186,14 +186,62 @@ static void TestInvariants() {
   EXPECT_EQ(header::ChecksumCombine(0xffff, 1), 1, "combine");
 }
 
+static void TestPrependable() {  // prependable.go
+  netstack::buffer::Prependable p = netstack::buffer::NewPrependable(10);
+  EXPECT_EQ(p.UsedLength(), 0u, "prependable empty");
+  std::memcpy(p.Prepend(4), "tcp!", 4);
+  std::memcpy(p.Prepend(2), "ip", 2);
+  View v = p.View();
+  EXPECT_EQ(std::string((const char*)v.data(), v.size()) == "iptcp!", true, "prepend order");
+  EXPECT_EQ(p.AvailableLength(), 4u, "available");
+  EXPECT_EQ(p.Prepend(5) == nullptr, true, "prepend past the front is nil");
+  netstack::buffer::Prependable q = p.DeepCopy();
+  q.Data()[0] = 'x';
+  EXPECT_EQ(p.View()[0], 'i', "deep copy does not alias");
+  p.TrimBack(1);
+  EXPECT_EQ(p.UsedLength(), 5u, "trim back");
+}
+
+// A TCP/IPv4 packet filled by FillPacketBuffers verifies with
+// VerifyPacketBuffers; one corrupted payload byte fails (tcp_test.go:3246-3254).
+static void TestPacketBuffers() {
+  using netstack::tcpip::PacketBuffer;
+  std::vector<uint8_t> payload(2000);
+  for (size_t i = 0; i < payload.size(); ++i) payload[i] = (uint8_t)(i * 29 + 1);
+  const uint8_t ip[20] = {0x45, 0, 0x08, 0x04, 0, 7, 0, 0, 64, 6, 0, 0, 10, 0, 0, 1, 10, 0, 0, 2};  // 2052 B
+  uint8_t tcp[32] = {0, 80, 0x1f, 0x90, 0, 0, 0, 1, 0, 0, 0, 2, 0x80, 0x18, 0xff, 0xff};         // offset 32
+  PacketBuffer out;
+  out.Header = netstack::buffer::NewPrependable(64);
+  std::memcpy(out.Header.Prepend(sizeof tcp), tcp, sizeof tcp);
+  std::memcpy(out.Header.Prepend(sizeof ip), ip, sizeof ip);
+  out.Data = NewVectorisedView(payload.size(), {View(payload.data(), 777), View(payload.data() + 777, 1223)});
+  std::vector<PacketBuffer> tx = {out};
+  header::FillPacketBuffers(tx);
+  View h = tx[0].Header.View();
+  EXPECT_EQ(header::Checksum(h, 0) != 0, true, "filled");
+  std::vector<uint8_t> wire(h.data(), h.data() + h.size());
+  wire.insert(wire.end(), payload.begin(), payload.end());
+  EXPECT_EQ(header::Checksum(std::vector<uint8_t>(wire.begin(), wire.begin() + 20), 0), 0xffff, "ipv4 header");
+  std::vector<uint8_t> bad = wire;
+  bad[1500] ^= 0x20;
+  std::vector<PacketBuffer> rx(2);
+  rx[0].Data = NewVectorisedView(wire.size(), {View(wire.data(), 128), View(wire.data() + 128, wire.size() - 128)});
+  rx[1].Data = NewVectorisedView(bad.size(), {View(bad.data(), bad.size())});
+  std::vector<uint8_t> v = header::VerifyPacketBuffers(rx);
+  EXPECT_EQ(v[0], header::PacketChecksumValid, "tcp valid");
+  EXPECT_EQ(v[1], header::PacketChecksumInvalid, "tcp corrupted");
+}
+
 int main(int argc, char** argv) {
   const bool cpu_only = argc > 1 && std::strcmp(argv[1], "--cpu-only") == 0;
   TestCapLength();
   TestTrimFront();
   TestToView();
+  TestPrependable();
   if (!cpu_only) {
     TestChecksumVVWithOffset();
     TestInvariants();
+    TestPacketBuffers();
   }
   std::printf("%d checks, %d failed%s\n", g_run, g_fail, cpu_only ? " (cpu-only)" : "");
   return g_fail ? 1 : 0;

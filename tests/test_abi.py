@@ -43,7 +43,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_strerror():
     L = _lib.lib()
-    assert L.ns_csum_abi_version() == 2
+    assert L.ns_csum_abi_version() == _lib.ABI_VERSION == 3
     for code in (0, -1, -2, -3, -4, -5):
         assert L.ns_csum_strerror(code)
 
@@ -51,6 +51,7 @@ def test_abi_version_and_strerror():
 def test_struct_layouts_match_header():
     assert ctypes.sizeof(_lib.NsPktDesc) == 16
     assert ctypes.sizeof(_lib.NsSeg) == 24
+    assert ctypes.sizeof(_lib.NsPktBuf) == 40 and _lib.NsPktBuf.data_size.offset == 32
     assert engine.DESC_DTYPE.itemsize == 16
     assert W.DESC_DTYPE == engine.DESC_DTYPE
 
@@ -142,21 +143,74 @@ def test_product_kernels_never_spill_and_keep_occupancy():
             assert v["Occupancy"] >= 6, (k, v)
 
 
-def test_go_shim_keeps_reference_signatures_and_binds_declared_symbols():
-    """No Go toolchain here, so the cgo shim (go/header/checksum_hip.go) is
-    checked statically: it declares netstack's exported checksum functions
-    with the reference's exact signatures (tcpip/header/checksum.go:52, 61,
-    69, 104, 112) and calls only functions include/netstack_csum.h declares."""
-    src = open(os.path.join(ROOT, "go", "header", "checksum_hip.go")).read()
-    for sig in (
-        "func Checksum(buf []byte, initial uint16) uint16",
-        "func ChecksumVV(vv buffer.VectorisedView, initial uint16) uint16",
-        "func ChecksumVVWithOffset(vv buffer.VectorisedView, initial uint16, off int, size int) uint16",
-        "func ChecksumCombine(a, b uint16) uint16",
-        "func PseudoHeaderChecksum(protocol tcpip.TransportProtocolNumber, srcAddr tcpip.Address, "
-        "dstAddr tcpip.Address, totalLen uint16) uint16",
-    ):
-        assert sig in src, sig
-    assert "// +build hipcsum" in src and "package header" in src
-    called = set(re.findall(r"C\.(ns_csum_\w+)\(", src))
+GO_SHIM = os.path.join(ROOT, "go", "header", "checksum_batch_hip.go")
+# Identifiers tcpip/header/checksum.go declares (checksum.go:26-122): the shim
+# is added NEXT to that file, so it must declare none of them.
+CHECKSUM_GO_NAMES = {"calculateChecksum", "Checksum", "ChecksumVV", "ChecksumVVWithOffset", "ChecksumCombine",
+                     "PseudoHeaderChecksum"}
+# APIs newer than the reference's Go (<= 1.14: tcpip/time_unsafe.go:15-16).
+POST_GO114 = (r"runtime\.Pinner", r"unsafe\.Slice", r"unsafe\.Add", r"unsafe\.String", r"\bany\b",
+              r"\[\s*\w+\s+(any|comparable)\b", r"\bcomparable\b", r"strings\.Cut\b", r"atomic\.(Int|Uint|Bool|Pointer)\w*\b",
+              r"errors\.Join", r"\bmin\(", r"\bmax\(", r"\bclear\(", r"//go:build", r"\bio\.ReadAll\b",
+              r"os\.ReadFile", r"os\.WriteFile")
+
+
+def _go_code(src):
+    """The Go source without comments and string literals (a cgo preamble
+    comment stays out of the scan too)."""
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    src = re.sub(r"//[^\n]*", "", src)
+    return re.sub(r'"(?:[^"\\\n]|\\.)*"|`[^`]*`', '""', src)
+
+
+def test_go_shim_builds_with_the_reference_go_version_and_adds_only_new_names():
+    """No Go toolchain exists here, so the cgo shim is checked statically:
+    it uses no API newer than Go 1.14 (the reference's newest supported Go),
+    carries the hipcsum build tag in the pre-1.17 form, declares none of
+    checksum.go's names (it is added next to that file, which stays
+    untouched), passes C only functions include/netstack_csum.h declares,
+    and checks the library's ABI version before use."""
+    raw = open(GO_SHIM).read()
+    code = _go_code(raw)
+    for pat in POST_GO114:
+        assert not re.search(pat, code), pat
+    # build tag: a +build line before the package clause, then a blank line
+    assert "\n\n// +build hipcsum\n\npackage header\n" in raw
+    declared = set(re.findall(r"^func (?:\([^)]*\)\s*)?(\w+)\(", code, flags=re.M))
+    declared |= set(re.findall(r"^type (\w+)\b", code, flags=re.M))
+    declared |= set(re.findall(r"^\s*(\w+)\s*=", code[code.index("const ("):] if "const (" in code else "",
+                               flags=re.M))
+    assert declared and not (declared & CHECKSUM_GO_NAMES), declared & CHECKSUM_GO_NAMES
+    for name in ("ChecksumVVBatch", "ChecksumChains", "ChecksumBatch", "VerifyPacketBuffers", "FillPacketBuffers"):
+        assert name in declared, name
+    called = set(re.findall(r"C\.(ns_csum_\w+)\(", code))
     assert called and called <= declared_symbols(), called - declared_symbols()
+    assert "C.ns_csum_abi_version()" in code and "C.NS_CSUM_ABI_VERSION" in code
+    # #cgo paths come from CGO_CFLAGS / CGO_LDFLAGS, not ${SRCDIR}-relative guesses
+    assert "${SRCDIR}" not in raw
+
+
+def test_go_shim_names_do_not_collide_with_the_reference_package():
+    """Where the reference tree is present (this container), every top-level
+    identifier of its package header, in any file, differs from the shim's."""
+    hdr = "/root/reference/tcpip/header"
+    if not os.path.isdir(hdr):
+        pytest.skip("reference tree absent")
+    ref = set()
+    for fn in os.listdir(hdr):
+        if fn.endswith(".go") and not fn.endswith("_test.go"):
+            code = _go_code(open(os.path.join(hdr, fn)).read())
+            ref |= set(re.findall(r"^func (?:\([^)]*\)\s*)?(\w+)\(", code, flags=re.M))
+            ref |= set(re.findall(r"^type (\w+)\b", code, flags=re.M))
+            ref |= set(re.findall(r"^(?:var|const)\s+(\w+)", code, flags=re.M))
+            for blk in re.findall(r"^(?:const|var) \((.*?)^\)", code, flags=re.M | re.S):
+                ref |= set(re.findall(r"^\s*(\w+)", blk, flags=re.M))
+    assert CHECKSUM_GO_NAMES <= ref
+    code = _go_code(open(GO_SHIM).read())
+    mine = set(re.findall(r"^func (\w+)\(", code, flags=re.M)) | set(re.findall(r"^type (\w+)\b", code, flags=re.M))
+    mine |= set(re.findall(r"^var \((.*?)^\)", code, flags=re.M | re.S) and
+                re.findall(r"^\s+(\w+)\s", re.findall(r"^var \((.*?)^\)", code, flags=re.M | re.S)[0], flags=re.M))
+    for blk in re.findall(r"^const \((.*?)^\)", code, flags=re.M | re.S):
+        mine |= set(re.findall(r"^\s*(\w+)\s*=", blk, flags=re.M))
+    mine |= set(re.findall(r"^const (\w+)", code, flags=re.M))
+    assert mine and not (mine & ref), mine & ref

@@ -69,3 +69,45 @@ def test_view_aliases_backing_bytes():
     assert bytes(v) == b"cXef"
     n = NewView(3)
     assert bytes(n) == b"\0\0\0"
+
+
+def test_prependable_grows_backwards():
+    """buffer.Prependable (prependable.go): Prepend reserves bytes in front,
+    View is the used part and aliases the backing buffer, Prepend past the
+    available space returns nil; TrimBack; the FromView constructors."""
+    from netstack_amd.buffer import NewEmptyPrependableFromView, NewPrependable, NewPrependableFromView, View
+
+    p = NewPrependable(10)
+    assert p.UsedLength() == 0 and p.AvailableLength() == 10 and len(p.View()) == 0
+    p.Prepend(4)[:] = b"tcp!"
+    p.Prepend(2)[:] = b"ip"
+    assert bytes(p.View()) == b"iptcp!" and p.UsedLength() == 6 and p.AvailableLength() == 4
+    assert p.Prepend(5) is None and p.UsedLength() == 6
+    v = p.View()
+    v.memory[0] = ord("I")  # aliases the backing bytes
+    assert bytes(p.View()) == b"Iptcp!"
+    q = p.DeepCopy()
+    q.View().memory[0] = ord("x")
+    assert bytes(p.View()) == b"Iptcp!" and bytes(q.View()) == b"xptcp!"
+    p.TrimBack(1)
+    assert bytes(p.View()) == b"Iptcp"
+    full = NewPrependableFromView(View(bytearray(b"abc")))
+    assert full.UsedLength() == 3 and full.Prepend(1) is None
+    empty = NewEmptyPrependableFromView(View(bytearray(b"abc")))
+    assert empty.UsedLength() == 0 and empty.AvailableLength() == 3
+
+
+def test_packet_buffer_clone_copies_the_vv_not_the_bytes():
+    """PacketBuffer.Clone (packet_buffer.go:55-58): Data is a new
+    VectorisedView over the same bytes; trimming the clone leaves the
+    original's views alone."""
+    from netstack_amd.buffer import NewVectorisedView, View
+    from netstack_amd.packet import PacketBuffer
+
+    b = bytearray(b"0123456789")
+    pk = PacketBuffer(Data=NewVectorisedView(10, [View(b)]))
+    c = pk.Clone()
+    c.Data.TrimFront(3)
+    assert pk.Data.Size() == 10 and bytes(pk.Data.First()) == b"0123456789"
+    b[5] = ord("X")
+    assert bytes(c.Data.First()) == b"34X6789"

@@ -236,3 +236,46 @@ def test_run_fold_scan_algebra():
                 got.append(value(st))
             carry = comb(carry, agg)
         assert got == want, (trial, parts, heads.tolist())
+
+
+def test_packet_oracle_fill_then_verify(oracle_mod):
+    """oracle/packets.py: what the transmit restatement fills, the receive
+    restatement accepts (TCP over IPv4/IPv6, ICMPv4 echo), for payloads cut
+    into views; one flipped byte is rejected; the IPv4 header then sums to
+    0xffff (checker.go:51-53)."""
+    import struct
+
+    import packets as P
+
+    rng = np.random.default_rng(8)
+    for v6 in (False, True):
+        for plen in (0, 1, 2, 1460, 3001):
+            payload = bytes(rng.integers(0, 256, plen, dtype=np.uint8))
+            tcp = bytearray(20)
+            struct.pack_into(">HHIIBBH", tcp, 0, 1, 2, 3, 4, 0x50, 0x18, 5)
+            if v6:
+                ip = bytearray(40)
+                ip[0] = 0x60
+                struct.pack_into(">HBB", ip, 4, 20 + plen, 6, 64)
+                ip[8:40] = bytes(rng.integers(0, 256, 32, dtype=np.uint8))
+            else:
+                ip = bytearray(20)
+                struct.pack_into(">BBHHHBBH", ip, 0, 0x45, 0, 40 + plen, 7, 0, 64, 6, 0)
+                ip[12:20] = bytes(rng.integers(0, 256, 8, dtype=np.uint8))
+            cut = plen // 3
+            hdr, net, tr = P.fill(bytes(ip + tcp), [payload[:cut], payload[cut:]], plen)
+            wire = hdr + payload
+            v, n2, t2 = P.verify(b"", [wire[:100], wire[100:]], len(wire))
+            assert v == P.VALID and t2 == 0xFFFF
+            if not v6:
+                assert n2 == 0xFFFF
+            if plen:
+                bad = bytearray(wire)
+                bad[-1] ^= 0x10
+                assert P.verify(b"", [bytes(bad)], len(bad))[0] == P.INVALID
+    icmp = bytearray(8)
+    icmp[0] = 8
+    ip = bytearray(20)
+    struct.pack_into(">BBHHHBBH", ip, 0, 0x45, 0, 20 + 8 + 5, 7, 0, 64, 1, 0)
+    hdr, _, _ = P.fill(bytes(ip + icmp), [b"hello"], 5)
+    assert P.verify(b"", [hdr + b"hello"], len(hdr) + 5)[0] == P.VALID
