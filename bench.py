@@ -56,7 +56,11 @@ def parse():
                     help="distinct batches cycled per step (0 = auto: enough to exceed the 256 MiB MALL)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline time budget")
     ap.add_argument("--cpu-threads", type=int, default=0, help="threads for the multi-core CPU figure")
-    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU-baseline leg (rank 0)")
+    ap.add_argument("--no-parity", action="store_true", help="skip every rank's parity sample")
+    ap.add_argument("--dist-backend", default="auto", choices=("auto", "nccl", "gloo"),
+                    help="control-plane backend for N > 1 (auto: nccl = RCCL on a GPU box); gloo lets "
+                         "several ranks share one GPU (RCCL refuses two ranks on one device)")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     args = ap.parse_args()
     if args.steps < 1 or args.warmup < 0:
@@ -72,6 +76,7 @@ class Dist:
         import torch.distributed as dist
 
         self.dist = dist
+        self.backend = backend
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         self.local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -88,7 +93,7 @@ class Dist:
             return x
         import torch
 
-        t = torch.tensor([x], dtype=torch.float64, device=device)
+        t = torch.tensor([x], dtype=torch.float64, device=device if self.backend == "nccl" else "cpu")
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
         return float(t.item())
 
@@ -97,7 +102,7 @@ class Dist:
             return x
         import torch
 
-        t = torch.tensor([x], dtype=torch.float64, device=device)
+        t = torch.tensor([x], dtype=torch.float64, device=device if self.backend == "nccl" else "cpu")
         self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
         return float(t.item())
 
@@ -298,12 +303,15 @@ def main():
 
     from netstack_amd import Engine
 
-    dist = Dist("nccl" if torch.cuda.is_available() else "gloo")
+    backend = args.dist_backend if args.dist_backend != "auto" else ("nccl" if torch.cuda.is_available() else "gloo")
+    dist = Dist(backend)
     if dist.on and args.gpus != dist.world:
         print(f"warning: --gpus {args.gpus} != WORLD_SIZE {dist.world}", file=sys.stderr)
-    torch.cuda.set_device(dist.local)
-    dev = torch.device("cuda", dist.local)
-    eng = Engine(dist.local)
+    # one rank per GPU; more ranks than GPUs share them (gloo control plane)
+    ordinal = dist.local % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(ordinal)
+    dev = torch.device("cuda", ordinal)
+    eng = Engine(ordinal)
 
     cfg = args.config
     if cfg in (7, 8):
@@ -420,12 +428,20 @@ def main():
         "bad_descriptors": bad,
     }
 
+    if not args.no_parity:
+        # Every rank checks its own measured launch's results (the first and
+        # last 65,536 packets of its batch or shard) against the oracle; the
+        # count of failing ranks is all-reduced.
+        ps = parity_sample(batch, out)
+        failed = dist.sum(0.0 if ps["bit_exact"] else 1.0, dev)
+        ps["scope"] = ("sampled: the first and last 65,536 results of the measured launch on every rank; "
+                       "every result is checked at full size by pytest -m gpu")
+        ps["ranks_checked"] = dist.world
+        ps["ranks_failed"] = int(failed)
+        ps["bit_exact"] = ps["bit_exact"] and failed == 0
+        result["parity_sample"] = ps
     if dist.rank == 0 and not args.no_cpu:
-        # The CPU leg (rank 0): the oracle as the checker of the measured
-        # kernel's own results, then as the timed scalar baseline.
-        result["parity_sample"] = parity_sample(batch, out)
-        result["parity_sample"]["scope"] = ("sampled: 131,072 results of the measured launch; "
-                                            "every result is checked at full size by pytest -m gpu")
+        # The CPU leg (rank 0): the oracle timed as the scalar baseline.
         cb, _ = cpu_baseline(batch, args.cpu_seconds, 1)
         result["cpu_baseline"] = cb
         th = args.cpu_threads or min(16, os.cpu_count() or 1)
