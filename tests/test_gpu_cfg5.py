@@ -59,7 +59,7 @@ def test_cfg5_whole_batch_on_one_gpu(engine):
     import bench
 
     b = bench.rank_batch(5, 0, 1)
-    assert b.n == 8 << 20 and b.arena_bytes > 3 * (4 << 30)
+    assert b.n == 8 << 20 and b.arena_bytes > 2 * (4 << 30)
     got, want = _run_shard(engine, b)
     assert np.array_equal(got, want), int((got != want).sum())
 
