@@ -402,6 +402,73 @@ hipError_t launch_tp(const uint8_t* arena, uint64_t arena_bytes, const void* des
   return launch_hyb_tp<TP, GB, UB, 4, 2, 0, 2>(arena, arena_bytes, desc, n, out, nullptr, err, s, kBigChunks);
 }
 
+// ---- cfg3 decomposition probes (not checksum kernels) ----------------------
+// The product's small-packet grid (n / 256 workgroups of 256 threads) doing
+// nothing: the cost of dispatching and retiring the grid.
+__global__ __launch_bounds__(256) void probe_empty(uint16_t* __restrict__ out, uint32_t n) {
+  if (threadIdx.x == 1023u) out[0] = (uint16_t)n;  // never true: keeps the kernel non-trivial
+}
+hipError_t launch_probe_empty(const uint8_t*, uint64_t, const void*, uint32_t n, uint16_t* out,
+                              unsigned long long*, hipStream_t s) {
+  hipLaunchKernelGGL(probe_empty, dim3((n + 255) / 256), dim3(256), 0, s, out, n);
+  return hipGetLastError();
+}
+// The same grid reading each lane's descriptor and writing its initial as the
+// result: the descriptor stream and the result stream alone (18 B/packet).
+__global__ __launch_bounds__(256) void probe_desc(const uint4* __restrict__ desc, uint32_t n, uint16_t* __restrict__ out) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) out[i] = (uint16_t)desc[i].w;
+}
+hipError_t launch_probe_desc(const uint8_t*, uint64_t, const void* desc, uint32_t n, uint16_t* out,
+                             unsigned long long*, hipStream_t s) {
+  hipLaunchKernelGGL(probe_desc, dim3((n + 255) / 256), dim3(256), 0, s, reinterpret_cast<const uint4*>(desc), n, out);
+  return hipGetLastError();
+}
+// A pure streaming read of the arena (the payload bytes only) in the
+// big-packet shape (calib_tile_x <8, 16>, 16-line runs, nt).
+hipError_t launch_probe_read(const uint8_t* arena, uint64_t arena_bytes, const void*, uint32_t, uint16_t* out,
+                             unsigned long long*, hipStream_t s) {
+  const uint64_t tile = 32ull * 16 * 128;
+  hipLaunchKernelGGL((calib_tile_x<8, 16, false>), dim3((uint32_t)(arena_bytes / tile)), dim3(256), 1024, s,
+                     reinterpret_cast<const uint4*>(arena), arena_bytes, 16u, 0u, reinterpret_cast<uint32_t*>(out));
+  return hipGetLastError();
+}
+// The floor with PER packets per lane whose descriptors are all loaded first
+// (in flight together), then every payload: 1M x 64 B only.
+template <int PER>
+__global__ __launch_bounds__(256) void floor_desc_first(const uint8_t* __restrict__ arena, const uint4* __restrict__ desc,
+                                                       uint32_t n, uint16_t* __restrict__ out) {
+  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)arena, (short)0, (int)0x7FFFFFF0, 0x00020000);
+  uint4 raw[PER];
+#pragma unroll
+  for (int p = 0; p < PER; ++p) {
+    const uint64_t i = ((uint64_t)blockIdx.x * PER + p) * 256 + threadIdx.x;
+    raw[p] = i < n ? desc[i] : make_uint4(0, 0, 0, 0);
+  }
+  uint4 v[PER][4];
+#pragma unroll
+  for (int p = 0; p < PER; ++p) {
+    const uint32_t off = raw[p].x;  // the 64-B layout: off < 2 GiB
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[p][j] = bload(rsrc, raw[p].z ? off + 16u * j : 0x7FFFFFF0u);
+  }
+#pragma unroll
+  for (int p = 0; p < PER; ++p) {
+    const uint64_t i = ((uint64_t)blockIdx.x * PER + p) * 256 + threadIdx.x;
+    uint32_t T = 0, W = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) sad_chunk(v[p][j], T, W);
+    if (i < n) out[i] = (uint16_t)fold1((raw[p].w & 0xFFFFu) + s_of(T, W, (raw[p].w >> 16) & 1u));
+  }
+}
+template <int PER>
+hipError_t launch_floor_df(const uint8_t* arena, uint64_t, const void* desc, uint32_t n, uint16_t* out,
+                           unsigned long long*, hipStream_t s) {
+  hipLaunchKernelGGL((floor_desc_first<PER>), dim3((n + 256 * PER - 1) / (256 * PER)), dim3(256), 0, s, arena,
+                     reinterpret_cast<const uint4*>(desc), n, out);
+  return hipGetLastError();
+}
+
 typedef hipError_t (*launch_fn)(const uint8_t*, uint64_t, const void*, uint32_t, uint16_t*,
                                 unsigned long long*, hipStream_t);
 struct Variant {
@@ -458,6 +525,12 @@ static const Variant kVariants[] = {
     {"floor_wg128_p1", launch_floor_wg<128, 1>},
     {"floor_wg64_p1", launch_floor_wg<64, 1>},
     {"quad_d4", launch_quad},
+    {"probe_empty", launch_probe_empty},
+    {"probe_desc", launch_probe_desc},
+    {"probe_read", launch_probe_read},
+    {"floor_df1", launch_floor_df<1>},
+    {"floor_df2", launch_floor_df<2>},
+    {"floor_df4", launch_floor_df<4>},
 };
 
 }  // namespace nsk
