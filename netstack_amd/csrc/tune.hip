@@ -469,104 +469,124 @@ hipError_t launch_floor_df(const uint8_t* arena, uint64_t, const void* desc, uin
   return hipGetLastError();
 }
 
-// Quad-lane shape without descriptors (1M x 64 B layout only): load
-// instruction j of a wave reads packets 16 j .. 16 j + 15 of its 64 whole
+// Quad-lane shape without descriptors (1M x 64 B layout only): a wave owns
+// 64 K packets; load instruction j reads packets 16 j .. 16 j + 15 of them
 // (1 KiB contiguous: 8 whole lines), lane l taking chunk l % 4 of packet
-// 16 j + l / 4; quad DPP sums; results shuffled back to one per lane.
+// 16 j + l / 4; quad DPP sums; results shuffled back to one per lane per
+// round of 64.
+template <int K>
 __global__ __launch_bounds__(256) void floor_quad(const uint8_t* __restrict__ arena, const uint4* __restrict__ desc,
                                                   uint32_t n, uint16_t* __restrict__ out) {
   const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)arena, (short)0, (int)0x7FFFFFF0, 0x00020000);
   const uint32_t l = threadIdx.x & 63;
-  const uint64_t wb = (uint64_t)blockIdx.x * 256 + (threadIdx.x & ~63u);
-  uint4 v[4];
+  const uint64_t wb = ((uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 64 * K;
+  uint4 v[4 * K];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) v[j] = bload(rsrc, (uint32_t)((wb + 16 * j + (l >> 2)) * 64 + 16 * (l & 3)));
-  uint32_t r[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    uint32_t W = 0, T = 0;
-    acc_chunk<false>(v[j], T, W);
-    r[j] = group_sum<4>(W);
+  for (int j = 0; j < 4 * K; ++j) {
+    const uint64_t p = wb + 16 * j + (l >> 2);
+    v[j] = bload(rsrc, p < n ? (uint32_t)(p * 64 + 16 * (l & 3)) : 0x7FFFFFF0u);
   }
-  const uint32_t src = 4u * (l & 15u);
-  uint32_t mine = 0;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const uint32_t x = (uint32_t)__shfl((int)r[j], (int)src, 64);
-    mine = (l >> 4) == (uint32_t)j ? x : mine;
+  for (int k = 0; k < K; ++k) {
+    uint32_t r[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      uint32_t W = 0, T = 0;
+      acc_chunk<false>(v[4 * k + j], T, W);
+      r[j] = group_sum<4>(W);
+    }
+    const uint32_t src = 4u * (l & 15u);
+    uint32_t mine = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t x = (uint32_t)__shfl((int)r[j], (int)src, 64);
+      mine = (l >> 4) == (uint32_t)j ? x : mine;
+    }
+    const uint64_t i = wb + 64 * k + l;
+    if (i < n) out[i] = (uint16_t)fold1((desc[i].w & 0xFFFFu) + s_class(mine, 0u));
   }
-  const uint64_t i = wb + l;
-  if (i < n) out[i] = (uint16_t)fold1((desc[i].w & 0xFFFFu) + s_class(mine, 0u));
 }
+template <int K>
 hipError_t launch_floor_quad(const uint8_t* arena, uint64_t, const void* desc, uint32_t n, uint16_t* out,
                              unsigned long long*, hipStream_t s) {
-  hipLaunchKernelGGL(floor_quad, dim3((n + 255) / 256), dim3(256), 0, s, arena, reinterpret_cast<const uint4*>(desc),
-                     n, out);
+  hipLaunchKernelGGL((floor_quad<K>), dim3((n + 256 * K - 1) / (256 * K)), dim3(256), 0, s, arena,
+                     reinterpret_cast<const uint4*>(desc), n, out);
   return hipGetLastError();
 }
 
 // The general quad-lane direct path for packets spanning <= 4 chunks, any
-// alignment and length (a wave whose packets all qualify): descriptors read
-// coalesced, one per lane; each packet's geometry broadcast to its quad by
-// __shfl; lane l loads chunk l % 4 of packet 16 j + l / 4 (whole lines when
-// packets are dense) and masks only its own chunk's edge bytes; W-only sums,
-// quad DPP reduction, results shuffled back to one per lane and stored
-// coalesced.  Arenas below 4 GiB (one SRD).
+// alignment and length: a wave owns 64 K packets; descriptors read
+// coalesced, one per lane per round; each packet's geometry broadcast to its
+// quad by __shfl; lane l loads chunk l % 4 of packet 16 j + l / 4 (whole
+// lines when packets are dense) and masks only its own chunk's edge bytes;
+// W-only sums, quad DPP reduction, results shuffled back to one per lane and
+// stored coalesced.  Arenas below 4 GiB (one SRD).
+template <int K>
 __global__ __launch_bounds__(256) void quad_direct(const uint8_t* __restrict__ arena, uint64_t arena_bytes,
                                                    const uint4* __restrict__ desc, uint32_t n,
                                                    uint16_t* __restrict__ out, unsigned long long* __restrict__ err) {
   const uint32_t l = threadIdx.x & 63;
-  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-  const bool mine = i < n;
-  const uint4 raw = mine ? desc[i] : make_uint4(0, 0, 0, 0);
+  const uint64_t wb = ((uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 64 * K;
   const uint64_t arena_abs = (uint64_t)(uintptr_t)arena;
-  const Pkt d = decode(raw, mine, arena_abs, arena_bytes, err);
   const uint64_t base = arena_abs & ~15ull;
   const Srd r = make_srd(base, arena_abs + arena_bytes - base);
-  const uint32_t nch = chunks_of(d);
-  // geometry word: nch (3 bits) | lo (4) | hiex (5) | phase (1) | initial (16)
-  const uint32_t lo = (uint32_t)(d.A & 15u), hiex = d.len ? (uint32_t)(((d.A + d.len - 1) & 15u) + 1u) : 16u;
-  const uint32_t ph = (uint32_t)((d.A + d.odd) & 1u);
-  const uint32_t geo = min(nch, 7u) | (lo << 3) | (hiex << 7) | (ph << 12) | (d.init << 16);
-  const uint32_t first = (uint32_t)((d.A & ~15ull) - base);
-  const uint32_t c = l & 3u;
-  uint4 v[4];
-  uint32_t g[4];
+  uint4 raw[K];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int src = (int)(16 * j + (l >> 2));
-    g[j] = (uint32_t)__shfl((int)geo, src, 64);
-    const uint32_t f = (uint32_t)__shfl((int)first, src, 64);
+  for (int k = 0; k < K; ++k) raw[k] = wb + 64 * k + l < n ? desc[wb + 64 * k + l] : make_uint4(0, 0, 0, 0);
+  uint32_t geo[K], first[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const Pkt d = decode(raw[k], wb + 64 * k + l < n, arena_abs, arena_bytes, err);
+    const uint32_t nch = chunks_of(d);
+    // geometry word: nch (3 bits) | lo (4) | hiex (5) | phase (1) | initial (16)
+    const uint32_t lo = (uint32_t)(d.A & 15u), hiex = d.len ? (uint32_t)(((d.A + d.len - 1) & 15u) + 1u) : 16u;
+    const uint32_t ph = (uint32_t)((d.A + d.odd) & 1u);
+    geo[k] = min(nch, 7u) | (lo << 3) | (hiex << 7) | (ph << 12) | (d.init << 16);
+    first[k] = (uint32_t)((d.A & ~15ull) - base);
+  }
+  const uint32_t c = l & 3u;
+  uint4 v[4 * K];
+  uint32_t g[4 * K];
+#pragma unroll
+  for (int j = 0; j < 4 * K; ++j) {
+    const int src = (int)(16 * (j & 3) + (l >> 2));
+    g[j] = (uint32_t)__shfl((int)geo[j >> 2], src, 64);
+    const uint32_t f = (uint32_t)__shfl((int)first[j >> 2], src, 64);
     v[j] = bload(r.rsrc, c < (g[j] & 7u) ? f + 16u * c : r.oob);
   }
-  uint32_t res[4];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const uint32_t gj = g[j], nc = gj & 7u;
-    const int lo_b = c == 0 ? (int)((gj >> 3) & 15u) : 0;
-    const int hi_b = c + 1 == nc ? (int)((gj >> 7) & 31u) : 16;
-    uint4 w = v[j];
-    w.x &= bytes_below(hi_b) & ~bytes_below(lo_b);
-    w.y &= bytes_below(hi_b - 4) & ~bytes_below(lo_b - 4);
-    w.z &= bytes_below(hi_b - 8) & ~bytes_below(lo_b - 8);
-    w.w &= bytes_below(hi_b - 12) & ~bytes_below(lo_b - 12);
-    uint32_t T = 0, W = 0;
-    acc_chunk<false>(w, T, W);
-    W = group_sum<4>(W);
-    res[j] = fold1((gj >> 16) + s_class(W, (gj >> 12) & 1u));
-  }
-  const int src = (int)(4u * (l & 15u));
-  uint32_t me = 0;
+  for (int k = 0; k < K; ++k) {
+    uint32_t res[4];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const uint32_t x = (uint32_t)__shfl((int)res[j], src, 64);
-    me = (l >> 4) == (uint32_t)j ? x : me;
+    for (int jj = 0; jj < 4; ++jj) {
+      const int j = 4 * k + jj;
+      const uint32_t gj = g[j], nc = gj & 7u;
+      const int lo_b = c == 0 ? (int)((gj >> 3) & 15u) : 0;
+      const int hi_b = c + 1 == nc ? (int)((gj >> 7) & 31u) : 16;
+      uint4 w = v[j];
+      w.x &= bytes_below(hi_b) & ~bytes_below(lo_b);
+      w.y &= bytes_below(hi_b - 4) & ~bytes_below(lo_b - 4);
+      w.z &= bytes_below(hi_b - 8) & ~bytes_below(lo_b - 8);
+      w.w &= bytes_below(hi_b - 12) & ~bytes_below(lo_b - 12);
+      uint32_t T = 0, W = 0;
+      acc_chunk<false>(w, T, W);
+      W = group_sum<4>(W);
+      res[jj] = fold1((gj >> 16) + s_class(W, (gj >> 12) & 1u));
+    }
+    const int src = (int)(4u * (l & 15u));
+    uint32_t me = 0;
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      const uint32_t x = (uint32_t)__shfl((int)res[jj], src, 64);
+      me = (l >> 4) == (uint32_t)jj ? x : me;
+    }
+    if (wb + 64 * k + l < n) out[wb + 64 * k + l] = (uint16_t)me;
   }
-  if (mine) out[i] = (uint16_t)me;
 }
+template <int K>
 hipError_t launch_quad_direct(const uint8_t* arena, uint64_t arena_bytes, const void* desc, uint32_t n,
                               uint16_t* out, unsigned long long* err, hipStream_t s) {
-  hipLaunchKernelGGL(quad_direct, dim3((n + 255) / 256), dim3(256), 0, s, arena, arena_bytes,
+  hipLaunchKernelGGL((quad_direct<K>), dim3((n + 256 * K - 1) / (256 * K)), dim3(256), 0, s, arena, arena_bytes,
                      reinterpret_cast<const uint4*>(desc), n, out, err);
   return hipGetLastError();
 }
@@ -633,8 +653,12 @@ static const Variant kVariants[] = {
     {"floor_df1", launch_floor_df<1>},
     {"floor_df2", launch_floor_df<2>},
     {"floor_df4", launch_floor_df<4>},
-    {"floor_quad", launch_floor_quad},
-    {"quad_direct", launch_quad_direct},
+    {"floor_quad", launch_floor_quad<1>},
+    {"floor_quad2", launch_floor_quad<2>},
+    {"floor_quad4", launch_floor_quad<4>},
+    {"quad_direct", launch_quad_direct<1>},
+    {"quad_direct2", launch_quad_direct<2>},
+    {"quad_direct4", launch_quad_direct<4>},
 };
 
 }  // namespace nsk
