@@ -474,7 +474,7 @@ hipError_t launch_floor_df(const uint8_t* arena, uint64_t, const void* desc, uin
 // (1 KiB contiguous: 8 whole lines), lane l taking chunk l % 4 of packet
 // 16 j + l / 4; quad DPP sums; results shuffled back to one per lane per
 // round of 64.
-template <int K>
+template <int K, int AUX = 0>
 __global__ __launch_bounds__(256) void floor_quad(const uint8_t* __restrict__ arena, const uint4* __restrict__ desc,
                                                   uint32_t n, uint16_t* __restrict__ out) {
   const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)arena, (short)0, (int)0x7FFFFFF0, 0x00020000);
@@ -484,7 +484,7 @@ __global__ __launch_bounds__(256) void floor_quad(const uint8_t* __restrict__ ar
 #pragma unroll
   for (int j = 0; j < 4 * K; ++j) {
     const uint64_t p = wb + 16 * j + (l >> 2);
-    v[j] = bload(rsrc, p < n ? (uint32_t)(p * 64 + 16 * (l & 3)) : 0x7FFFFFF0u);
+    v[j] = bload<AUX>(rsrc, p < n ? (uint32_t)(p * 64 + 16 * (l & 3)) : 0x7FFFFFF0u);
   }
 #pragma unroll
   for (int k = 0; k < K; ++k) {
@@ -506,10 +506,10 @@ __global__ __launch_bounds__(256) void floor_quad(const uint8_t* __restrict__ ar
     if (i < n) out[i] = (uint16_t)fold1((desc[i].w & 0xFFFFu) + s_class(mine, 0u));
   }
 }
-template <int K>
+template <int K, int AUX = 0>
 hipError_t launch_floor_quad(const uint8_t* arena, uint64_t, const void* desc, uint32_t n, uint16_t* out,
                              unsigned long long*, hipStream_t s) {
-  hipLaunchKernelGGL((floor_quad<K>), dim3((n + 256 * K - 1) / (256 * K)), dim3(256), 0, s, arena,
+  hipLaunchKernelGGL((floor_quad<K, AUX>), dim3((n + 256 * K - 1) / (256 * K)), dim3(256), 0, s, arena,
                      reinterpret_cast<const uint4*>(desc), n, out);
   return hipGetLastError();
 }
@@ -521,7 +521,7 @@ hipError_t launch_floor_quad(const uint8_t* arena, uint64_t, const void* desc, u
 // lines when packets are dense) and masks only its own chunk's edge bytes;
 // W-only sums, quad DPP reduction, results shuffled back to one per lane and
 // stored coalesced.  Arenas below 4 GiB (one SRD).
-template <int K>
+template <int K, int AUX = 0>
 __global__ __launch_bounds__(256) void quad_direct(const uint8_t* __restrict__ arena, uint64_t arena_bytes,
                                                    const uint4* __restrict__ desc, uint32_t n,
                                                    uint16_t* __restrict__ out, unsigned long long* __restrict__ err) {
@@ -552,7 +552,7 @@ __global__ __launch_bounds__(256) void quad_direct(const uint8_t* __restrict__ a
     const int src = (int)(16 * (j & 3) + (l >> 2));
     g[j] = (uint32_t)__shfl((int)geo[j >> 2], src, 64);
     const uint32_t f = (uint32_t)__shfl((int)first[j >> 2], src, 64);
-    v[j] = bload(r.rsrc, c < (g[j] & 7u) ? f + 16u * c : r.oob);
+    v[j] = bload<AUX>(r.rsrc, c < (g[j] & 7u) ? f + 16u * c : r.oob);
   }
 #pragma unroll
   for (int k = 0; k < K; ++k) {
@@ -583,10 +583,10 @@ __global__ __launch_bounds__(256) void quad_direct(const uint8_t* __restrict__ a
     if (wb + 64 * k + l < n) out[wb + 64 * k + l] = (uint16_t)me;
   }
 }
-template <int K>
+template <int K, int AUX = 0>
 hipError_t launch_quad_direct(const uint8_t* arena, uint64_t arena_bytes, const void* desc, uint32_t n,
                               uint16_t* out, unsigned long long* err, hipStream_t s) {
-  hipLaunchKernelGGL((quad_direct<K>), dim3((n + 256 * K - 1) / (256 * K)), dim3(256), 0, s, arena, arena_bytes,
+  hipLaunchKernelGGL((quad_direct<K, AUX>), dim3((n + 256 * K - 1) / (256 * K)), dim3(256), 0, s, arena, arena_bytes,
                      reinterpret_cast<const uint4*>(desc), n, out, err);
   return hipGetLastError();
 }
@@ -659,6 +659,10 @@ static const Variant kVariants[] = {
     {"quad_direct", launch_quad_direct<1>},
     {"quad_direct2", launch_quad_direct<2>},
     {"quad_direct4", launch_quad_direct<4>},
+    {"floor_quad_nt", launch_floor_quad<1, 2>},
+    {"floor_quad2_nt", launch_floor_quad<2, 2>},
+    {"quad_direct_nt", launch_quad_direct<1, 2>},
+    {"quad_direct2_nt", launch_quad_direct<2, 2>},
 };
 
 }  // namespace nsk
