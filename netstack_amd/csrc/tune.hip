@@ -591,6 +591,91 @@ hipError_t launch_quad_direct(const uint8_t* arena, uint64_t arena_bytes, const 
   return hipGetLastError();
 }
 
+// quad_direct software-pipelined over K groups of 64 packets per wave: the
+// descriptors of group k + 2 and the payload of group k + 1 are in flight
+// while group k is summed and stored.
+template <int K, int AUX>
+__global__ __launch_bounds__(256) void quad_pipe(const uint8_t* __restrict__ arena, uint64_t arena_bytes,
+                                                 const uint4* __restrict__ desc, uint32_t n,
+                                                 uint16_t* __restrict__ out, unsigned long long* __restrict__ err) {
+  const uint32_t l = threadIdx.x & 63;
+  const uint64_t wb = ((uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 64 * K;
+  const uint64_t arena_abs = (uint64_t)(uintptr_t)arena;
+  const uint64_t base = arena_abs & ~15ull;
+  const Srd r = make_srd(base, arena_abs + arena_bytes - base);
+  const uint32_t c = l & 3u;
+  auto ldd = [&](int k) { const uint64_t i = wb + 64 * k + l; return i < n ? desc[i] : make_uint4(0, 0, 0, 0); };
+  auto issue = [&](uint4 raw, int k, uint4 (&v)[4], uint32_t (&g)[4]) {
+    const Pkt d = decode(raw, wb + 64 * k + l < n, arena_abs, arena_bytes, err);
+    const uint32_t nch = chunks_of(d);
+    const uint32_t lo = (uint32_t)(d.A & 15u), hiex = d.len ? (uint32_t)(((d.A + d.len - 1) & 15u) + 1u) : 16u;
+    const uint32_t ph = (uint32_t)((d.A + d.odd) & 1u);
+    const uint32_t geo = min(nch, 7u) | (lo << 3) | (hiex << 7) | (ph << 12) | (d.init << 16);
+    const uint32_t first = (uint32_t)((d.A & ~15ull) - base);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int src = (int)(16 * j + (l >> 2));
+      g[j] = (uint32_t)__shfl((int)geo, src, 64);
+      const uint32_t f = (uint32_t)__shfl((int)first, src, 64);
+      v[j] = bload<AUX>(r.rsrc, c < (g[j] & 7u) ? f + 16u * c : r.oob);
+    }
+  };
+  auto finish = [&](const uint4 (&v)[4], const uint32_t (&g)[4], int k) {
+    uint32_t res[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t gj = g[j], nc = gj & 7u;
+      const int lo_b = c == 0 ? (int)((gj >> 3) & 15u) : 0;
+      const int hi_b = c + 1 == nc ? (int)((gj >> 7) & 31u) : 16;
+      uint4 w = v[j];
+      w.x &= bytes_below(hi_b) & ~bytes_below(lo_b);
+      w.y &= bytes_below(hi_b - 4) & ~bytes_below(lo_b - 4);
+      w.z &= bytes_below(hi_b - 8) & ~bytes_below(lo_b - 8);
+      w.w &= bytes_below(hi_b - 12) & ~bytes_below(lo_b - 12);
+      uint32_t T = 0, W = 0;
+      acc_chunk<false>(w, T, W);
+      W = group_sum<4>(W);
+      res[j] = fold1((gj >> 16) + s_class(W, (gj >> 12) & 1u));
+    }
+    const int src = (int)(4u * (l & 15u));
+    uint32_t me = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t x = (uint32_t)__shfl((int)res[j], src, 64);
+      me = (l >> 4) == (uint32_t)j ? x : me;
+    }
+    if (wb + 64 * k + l < n) out[wb + 64 * k + l] = (uint16_t)me;
+  };
+  uint4 dn = ldd(0);
+  uint4 dn2 = K > 1 ? ldd(1) : make_uint4(0, 0, 0, 0);
+  uint4 va[4];
+  uint32_t ga[4];
+  issue(dn, 0, va, ga);
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    uint4 vb[4];
+    uint32_t gb[4];
+    if (k + 1 < K) {
+      const uint4 d3 = k + 2 < K ? ldd(k + 2) : make_uint4(0, 0, 0, 0);
+      issue(dn2, k + 1, vb, gb);
+      dn2 = d3;
+    }
+    finish(va, ga, k);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      va[j] = vb[j];
+      ga[j] = gb[j];
+    }
+  }
+}
+template <int K, int AUX>
+hipError_t launch_quad_pipe(const uint8_t* arena, uint64_t arena_bytes, const void* desc, uint32_t n,
+                            uint16_t* out, unsigned long long* err, hipStream_t s) {
+  hipLaunchKernelGGL((quad_pipe<K, AUX>), dim3((n + 256 * K - 1) / (256 * K)), dim3(256), 0, s, arena, arena_bytes,
+                     reinterpret_cast<const uint4*>(desc), n, out, err);
+  return hipGetLastError();
+}
+
 typedef hipError_t (*launch_fn)(const uint8_t*, uint64_t, const void*, uint32_t, uint16_t*,
                                 unsigned long long*, hipStream_t);
 struct Variant {
@@ -663,6 +748,10 @@ static const Variant kVariants[] = {
     {"floor_quad2_nt", launch_floor_quad<2, 2>},
     {"quad_direct_nt", launch_quad_direct<1, 2>},
     {"quad_direct2_nt", launch_quad_direct<2, 2>},
+    {"quad_direct4_nt", launch_quad_direct<4, 2>},
+    {"quad_pipe2_nt", launch_quad_pipe<2, 2>},
+    {"quad_pipe4_nt", launch_quad_pipe<4, 2>},
+    {"quad_pipe8_nt", launch_quad_pipe<8, 2>},
 };
 
 }  // namespace nsk
