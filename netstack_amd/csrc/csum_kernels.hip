@@ -360,6 +360,54 @@ __device__ __forceinline__ uint32_t direct_sum(const Srd& r, const PktInfo& p) {
   return s_class(W, p.ew >> 31);
 }
 
+// The quad-lane direct path: a wave whose 64 packets all span <= 4 chunks
+// (any alignment and length; every 16-B-aligned packet of <= 64 B).  Load
+// instruction j of the wave reads packets 16 j .. 16 j + 15 — lane l takes
+// chunk l % 4 of packet 16 j + l / 4, so dense packets give whole 128-B
+// lines per instruction and the loads are nontemporal (cdna: a line split
+// across instructions must stay cached).  Each packet's
+// geometry reaches its quad by __shfl, a lane masks only its own chunk's edge
+// bytes, a quad DPP sum gives the packet's W, and the W-only class values
+// (s_class) shuffle back to one per lane.  1M x 64 B: 14.7 vs 16.3 us for the
+// lane-per-packet path (tools/tune.py, profiles/r02/tune_cfg3_quad.log).
+__device__ __forceinline__ uint32_t quad_sum(const Srd& r, const PktInfo& p) {
+  const uint32_t l = threadIdx.x & 63u, c = l & 3u;
+  // nch (3 bits) | lo (4) | hiex (5) | phase (1)
+  const uint32_t geo = p.nch | ((p.ew & 15u) << 3) | (((p.ew >> 5) & 31u) << 7) | ((p.ew >> 31) << 12);
+  uint4 v[4];
+  uint32_t g[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int src = (int)(16 * j + (l >> 2));
+    g[j] = (uint32_t)__shfl((int)geo, src, 64);
+    const uint32_t f = (uint32_t)__shfl((int)p.first, src, 64);
+    v[j] = bload<2>(r.rsrc, c < (g[j] & 7u) ? f + 16u * c : r.oob);
+  }
+  uint32_t sv[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const uint32_t gj = g[j];
+    const int lo_b = c == 0 ? (int)((gj >> 3) & 15u) : 0;
+    const int hi_b = c + 1 == (gj & 7u) ? (int)((gj >> 7) & 31u) : 16;
+    uint4 w = v[j];
+    w.x &= bytes_below(hi_b) & ~bytes_below(lo_b);
+    w.y &= bytes_below(hi_b - 4) & ~bytes_below(lo_b - 4);
+    w.z &= bytes_below(hi_b - 8) & ~bytes_below(lo_b - 8);
+    w.w &= bytes_below(hi_b - 12) & ~bytes_below(lo_b - 12);
+    uint32_t T = 0, W = 0;
+    acc_chunk<false>(w, T, W);
+    sv[j] = s_class(group_sum<4>(W), (gj >> 12) & 1u);
+  }
+  const int src = (int)(4u * (l & 15u));
+  uint32_t me = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const uint32_t x = (uint32_t)__shfl((int)sv[j], src, 64);
+    me = (l >> 4) == (uint32_t)j ? x : me;
+  }
+  return me;
+}
+
 // One tile through the scan path (thread t holds packet p of global index i).
 // GL = 64-bit global loads (tile span >= 4 GiB) instead of the window SRD.
 // Every thread of the block must call it.
@@ -651,7 +699,10 @@ __global__ __launch_bounds__(WG) void csum_hyb(
     const Srd r = make_srd(w.base, w.span);
     const PktInfo p = pkt_info(d, w.base);
     if (UD > 0 && w.small) {
-      const uint32_t s = direct_sum<UD ? UD : 1>(r, p);
+      // per wave: the quad-lane shape when every packet spans <= 4 chunks
+      // (a full tile: lane t holds packet blockIdx.x * WG + t), else one lane
+      // per packet
+      const uint32_t s = (TP == WG && __all(p.nch <= 4u)) ? quad_sum(r, p) : direct_sum<UD ? UD : 1>(r, p);
       finish_tile<WG, CH>(L, s, d, mine, i, n, out, partial, store);
       return;
     }

@@ -169,6 +169,58 @@ def test_small_unaligned_packets(engine, maxlen):
     assert np.array_equal(dev_batch(engine, arena, d[perm]), want[perm])
 
 
+@pytest.mark.parametrize("chained,store", [(False, False), (True, False), (False, True), (True, True)])
+def test_quad_lane_direct_path_per_wave(engine, chained, store):
+    """The small-packet tiles' two direct shapes, chosen per wave: waves whose
+    64 packets all span <= 4 chunks take the quad-lane path (nontemporal
+    whole-line loads, quad sums), the others one lane per packet.  Packets of
+    0-64 B at every start alignment, odd carry-ins, empties, one 5-chunk
+    packet in some waves, chained runs and in-packet stores; all against the
+    oracle."""
+    import oracle as O
+    from netstack_amd import workloads as W
+
+    torch = _torch()
+    rng = np.random.default_rng(1234 + 2 * chained + store)
+    n = 256 * 24 + 77
+    lengths = rng.integers(0, 65, n).astype(np.uint32)
+    starts = rng.integers(0, 16, n)
+    # a packet spanning 5 chunks in every third wave
+    for wv in range(0, n // 64, 3):
+        lengths[wv * 64 + int(rng.integers(0, 64))] = 70
+    flags = rng.integers(0, 2, n).astype(np.uint16)
+    if chained:
+        flags |= (2 * (rng.random(n) < 0.4)).astype(np.uint16)
+    # packets placed at random 16-B phases with gaps
+    off = np.zeros(n, np.uint64)
+    pos = 3
+    for k in range(n):
+        pos = (pos // 16) * 16 + int(starts[k])
+        off[k] = pos
+        pos += int(lengths[k]) + int(rng.integers(0, 40))
+    d = np.zeros(n, dtype=O.DESC_DTYPE)
+    d["off"], d["len"], d["flags"] = off, lengths, flags
+    d["initial"] = rng.integers(0, 65536, n)
+    arena = rng.integers(0, 256, pos + 64, dtype=np.uint8)
+    arena[int(off[7]):int(off[7]) + int(lengths[7])] = 0
+    if store:
+        st = np.flatnonzero((rng.random(n) < 0.3) & (lengths >= 2))
+        at = (rng.random(st.size) * (lengths[st] - 1)).astype(np.uint16)
+        d["flags"][st] |= (0x4 | (at << 4)).astype(np.uint16)
+    want, bad = O.c_batch(arena, d, chained=chained)
+    assert bad == 0
+    dt = torch.from_numpy(arena).cuda()
+    desc = torch.from_numpy(d.view(np.uint8).copy()).cuda()
+    out = engine.batch_tensors(dt, desc, chained=chained, store=store)
+    torch.cuda.synchronize()
+    assert engine.sync() == 0
+    got = out.cpu().numpy().view(np.uint16)
+    assert np.array_equal(got, want), np.flatnonzero(got != want)[:8]
+    if store:
+        expect, dropped = O.apply_stores(arena, d, want)
+        assert dropped == 0 and np.array_equal(dt.cpu().numpy(), expect)
+
+
 @pytest.mark.slow
 def test_arena_over_4gib_windowed_and_scattered(engine):
     """A 4.5 GiB arena (288 GB HBM makes such batches natural): sorted tiles
