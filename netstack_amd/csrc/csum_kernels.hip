@@ -692,7 +692,29 @@ __global__ __launch_bounds__(WG) void csum_hyb(
   } else {
     w.base = arena_abs & ~15ull;
     w.span = arena_abs + arena_bytes - w.base;
-    w.small = UD > 0 ? __syncthreads_and(chunks_of(d) <= (uint32_t)UD) != 0 : false;
+    w.small = false;
+  }
+
+  if constexpr (!WIN && UD > 0) {
+    // Small-packet tiles, decided per wave: a wave whose packets all span
+    // <= UD chunks sums them directly and finishes at once — the quad-lane
+    // shape when all span <= 4 (a full tile: lane t holds packet
+    // blockIdx.x * WG + t), else one lane per packet — without waiting for
+    // the other waves (a block-wide vote before the loads held every wave
+    // of the tile until the slowest descriptor arrived).  Only if some wave
+    // of the tile has a longer packet does the block run the scan path,
+    // the finished waves taking part with no packets.
+    const Srd r = make_srd(w.base, w.span);
+    const PktInfo p = pkt_info(d, w.base);
+    const bool small = __all(p.nch <= (uint32_t)UD) != 0;
+    if (small) {
+      const uint32_t s = (TP == WG && __all(p.nch <= 4u)) ? quad_sum(r, p) : direct_sum<UD ? UD : 1>(r, p);
+      finish_tile<WG, CH>(L, s, d, mine, i, n, out, partial, store);
+    }
+    if (!__syncthreads_or(!small)) return;
+    const uint32_t s = hyb_scan_tile<WG, TP, GB, UB, US, AUXB, false, SU>(L, r, small ? PktInfo{} : p, big_chunks);
+    if (!small) finish_tile<WG, CH>(L, s, d, mine, i, n, out, partial, store);
+    return;
   }
 
   if (!WIN || w.span + 64 < kMaxSrdBytes) {
