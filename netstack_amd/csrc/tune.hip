@@ -474,12 +474,12 @@ hipError_t launch_floor_df(const uint8_t* arena, uint64_t, const void* desc, uin
 // (1 KiB contiguous: 8 whole lines), lane l taking chunk l % 4 of packet
 // 16 j + l / 4; quad DPP sums; results shuffled back to one per lane per
 // round of 64.
-template <int K, int AUX = 0>
-__global__ __launch_bounds__(256) void floor_quad(const uint8_t* __restrict__ arena, const uint4* __restrict__ desc,
+template <int K, int AUX = 0, int WGQ = 256>
+__global__ __launch_bounds__(WGQ) void floor_quad(const uint8_t* __restrict__ arena, const uint4* __restrict__ desc,
                                                   uint32_t n, uint16_t* __restrict__ out) {
   const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)arena, (short)0, (int)0x7FFFFFF0, 0x00020000);
   const uint32_t l = threadIdx.x & 63;
-  const uint64_t wb = ((uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 64 * K;
+  const uint64_t wb = ((uint64_t)blockIdx.x * (WGQ / 64) + (threadIdx.x >> 6)) * 64 * K;
   uint4 v[4 * K];
 #pragma unroll
   for (int j = 0; j < 4 * K; ++j) {
@@ -506,10 +506,10 @@ __global__ __launch_bounds__(256) void floor_quad(const uint8_t* __restrict__ ar
     if (i < n) out[i] = (uint16_t)fold1((desc[i].w & 0xFFFFu) + s_class(mine, 0u));
   }
 }
-template <int K, int AUX = 0>
+template <int K, int AUX = 0, int WGQ = 256>
 hipError_t launch_floor_quad(const uint8_t* arena, uint64_t, const void* desc, uint32_t n, uint16_t* out,
                              unsigned long long*, hipStream_t s) {
-  hipLaunchKernelGGL((floor_quad<K, AUX>), dim3((n + 256 * K - 1) / (256 * K)), dim3(256), 0, s, arena,
+  hipLaunchKernelGGL((floor_quad<K, AUX, WGQ>), dim3((n + WGQ * K - 1) / (WGQ * K)), dim3(WGQ), 0, s, arena,
                      reinterpret_cast<const uint4*>(desc), n, out);
   return hipGetLastError();
 }
@@ -521,12 +521,12 @@ hipError_t launch_floor_quad(const uint8_t* arena, uint64_t, const void* desc, u
 // lines when packets are dense) and masks only its own chunk's edge bytes;
 // W-only sums, quad DPP reduction, results shuffled back to one per lane and
 // stored coalesced.  Arenas below 4 GiB (one SRD).
-template <int K, int AUX = 0>
-__global__ __launch_bounds__(256) void quad_direct(const uint8_t* __restrict__ arena, uint64_t arena_bytes,
+template <int K, int AUX = 0, int WGQ = 256>
+__global__ __launch_bounds__(WGQ) void quad_direct(const uint8_t* __restrict__ arena, uint64_t arena_bytes,
                                                    const uint4* __restrict__ desc, uint32_t n,
                                                    uint16_t* __restrict__ out, unsigned long long* __restrict__ err) {
   const uint32_t l = threadIdx.x & 63;
-  const uint64_t wb = ((uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 64 * K;
+  const uint64_t wb = ((uint64_t)blockIdx.x * (WGQ / 64) + (threadIdx.x >> 6)) * 64 * K;
   const uint64_t arena_abs = (uint64_t)(uintptr_t)arena;
   const uint64_t base = arena_abs & ~15ull;
   const Srd r = make_srd(base, arena_abs + arena_bytes - base);
@@ -583,10 +583,10 @@ __global__ __launch_bounds__(256) void quad_direct(const uint8_t* __restrict__ a
     if (wb + 64 * k + l < n) out[wb + 64 * k + l] = (uint16_t)me;
   }
 }
-template <int K, int AUX = 0>
+template <int K, int AUX = 0, int WGQ = 256>
 hipError_t launch_quad_direct(const uint8_t* arena, uint64_t arena_bytes, const void* desc, uint32_t n,
                               uint16_t* out, unsigned long long* err, hipStream_t s) {
-  hipLaunchKernelGGL((quad_direct<K, AUX>), dim3((n + 256 * K - 1) / (256 * K)), dim3(256), 0, s, arena, arena_bytes,
+  hipLaunchKernelGGL((quad_direct<K, AUX, WGQ>), dim3((n + WGQ * K - 1) / (WGQ * K)), dim3(WGQ), 0, s, arena, arena_bytes,
                      reinterpret_cast<const uint4*>(desc), n, out, err);
   return hipGetLastError();
 }
@@ -750,6 +750,12 @@ static const Variant kVariants[] = {
     {"quad_direct2_nt", launch_quad_direct<2, 2>},
     {"quad_direct4_nt", launch_quad_direct<4, 2>},
     {"quad_pipe2_nt", launch_quad_pipe<2, 2>},
+    {"quad_direct_nt_wg512", launch_quad_direct<1, 2, 512>},
+    {"quad_direct_nt_wg1024", launch_quad_direct<1, 2, 1024>},
+    {"quad_direct_nt_wg128", launch_quad_direct<1, 2, 128>},
+    {"quad_direct_nt_wg64", launch_quad_direct<1, 2, 64>},
+    {"floor_quad_nt_wg1024", launch_floor_quad<1, 2, 1024>},
+    {"floor_quad_nt_wg64", launch_floor_quad<1, 2, 64>},
     {"quad_pipe4_nt", launch_quad_pipe<4, 2>},
     {"quad_pipe8_nt", launch_quad_pipe<8, 2>},
 };
