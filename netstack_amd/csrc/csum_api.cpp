@@ -19,6 +19,7 @@
 #include <vector>
 
 #include "csum_kernels.h"
+#include "host_logic.h"
 #include "netstack_csum.h"
 
 static_assert(sizeof(ns_pkt_desc) == 16, "ns_pkt_desc must be 16 bytes");
@@ -28,12 +29,10 @@ static_assert(sizeof(ns_pkt_buf) == 40, "ns_pkt_buf layout");
 
 namespace {
 
-// Largest run of VectorisedView pieces that may be merged into ONE descriptor
-// and still equal Go's per-view chain (checksum.go:89): with initial <= 0xFFFF
-// and L <= 131072 bytes the uint32 accumulator cannot wrap, neither in the
-// chain nor in the merged sum (65535 * (1 + 65536) = 2^32 - 1).  A single
-// piece is never split (its own wrap is reproduced exactly by the kernel).
-constexpr uint64_t kMergeMax = 131072;
+using nsh::any_cont;
+using nsh::clip_views;
+using nsh::Piece;
+
 constexpr uint64_t kDefaultStaging = 64ull << 20;
 // Small host calls (bytes up to kStageBytes, below) run zero-copy: the kernel
 // reads the table and the bytes from mapped pinned host memory over PCIe and
@@ -197,12 +196,10 @@ struct ns_csum_ctx {
   PinBuf<uint16_t> h_out[2];
   // zero-copy pass buffer for small calls: [table | results]
   MappedPin z_buf;
-  // flat combining of concurrent small calls (submit_small) and the pool of
-  // mapped staging buffers they gather into; guarded by qmu
+  // flat combining of concurrent small calls (nsh::FlatCombiner)
+  nsh::FlatCombiner<SmallReq> combiner{kPassTableBytes};
+  // the pool of mapped staging buffers small calls gather into; guarded by qmu
   std::mutex qmu;
-  std::condition_variable qcv;
-  std::vector<SmallReq*> pending;
-  bool combining = false;
   std::vector<MappedPin*> stage_free;
   std::vector<MappedPin*> stage_all;
   std::vector<MappedPin*> big_free;  // pooled caller stages above kStageBytes
@@ -225,12 +222,6 @@ struct DeviceGuard {
     if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
   }
 };
-
-bool any_cont(const ns_pkt_desc* d, uint32_t n) {
-  for (uint32_t i = 0; i < n; ++i)
-    if (d[i].flags & NS_DESC_CONT) return true;
-  return false;
-}
 
 // Validates a host table against its arena and returns the byte span its
 // non-empty descriptors cover ([0, 0) if none).
@@ -340,69 +331,18 @@ void return_stage(ns_csum_ctx* ctx, MappedPin* b) {
   ctx->stage_free.push_back(b);
 }
 
-// Flat combining of concurrent small synchronous calls.  netstack calls the
-// checksum from every endpoint's goroutine at once; one
-// launch + wait costs ~15-20 us whatever its size, so serialising calls on
-// the context would cap a context at ~50K calls/s.  Instead a caller queues
-// its request; if no pass is running it becomes the combiner: it takes every
-// queued request (while their tables fit kPassTableBytes), runs them as ONE
-// zero-copy pass, hands out the results and repeats while requests remain.
-// Each caller has already gathered its bytes into its own leased staging, so
-// the only serial host work per request is copying its descriptors.
-// Everyone else sleeps until its request is done.  Results are identical to
-// separate calls (descriptors are independent; chains never cross requests).
+// Flat combining of concurrent small synchronous calls (nsh::FlatCombiner):
+// concurrent callers' requests run as one zero-copy pass.  Each caller has
+// already gathered its bytes into its own leased staging, so the only serial
+// host work per request is copying its descriptors.  Results are identical
+// to separate calls (descriptors are independent; chains never cross
+// requests).
 int submit_small(ns_csum_ctx* ctx, SmallReq* req) {
-  // A combiner keeps serving queued requests after its own is done, up to
-  // kMaxPasses passes, so back-to-back passes do not wait for a sleeping
-  // thread to wake up and take the role over.
-  constexpr int kMaxPasses = 8;
-  std::unique_lock<std::mutex> ql(ctx->qmu);
-  ctx->pending.push_back(req);
-  while (!req->done.load(std::memory_order_acquire)) {
-    if (ctx->combining) {
-      // Spin briefly (a pass is ~20-60 us) before sleeping: a woken thread
-      // costs more than the spin.
-      ql.unlock();
-      const auto t0 = std::chrono::steady_clock::now();
-      while (!req->done.load(std::memory_order_acquire) &&
-             std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(50))
-        std::this_thread::yield();
-      ql.lock();
-      if (req->done.load(std::memory_order_acquire)) break;
-      if (ctx->combining) ctx->qcv.wait(ql);
-      continue;
-    }
-    ctx->combining = true;
-    for (int pass = 0; pass < kMaxPasses && !ctx->pending.empty(); ++pass) {
-      std::vector<SmallReq*> take;
-      uint64_t staged = 0;
-      size_t i = 0;
-      for (; i < ctx->pending.size(); ++i) {
-        const uint64_t sz = ctx->pending[i]->table_bytes();
-        if (!take.empty() && staged + sz > kPassTableBytes) break;
-        take.push_back(ctx->pending[i]);
-        staged += sz;
-      }
-      ctx->pending.erase(ctx->pending.begin(), ctx->pending.begin() + (long)i);
-      ql.unlock();
-      int rc;
-      {
-        std::lock_guard<std::mutex> lk(ctx->mu);
-        DeviceGuard g(ctx->device);
-        rc = run_zero_copy(ctx, take.data(), take.size());
-      }
-      for (SmallReq* t : take) {
-        t->rc = rc;
-        t->done.store(true, std::memory_order_release);
-      }
-      ql.lock();
-      ctx->qcv.notify_all();
-      if (req->done.load(std::memory_order_relaxed) && pass + 1 >= kMaxPasses) break;
-    }
-    ctx->combining = false;
-    ctx->qcv.notify_all();  // a waiter takes the role over if requests remain
-  }
-  return req->rc;
+  return ctx->combiner.submit(req, [ctx](SmallReq* const* reqs, size_t nreq) {
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    DeviceGuard g(ctx->device);
+    return run_zero_copy(ctx, reqs, nreq);
+  });
 }
 
 // Host batch core, caller holds ctx->mu and the device guard.  Pipelines
@@ -437,44 +377,20 @@ int run_host_batch(ns_csum_ctx* ctx, const uint8_t* h_arena, uint64_t arena_byte
   uint32_t k = 0;
   int slot = 0;
   while (k < n) {
-    // Grow the chunk while its byte span stays within budget and it holds at
-    // most kHostChunkDesc descriptors (so that the CPU's table copy of one
-    // chunk overlaps the other chunk's transfers).  Descriptors are
-    // range-checked on the way.  1M x 64 B: 4.27 ms -> 2.15 ms per call
-    // with this, the skipped span pass and the device-side table rebase
+    // The next chunk (nsh::cut_chunk): at most kHostChunkDesc descriptors
+    // and `budget` bytes of span, never inside a chained run; descriptors are
+    // range-checked on the way.  1M x 64 B: 4.27 ms -> 2.15 ms per call with
+    // this, the skipped span pass and the device-side table rebase
     // (profiles/r01/bench_host3.json).
-    uint64_t lo = UINT64_MAX, hi = 0;
-    uint32_t j = k;
-    uint32_t cut = k;  // last index (exclusive) at which we may cut
+    uint32_t cut = k;
     uint64_t cut_lo = 0, cut_hi = 0;
-    while (j < n) {
-      const uint64_t off = h_desc[j].off, len = h_desc[j].len;
-      if (off > arena_bytes || len > arena_bytes - off) {
-        const int rc = drain(slot);
-        return rc != NS_OK ? rc : NS_ERANGE;
-      }
-      uint64_t nlo = lo, nhi = hi;  // empty descriptors do not widen the span
-      if (len) {
-        nlo = std::min(lo, off);
-        nhi = std::max(hi, off + len);
-      }
-      if (j > k && cut > k && ((nlo != UINT64_MAX && nhi - nlo > budget) || j - k >= kHostChunkDesc)) break;
-      lo = nlo;
-      hi = nhi;
-      ++j;
-      if (j == n || !(chained && (h_desc[j].flags & NS_DESC_CONT))) {
-        cut = j;
-        cut_lo = lo;
-        cut_hi = hi;
-      }
-    }
-    if (cut == k) {  // only possible at the end: take everything left
-      cut = j;
-      cut_lo = lo;
-      cut_hi = hi;
+    const int crc = nsh::cut_chunk(h_desc, n, k, arena_bytes, budget, kHostChunkDesc, chained, &cut, &cut_lo,
+                                   &cut_hi);
+    if (crc != NS_OK) {
+      const int rc = drain(slot);
+      return rc != NS_OK ? rc : crc;
     }
     const uint32_t cnt = cut - k;
-    if (cut_lo == UINT64_MAX || cut_hi < cut_lo) cut_lo = cut_hi = 0;
     const uint64_t span = cut_hi - cut_lo;
 
     // Retire the slot's previous chunk before reusing its staging.
@@ -645,108 +561,33 @@ struct ByteSink {
   }
 };
 
-// One piece of a checksum chain: `restart` = a fresh Checksum(piece, xsum)
-// (alignment restarts, checksum.go:52-55); otherwise the piece continues the
-// previous piece's byte stream with its odd-byte carry (the view chaining of
-// ChecksumVVWithOffset, checksum.go:89).
-struct Piece {
-  const uint8_t* p;
-  uint64_t len;
-  bool restart;
-};
-
 // ---- gather of VectorisedView pieces (tcpip/buffer -> staging arena) -----
-struct Gather {
+// The descriptors come from nsh::ChainBuilder (host_logic.h) over a ByteSink.
+struct SinkHolder {
+  ByteSink sink;  // assembled in mapped staging (or spilled host memory), or adopted in place
+  SinkHolder(ns_csum_ctx* c, MappedPin* adopt) : sink(c, adopt) {}
+};
+struct Gather : SinkHolder, nsh::ChainBuilder<ByteSink> {  // the sink is constructed first
   ns_csum_ctx* ctx;
-  ByteSink bytes;  // assembled in mapped staging (or spilled host memory)
-  std::vector<ns_pkt_desc> desc;
-  std::vector<uint32_t> result_at;  // index of the descriptor holding each result
-  explicit Gather(ns_csum_ctx* c, MappedPin* adopt = nullptr) : ctx(c), bytes(c, adopt) {}
-
-  // One chain (include/netstack_csum.h, ns_csum_chains): sum = initial,
-  // odd = false; per piece (sum, odd) = calculateChecksum(piece, odd', sum)
-  // with odd' = false on a restart piece.  Continue pieces that follow each
-  // other in the arena merge into the open descriptor up to kMergeMax bytes
-  // (exact, see kMergeMax); a restart piece opens a new descriptor with
-  // odd = 0; empty pieces are skipped (checksum.go:73-75; Checksum(empty, x)
-  // == x).  A piece is never split: its own > 128 KiB wrap is reproduced
-  // exactly by the kernel.
-  void chain(const Piece* p, size_t np, uint16_t initial) {
-    bool first_desc = true;
-    uint32_t parity = 0;  // odd flag carried to the next continue piece
-    ns_pkt_desc cur{};
-    bool open = false;
-    auto close = [&]() {
-      if (!open) return;
-      desc.push_back(cur);
-      open = false;
-    };
-    for (size_t k = 0; k < np; ++k) {
-      const uint64_t len = p[k].len;
-      if (p[k].restart) {
-        close();
-        parity = 0;
-      }
-      if (len == 0) continue;
-      const bool big = len > kMergeMax;
-      const uint64_t at = bytes.append(p[k].p, len);
-      if (open && (big || cur.len + len > kMergeMax || at != cur.off + cur.len)) close();
-      if (!open) {
-        cur.off = at;
-        cur.len = 0;
-        cur.initial = first_desc ? initial : 0;
-        cur.flags = (uint16_t)((first_desc ? 0u : NS_DESC_CONT) | (parity ? NS_DESC_ODD : 0u));
-        first_desc = false;
-        open = true;
-      }
-      cur.len += (uint32_t)len;
-      parity ^= (uint32_t)(len & 1);
-      if (big) close();
-    }
-    close();
-    if (first_desc) {  // no bytes at all: result = initial (checksum.go:97)
-      ns_pkt_desc z{};
-      z.initial = initial;
-      desc.push_back(z);
-    }
-    result_at.push_back((uint32_t)desc.size() - 1);
-  }
-
-  // ChecksumVVWithOffset's view walk over already clipped pieces: the first
-  // restarts, the rest continue (checksum.go:69-98).
-  void segment(const std::vector<std::pair<const uint8_t*, uint64_t>>& pieces, uint16_t initial) {
-    std::vector<Piece> ps;
-    ps.reserve(pieces.size());
-    for (size_t k = 0; k < pieces.size(); ++k) ps.push_back(Piece{pieces[k].first, pieces[k].second, k == 0});
-    chain(ps.data(), ps.size(), initial);
-  }
-
-  // Each view its own calculateChecksum with odd=false, chained
-  // (xsum = Checksum(v, xsum): udp/endpoint.go:811-813).
-  void restart_chain(const std::vector<std::pair<const uint8_t*, uint64_t>>& pieces, uint16_t initial) {
-    std::vector<Piece> ps;
-    ps.reserve(pieces.size());
-    for (const auto& pc : pieces) ps.push_back(Piece{pc.first, pc.second, true});
-    chain(ps.data(), ps.size(), initial);
-  }
+  explicit Gather(ns_csum_ctx* c, MappedPin* adopt = nullptr)
+      : SinkHolder(c, adopt), nsh::ChainBuilder<ByteSink>(sink), ctx(c) {}
 
   int run(uint16_t* out) {
-    if (bytes.rc != NS_OK) return bytes.rc;
+    if (sink.rc != NS_OK) return sink.rc;
     std::vector<uint16_t> res(desc.size());
     int rc;
     const bool chained = any_cont(desc.data(), (uint32_t)desc.size());
-    if (bytes.adopted && !(zero_copy_enabled() && bytes.size() <= kStageBytes)) {
+    if (sink.adopted && !(zero_copy_enabled() && sink.size() <= kStageBytes)) {
       // A large caller stage: pinned already, so the DMA pipeline reads it.
       std::lock_guard<std::mutex> lk(ctx->mu);
       DeviceGuard g(ctx->device);
-      rc = run_host_batch(ctx, bytes.base(), bytes.size(), desc.data(), (uint32_t)desc.size(), res.data(),
-                          chained);
-    } else if (!bytes.in_big()) {
+      rc = run_host_batch(ctx, sink.base(), sink.size(), desc.data(), (uint32_t)desc.size(), res.data(), chained);
+    } else if (!sink.in_big()) {
       // Small: zero-copy from the leased (or the caller's) staging, combined
       // with concurrent calls.
       SmallReq rq;
-      rq.dbytes = bytes.adopted ? bytes.adopted->dev : bytes.stage->dev;
-      rq.nbytes = bytes.size();
+      rq.dbytes = sink.adopted ? sink.adopted->dev : sink.stage->dev;
+      rq.nbytes = sink.size();
       rq.desc = desc.data();
       rq.ndesc = (uint32_t)desc.size();
       rq.res = res.data();
@@ -755,7 +596,7 @@ struct Gather {
     } else {
       // Large: the bytes are in the pinned g_arena and ctx->mu is held.
       DeviceGuard g(ctx->device);
-      rc = run_host_batch(ctx, ctx->g_arena.p, bytes.size(), desc.data(), (uint32_t)desc.size(), res.data(),
+      rc = run_host_batch(ctx, ctx->g_arena.p, sink.size(), desc.data(), (uint32_t)desc.size(), res.data(),
                           chained);
     }
     if (rc != NS_OK) return rc;
@@ -763,321 +604,6 @@ struct Gather {
     return NS_OK;
   }
 };
-
-// Clip a VectorisedView to [off, off+size) exactly like checksum.go:72-96.
-int clip_views(const ns_view* views, uint32_t nviews, int64_t off, int64_t size,
-               std::vector<std::pair<const uint8_t*, uint64_t>>* pieces) {
-  if (off < 0 || size < 0) return NS_EINVAL;
-  pieces->clear();
-  uint64_t o = (uint64_t)off, s = (uint64_t)size;
-  for (uint32_t k = 0; k < nviews; ++k) {
-    const uint64_t vl = views[k].len;
-    if (vl == 0) continue;  // :73-75
-    if (!views[k].data) return NS_EINVAL;
-    if (o >= vl) {  // :77-80
-      o -= vl;
-      continue;
-    }
-    const uint64_t l = std::min<uint64_t>(vl - o, s);  // :81-87
-    if (l > 0xFFFFFFFFull) return NS_EINVAL;
-    pieces->emplace_back(views[k].data + o, l);
-    s -= l;  // :91-94
-    if (s == 0) break;
-    o = 0;
-  }
-  return NS_OK;
-}
-
-// ---- tcpip.PacketBuffer batches (ns_csum_packet_buffers) -------------------
-// A packet as one byte stream: its Header bytes, then its Data views clipped
-// to Data.Size() (packet_buffer.go:25-50).  The host reads header fields from
-// it (plumbing: lengths, addresses' positions, protocol numbers) and cuts it
-// into the pieces of each reference call sequence; every sum is computed by
-// the kernel.
-struct PacketBytes {
-  std::vector<std::pair<const uint8_t*, uint64_t>> seg;  // non-empty segments in order
-  std::vector<uint64_t> at;                             // byte offset of each segment
-  uint64_t size = 0;
-  uint64_t hdr_len = 0;  // bytes [0, hdr_len) are the Header's (writable)
-
-  int init(const ns_pkt_buf& pk) {
-    if (pk.hdr_len && !pk.hdr) return NS_EINVAL;
-    hdr_len = pk.hdr_len;
-    if (pk.ndata && !pk.data) return NS_EINVAL;
-    add(pk.hdr, pk.hdr_len);
-    uint64_t left = pk.data_size;
-    for (uint32_t k = 0; k < pk.ndata && left; ++k) {
-      const uint64_t l = std::min<uint64_t>(pk.data[k].len, left);
-      if (l && !pk.data[k].data) return NS_EINVAL;
-      add(pk.data[k].data, l);
-      left -= l;
-    }
-    return NS_OK;
-  }
-  void add(const uint8_t* p, uint64_t l) {
-    if (!l) return;
-    seg.emplace_back(p, l);
-    at.push_back(size);
-    size += l;
-  }
-  // Segment holding byte k (k < size).
-  size_t seg_of(uint64_t k) const {
-    size_t lo = 0, hi = seg.size();
-    while (hi - lo > 1) {
-      const size_t mid = (lo + hi) / 2;
-      if (at[mid] <= k) lo = mid;
-      else hi = mid;
-    }
-    return lo;
-  }
-  // End of the segment (view) holding byte k: "Data.First()" after a trim to k.
-  uint64_t seg_end(uint64_t k) const {
-    if (k >= size) return size;
-    const size_t s = seg_of(k);
-    return at[s] + seg[s].second;
-  }
-  bool read(uint64_t k, uint8_t* out, uint64_t n) const {
-    if (k + n > size) return false;
-    while (n) {
-      const size_t s = seg_of(k);
-      const uint64_t o = k - at[s], l = std::min<uint64_t>(n, seg[s].second - o);
-      std::memcpy(out, seg[s].first + o, l);
-      out += l;
-      k += l;
-      n -= l;
-    }
-    return true;
-  }
-  uint8_t* mut(uint64_t k) const {  // address of byte k (a Header byte for stores)
-    const size_t s = seg_of(k);
-    return const_cast<uint8_t*>(seg[s].first) + (k - at[s]);
-  }
-  // Pieces covering [a, b), cut at view boundaries: the first `first_restart`,
-  // then each next view restarting (`per_view`, the `xsum = Checksum(v, xsum)`
-  // loops) or continuing (ChecksumVV's view walk).
-  void pieces(uint64_t a, uint64_t b, bool first_restart, bool per_view, std::vector<Piece>* out) const {
-    bool first = true;
-    while (a < b) {
-      const size_t s = seg_of(a);
-      const uint64_t o = a - at[s], l = std::min<uint64_t>(b - a, seg[s].second - o);
-      out->push_back(Piece{seg[s].first + o, l, first ? first_restart : per_view});
-      first = false;
-      a += l;
-    }
-  }
-};
-
-constexpr uint8_t kProtoICMPv4 = 1, kProtoTCP = 6, kProtoUDP = 17, kProtoICMPv6 = 58;
-
-// One packet's plan: up to two chains (network header, transport) and where
-// their results go.
-struct PacketPlan {
-  int net_chain = -1, tr_chain = -1;  // result indices in the Gather
-  uint8_t verdict = NS_PKB_UNCHECKED;
-  uint8_t kind = 0;                   // transport protocol for the verdict
-  uint64_t net_store = UINT64_MAX, tr_store = UINT64_MAX;  // FILL: field offsets
-  uint16_t field = 0;                 // VERIFY (ICMP): the received checksum field
-};
-
-// ChecksumCombine (checksum.go:104-107): folds the pseudo-header's length and
-// protocol words into the initial of the address piece.  The pseudo-header
-// pieces are all even-length restarts, so any grouping of them gives Go's
-// value (both are fold1 of the same total, and 0 only when all
-// pieces are 0).
-uint16_t combine(uint16_t a, uint16_t b) { return ns_csum_combine(a, b); }
-
-// The IP layer of a packet: header length, transport range and protocol, the
-// pseudo-header address bytes.  Returns false for what IPv4/IPv6 IsValid
-// (header/ipv4.go:280-296, ipv6.go:207-222) and HandlePacket reject.
-struct IpInfo {
-  bool v4 = false;
-  uint64_t hlen = 0, tbeg = 0, tend = 0, addr = 0, addr_len = 0;
-  uint8_t proto = 0;
-  bool fragment = false;
-};
-
-bool parse_ip(const PacketBytes& pb, bool rx, IpInfo* ip) {
-  uint8_t h[40];
-  if (pb.size < 1 || !pb.read(0, h, 1)) return false;
-  const uint8_t ver = h[0] >> 4;
-  // RX: the network header lies in Data.First() (packet_buffer.go:27-29);
-  // IsValid looks at that view alone.
-  const uint64_t first = pb.seg_end(0);
-  if (ver == 4) {
-    if ((rx && first < 20) || !pb.read(0, h, 20)) return false;
-    ip->v4 = true;
-    ip->hlen = (uint64_t)(h[0] & 0xF) * 4;
-    const uint64_t tlen = ((uint64_t)h[2] << 8) | h[3];
-    if (rx) {
-      if (ip->hlen < 20 || ip->hlen > tlen || tlen > pb.size || ip->hlen > first) return false;
-      ip->tend = tlen;  // Data.CapLength(tlen - hlen), ipv4.go:353
-    } else {
-      if (ip->hlen < 20 || ip->hlen > pb.size) return false;
-      ip->tend = pb.size;
-    }
-    ip->proto = h[9];
-    ip->addr = 12;
-    ip->addr_len = 8;
-    ip->fragment = (h[6] & 0x20) || (((h[6] & 0x1F) << 8) | h[7]);  // MF or a fragment offset
-  } else if (ver == 6) {
-    if ((rx && first < 40) || !pb.read(0, h, 40)) return false;
-    ip->hlen = 40;
-    const uint64_t plen = ((uint64_t)h[4] << 8) | h[5];
-    if (rx) {
-      if (plen > pb.size - 40) return false;
-      ip->tend = 40 + plen;  // Data.CapLength(PayloadLength), ipv6.go:177
-    } else {
-      ip->tend = pb.size;
-    }
-    ip->proto = h[6];
-    ip->addr = 8;
-    ip->addr_len = 32;
-  } else {
-    return false;
-  }
-  ip->tbeg = ip->hlen;
-  return true;
-}
-
-// Builds one packet's chains into g.  RX (NS_PKB_VERIFY) mirrors the receive
-// path's checks; TX (NS_PKB_FILL) the transmit path's sums (see the header).
-int plan_packet(Gather& g, const PacketBytes& pb, uint32_t op, PacketPlan* pp) {
-  IpInfo ip;
-  const bool rx = op == NS_PKB_VERIFY;
-  if (!parse_ip(pb, rx, &ip)) {
-    if (rx) {
-      pp->verdict = NS_PKB_MALFORMED;
-      return NS_OK;
-    }
-    return NS_EINVAL;
-  }
-  std::vector<Piece> ps;
-  const int nres = (int)g.result_at.size();
-  auto add_chain = [&](uint16_t init) {
-    g.chain(ps.data(), ps.size(), init);
-    ps.clear();
-    return (int)g.result_at.size() - 1;
-  };
-  if (ip.v4 && !rx) {
-    // addIPHeader: ip.SetChecksum(^ip.CalculateChecksum()) (ipv4.go:236),
-    // CalculateChecksum = Checksum(b[:HeaderLength()], 0) (ipv4.go:251-253)
-    pb.pieces(0, ip.hlen, true, false, &ps);
-    pp->net_chain = add_chain(0);
-    pp->net_store = 10;
-  } else if (ip.v4) {
-    // not verified on receive in the reference; reported for the caller
-    pb.pieces(0, ip.hlen, true, false, &ps);
-    pp->net_chain = add_chain(0);
-  }
-  (void)nres;
-  const uint64_t t0 = ip.tbeg, te = ip.tend, tl = te - t0;
-  const uint64_t first_end = std::min(pb.seg_end(t0), te);  // Data.First() after the IP trim
-  pp->kind = ip.proto;
-  auto pseudo = [&](uint8_t proto, uint64_t len, bool icmpv6) -> uint16_t {
-    // PseudoHeaderChecksum (checksum.go:112-122) / ICMPv6Checksum's
-    // pseudo-header (icmpv6.go:204-210): the addresses in place, the length
-    // and protocol words as the initial.
-    pb.pieces(ip.addr, ip.addr + ip.addr_len, true, false, &ps);
-    if (icmpv6) return combine(combine((uint16_t)(len >> 16), (uint16_t)len), proto);
-    return combine((uint16_t)len, proto);
-  };
-  if (rx) {
-    if (ip.fragment) return NS_OK;  // reassembled before the transport layer sees it
-    if (ip.proto == kProtoTCP) {
-      // stack.DeliverTransportPacket: First() >= TCPMinimumSize; segment.parse
-      // (segment.go:145-181): offset in [20, len(First())]
-      uint8_t h[13];
-      if (first_end - t0 < 20 || !pb.read(t0, h, 13)) {
-        pp->verdict = NS_PKB_MALFORMED;
-        return NS_OK;
-      }
-      const uint64_t off = (uint64_t)(h[12] >> 4) * 4;
-      if (off < 20 || off > first_end - t0) {
-        pp->verdict = NS_PKB_MALFORMED;
-        return NS_OK;
-      }
-      const uint16_t init = pseudo(kProtoTCP, (uint16_t)tl, false);  // :176 PseudoHeaderChecksum(data.Size())
-      pb.pieces(t0, t0 + off, true, false, &ps);                     // :177 h.CalculateChecksum(xsum)
-      pb.pieces(t0 + off, te, true, false, &ps);                     // :179 ChecksumVV(s.data, xsum)
-      pp->tr_chain = add_chain(init);
-      pp->verdict = NS_PKB_INVALID;  // decided from the result (:180)
-    } else if (ip.proto == kProtoICMPv4 && ip.v4) {
-      // handleICMP (network/ipv4/icmp.go:60-80): echo requests only
-      uint8_t h[4];
-      if (first_end - t0 < 8 || !pb.read(t0, h, 4)) {
-        pp->verdict = NS_PKB_MALFORMED;
-        return NS_OK;
-      }
-      if (h[0] != 8) return NS_OK;
-      pp->field = (uint16_t)((h[2] << 8) | h[3]);
-      // h.SetChecksum(0); ^ChecksumVV(pkt.Data, 0): bytes [2, 4) as zeros
-      pb.pieces(t0, t0 + 2, true, false, &ps);
-      pb.pieces(t0 + 4, te, false, false, &ps);
-      pp->tr_chain = add_chain(0);
-      pp->verdict = NS_PKB_INVALID;
-    } else if (ip.proto == kProtoICMPv6 && !ip.v4) {
-      // handleICMP (network/ipv6/icmp.go:62-84): h = the first view, payload
-      // = the other views, ICMPv6Checksum (header/icmpv6.go:202-221)
-      uint8_t h[4];
-      if (first_end - t0 < 4 || !pb.read(t0, h, 4)) {
-        pp->verdict = NS_PKB_MALFORMED;
-        return NS_OK;
-      }
-      pp->field = (uint16_t)((h[2] << 8) | h[3]);
-      const uint16_t init = pseudo(kProtoICMPv6, tl, true);
-      pb.pieces(first_end, te, true, true, &ps);        // for v in vv.Views(): Checksum(v, xsum)
-      pb.pieces(t0, t0 + 2, true, false, &ps);          // Checksum(h with h[2:4] = 0, xsum)
-      pb.pieces(t0 + 4, first_end, false, false, &ps);
-      pp->tr_chain = add_chain(init);
-      pp->verdict = NS_PKB_INVALID;
-    }
-    return NS_OK;
-  }
-  // TX: the transport header follows the IP header in Header; its checksum
-  // field must lie in Header (it is written there).
-  const uint64_t hdr_end = pb.hdr_len;
-  auto need = [&](uint64_t field_end) { return field_end <= hdr_end; };
-  if (ip.proto == kProtoTCP) {
-    uint8_t h[13];
-    if (!pb.read(t0, h, 13)) return NS_EINVAL;
-    const uint64_t thl = (uint64_t)(h[12] >> 4) * 4;
-    if (thl < 20 || t0 + thl > te || !need(t0 + 18)) return NS_EINVAL;
-    // buildTCPHdr (connect.go:653-663): PseudoHeaderChecksum(length),
-    // ChecksumVVWithOffset(payload), tcp.CalculateChecksum(xsum) = Checksum(tcp[:DataOffset])
-    const uint16_t init = pseudo(kProtoTCP, (uint16_t)tl, false);
-    pb.pieces(t0 + thl, te, true, false, &ps);
-    pb.pieces(t0, t0 + thl, true, false, &ps);
-    pp->tr_chain = add_chain(init);
-    pp->tr_store = t0 + 16;
-  } else if (ip.proto == kProtoUDP) {
-    if (t0 + 8 > te || !need(t0 + 8)) return NS_EINVAL;
-    // sendUDP (udp/endpoint.go:808-815): per-view restart, then the header
-    const uint16_t init = pseudo(kProtoUDP, (uint16_t)tl, false);
-    pb.pieces(t0 + 8, te, true, true, &ps);
-    pb.pieces(t0, t0 + 8, true, false, &ps);
-    pp->tr_chain = add_chain(init);
-    pp->tr_store = t0 + 6;
-  } else if (ip.proto == kProtoICMPv4 && ip.v4) {
-    // the echo reply (network/ipv4/icmp.go:96-100): pkt = the ICMP bytes in
-    // Header, SetChecksum(0), ^Checksum(pkt, ChecksumVV(vv, 0))
-    if (!need(t0 + 4)) return NS_EINVAL;
-    pb.pieces(hdr_end, te, true, false, &ps);
-    pb.pieces(t0, t0 + 2, true, false, &ps);
-    pb.pieces(t0 + 4, hdr_end, false, false, &ps);
-    pp->tr_chain = add_chain(0);
-    pp->tr_store = t0 + 2;
-  } else if (ip.proto == kProtoICMPv6 && !ip.v4) {
-    // ICMPv6Checksum(h = the ICMP bytes in Header, src, dst, Data) (icmpv6.go:202-221)
-    if (!need(t0 + 4)) return NS_EINVAL;
-    const uint16_t init = pseudo(kProtoICMPv6, tl, true);
-    pb.pieces(hdr_end, te, true, true, &ps);
-    pb.pieces(t0, t0 + 2, true, false, &ps);
-    pb.pieces(t0 + 4, hdr_end, false, false, &ps);
-    pp->tr_chain = add_chain(init);
-    pp->tr_store = t0 + 2;
-  }
-  return NS_OK;
-}
 
 }  // namespace
 
@@ -1428,7 +954,7 @@ int ns_csum_packet_buffers(ns_csum_ctx* ctx, const ns_pkt_buf* pkts, uint32_t n,
                            uint16_t* sums, uint8_t* verdict) {
   if (!ctx || (n && !pkts) || (op != NS_PKB_VERIFY && op != NS_PKB_FILL)) return NS_EINVAL;
   if (n == 0) return NS_OK;
-  std::vector<PacketBytes> pb(n);
+  std::vector<nsh::PacketBytes> pb(n);
   SpanProbe pr;
   for (uint32_t i = 0; i < n; ++i) {
     const int rc = pb[i].init(pkts[i]);
@@ -1436,9 +962,9 @@ int ns_csum_packet_buffers(ns_csum_ctx* ctx, const ns_pkt_buf* pkts, uint32_t n,
     for (const auto& sg : pb[i].seg) pr.add(sg.first, sg.second);
   }
   Gather gt(ctx, pr.stage(ctx));
-  std::vector<PacketPlan> plan(n);
+  std::vector<nsh::PacketPlan> plan(n);
   for (uint32_t i = 0; i < n; ++i) {
-    const int rc = plan_packet(gt, pb[i], op, &plan[i]);
+    const int rc = nsh::plan_packet(gt, pb[i], op, &plan[i]);
     if (rc != NS_OK) return rc;
   }
   std::vector<uint16_t> res(gt.result_at.size());
@@ -1446,32 +972,8 @@ int ns_csum_packet_buffers(ns_csum_ctx* ctx, const ns_pkt_buf* pkts, uint32_t n,
     const int rc = gt.run(res.data());
     if (rc != NS_OK) return rc;
   }
-  for (uint32_t i = 0; i < n; ++i) {
-    PacketPlan& p = plan[i];
-    const uint16_t net = p.net_chain >= 0 ? res[(size_t)p.net_chain] : 0;
-    const uint16_t tr = p.tr_chain >= 0 ? res[(size_t)p.tr_chain] : 0;
-    if (sums) {
-      sums[2 * i] = net;
-      sums[2 * i + 1] = tr;
-    }
-    if (op == NS_PKB_FILL) {
-      // SetChecksum(^sum), big-endian, into the packet's Header
-      auto put = [&](uint64_t at, uint16_t v) {
-        uint8_t* q = pb[i].mut(at);
-        q[0] = (uint8_t)(v >> 8);
-        q[1] = (uint8_t)v;
-      };
-      if (p.net_store != UINT64_MAX) put(p.net_store, (uint16_t)~net);
-      if (p.tr_store != UINT64_MAX) put(p.tr_store, (uint16_t)~tr);
-    } else if (verdict) {
-      if (p.tr_chain >= 0) {
-        // TCP: xsum == 0xffff (segment.go:180); ICMP: ^sum == the received field
-        const bool ok = p.kind == kProtoTCP ? tr == 0xFFFF : (uint16_t)~tr == p.field;
-        p.verdict = ok ? NS_PKB_VALID : NS_PKB_INVALID;
-      }
-      verdict[i] = p.verdict;
-    }
-  }
+  for (uint32_t i = 0; i < n; ++i)
+    nsh::finish_packet(pb[i], plan[i], op, res.data(), sums ? sums + 2 * i : nullptr, verdict ? verdict + i : nullptr);
   return NS_OK;
 }
 
@@ -1509,25 +1011,7 @@ int ns_csum_batch_multi(ns_csum_ctx* const* ctxs, uint32_t nctx, const uint8_t* 
 
 int ns_csum_shard_plan(const ns_pkt_desc* h_desc, uint32_t n, uint32_t parts, uint32_t* first) {
   if (!first || parts == 0 || (n && !h_desc)) return NS_EINVAL;
-  uint64_t total = 0;
-  for (uint32_t i = 0; i < n; ++i) total += h_desc[i].len;
-  first[0] = 0;
-  uint64_t run = 0;
-  uint32_t i = 0;
-  for (uint32_t p = 1; p < parts; ++p) {
-    // Cut at the first descriptor whose prefix reaches p/parts of the bytes;
-    // with all-empty tables fall back to equal descriptor counts.
-    const uint64_t target = total ? (total * p + parts - 1) / parts : 0;
-    if (total == 0) {
-      i = (uint32_t)(((uint64_t)n * p) / parts);
-    } else {
-      while (i < n && run + h_desc[i].len <= target) run += h_desc[i++].len;
-    }
-    // never split a chained run
-    while (i > 0 && i < n && (h_desc[i].flags & NS_DESC_CONT)) run += h_desc[i++].len;
-    first[p] = std::max(i, first[p - 1]);
-  }
-  first[parts] = n;
+  nsh::shard_plan(h_desc, n, parts, first);
   return NS_OK;
 }
 

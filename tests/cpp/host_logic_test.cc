@@ -1,0 +1,442 @@
+// The HIP-free host logic of the C ABI (netstack_amd/csrc/host_logic.h)
+// under sanitizers — built by `make -C netstack_amd/csrc sanitize` twice:
+// with -fsanitize=address,undefined and with -fsanitize=thread — and run by
+// tests/test_host_sanitizers.py (CPU only).  Results are checked against the
+// oracle's C restatement of checksum.go (oracle/csum_oracle.c, test
+// infrastructure), everything else against the invariants the C ABI relies
+// on:
+//   ChainBuilder  chains of restart/continue pieces (copied or adopted in
+//                 place) -> descriptors whose chained sums equal Go's chain;
+//   clip_views    == ChecksumVVWithOffset (checksum.go:69-98);
+//   plan_packet   random and garbage packets, both directions: no memory
+//                 error, fields written only inside Header, filled TCP
+//                 packets verify;
+//   cut_chunk     chunks tile the table, never end inside a chained run,
+//                 spans within budget, NS_ERANGE on a bad descriptor;
+//   shard_plan    contiguous, ordered, whole runs, byte-balanced;
+//   FlatCombiner  many threads x many requests: every request done once
+//                 with its own result (the point of the -fsanitize=thread
+//                 build).
+// Usage: host_logic_test [--quick]   (exit status 0 = all passed)
+#include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <random>
+#include <thread>
+#include <vector>
+
+#include "csum_oracle.h"
+#include "host_logic.h"
+
+static int g_fail = 0, g_run = 0;
+#define CHECK(cond, ...)                                         \
+  do {                                                           \
+    ++g_run;                                                     \
+    if (!(cond)) {                                               \
+      ++g_fail;                                                  \
+      std::printf("FAIL %s:%d: %s: ", __FILE__, __LINE__, #cond); \
+      std::printf(__VA_ARGS__);                                  \
+      std::printf("\n");                                         \
+    }                                                            \
+  } while (0)
+
+using Rng = std::mt19937_64;
+
+// Copying sink: the arena is a vector.
+struct VecSink {
+  std::vector<uint8_t> a;
+  uint64_t append(const uint8_t* p, uint64_t len) {
+    const uint64_t at = a.size();
+    a.insert(a.end(), p, p + len);
+    return at;
+  }
+};
+// Adopting sink: the pieces already lie in `base` (a caller's stage).
+struct AdoptSink {
+  const uint8_t* base;
+  uint64_t n = 0;
+  uint64_t append(const uint8_t* p, uint64_t len) {
+    const uint64_t at = len ? (uint64_t)(p - base) : n;
+    n = std::max(n, at + len);
+    return at;
+  }
+};
+
+// Go's chain over pieces: xsum = initial, odd = false; each piece through
+// calculateChecksum (checksum.go:26-46), odd reset on a restart; empty
+// pieces skipped.
+static uint16_t go_chain(const std::vector<nsh::Piece>& ps, uint16_t initial) {
+  uint32_t x = initial;
+  int odd = 0;
+  for (const nsh::Piece& p : ps) {
+    if (p.restart) odd = 0;
+    if (!p.len) continue;
+    int o2 = 0;
+    x = oracle_calculate_checksum(p.p, p.len, odd, x, &o2);
+    odd = o2;
+  }
+  return (uint16_t)x;
+}
+
+template <class Sink>
+static std::vector<uint16_t> eval(const Sink& s, const uint8_t* arena, uint64_t arena_bytes,
+                                  const nsh::ChainBuilder<Sink>& b) {
+  std::vector<uint16_t> res(b.desc.size());
+  const int bad = oracle_batch(arena, arena_bytes, reinterpret_cast<const oracle_desc*>(b.desc.data()),
+                               (uint32_t)b.desc.size(), res.data(), 1);
+  CHECK(bad == 0, "%d out-of-range descriptors", bad);
+  std::vector<uint16_t> out;
+  for (uint32_t r : b.result_at) out.push_back(res[r]);
+  (void)s;
+  return out;
+}
+
+static void TestChains(Rng& rng, int rounds) {
+  std::vector<uint8_t> pool(1 << 20);
+  for (auto& b : pool) b = (uint8_t)rng();
+  for (int round = 0; round < rounds; ++round) {
+    const int nch = 1 + (int)(rng() % 40);
+    std::vector<std::vector<nsh::Piece>> chains(nch);
+    std::vector<uint16_t> inits(nch), want(nch);
+    for (int c = 0; c < nch; ++c) {
+      const int np = (int)(rng() % 7);
+      for (int k = 0; k < np; ++k) {
+        uint64_t len = rng() % 4 == 0 ? 0 : rng() % 3000;
+        if (rng() % 50 == 0) len = 131072 + rng() % 20000;  // above the merge limit
+        const uint64_t off = rng() % (pool.size() - len);
+        // sometimes the next piece continues the previous one's bytes in place
+        const uint8_t* p = pool.data() + off;
+        if (k > 0 && rng() % 3 == 0) {
+          const nsh::Piece& prev = chains[c].back();
+          if (prev.p + prev.len + len <= pool.data() + pool.size()) p = prev.p + prev.len;
+        }
+        chains[c].push_back(nsh::Piece{p, len, k == 0 || rng() % 3 == 0});
+      }
+      inits[c] = (uint16_t)rng();
+      want[c] = go_chain(chains[c], inits[c]);
+    }
+    VecSink vs;
+    nsh::ChainBuilder<VecSink> bv(vs);
+    AdoptSink as{pool.data()};
+    nsh::ChainBuilder<AdoptSink> ba(as);
+    for (int c = 0; c < nch; ++c) {
+      bv.chain(chains[c].data(), chains[c].size(), inits[c]);
+      ba.chain(chains[c].data(), chains[c].size(), inits[c]);
+    }
+    for (const ns_pkt_desc& d : bv.desc) CHECK(d.off + d.len <= vs.a.size(), "descriptor inside the arena");
+    for (const ns_pkt_desc& d : ba.desc) CHECK(d.off + d.len <= pool.size(), "adopted descriptor inside the stage");
+    const auto gv = eval(vs, vs.a.data(), vs.a.size(), bv);
+    const auto ga = eval(as, pool.data(), pool.size(), ba);
+    for (int c = 0; c < nch; ++c) {
+      CHECK(gv[c] == want[c], "copied chain %d: %04x vs %04x", c, gv[c], want[c]);
+      CHECK(ga[c] == want[c], "adopted chain %d: %04x vs %04x", c, ga[c], want[c]);
+    }
+  }
+}
+
+static void TestClipViews(Rng& rng, int rounds) {
+  std::vector<uint8_t> pool(200000);
+  for (auto& b : pool) b = (uint8_t)rng();
+  for (int round = 0; round < rounds; ++round) {
+    const uint32_t nv = (uint32_t)(rng() % 8);
+    std::vector<ns_view> views(nv);
+    std::vector<const uint8_t*> vp(nv);
+    std::vector<uint64_t> vl(nv);
+    uint64_t total = 0;
+    for (uint32_t k = 0; k < nv; ++k) {
+      const uint64_t len = rng() % 5 == 0 ? 0 : rng() % 5000;
+      const uint64_t off = rng() % (pool.size() - len);
+      views[k] = ns_view{pool.data() + off, len};
+      vp[k] = views[k].data;
+      vl[k] = len;
+      total += len;
+    }
+    const int64_t off = (int64_t)(rng() % (total + 10));
+    const int64_t size = (int64_t)(rng() % (total + 10));
+    std::vector<std::pair<const uint8_t*, uint64_t>> pieces;
+    CHECK(nsh::clip_views(views.data(), nv, off, size, &pieces) == NS_OK, "clip");
+    VecSink vs;
+    nsh::ChainBuilder<VecSink> b(vs);
+    const uint16_t init = (uint16_t)rng();
+    b.segment(pieces, init);
+    uint16_t want = 0;
+    oracle_vv_with_offset(vp.data(), vl.data(), nv, init, off, size, &want);
+    const auto got = eval(vs, vs.a.data(), vs.a.size(), b);
+    CHECK(got[0] == want, "vv_with_offset %04x vs %04x", got[0], want);
+  }
+  std::vector<std::pair<const uint8_t*, uint64_t>> pieces;
+  CHECK(nsh::clip_views(nullptr, 0, -1, 0, &pieces) == NS_EINVAL, "negative off");
+  CHECK(nsh::clip_views(nullptr, 0, 0, -1, &pieces) == NS_EINVAL, "negative size");
+}
+
+// A random, often broken, packet: IPv4 or IPv6 (or garbage), a transport
+// header of a random protocol, random lengths, split into random views.
+struct RandPacket {
+  std::vector<uint8_t> bytes;
+  size_t hdr_len = 0;
+  std::vector<size_t> cuts;  // data view boundaries after hdr_len
+};
+
+static RandPacket make_packet(Rng& rng, bool tx) {
+  RandPacket rp;
+  const int kind = (int)(rng() % 10);
+  const uint8_t protos[] = {6, 17, 1, 58, 6, 6, 99};
+  const uint8_t proto = protos[rng() % 7];
+  const size_t payload = rng() % 3 == 0 ? rng() % 8 : rng() % 2000;
+  std::vector<uint8_t>& b = rp.bytes;
+  size_t ihl = 20, thl = proto == 6 ? 20 + 4 * (rng() % 11) : proto == 17 ? 8 : 8 + 4 * (rng() % 5);
+  if (kind < 6) {  // IPv4
+    if (rng() % 6 == 0) ihl = 4 * (rng() % 16);
+    b.assign(std::max<size_t>(ihl, 20) + thl + payload, 0);
+    for (auto& x : b) x = (uint8_t)rng();
+    b[0] = (uint8_t)(0x40 | (ihl / 4));
+    const size_t tlen = rng() % 8 == 0 ? rng() % 70000 : b.size();
+    b[2] = (uint8_t)(tlen >> 8);
+    b[3] = (uint8_t)tlen;
+    b[6] = rng() % 10 == 0 ? 0x20 : 0;
+    b[7] = rng() % 10 == 0 ? (uint8_t)rng() : 0;
+    b[9] = proto;
+    if (ihl >= 20 && proto == 6 && ihl + 12 < b.size()) b[ihl + 12] = (uint8_t)((thl / 4) << 4);
+  } else if (kind < 9) {  // IPv6
+    b.assign(40 + thl + payload, 0);
+    for (auto& x : b) x = (uint8_t)rng();
+    b[0] = 0x60;
+    const size_t plen = rng() % 8 == 0 ? rng() % 70000 : b.size() - 40;
+    b[4] = (uint8_t)(plen >> 8);
+    b[5] = (uint8_t)plen;
+    b[6] = proto;
+    if (proto == 6) b[40 + 12] = (uint8_t)((thl / 4) << 4);
+  } else {  // garbage, possibly tiny
+    b.assign(rng() % 64, 0);
+    for (auto& x : b) x = (uint8_t)rng();
+  }
+  const size_t ipl = b.empty() ? 0 : ((b[0] >> 4) == 6 ? 40 : (size_t)(b[0] & 0xF) * 4);
+  if (tx && kind < 9) {
+    // as Encode leaves them (checksum fields 0): a filled packet then verifies
+    if ((b[0] >> 4) == 4 && b.size() >= 12) b[10] = b[11] = 0;
+    if (ipl + 18 <= b.size()) b[ipl + 16] = b[ipl + 17] = 0;
+  }
+  if (rng() % 12 == 0 && !b.empty()) b.resize(rng() % b.size());  // truncated
+  rp.hdr_len = tx ? std::min(b.size(), ipl + thl + (rng() % 4 == 0 ? rng() % 16 : 0)) : 0;
+  for (size_t p = rp.hdr_len; p < b.size();) {
+    p += 1 + rng() % 700;
+    if (p < b.size()) rp.cuts.push_back(p);
+  }
+  return rp;
+}
+
+static void TestPackets(Rng& rng, int rounds) {
+  int valid_tcp = 0;
+  for (int round = 0; round < rounds; ++round) {
+    for (uint32_t op : {NS_PKB_VERIFY, NS_PKB_FILL}) {
+      RandPacket rp = make_packet(rng, op == NS_PKB_FILL);
+      std::vector<uint8_t> before = rp.bytes;
+      std::vector<ns_view> views;
+      size_t prev = rp.hdr_len;
+      for (size_t c : rp.cuts) {
+        views.push_back(ns_view{rp.bytes.data() + prev, c - prev});
+        prev = c;
+      }
+      views.push_back(ns_view{rp.bytes.data() + prev, rp.bytes.size() - prev});
+      ns_pkt_buf pk{};
+      pk.hdr = rp.hdr_len ? rp.bytes.data() : nullptr;
+      pk.hdr_len = rp.hdr_len;
+      pk.data = views.data();
+      pk.ndata = (uint32_t)views.size();
+      pk.data_size = rp.bytes.size() - rp.hdr_len - (rng() % 5 == 0 && rp.bytes.size() > rp.hdr_len ? 1 : 0);
+      nsh::PacketBytes pb;
+      CHECK(pb.init(pk) == NS_OK, "init");
+      VecSink vs;
+      nsh::ChainBuilder<VecSink> b(vs);
+      nsh::PacketPlan plan;
+      const int rc = nsh::plan_packet(b, pb, op, &plan);
+      CHECK(rc == NS_OK || (op == NS_PKB_FILL && rc == NS_EINVAL), "plan rc %d", rc);
+      if (rc != NS_OK) {
+        CHECK(rp.bytes == before, "a rejected packet is not written");
+        continue;
+      }
+      std::vector<uint16_t> res(b.result_at.size());
+      if (!res.empty()) res = eval(vs, vs.a.data(), vs.a.size(), b);
+      uint16_t sums[2] = {0, 0};
+      uint8_t verdict = 0xEE;
+      nsh::finish_packet(pb, plan, op, res.data(), sums, &verdict);
+      if (op == NS_PKB_FILL) {
+        // only the checksum fields inside Header may change
+        for (size_t k = 0; k < rp.bytes.size(); ++k) {
+          const bool field = k == plan.net_store || k == plan.net_store + 1 || k == plan.tr_store ||
+                             k == plan.tr_store + 1;
+          if (rp.bytes[k] != before[k]) CHECK(field && k < rp.hdr_len, "byte %zu written", k);
+        }
+        // a filled TCP packet (whole, one view) verifies on receive
+        const bool ipv4 = !rp.bytes.empty() && (rp.bytes[0] >> 4) == 4;
+        const bool tcp = ipv4 && rp.bytes.size() > 9 && rp.bytes[9] == 6;
+        const size_t tlen = rp.bytes.size() >= 4 ? ((size_t)rp.bytes[2] << 8 | rp.bytes[3]) : 0;
+        if (tcp && !(rp.bytes[6] & 0x3F) && !rp.bytes[7] && tlen == rp.bytes.size() &&
+            pk.data_size + rp.hdr_len == rp.bytes.size() && plan.tr_store != UINT64_MAX) {
+          ns_view one{rp.bytes.data(), rp.bytes.size()};
+          ns_pkt_buf rx{};
+          rx.data = &one;
+          rx.ndata = 1;
+          rx.data_size = rp.bytes.size();
+          nsh::PacketBytes pr;
+          pr.init(rx);
+          VecSink v2;
+          nsh::ChainBuilder<VecSink> b2(v2);
+          nsh::PacketPlan p2;
+          CHECK(nsh::plan_packet(b2, pr, NS_PKB_VERIFY, &p2) == NS_OK, "verify plan");
+          std::vector<uint16_t> r2 = eval(v2, v2.a.data(), v2.a.size(), b2);
+          uint8_t v = 0xEE;
+          nsh::finish_packet(pr, p2, NS_PKB_VERIFY, r2.data(), nullptr, &v);
+          if (p2.verdict != NS_PKB_MALFORMED) {
+            CHECK(v == NS_PKB_VALID, "filled TCP packet verdict %d", v);
+            ++valid_tcp;
+          }
+        }
+      } else {
+        CHECK(verdict <= NS_PKB_MALFORMED, "verdict %d", verdict);
+        CHECK(rp.bytes == before, "verify writes nothing");
+      }
+    }
+  }
+  CHECK(valid_tcp > 0 || rounds < 50, "no filled TCP packet was checked");
+}
+
+static void TestCutChunk(Rng& rng, int rounds) {
+  for (int round = 0; round < rounds; ++round) {
+    const uint32_t n = (uint32_t)(rng() % 3000);
+    std::vector<ns_pkt_desc> d(n);
+    uint64_t pos = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+      d[i].len = rng() % 6 == 0 ? 0 : (uint32_t)(rng() % 3000);
+      d[i].off = rng() % 10 == 0 ? rng() % (pos + 1) : pos;  // mostly packed, some overlap
+      d[i].flags = (uint16_t)(i && rng() % 3 == 0 ? NS_DESC_CONT : 0);
+      pos = std::max<uint64_t>(pos, d[i].off + d[i].len) + rng() % 16;
+    }
+    const uint64_t arena = pos + 16;
+    const uint64_t budget = 1 + rng() % 200000;
+    const uint32_t max_desc = 1 + (uint32_t)(rng() % 500);
+    const bool chained = rng() % 2;
+    uint32_t k = 0;
+    while (k < n) {
+      uint32_t cut = 0;
+      uint64_t lo = 0, hi = 0;
+      CHECK(nsh::cut_chunk(d.data(), n, k, arena, budget, max_desc, chained, &cut, &lo, &hi) == NS_OK, "cut");
+      CHECK(cut > k && cut <= n, "progress %u -> %u", k, cut);
+      if (cut <= k || cut > n) break;
+      if (chained && cut < n) CHECK(!(d[cut].flags & NS_DESC_CONT), "chunk ends inside a run at %u", cut);
+      uint64_t l = UINT64_MAX, h = 0;
+      bool run_start = true;  // whether [k, cut) holds more than one run
+      uint32_t heads = 0;
+      for (uint32_t i = k; i < cut; ++i) {
+        if (d[i].len) {
+          l = std::min<uint64_t>(l, d[i].off);
+          h = std::max<uint64_t>(h, d[i].off + d[i].len);
+        }
+        if (i == k || !(chained && (d[i].flags & NS_DESC_CONT))) ++heads;
+      }
+      (void)run_start;
+      if (l == UINT64_MAX) l = h = 0;
+      CHECK(lo == l && hi == h, "span [%llu, %llu) vs [%llu, %llu)", (unsigned long long)lo,
+            (unsigned long long)hi, (unsigned long long)l, (unsigned long long)h);
+      if (heads > 1) CHECK(hi - lo <= budget && cut - k <= max_desc, "chunk over budget");
+      k = cut;
+    }
+    if (n) {
+      std::vector<ns_pkt_desc> bad = d;
+      bad[n / 2].off = arena + 1;
+      bad[n / 2].len = 1;
+      uint32_t kk = 0, cut = 0;
+      uint64_t lo, hi;
+      int rc = NS_OK;
+      while (kk < n && (rc = nsh::cut_chunk(bad.data(), n, kk, arena, budget, max_desc, chained, &cut, &lo, &hi)) ==
+                           NS_OK)
+        kk = cut;
+      CHECK(rc == NS_ERANGE, "bad descriptor -> NS_ERANGE (%d)", rc);
+    }
+  }
+}
+
+static void TestShardPlan(Rng& rng, int rounds) {
+  for (int round = 0; round < rounds; ++round) {
+    const uint32_t n = (uint32_t)(rng() % 5000);
+    const uint32_t parts = 1 + (uint32_t)(rng() % 9);
+    std::vector<ns_pkt_desc> d(n);
+    uint64_t total = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+      d[i].len = (uint32_t)(rng() % 9000);
+      d[i].flags = (uint16_t)(i && rng() % 4 == 0 ? NS_DESC_CONT : 0);
+      total += d[i].len;
+    }
+    std::vector<uint32_t> first(parts + 1);
+    nsh::shard_plan(d.data(), n, parts, first.data());
+    CHECK(first[0] == 0 && first[parts] == n, "ends");
+    for (uint32_t p = 0; p < parts; ++p) {
+      CHECK(first[p] <= first[p + 1], "ordered");
+      if (first[p] < n && p > 0 && first[p] > 0) CHECK(!(d[first[p]].flags & NS_DESC_CONT), "whole runs");
+    }
+    (void)total;
+  }
+}
+
+struct Req {
+  uint64_t in = 0, out = 0;
+  uint32_t ndesc = 1;
+  int rc = NS_OK;
+  std::atomic<bool> done{false};
+  uint64_t table_bytes() const { return (uint64_t)ndesc * 18 + 16; }
+};
+
+static void TestCombiner(int threads, int per_thread) {
+  nsh::FlatCombiner<Req> fc(4096);
+  std::atomic<uint64_t> passes{0}, served{0};
+  std::atomic<int> in_pass{0}, overlap{0};
+  std::atomic<size_t> max_batch{0};
+  auto run = [&](Req* const* rs, size_t n) {
+    if (in_pass.fetch_add(1) != 0) overlap.fetch_add(1);  // passes never overlap
+    // a pass takes a while (a GPU round trip): callers queue up meanwhile
+    const auto t0 = std::chrono::steady_clock::now();
+    while (std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(20)) {
+    }
+    for (size_t i = 0; i < n; ++i) rs[i]->out = rs[i]->in * 2654435761ull + 7;
+    if (n > max_batch.load()) max_batch.store(n);
+    passes.fetch_add(1);
+    served.fetch_add(n);
+    in_pass.fetch_sub(1);
+    return NS_OK;
+  };
+  std::atomic<int> wrong{0};
+  std::vector<std::thread> th;
+  for (int t = 0; t < threads; ++t) {
+    th.emplace_back([&, t]() {
+      Rng r((uint64_t)t * 7919 + 1);
+      for (int k = 0; k < per_thread; ++k) {
+        Req q;
+        q.in = r();
+        q.ndesc = 1 + (uint32_t)(r() % 100);
+        const int rc = fc.submit(&q, run);
+        if (rc != NS_OK || q.out != q.in * 2654435761ull + 7 || !q.done.load()) wrong.fetch_add(1);
+      }
+    });
+  }
+  for (auto& x : th) x.join();
+  CHECK(wrong.load() == 0, "%d wrong results", wrong.load());
+  CHECK(served.load() == (uint64_t)threads * per_thread, "served %llu", (unsigned long long)served.load());
+  CHECK(overlap.load() == 0, "passes overlapped");
+  std::printf("combiner: %d threads x %d requests in %llu passes (largest %zu requests)\n", threads, per_thread,
+              (unsigned long long)passes.load(), max_batch.load());
+}
+
+int main(int argc, char** argv) {
+  const bool quick = argc > 1 && std::strcmp(argv[1], "--quick") == 0;
+  Rng rng(20261016);
+  const int r = quick ? 20 : 200;
+  TestChains(rng, r);
+  TestClipViews(rng, 5 * r);
+  TestPackets(rng, 10 * r);
+  TestCutChunk(rng, r);
+  TestShardPlan(rng, r);
+  TestCombiner(16, quick ? 200 : 2000);
+  std::printf("%d checks, %d failed\n", g_run, g_fail);
+  return g_fail ? 1 : 0;
+}
