@@ -62,7 +62,9 @@ def main():
     for lab in ("cfg2", "cfg3", "cfg4"):
         if lab in out and "FETCH_SIZE" in out[lab]["avg"]:
             raw = out[lab]["avg"]["FETCH_SIZE"] * 1024.0
-            big = float(out[lab]["meta"].get("big_share", 0.0)) if lab != "cfg3" else 0.0
+            # cfg3's 64-B packets take the quad-lane direct path: nontemporal
+            # whole-line loads, the 16-lane-group shape (calib2164)
+            big = float(out[lab]["meta"].get("big_share", 0.0)) if lab != "cfg3" else 1.0
             shape = {"calib2164": big, "calib400": 1.0 - big}
             f = None
             if all(cal.get(m) for m, w in shape.items() if w > 0):
