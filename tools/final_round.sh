@@ -1,12 +1,14 @@
 set -e
-mkdir -p gpurun_out/final
-for c in 2 3 4 5 7 8; do
+# Every bench line of a round, on the GPU box: tools/final_round.sh TAG
+TAG=${1:-r02}
+OUT=gpurun_out/final_$TAG
+mkdir -p $OUT
+for c in 1 2 3 4 5 7 8; do
   echo "bench cfg$c"
-  timeout -k 10 300 python bench.py --config $c > gpurun_out/final/bench_cfg$c.json 2> gpurun_out/final/bench_cfg$c.err
+  timeout -k 10 300 python bench.py --config $c > $OUT/bench_cfg$c.json 2> $OUT/bench_cfg$c.err
 done
 echo "host modes"
-timeout -k 10 200 python bench.py --mode host --config 2 --no-cpu > gpurun_out/final/bench_host2.json 2>/dev/null
-timeout -k 10 200 python bench.py --mode host --config 4 --no-cpu > gpurun_out/final/bench_host4.json 2>/dev/null
-echo "profile"
-timeout -k 10 900 bash tools/profile.sh r01
+for c in 2 3 4; do
+  timeout -k 10 200 python bench.py --mode host --config $c --no-cpu --no-parity > $OUT/bench_host$c.json 2>/dev/null
+done
 echo done
