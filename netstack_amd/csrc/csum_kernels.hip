@@ -414,7 +414,12 @@ __device__ __forceinline__ uint32_t quad_sum(const Srd& r, const PktInfo& p) {
 // Returns this thread's packet sum (finish_tile turns it into the result).
 // FX = always the exact (T, W) accumulator (csum_split: its pieces' sums are
 // added, so they must be exact mod 2^32, not W-only class values).
-template <int WG, int TP, int GB, int UB, int US, int AUXB, bool GL, int SU, bool FX = false>
+// QS = quad-lane small runs (US = 4, SRD path only): a wave takes 64
+// consecutive small runs per iteration, lane l looking up run l and quad q of
+// load instruction j loading run 16 j + q, one chunk per lane; consecutive
+// runs lie back to back in memory when packets are packed, so one
+// instruction reads ~1 KiB contiguous and the loads are nontemporal.
+template <int WG, int TP, int GB, int UB, int US, int AUXB, bool GL, int SU, bool FX = false, bool QS = false>
 __device__ __forceinline__ uint32_t hyb_scan_tile(HybLds<WG>& L, const Srd& r, const PktInfo& p,
                                                   uint32_t big_chunks) {
   constexpr int P = WG;
@@ -567,6 +572,60 @@ __device__ __forceinline__ uint32_t hyb_scan_tile(HybLds<WG>& L, const Srd& r, c
       if (li == 0) atomicAdd(&L.acc[pk], sg);
     }
 
+    if constexpr (QS && !GL) {
+      static_assert(US == 4, "quad-lane small runs are runs of 4 chunks");
+      const uint32_t c = (uint32_t)lane & 3u;
+      for (uint32_t qb = (uint32_t)wv * 64u; qb < RSt; qb += (uint32_t)NW * 64u) {
+        // lane l describes run qb + l: SRD offset of its first chunk and a
+        // meta word nvalid (3 bits) | lo (4) | last chunk in run (1) | its
+        // index (2) | hiex (5) | phase (1) | packet (8)
+        const uint32_t q = qb + (uint32_t)lane;
+        uint32_t roff = r.oob, meta = 0u;
+        if (q < RSt) {
+          const int pk = search(L.rs, q);
+          const uint32_t k = q - L.rs[pk];
+          const uint4 inf = L.info[pk];
+          uint32_t ci0 = k * 4u, cend = inf.y;
+          if (inf.z & kSplitBit) {  // head runs cover [0, h), tail runs [ts, nch)
+            const uint32_t hh = (inf.z >> 10) & 15u, nh = (hh + 3u) / 4u;
+            if (k < nh) cend = hh;
+            else ci0 = inf.w + (k - nh) * 4u;
+          }
+          const uint32_t nv = min(cend - ci0, 4u);
+          const uint32_t lo = ci0 == 0u ? (inf.z & 15u) : 0u;
+          const uint32_t jl = inf.y - 1u - ci0;
+          const uint32_t has_last = jl < nv ? 1u : 0u;
+          meta = nv | (lo << 3) | (has_last << 7) | ((jl & 3u) << 8) | (((inf.z >> 5) & 31u) << 10) |
+                 ((inf.z >> 31) << 15) | ((uint32_t)pk << 16);
+          roff = inf.x + ci0 * 16u;
+        }
+        uint4 v[4];
+        uint32_t mj[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int src = (int)(16 * j + (lane >> 2));
+          mj[j] = (uint32_t)__shfl((int)meta, src, 64);
+          const uint32_t o = (uint32_t)__shfl((int)roff, src, 64);
+          v[j] = bload<2>(r.rsrc, c < (mj[j] & 7u) ? o + 16u * c : r.oob);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t m = mj[j];
+          const int lo_b = c == 0u ? (int)((m >> 3) & 15u) : 0;
+          const int hi_b = ((m >> 7) & 1u) && c == ((m >> 8) & 3u) ? (int)((m >> 10) & 31u) : 16;
+          uint4 w = v[j];
+          w.x &= bytes_below(hi_b) & ~bytes_below(lo_b);
+          w.y &= bytes_below(hi_b - 4) & ~bytes_below(lo_b - 4);
+          w.z &= bytes_below(hi_b - 8) & ~bytes_below(lo_b - 8);
+          w.w &= bytes_below(hi_b - 12) & ~bytes_below(lo_b - 12);
+          uint32_t T = 0, W = 0;
+          acc_chunk<EX>(w, T, W);
+          const uint32_t val = group_sum<4>(run_value<EX>(T, W, (m >> 15) & 1u));
+          if (c == 0u && (m & 7u)) atomicAdd(&L.acc[m >> 16], val);
+        }
+      }
+      return;
+    }
     static_assert(SU == 1 || SU == 2, "the small loop issues one or two runs per iteration");
     for (uint32_t q = (uint32_t)t; q < RSt; q += SU * WG) {
       uint4 va[US];
@@ -671,7 +730,7 @@ __device__ __forceinline__ void finish_tile(HybLds<P>& L, uint32_t s, const Pkt&
 // SU = small runs issued per lane per iteration; CH = chained batch
 // (finish_tile writes partials and continuation flags for fold_scan).
 template <int WG, int TP, int GB, int UB, int US, int AUXB, int UD = 0, bool WIN = false,
-          int SU = 1, bool CH = false>
+          int SU = 1, bool QS = false, bool CH = false>
 __global__ __launch_bounds__(WG) void csum_hyb(
     const uint8_t* __restrict__ arena, uint64_t arena_bytes,
     const uint4* __restrict__ desc, uint32_t n, uint16_t* __restrict__ out,
@@ -712,7 +771,8 @@ __global__ __launch_bounds__(WG) void csum_hyb(
       finish_tile<WG, CH>(L, s, d, mine, i, n, out, partial, store);
     }
     if (!__syncthreads_or(!small)) return;
-    const uint32_t s = hyb_scan_tile<WG, TP, GB, UB, US, AUXB, false, SU>(L, r, small ? PktInfo{} : p, big_chunks);
+    const uint32_t s =
+        hyb_scan_tile<WG, TP, GB, UB, US, AUXB, false, SU, false, QS>(L, r, small ? PktInfo{} : p, big_chunks);
     if (!small) finish_tile<WG, CH>(L, s, d, mine, i, n, out, partial, store);
     return;
   }
@@ -728,7 +788,7 @@ __global__ __launch_bounds__(WG) void csum_hyb(
       finish_tile<WG, CH>(L, s, d, mine, i, n, out, partial, store);
       return;
     }
-    const uint32_t s = hyb_scan_tile<WG, TP, GB, UB, US, AUXB, false, SU>(L, r, p, big_chunks);
+    const uint32_t s = hyb_scan_tile<WG, TP, GB, UB, US, AUXB, false, SU, false, QS>(L, r, p, big_chunks);
     finish_tile<WG, CH>(L, s, d, mine, i, n, out, partial, store);
   } else if constexpr (WIN) {
     // The tile spans >= 4 GiB: 64-bit global loads, fewer in flight per lane
@@ -1085,7 +1145,7 @@ static void launch_fold(ChainScratch ch, uint32_t n, uint16_t* out, const void* 
                      reinterpret_cast<const uint4*>(desc), arena);
 }
 
-template <int TP, int GB, int UB, int US, int AUXB, int UD, int SU = 1>
+template <int TP, int GB, int UB, int US, int AUXB, int UD, int SU = 1, bool QS = false>
 static hipError_t launch_hyb_tp(const uint8_t* arena, uint64_t arena_bytes, const void* desc,
                                 uint32_t n, uint16_t* out, uint32_t* partial,
                                 unsigned long long* err, hipStream_t stream, uint32_t big_chunks,
@@ -1097,7 +1157,7 @@ static hipError_t launch_hyb_tp(const uint8_t* arena, uint64_t arena_bytes, cons
   // plus the arena), else per-tile windows.
   const bool win = ((uintptr_t)arena & 15u) + arena_bytes + 64 >= kMaxSrdBytes;
 #define NSK_LAUNCH(W, C)                                                                              \
-  hipLaunchKernelGGL((csum_hyb<WG, TP, GB, UB, US, AUXB, UD, W, SU, C>), dim3(grid), dim3(WG), 0, \
+  hipLaunchKernelGGL((csum_hyb<WG, TP, GB, UB, US, AUXB, UD, W, SU, QS, C>), dim3(grid), dim3(WG), 0, \
                      stream, arena, arena_bytes, d, n, out, partial, err, big_chunks, store)
   if (partial) {
     if (win) NSK_LAUNCH(true, true);
@@ -1118,7 +1178,7 @@ static hipError_t launch_hyb_tp(const uint8_t* arena, uint64_t arena_bytes, cons
 // at 128 and 114 at 32; 64 KiB GSO buffers flat).
 constexpr uint64_t kTileBytes = 64u << 10;
 constexpr uint32_t kBigChunks = 40;  // packets of >= this many 16-B chunks take the 8-lane groups
-template <int GB, int UB, int US, int AUXB, int UD = 0, int SU = 1>
+template <int GB, int UB, int US, int AUXB, int UD = 0, int SU = 1, bool QS = false>
 static hipError_t launch_hyb(const uint8_t* arena, uint64_t arena_bytes, const void* desc,
                              uint32_t n, uint16_t* out, uint32_t* partial,
                              unsigned long long* err, hipStream_t stream, uint32_t big_chunks,
@@ -1127,12 +1187,12 @@ static hipError_t launch_hyb(const uint8_t* arena, uint64_t arena_bytes, const v
   const uint64_t want = tile_bytes / avg;
 #define NSK_TP(tp) \
   if (want >= tp)              \
-  return launch_hyb_tp<tp, GB, UB, US, AUXB, UD, SU>(arena, arena_bytes, desc, n, out, partial, err, stream, big_chunks, store)
+  return launch_hyb_tp<tp, GB, UB, US, AUXB, UD, SU, QS>(arena, arena_bytes, desc, n, out, partial, err, stream, big_chunks, store)
   if constexpr (UD > 0) {
     // The small-packet variant (launch_batch: < 256 B per descriptor) keeps
     // full tiles: its direct path is one packet per lane.
-    return launch_hyb_tp<256, GB, UB, US, AUXB, UD, SU>(arena, arena_bytes, desc, n, out, partial, err,
-                                                        stream, big_chunks, store);
+    return launch_hyb_tp<256, GB, UB, US, AUXB, UD, SU, QS>(arena, arena_bytes, desc, n, out, partial, err,
+                                                            stream, big_chunks, store);
   } else {
     NSK_TP(256);
     NSK_TP(128);
@@ -1142,8 +1202,8 @@ static hipError_t launch_hyb(const uint8_t* arena, uint64_t arena_bytes, const v
     NSK_TP(8);
     NSK_TP(4);
     NSK_TP(2);
-    return launch_hyb_tp<1, GB, UB, US, AUXB, UD, SU>(arena, arena_bytes, desc, n, out, partial, err, stream,
-                                                      big_chunks, store);
+    return launch_hyb_tp<1, GB, UB, US, AUXB, UD, SU, QS>(arena, arena_bytes, desc, n, out, partial, err, stream,
+                                                          big_chunks, store);
   }
 #undef NSK_TP
 }

@@ -220,10 +220,10 @@ __global__ __launch_bounds__(256) void calib_tile_x(const uint4* __restrict__ p,
   }
 }
 
-template <int GB, int UB, int US, int AUXB, uint32_t BIG, int UD = 0, int SU = 1>
+template <int GB, int UB, int US, int AUXB, uint32_t BIG, int UD = 0, int SU = 1, bool QS = false>
 hipError_t launch_h(const uint8_t* arena, uint64_t arena_bytes, const void* desc, uint32_t n,
                     uint16_t* out, unsigned long long* err, hipStream_t s) {
-  return launch_hyb<GB, UB, US, AUXB, UD, SU>(arena, arena_bytes, desc, n, out, nullptr, err, s, BIG);
+  return launch_hyb<GB, UB, US, AUXB, UD, SU, QS>(arena, arena_bytes, desc, n, out, nullptr, err, s, BIG);
 }
 
 // Floor for the 1M x 64 B layout only (desc[i].off == 64 * i): the same
@@ -391,7 +391,7 @@ template <int WG, int TP>
 hipError_t launch_wg(const uint8_t* arena, uint64_t arena_bytes, const void* desc, uint32_t n,
                      uint16_t* out, unsigned long long* err, hipStream_t s) {
   const uint32_t grid = (uint32_t)(((uint64_t)n + TP - 1) / TP);
-  hipLaunchKernelGGL((csum_hyb<WG, TP, 8, 16, 4, 2, 0, false, 2, false>), dim3(grid), dim3(WG), 0, s, arena,
+  hipLaunchKernelGGL((csum_hyb<WG, TP, 8, 16, 4, 2, 0, false, 2, false, false>), dim3(grid), dim3(WG), 0, s, arena,
                      arena_bytes, reinterpret_cast<const uint4*>(desc), n, out, nullptr, err, 64u, 0u);
   return hipGetLastError();
 }
@@ -687,6 +687,11 @@ struct Variant {
 // and DESIGN.md §4.2.
 static const Variant kVariants[] = {
     {"prod", launch_h<8, 16, 4, 2, kBigChunks, 0, 2>},  // the production big-packet launch
+    {"qs_b40", launch_h<8, 16, 4, 2, kBigChunks, 0, 2, true>},   // quad-lane nt small runs
+    {"qs_b24", launch_h<8, 16, 4, 2, 24, 0, 2, true>},
+    {"qs_b64", launch_h<8, 16, 4, 2, 64, 0, 2, true>},
+    {"qs_b1000", launch_h<8, 16, 4, 2, 1000, 0, 2, true>},     // every packet below 16 KB through small runs
+    {"prod_small_qs", launch_h<16, 8, 4, 2, 64, 5, 1, true>},
     {"prod_g8u16_b64", launch_h<8, 16, 4, 2, 64, 0, 2>},
     {"g8u16_su1", launch_h<8, 16, 4, 2, 64>},
     {"chained_main", launch_chained<false>},
