@@ -1145,12 +1145,12 @@ static void launch_fold(ChainScratch ch, uint32_t n, uint16_t* out, const void* 
                      reinterpret_cast<const uint4*>(desc), arena);
 }
 
-template <int TP, int GB, int UB, int US, int AUXB, int UD, int SU = 1, bool QS = false>
+template <int TP, int GB, int UB, int US, int AUXB, int UD, int SU = 1, bool QS = false, int WG = 256>
 static hipError_t launch_hyb_tp(const uint8_t* arena, uint64_t arena_bytes, const void* desc,
                                 uint32_t n, uint16_t* out, uint32_t* partial,
                                 unsigned long long* err, hipStream_t stream, uint32_t big_chunks,
                                 uint32_t store = 0) {
-  constexpr int WG = 256;
+  static_assert(TP <= WG, "a tile holds at most one descriptor per thread");
   const uint32_t grid = (uint32_t)(((uint64_t)n + TP - 1) / TP);
   const uint4* d = reinterpret_cast<const uint4*>(desc);
   // One SRD over the whole arena when it fits (arena base rounded down to 16 B

@@ -706,6 +706,14 @@ hipError_t launch_quad_prefetch(const uint8_t* arena, uint64_t arena_bytes, cons
   return hipGetLastError();
 }
 
+// The small-packet instance with one-wave workgroups (64 descriptors per
+// tile): the end-of-tile vote is then a one-wave barrier.
+template <int WGT>
+hipError_t launch_small_wg(const uint8_t* arena, uint64_t arena_bytes, const void* desc, uint32_t n,
+                           uint16_t* out, unsigned long long* err, hipStream_t s) {
+  return launch_hyb_tp<WGT, 16, 8, 4, 2, 5, 1, false, WGT>(arena, arena_bytes, desc, n, out, nullptr, err, s, 64u);
+}
+
 typedef hipError_t (*launch_fn)(const uint8_t*, uint64_t, const void*, uint32_t, uint16_t*,
                                 unsigned long long*, hipStream_t);
 struct Variant {
@@ -787,6 +795,8 @@ static const Variant kVariants[] = {
     {"quad_pipe2_nt", launch_quad_pipe<2, 2>},
     {"quad_direct_nt_wg512", launch_quad_direct<1, 2, 512>},
     {"quad_pf0", launch_quad_prefetch<0xFFFFFFFFu>},
+    {"small_wg64", launch_small_wg<64>},
+    {"small_wg128", launch_small_wg<128>},
     {"quad_pf256k", launch_quad_prefetch<262144u>},
     {"quad_pf512k", launch_quad_prefetch<524288u>},
     {"quad_pf128k", launch_quad_prefetch<131072u>},
