@@ -684,7 +684,6 @@ template <uint32_t D>
 __global__ __launch_bounds__(256) void quad_prefetch(const uint8_t* __restrict__ arena, uint64_t arena_bytes,
                                                      const uint4* __restrict__ desc, uint32_t n,
                                                      uint16_t* __restrict__ out, unsigned long long* __restrict__ err) {
-  const uint32_t l = threadIdx.x & 63;
   const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   const bool mine = i < n;
   const uint4 raw = mine ? desc[i] : make_uint4(0, 0, 0, 0);
