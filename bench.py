@@ -52,6 +52,8 @@ def parse():
                     help="BASELINE.json configs[k-1]; 7 = device-resident RX verification, "
                          "8 = device-resident TX checksum fill (SURVEY §8(f) ranks 2 and 1)")
     ap.add_argument("--mode", default="dev", choices=("dev", "host"))
+    ap.add_argument("--rx-layout", default="fused", choices=("fused", "chained"),
+                    help="--config 7/8 descriptor table: 2 independent descriptors per packet, or 3 chained")
     ap.add_argument("--rotate", type=int, default=0,
                     help="distinct batches cycled per step (0 = auto: enough to exceed the 256 MiB MALL)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline time budget")
@@ -459,11 +461,12 @@ RX_N = 1 << 20
 
 def packet_mode(args, dist, eng, dev, tx: bool):
     """Device-resident IPv4/TCP packet batches: 1M 1500-B
-    packets per GPU in HBM, three chained descriptors per packet (IPv4 header;
-    pseudo-header addresses; TCP header + payload), one
-    ns_csum_batch_dev(NS_BATCH_CHAINED) per step = the checksum kernel
-    (partial sums and continuation flags) plus the fold_scan pass that folds
-    the runs.
+    packets per GPU in HBM, two independent descriptors per packet
+    (workloads._tcp_desc, fused: the IPv4 header; the pseudo-header addresses
+    followed by the TCP header and payload, one contiguous piece with the
+    length and protocol words as its initial), one ns_csum_batch_dev per
+    step.  `--rx-layout chained` measures the three-descriptor chained table
+    instead (the checksum kernel plus the fold_scan pass that folds runs).
 
     RX (config 7, rank 2: segment.parse / the IPv4 header check): every
     1000th packet has a corrupted payload byte; the check after the timed
@@ -484,11 +487,14 @@ def packet_mode(args, dist, eng, dev, tx: bool):
     from netstack_amd import workloads as W
 
     seed = 7000 + dist.rank
+    fused = args.rx_layout == "fused"
+    chained = not fused
+    k = W.per_packet(fused)
     if tx:
-        arena, d = W.tx_batch(RX_N, seed, dev)
+        arena, d = W.tx_batch(RX_N, seed, dev, fused=fused)
         bad_idx = np.zeros(0, np.int64)
     else:
-        arena, d, bad_idx = W.rx_batch(RX_N, seed, dev, corrupt_every=1000)
+        arena, d, bad_idx = W.rx_batch(RX_N, seed, dev, corrupt_every=1000, fused=fused)
     desc = torch.from_numpy(d.view(np.uint8).copy()).to(dev)
     out = torch.empty(len(d), dtype=torch.int16, device=dev)
     stream = torch.cuda.current_stream(dev)
@@ -499,7 +505,7 @@ def packet_mode(args, dist, eng, dev, tx: bool):
         k = state["i"]
         if k == args.warmup:
             ev[0].record(stream)
-        eng.batch_tensors(arena, desc, out, chained=True, stream=stream, store=tx)
+        eng.batch_tensors(arena, desc, out, chained=chained, stream=stream, store=tx)
         state["i"] = k + 1
         if state["i"] == args.warmup + args.steps:
             ev[1].record(stream)
@@ -507,7 +513,7 @@ def packet_mode(args, dist, eng, dev, tx: bool):
     wall, _ = timed_region(step, torch.cuda.synchronize, dist, args.steps, args.warmup, dev)
     bad = eng.sync()
     kern_avg_s = ev[0].elapsed_time(ev[1]) / 1e3 / args.steps
-    k_cpu = 3 * 65536
+    k_cpu = k * 65536
     span = int(d["off"][k_cpu - 1] + d["len"][k_cpu - 1])
     if tx:
         # untimed: re-zero both fields, fill them with one launch, check
@@ -515,32 +521,32 @@ def packet_mode(args, dist, eng, dev, tx: bool):
         p[:, 10:12] = 0
         p[:, 36:38] = 0
         before = arena[:span].cpu().numpy() if dist.rank == 0 and not args.no_cpu else None
-        eng.batch_tensors(arena, desc, out, chained=True, stream=stream, store=True)
+        eng.batch_tensors(arena, desc, out, chained=chained, stream=stream, store=True)
         torch.cuda.synchronize()
         bad += eng.sync()
         rx, _, _ = W.rx_batch(RX_N, seed, dev)
         arena_ok = bool(torch.equal(arena, rx))
         del rx
-        chk = torch.from_numpy(W._tcp_desc(RX_N).view(np.uint8).copy()).to(dev)
-        vres = eng.batch_tensors(arena, chk, chained=True, stream=stream).cpu().numpy().view(np.uint16)
+        chk = torch.from_numpy(W._tcp_desc(RX_N, fused).view(np.uint8).copy()).to(dev)
+        vres = eng.batch_tensors(arena, chk, chained=chained, stream=stream).cpu().numpy().view(np.uint16)
         res = out.cpu().numpy().view(np.uint16)
-        ip_ok = vres[0::3] == 0xFFFF
-        tcp_fail = np.flatnonzero(vres[2::3] != 0xFFFF)
+        ip_ok = vres[0::k] == 0xFFFF
+        tcp_fail = np.flatnonzero(vres[k - 1::k] != 0xFFFF)
         prop_ok = arena_ok and bool(ip_ok.all()) and tcp_fail.size == 0
     else:
         before = None
         res = out.cpu().numpy().view(np.uint16)
-        ip_ok = res[0::3] == 0xFFFF
-        tcp_fail = np.flatnonzero(res[2::3] != 0xFFFF)
+        ip_ok = res[0::k] == 0xFFFF
+        tcp_fail = np.flatnonzero(res[k - 1::k] != 0xFFFF)
         prop_ok = bool(ip_ok.all()) and np.array_equal(tcp_fail, bad_idx)
     fails = dist.sum(0.0 if prop_ok else 1.0, dev)
     pkt_bytes = RX_N * W.RX_PKT
     total = dist.sum(float(pkt_bytes), dev)
     n_desc = len(d)
-    # packet bytes + the 8-B address re-read + per descriptor: 16-B read,
-    # u32 partial + u16 flag written, then read back, and a u16 result
-    # written; TX adds the two 2-B field stores per packet
-    algo = pkt_bytes + 8 * RX_N + n_desc * (16 + 6 + 6 + 2) + (4 * RX_N if tx else 0)
+    # packet bytes + the 8-B address re-read + per descriptor: 16-B read and
+    # a u16 result written (chained: also a u32 partial + u16 flag written,
+    # then read back); TX adds the two 2-B field stores per packet
+    algo = pkt_bytes + 8 * RX_N + n_desc * (16 + 2 + (12 if chained else 0)) + (4 * RX_N if tx else 0)
     achieved = algo / kern_avg_s / 1e9
     check = {"ipv4_all_valid": bool(ip_ok.all()), "tcp_failures": int(tcp_fail.size),
              "expected_failures": int(bad_idx.size), "ok": prop_ok, "ranks_failed": int(fails)}
@@ -555,11 +561,12 @@ def packet_mode(args, dist, eng, dev, tx: bool):
         "data": ("synthetic packets to send (checksum fields zero), resident in HBM" if tx else
                  "synthetic received packets (valid IPv4/TCP checksums, 1 in 1000 corrupted), resident in HBM"),
         "config": {"workload": ("tx" if tx else "rx") + ": 1,048,576 x 1500-B IPv4/TCP packets per GPU, "
-                   "3 chained descriptors each" + (", 2 checksum stores" if tx else ""),
+                   + ("2 descriptors each (IPv4 header; pseudo-header addresses + TCP segment)" if fused
+                      else "3 chained descriptors each") + (", 2 checksum stores" if tx else ""),
                    "packets_per_gpu": RX_N, "descriptors_per_gpu": n_desc},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "kernel": kernel_name(arena.numel(), n_desc, chained=True) + " + nsk::fold_scan",
+                     "kernel": kernel_name(arena.numel(), n_desc, chained=chained) + (" + nsk::fold_scan" if chained else ""),
                      "algorithmic_bytes_per_launch": algo, "avg_launch_us": kern_avg_s * 1e6},
         "bad_descriptors": bad,
         "property_check": check,
@@ -570,8 +577,8 @@ def packet_mode(args, dist, eng, dev, tx: bool):
         # CPU leg: the oracle on the first 65,536 packets' descriptors, same
         # bytes (TX: the bytes before the checked launch, and its stores)
         src = before if tx else arena[:span].cpu().numpy()
-        want, _ = O.c_batch(src, d[:k_cpu], chained=True)
-        ps = {"packets": k_cpu // 3, "bit_exact": bool(np.array_equal(res[:k_cpu], want))}
+        want, _ = O.c_batch(src, d[:k_cpu], chained=chained)
+        ps = {"packets": k_cpu // k, "bit_exact": bool(np.array_equal(res[:k_cpu], want))}
         if tx:
             stored, _ = O.apply_stores(src, d[:k_cpu], want)
             ps["stores_bit_exact"] = bool(np.array_equal(arena[:span].cpu().numpy(), stored))

@@ -92,11 +92,15 @@ struct ChainBuilder {
 
   // One chain (include/netstack_csum.h, ns_csum_chains): sum = initial,
   // odd = false; per piece (sum, odd) = calculateChecksum(piece, odd', sum)
-  // with odd' = false on a restart piece.  Continue pieces that follow each
-  // other in the arena merge into the open descriptor up to kMergeMax bytes
-  // (exact, see kMergeMax); a restart piece opens a new descriptor with
-  // odd = 0; empty pieces are skipped (checksum.go:73-75; Checksum(empty, x)
-  // == x).  A piece is never split.
+  // with odd' = false on a restart piece.  A piece that follows the open
+  // descriptor's bytes in the arena merges into it, up to kMergeMax bytes
+  // (exact, see kMergeMax): a continue piece always, a restart piece when the
+  // open descriptor ends on an even byte count (its first byte is then the
+  // high byte of a word either way, and Go's fold between the two calls
+  // gives the same value as summing on — DESIGN.md §2).  Otherwise a restart
+  // piece opens a new descriptor with odd = 0.  Empty pieces are skipped
+  // (checksum.go:73-75; Checksum(empty, x) == x), an empty restart piece
+  // still clearing the odd carry.  A piece is never split.
   void chain(const Piece* p, size_t np, uint16_t initial) {
     bool first_desc = true;
     uint32_t parity = 0;  // odd flag carried to the next continue piece
@@ -109,13 +113,17 @@ struct ChainBuilder {
     };
     for (size_t k = 0; k < np; ++k) {
       const uint64_t len = p[k].len;
-      if (p[k].restart) {
-        close();
-        parity = 0;
+      if (len == 0) {
+        if (p[k].restart) {
+          close();
+          parity = 0;
+        }
+        continue;
       }
-      if (len == 0) continue;
       const bool big = len > kMergeMax;
       const uint64_t at = bytes.append(p[k].p, len);
+      if (p[k].restart && parity != 0) close();  // odd carry pending: a new descriptor at odd = 0
+      if (p[k].restart) parity = 0;
       if (open && (big || cur.len + len > kMergeMax || at != cur.off + cur.len)) close();
       if (!open) {
         cur.off = at;

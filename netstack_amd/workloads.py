@@ -241,9 +241,34 @@ def _tcp_packets(n: int, seed: int, device):
     return arena, p
 
 
-def _tcp_desc(n: int) -> np.ndarray:
-    """The three-descriptor table over _tcp_packets (see rx_batch)."""
+def _tcp_desc(n: int, fused: bool = True) -> np.ndarray:
+    """The descriptor table over _tcp_packets (see rx_batch); per packet:
+
+    fused (2 independent descriptors):
+      2i    IPv4 header [0, 20), initial 0                  -> must sum to 0xffff
+      2i+1  [12, 1500): the pseudo-header addresses (in place in the packet)
+            followed directly by the TCP header and payload, initial =
+            ChecksumCombine(1480, 6), the length and protocol words
+    chained (3 descriptors, the second and third one NS_DESC_CONT run):
+      3i    IPv4 header [0, 20)
+      3i+1  src+dst addresses [12, 20), initial = ChecksumCombine(1480, 6)
+      3i+2  TCP header + payload [20, 1500), NS_DESC_CONT
+
+    Both compute segment.parse's xsum (segment.go:174-180): PseudoHeaderChecksum
+    then Checksum(h[:offset]) then ChecksumVV(payload) are restarts at even
+    offsets over contiguous bytes, and without a uint32 wrap (< 128 KiB) the
+    sum of the concatenation folds to the same value as the chain of folds
+    (both are fold1 of the same total, 0 only if every piece is
+    0).  The fused table needs no run folding."""
     base = np.arange(n, dtype=np.uint64) * np.uint64(RX_STRIDE)
+    if fused:
+        d = np.zeros(2 * n, dtype=DESC_DTYPE)
+        d["off"][0::2] = base
+        d["len"][0::2] = RX_IHL
+        d["off"][1::2] = base + np.uint64(12)
+        d["len"][1::2] = RX_PKT - 12
+        d["initial"][1::2] = RX_TCP + 6  # ChecksumCombine(1480, 6): no carry
+        return d
     d = np.zeros(3 * n, dtype=DESC_DTYPE)
     d["off"][0::3] = base
     d["len"][0::3] = RX_IHL
@@ -256,17 +281,20 @@ def _tcp_desc(n: int) -> np.ndarray:
     return d
 
 
-def rx_batch(n: int, seed: int, device, corrupt_every: int = 0):
+def per_packet(fused: bool) -> int:
+    """Descriptors per packet of _tcp_desc: the IPv4 header result is
+    out[0::k], the TCP result out[k-1::k]."""
+    return 2 if fused else 3
+
+
+def rx_batch(n: int, seed: int, device, corrupt_every: int = 0, fused: bool = True):
     """n received 1500-B IPv4/TCP packets packed at RX_STRIDE in HBM, with
     valid IPv4 and TCP checksums (RFC 1071, computed here with torch integer
     ops as plain data generation), and the descriptor table that verifies
-    them: per packet
-      3i    IPv4 header [0, 20), initial 0           -> must sum to 0xffff
-      3i+1  src+dst addresses [12, 20), initial = ChecksumCombine(1480, 6)
-            (PseudoHeaderChecksum, checksum.go:112-122: the length and
-            protocol words are host-known, the addresses are in the packet)
-      3i+2  TCP header + payload [20, 1500), NS_DESC_CONT (a restart over an
-            even-length piece: segment.go:177-179)  -> must sum to 0xffff
+    them (_tcp_desc: the IPv4 header must sum to 0xffff, and so must the TCP
+    segment with its pseudo-header — PseudoHeaderChecksum, checksum.go:
+    112-122: the length and protocol words are host-known, the addresses are
+    in the packet).
     With corrupt_every = k > 0, one payload byte of every k-th packet is
     flipped after its checksum was written (tcp_test.go:3246-3254): exactly
     those TCP sums fail.  Returns (arena uint8 tensor, desc, bad indices)."""
@@ -288,29 +316,33 @@ def rx_batch(n: int, seed: int, device, corrupt_every: int = 0):
     if bad.size:
         idx = torch.from_numpy(bad).to(device)
         p[idx, 100] ^= 0x5A
-    return arena, _tcp_desc(n), bad
+    return arena, _tcp_desc(n, fused), bad
 
 
 TX_IP_CSUM = 10   # header.IPv4 checksum field (ipv4.go:35 checksum offset)
 TX_TCP_CSUM = 16  # header.TCP checksum field, from the TCP header start
 
 
-def tx_desc(n: int) -> np.ndarray:
+def tx_desc(n: int, fused: bool = True) -> np.ndarray:
     """rx_batch's table with the stores of the transmit side (flags for
     ns_csum_batch_dev_store): the IPv4 run stores ^sum at byte 10
     (addIPHeader: ip.SetChecksum(^ip.CalculateChecksum()), ipv4.go:236) and
     the pseudo-header + TCP run stores ^sum at TCP byte 16 (buildTCPHdr:
     tcp.SetChecksum(^tcp.CalculateChecksum(xsum)), connect.go:662-663)."""
-    d = _tcp_desc(n)
-    d["flags"][0::3] |= 0x4 | (TX_IP_CSUM << 4)
-    d["flags"][2::3] |= 0x4 | (TX_TCP_CSUM << 4)
+    d = _tcp_desc(n, fused)
+    k = per_packet(fused)
+    d["flags"][0::k] |= 0x4 | (TX_IP_CSUM << 4)
+    # the TCP checksum field: TCP byte 16 = packet byte 36, from the TCP
+    # descriptor's start (byte 12 fused, byte 20 chained)
+    d["flags"][k - 1::k] |= 0x4 | ((RX_IHL + TX_TCP_CSUM - (12 if fused else RX_IHL)) << 4)
     return d
 
 
-def tx_batch(n: int, seed: int, device):
+def tx_batch(n: int, seed: int, device, fused: bool = True):
     """The transmit side of rx_batch: the same n packets with both checksum
-    fields zero, and tx_desc(n).  One ns_csum_batch_dev_store(CHAINED) launch
-    fills the fields in place; afterwards the arena equals
-    rx_batch(n, seed)'s byte for byte.  Returns (arena, desc)."""
+    fields zero, and tx_desc(n).  One ns_csum_batch_dev_store launch (with
+    NS_BATCH_CHAINED for the chained table) fills the fields in place;
+    afterwards the arena equals rx_batch(n, seed)'s byte for byte.  Returns
+    (arena, desc)."""
     arena, _ = _tcp_packets(n, seed, device)
-    return arena, tx_desc(n)
+    return arena, tx_desc(n, fused)

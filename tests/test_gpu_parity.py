@@ -569,24 +569,28 @@ def test_concurrent_small_calls_are_combined_bit_exact(engine):
     assert not errors, errors[:5]
 
 
-def test_rx_verification_batch_device_resident(engine):
+@pytest.mark.parametrize("fused", [True, False])
+def test_rx_verification_batch_device_resident(engine, fused):
     """SURVEY §8(f) rank 2 on the device: received IPv4/TCP packets in HBM,
-    three chained descriptors per packet (workloads.rx_batch), one chained
-    batch_dev.  Every result bit-exact with the oracle, every IPv4 header and
-    every intact TCP segment sums to 0xffff, exactly the corrupted ones fail."""
+    two independent descriptors per packet (fused: the pseudo-header
+    addresses and the TCP segment as one contiguous piece) or three chained
+    ones (workloads.rx_batch), one batch_dev.  Every result bit-exact with
+    the oracle, every IPv4 header and every intact TCP segment sums to
+    0xffff, exactly the corrupted ones fail."""
     import oracle as O
     from netstack_amd import workloads as W
 
     torch = _torch()
-    arena, d, bad_idx = W.rx_batch(20000, 77, "cuda", corrupt_every=97)
+    k = W.per_packet(fused)
+    arena, d, bad_idx = W.rx_batch(20000, 77, "cuda", corrupt_every=97, fused=fused)
     desc = torch.from_numpy(d.view(np.uint8).copy()).cuda()
-    out = engine.batch_tensors(arena, desc, chained=True)
+    out = engine.batch_tensors(arena, desc, chained=not fused)
     torch.cuda.synchronize()
     got = out.cpu().numpy().view(np.uint16)
-    want, nbad = O.c_batch(arena.cpu().numpy(), d, chained=True)
+    want, nbad = O.c_batch(arena.cpu().numpy(), d, chained=not fused)
     assert nbad == 0 and np.array_equal(got, want)
-    assert (got[0::3] == 0xFFFF).all()
-    assert np.array_equal(np.flatnonzero(got[2::3] != 0xFFFF), bad_idx)
+    assert (got[0::k] == 0xFFFF).all()
+    assert np.array_equal(np.flatnonzero(got[k - 1::k] != 0xFFFF), bad_idx)
 
 
 @pytest.mark.parametrize("seed", range(12))
@@ -623,24 +627,27 @@ def test_randomized_layouts(engine, seed):
         assert np.array_equal(engine.batch_host(arena, d, chained=chained), want)
 
 
-def test_tx_store_device_resident(engine):
+@pytest.mark.parametrize("fused", [True, False])
+def test_tx_store_device_resident(engine, fused):
     """The transmit side on the device (ns_csum_batch_dev_store): tx_batch's
-    packets with zeroed IPv4/TCP checksum fields, one chained launch computes
-    and stores both fields in place (ipv4.go:236, connect.go:662-663).  The
-    arena afterwards equals rx_batch's (checksums made independently by torch
-    integer ops), the results match the oracle over the pre-store bytes, and
-    the RX table over the stored packets sums every run to 0xffff."""
+    packets with zeroed IPv4/TCP checksum fields, one launch computes and
+    stores both fields in place (ipv4.go:236, connect.go:662-663): from the
+    main kernel (fused table) or from the run-folding pass (chained table).
+    The arena afterwards equals rx_batch's (checksums made independently by
+    torch integer ops), the results match the oracle over the pre-store
+    bytes, and the RX table over the stored packets verifies."""
     import oracle as O
     from netstack_amd import workloads as W
 
     torch = _torch()
     n = 20000
-    arena, d = W.tx_batch(n, 77, "cuda")
+    k = W.per_packet(fused)
+    arena, d = W.tx_batch(n, 77, "cuda", fused=fused)
     before = arena.cpu().numpy()
-    want, nbad = O.c_batch(before, d, chained=True)
+    want, nbad = O.c_batch(before, d, chained=not fused)
     assert nbad == 0
     desc = torch.from_numpy(d.view(np.uint8).copy()).cuda()
-    out = engine.batch_tensors(arena, desc, chained=True, store=True)
+    out = engine.batch_tensors(arena, desc, chained=not fused, store=True)
     torch.cuda.synchronize()
     assert engine.sync() == 0
     assert np.array_equal(out.cpu().numpy().view(np.uint16), want)
@@ -649,11 +656,11 @@ def test_tx_store_device_resident(engine):
     assert dropped == 0 and np.array_equal(after, expect)
     rx, _, _ = W.rx_batch(n, 77, "cuda")
     assert torch.equal(arena, rx)
-    rd = torch.from_numpy(W._tcp_desc(n).view(np.uint8).copy()).cuda()
-    chk = engine.batch_tensors(arena, rd, chained=True)
+    rd = torch.from_numpy(W._tcp_desc(n, fused).view(np.uint8).copy()).cuda()
+    chk = engine.batch_tensors(arena, rd, chained=not fused)
     torch.cuda.synchronize()
-    assert (chk.cpu().numpy().view(np.uint16)[0::3] == 0xFFFF).all()
-    assert (chk.cpu().numpy().view(np.uint16)[2::3] == 0xFFFF).all()
+    assert (chk.cpu().numpy().view(np.uint16)[0::k] == 0xFFFF).all()
+    assert (chk.cpu().numpy().view(np.uint16)[k - 1::k] == 0xFFFF).all()
 
 
 def _store_batch(rng, n, chained, big):

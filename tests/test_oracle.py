@@ -119,20 +119,23 @@ def test_batch_mt_matches(oracle_mod):
     assert (got == want).all()
 
 
-def test_rx_batch_generator_valid_packets():
+@pytest.mark.parametrize("fused", [True, False])
+def test_rx_batch_generator_valid_packets(fused):
     """workloads.rx_batch writes valid IPv4 and TCP checksums (checked by the
     oracle composed as segment.parse and the IPv4 header check do) and breaks
-    exactly the packets it says it corrupts."""
+    exactly the packets it says it corrupts; the fused table (2 independent
+    descriptors per packet) gives exactly the chained table's results."""
     import torch  # noqa: F401  (generator runs on the CPU device here)
 
     import oracle as O
     from netstack_amd import workloads as W
 
-    arena, d, bad = W.rx_batch(700, 3, "cpu", corrupt_every=11)
-    out, nbad = O.c_batch(arena.numpy(), d, chained=True)
+    k = W.per_packet(fused)
+    arena, d, bad = W.rx_batch(700, 3, "cpu", corrupt_every=11, fused=fused)
+    out, nbad = O.c_batch(arena.numpy(), d, chained=not fused)
     assert nbad == 0
-    assert (out[0::3] == 0xFFFF).all()
-    assert np.array_equal(np.flatnonzero(out[2::3] != 0xFFFF), bad)
+    assert (out[0::k] == 0xFFFF).all()
+    assert np.array_equal(np.flatnonzero(out[k - 1::k] != 0xFFFF), bad)
     # the same TCP sums from the pure-Python chain of segment.parse (:176-180)
     a = arena.numpy()
     for i in (0, 1, 11, 699):
@@ -140,10 +143,14 @@ def test_rx_batch_generator_valid_packets():
         xsum = O.py_pseudo_header(6, bytes(a[b + 12:b + 16]), bytes(a[b + 16:b + 20]), 1480)
         xsum = O.py_checksum(bytes(a[b + 20:b + 40]), xsum)
         xsum = O.py_checksum(bytes(a[b + 40:b + 1500]), xsum)
-        assert xsum == out[3 * i + 2]
+        assert xsum == out[k * i + k - 1]
+    other, _ = O.c_batch(a, W._tcp_desc(700, not fused), chained=fused)
+    kk = W.per_packet(not fused)
+    assert np.array_equal(other[0::kk], out[0::k]) and np.array_equal(other[kk - 1::kk], out[k - 1::k])
 
 
-def test_tx_stores_reproduce_rx_packets():
+@pytest.mark.parametrize("fused", [True, False])
+def test_tx_stores_reproduce_rx_packets(fused):
     """oracle.apply_stores over tx_batch (zeroed checksum fields, the store
     flags of ns_csum_batch_dev_store) yields exactly rx_batch's packets, whose
     checksums torch integer ops wrote independently; the IPv4 store matches
@@ -152,10 +159,10 @@ def test_tx_stores_reproduce_rx_packets():
     import oracle as O
     from netstack_amd import workloads as W
 
-    tx, d = W.tx_batch(300, 9, "cpu")
+    tx, d = W.tx_batch(300, 9, "cpu", fused=fused)
     rx, _, _ = W.rx_batch(300, 9, "cpu")
     before = tx.numpy()
-    res, nbad = O.c_batch(before, d, chained=True)
+    res, nbad = O.c_batch(before, d, chained=not fused)
     assert nbad == 0
     after, dropped = O.apply_stores(before, d, res)
     assert dropped == 0 and np.array_equal(after, rx.numpy())
