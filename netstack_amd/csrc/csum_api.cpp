@@ -120,6 +120,13 @@ struct PinBuf {
 // the launch and reads results only after hipStreamSynchronize — but it is
 // not safe for polling a buffer while a kernel runs.
 using MappedPin = PinBuf<uint8_t, hipHostMallocMapped | hipHostMallocNonCoherent | hipHostMallocPortable>;
+// Mapped, fine-grained (coherent) host memory: device stores reach it
+// uncached, in order, so the host may poll it while kernels run.  A zero-copy
+// pass writes its results here and then a completion word (nsk::launch_signal,
+// a system-scope release store), which the caller spins on instead of
+// hipStreamSynchronize: the stream's own completion arrives ~10 us after the
+// kernel's last store (tools/sync_probe.hip).
+using CoherentPin = PinBuf<uint8_t, hipHostMallocMapped | hipHostMallocCoherent | hipHostMallocPortable>;
 
 // Chained-batch scratch (csum_kernels.h ChainScratch): partials + flags, and
 // the fold statuses in a buffer of their own, zeroed once at allocation.
@@ -194,8 +201,12 @@ struct ns_csum_ctx {
   ChainBuf d_chain[2];
   PinBuf<ns_pkt_desc> h_desc[2];
   PinBuf<uint16_t> h_out[2];
-  // zero-copy pass buffer for small calls: [table | results]
+  // zero-copy pass buffers for small calls: the table (read by the kernel),
+  // the results and the completion word (written by it)
   MappedPin z_buf;
+  CoherentPin z_res;
+  CoherentPin z_done;
+  uint32_t z_seq = 0;
   // flat combining of concurrent small calls (nsh::FlatCombiner)
   nsh::FlatCombiner<SmallReq> combiner{kPassTableBytes};
   // the pool of mapped staging buffers small calls gather into; guarded by qmu
@@ -261,9 +272,10 @@ int run_zero_copy(ns_csum_ctx* ctx, SmallReq* const* reqs, size_t nreq) {
     chained = chained || reqs[r]->chained;
   }
   if (nd == 0) return NS_OK;
-  const uint64_t o_off = nd * sizeof(ns_pkt_desc);
   int rc;
-  if ((rc = ctx->z_buf.ensure(std::max<uint64_t>(kPassTableBytes, o_off + nd * 2))) != NS_OK) return rc;
+  if ((rc = ctx->z_buf.ensure(std::max<uint64_t>(kPassTableBytes, nd * sizeof(ns_pkt_desc)))) != NS_OK) return rc;
+  if ((rc = ctx->z_res.ensure(std::max<uint64_t>(kPassTableBytes / 8, nd * 2))) != NS_OK) return rc;
+  if ((rc = ctx->z_done.ensure(64)) != NS_OK) return rc;
   if (chained && (rc = ctx->d_chain[0].ensure(nd)) != NS_OK) return rc;
   uint8_t* z = ctx->z_buf.p;
   ns_pkt_desc* zd = reinterpret_cast<ns_pkt_desc*>(z);
@@ -284,13 +296,28 @@ int run_zero_copy(ns_csum_ctx* ctx, SmallReq* const* reqs, size_t nreq) {
       }
     }
   }
-  uint8_t* zdev = ctx->z_buf.dev;
   hipStream_t s = ctx->stream[0];
-  HIP_TRY(nsk::launch_batch(nullptr, kWholeSpace, zdev, (uint32_t)nd, reinterpret_cast<uint16_t*>(zdev + o_off),
+  HIP_TRY(nsk::launch_batch(nullptr, kWholeSpace, ctx->z_buf.dev, (uint32_t)nd,
+                            reinterpret_cast<uint16_t*>(ctx->z_res.dev),
                             chained ? ctx->d_chain[0].get() : nsk::ChainScratch{}, ctx->d_err, s,
                             std::max<uint64_t>(nb, 1)));
-  HIP_TRY(hipStreamSynchronize(s));
-  const uint16_t* res = reinterpret_cast<const uint16_t*>(z + o_off);
+  // Completion: the pass's last kernel is followed on the stream by a store of
+  // the pass's sequence number into coherent host memory; spin for it, and
+  // only if it is late (a fault, or a busy device) wait on the stream itself,
+  // which also reports a failed kernel.
+  uint32_t seq = ++ctx->z_seq;
+  if (seq == 0) seq = ++ctx->z_seq;
+  uint32_t* done = reinterpret_cast<uint32_t*>(ctx->z_done.p);
+  HIP_TRY(nsk::launch_signal(reinterpret_cast<uint32_t*>(ctx->z_done.dev), seq, s));
+  const auto t0 = std::chrono::steady_clock::now();
+  for (uint32_t spin = 0; __atomic_load_n(done, __ATOMIC_ACQUIRE) != seq; ++spin) {
+    if ((spin & 255u) == 255u && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) {
+      HIP_TRY(hipStreamSynchronize(s));
+      if (__atomic_load_n(done, __ATOMIC_ACQUIRE) != seq) return NS_EHIP;
+      break;
+    }
+  }
+  const uint16_t* res = reinterpret_cast<const uint16_t*>(ctx->z_res.p);
   for (size_t r = 0; r < nreq; ++r) {
     std::memcpy(reqs[r]->res, res, (size_t)reqs[r]->ndesc * 2);
     res += reqs[r]->ndesc;
@@ -686,6 +713,8 @@ void ns_csum_destroy(ns_csum_ctx* ctx) {
     ctx->scratch.clear();
     ctx->err_taken.release();
     ctx->z_buf.release();
+    ctx->z_res.release();
+    ctx->z_done.release();
     for (MappedPin* b : ctx->stage_all) {
       b->release();
       delete b;

@@ -53,6 +53,11 @@ hipError_t launch_batch(const uint8_t* arena, uint64_t arena_bytes,
 // `taken` must be device-visible (mapped host memory).
 hipError_t launch_take_err(unsigned long long* err, unsigned long long* taken, hipStream_t stream);
 
+// Store `seq` into *flag (mapped fine-grained host memory) with a
+// system-scope release once the stream's earlier work is done: the completion
+// word a zero-copy pass's caller spins on.
+hipError_t launch_signal(uint32_t* flag, uint32_t seq, hipStream_t stream);
+
 // Rewrite n device-resident descriptors' offsets relative to `bias` (empty
 // descriptors get 0): the host pipeline's per-chunk table rebase.
 hipError_t launch_rebase(void* desc, uint32_t n, uint64_t bias, hipStream_t stream);

@@ -1221,6 +1221,15 @@ __global__ void take_err(unsigned long long* __restrict__ err, unsigned long lon
   if (threadIdx.x == 0) *taken = atomicExch(err, 0ull);
 }
 
+__global__ void signal_host(uint32_t* __restrict__ flag, uint32_t seq) {
+  if (threadIdx.x == 0) __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+hipError_t launch_signal(uint32_t* flag, uint32_t seq, hipStream_t stream) {
+  hipLaunchKernelGGL(signal_host, dim3(1), dim3(64), 0, stream, flag, seq);
+  return hipGetLastError();
+}
+
 hipError_t launch_take_err(unsigned long long* err, unsigned long long* taken, hipStream_t stream) {
   hipLaunchKernelGGL(take_err, dim3(1), dim3(64), 0, stream, err, taken);
   return hipGetLastError();
