@@ -296,7 +296,7 @@ def kernel_name(arena_bytes: int, n: int, chained: bool = False) -> str:
         want = (64 << 10) // max(arena_bytes // n, 1)  # kTileBytes
         tp = next((t for t in (256, 128, 64, 32, 16, 8, 4, 2) if want >= t), 1)
         return f"nsk::csum_hyb<256,{tp},8,16,4,2,0,{win},2,{ch}>"
-    return f"nsk::csum_hyb<256,256,16,8,4,2,5,{win},1,{ch}>"
+    return f"nsk::csum_hyb<64,64,16,8,4,2,5,{win},1,{ch}>"
 
 
 def main():

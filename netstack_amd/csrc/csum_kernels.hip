@@ -1190,9 +1190,14 @@ static hipError_t launch_hyb(const uint8_t* arena, uint64_t arena_bytes, const v
   return launch_hyb_tp<tp, GB, UB, US, AUXB, UD, SU, QS>(arena, arena_bytes, desc, n, out, partial, err, stream, big_chunks, store)
   if constexpr (UD > 0) {
     // The small-packet variant (launch_batch: < 256 B per descriptor) keeps
-    // full tiles: its direct path is one packet per lane.
-    return launch_hyb_tp<256, GB, UB, US, AUXB, UD, SU, QS>(arena, arena_bytes, desc, n, out, partial, err,
-                                                            stream, big_chunks, store);
+    // full tiles of one-wave workgroups: its direct path is one packet per
+    // lane, and a one-wave workgroup retires (and frees its slot for the next
+    // tile) as soon as its own packets are done.  1M x 64 B with the
+    // descriptor tables rotated past the MALL, as bench.py runs it: 15.5-15.7
+    // vs 16.7 us for 256-thread tiles (tools/tune.py --rot-desc,
+    // profiles/r02/tune_small_wg_rotdesc.log; 128-B packets -1%, 192-B +2%).
+    return launch_hyb_tp<64, GB, UB, US, AUXB, UD, SU, QS, 64>(arena, arena_bytes, desc, n, out, partial, err,
+                                                               stream, big_chunks, store);
   } else {
     NSK_TP(256);
     NSK_TP(128);

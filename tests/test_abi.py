@@ -133,7 +133,7 @@ def test_product_kernels_never_spill_and_keep_occupancy():
     for k, v in kernels.items():
         assert v["ScratchSize"] == 0, (k, v)
     for k, v in hyb.items():
-        small = "ILi256ELi256ELi16ELi8ELi4ELi2ELi5E" in k
+        small = "ILi64ELi64ELi16ELi8ELi4ELi2ELi5E" in k
         windowed = "Li5ELb1E" in k or "Li0ELb1E" in k  # WIN = true: carries the 64-bit-address fallback too
         chained = "Lb1EEEv" in k  # CH = true (the last template argument)
         assert v["Occupancy"] >= (8 if small else 4 if (windowed or chained) else 6), (k, v)

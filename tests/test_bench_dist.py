@@ -120,4 +120,4 @@ def test_cfg5_strong_scaling_shards_reproduce_the_whole_batch():
         assert np.array_equal(np.concatenate(got), want)
     assert "true" in bench.kernel_name(12_583_000_000, 8 << 20)
     assert bench.kernel_name(1_577_058_304, 1 << 20) == "nsk::csum_hyb<256,32,8,16,4,2,0,false,2,false>"
-    assert bench.kernel_name(67_108_864, 1 << 20) == "nsk::csum_hyb<256,256,16,8,4,2,5,false,1,false>"
+    assert bench.kernel_name(67_108_864, 1 << 20) == "nsk::csum_hyb<64,64,16,8,4,2,5,false,1,false>"

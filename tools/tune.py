@@ -76,6 +76,8 @@ def main():
     ap.add_argument("--calib-blocks", default="4096,8192,16384")
     ap.add_argument("--json", default="")
     ap.add_argument("--b2b", action="store_true", help="time back-to-back launches (as bench.py does)")
+    ap.add_argument("--rot-desc", action="store_true",
+                    help="rotate copies of the descriptor table with the arenas (cold tables, as bench.py)")
     ap.add_argument("--n", default="", help="packet counts per config, e.g. 2:2097152")
     args = ap.parse_args()
 
@@ -106,6 +108,7 @@ def main():
             arenas = [b.arena_device(dev)] + [W.random_bytes_torch(b.seed + 77 * r, b.arena_bytes, dev)
                                               for r in range(1, rot)]
         desc = torch.from_numpy(b.desc.view(np.uint8).copy()).to(dev)
+        descs = [desc] + [desc.clone() for _ in range(1, rot)] if args.rot_desc else [desc] * rot
         ref = eng.batch_tensors(arenas[0], desc)
         torch.cuda.synchronize()
         ref = ref.cpu()
@@ -117,8 +120,9 @@ def main():
         def launcher(v):
             def f():
                 a = arenas[state["k"] % rot]
+                dd = descs[state["k"] % rot]
                 state["k"] += 1
-                rc = L.nsk_tune_launch(v, a.data_ptr(), b.arena_bytes, desc.data_ptr(), b.n,
+                rc = L.nsk_tune_launch(v, a.data_ptr(), b.arena_bytes, dd.data_ptr(), b.n,
                                        out.data_ptr(), err.data_ptr(), sp)
                 assert rc == 0
             return f
