@@ -387,12 +387,12 @@ hipError_t launch_fold_walk(const uint8_t* arena, uint64_t arena_bytes, const vo
 }
 
 // Workgroup size with the tile: WG threads own TP descriptors.
-template <int WG, int TP>
+template <int WG, int TP, uint32_t BIG = 64>
 hipError_t launch_wg(const uint8_t* arena, uint64_t arena_bytes, const void* desc, uint32_t n,
                      uint16_t* out, unsigned long long* err, hipStream_t s) {
   const uint32_t grid = (uint32_t)(((uint64_t)n + TP - 1) / TP);
   hipLaunchKernelGGL((csum_hyb<WG, TP, 8, 16, 4, 2, 0, false, 2, false, false>), dim3(grid), dim3(WG), 0, s, arena,
-                     arena_bytes, reinterpret_cast<const uint4*>(desc), n, out, nullptr, err, 64u, 0u);
+                     arena_bytes, reinterpret_cast<const uint4*>(desc), n, out, nullptr, err, BIG, 0u);
   return hipGetLastError();
 }
 
@@ -806,6 +806,13 @@ static const Variant kVariants[] = {
     {"floor_quad_nt_wg64", launch_floor_quad<1, 2, 64>},
     {"quad_pipe4_nt", launch_quad_pipe<4, 2>},
     {"quad_pipe8_nt", launch_quad_pipe<8, 2>},
+    // the group kernel at smaller workgroups, production group threshold
+    {"wg64_tp8_b40", launch_wg<64, 8, kBigChunks>},
+    {"wg64_tp16_b40", launch_wg<64, 16, kBigChunks>},
+    {"wg128_tp16_b40", launch_wg<128, 16, kBigChunks>},
+    {"wg128_tp32_b40", launch_wg<128, 32, kBigChunks>},
+    {"wg256_tp32_b40", launch_wg<256, 32, kBigChunks>},
+    {"wg256_tp64_b40", launch_wg<256, 64, kBigChunks>},
 };
 
 }  // namespace nsk

@@ -76,6 +76,7 @@ def main():
     ap.add_argument("--calib-blocks", default="4096,8192,16384")
     ap.add_argument("--json", default="")
     ap.add_argument("--b2b", action="store_true", help="time back-to-back launches (as bench.py does)")
+    ap.add_argument("--rot", type=int, default=0, help="distinct arenas cycled (0: 4 for cfg3, else 1)")
     ap.add_argument("--rot-desc", action="store_true",
                     help="rotate copies of the descriptor table with the arenas (cold tables, as bench.py)")
     ap.add_argument("--n", default="", help="packet counts per config, e.g. 2:2097152")
@@ -95,7 +96,7 @@ def main():
 
     nover = dict((int(k), int(v)) for k, v in (x.split(":") for x in args.n.split(",") if x))
     for cfg in [int(c) for c in args.configs.split(",")]:
-        rot = 4 if cfg == 3 else 1
+        rot = args.rot or (4 if cfg == 3 else 1)
         if cfg == 7:  # bench.py --config 7's RX batch, timed unchained (the main kernel)
             a7, d7, _ = W.rx_batch(nover.get(7, 1 << 20), 7000, dev)
             b = W.Batch("rx_1Mx1500_3desc", 7000, d7, a7.numel())
