@@ -1178,6 +1178,12 @@ static hipError_t launch_hyb_tp(const uint8_t* arena, uint64_t arena_bytes, cons
 // at 128 and 114 at 32; 64 KiB GSO buffers flat).
 constexpr uint64_t kTileBytes = 64u << 10;
 constexpr uint32_t kBigChunks = 40;  // packets of >= this many 16-B chunks take the 8-lane groups
+// ... in a zero-copy pass: 32 KiB, what one workgroup's lane loop covers in
+// one iteration (256 lanes x 2 runs x 4 chunks); a larger packet's body goes
+// to the groups, 64 KiB per iteration (one 64 KiB Checksum: 19.4 us that
+// way, 26.8 us through the lane runs)
+constexpr uint32_t kZeroCopyBigChunks = 2048;
+constexpr uint64_t kZeroCopyTileBytes = 16u << 10;  // ... and its tiles
 template <int GB, int UB, int US, int AUXB, int UD = 0, int SU = 1, bool QS = false>
 static hipError_t launch_hyb(const uint8_t* arena, uint64_t arena_bytes, const void* desc,
                              uint32_t n, uint16_t* out, uint32_t* partial,
@@ -1269,8 +1275,19 @@ hipError_t launch_batch(const uint8_t* arena, uint64_t arena_bytes,
     // 704-960-B packets (960 B: 219.8 vs 253.5 us per 1.5 GB) and ties it
     // elsewhere; at 36 chunks and below the groups lose (576 B: 277.7 vs
     // 253.4 us).
-    e = launch_hyb<8, 16, 4, 2, 0, 2>(arena, arena_bytes, desc, n, out, part, err, stream, kBigChunks,
-                                      sizing_bytes, kTileBytes, store);
+    // A zero-copy pass (arena == nullptr: descriptors hold absolute addresses
+    // of mapped host memory, csum_api.cpp run_zero_copy) is PCIe-latency
+    // bound, not bandwidth bound: it sends packets below 32 KiB through the
+    // lane runs (the group loop and the lane loop are two dependent PCIe
+    // round trips per tile, the lane loop alone one) and cuts 16 KiB tiles
+    // (more workgroups, so a 64 KiB call's lane runs are all in flight at
+    // once).  tools/latency.cc, same box, against groups and 64 KiB tiles:
+    // Checksum(1500 B) 12.7-13.1 vs 14.8-14.9 us, the 45-segment VV batch
+    // 15.8-16.0 vs 18.9-19.5, 45 chained segments 14.9-15.5 vs 18.2,
+    // 1 MiB of packets 44.7-45.3 vs 50.7-50.9 (profiles/r02/latency_zc_ab.txt).
+    e = launch_hyb<8, 16, 4, 2, 0, 2>(arena, arena_bytes, desc, n, out, part, err, stream,
+                                      arena ? kBigChunks : kZeroCopyBigChunks, sizing_bytes,
+                                      arena ? kTileBytes : kZeroCopyTileBytes, store);
   } else {
     // Small packets: the same kernel plus the direct path — a tile whose
     // packets all span <= 5 chunks (any <= 65-B packet) has each lane read its

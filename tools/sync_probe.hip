@@ -54,6 +54,35 @@ __global__ void tiny(const uint8_t* __restrict__ in, uint32_t n, uint32_t* __res
   }
 }
 
+// One 16-B descriptor {off, len} then its payload, 16-B chunks, all from
+// mapped host memory (two dependent PCIe round trips), or the descriptor by
+// value in the kernel arguments (one): res[0] = byte sum, then the flag.
+struct Desc {
+  uint64_t off;
+  uint32_t len, pad;
+};
+template <bool BYVAL>
+__global__ void desc_then_payload(const uint8_t* __restrict__ base, const Desc* __restrict__ dptr, Desc dval,
+                                  uint32_t* __restrict__ res, uint32_t* __restrict__ flag, uint32_t seq) {
+  __shared__ uint32_t tot;
+  if (threadIdx.x == 0) tot = 0;
+  const Desc d = BYVAL ? dval : dptr[0];
+  __syncthreads();
+  uint32_t s = 0;
+  const uint4* p = reinterpret_cast<const uint4*>(base + d.off);
+  for (uint32_t i = threadIdx.x; i < d.len / 16; i += blockDim.x) {
+    const uint4 v = p[i];
+    s += __builtin_amdgcn_sad_u8(v.x, 0u, 0u) + __builtin_amdgcn_sad_u8(v.y, 0u, 0u) +
+         __builtin_amdgcn_sad_u8(v.z, 0u, 0u) + __builtin_amdgcn_sad_u8(v.w, 0u, 0u);
+  }
+  atomicAdd(&tot, s);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    res[0] = tot;
+    __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 // Publishes seq into fine-grained host memory (system-scope release).
 __global__ void signal(uint32_t* __restrict__ flag, uint32_t seq) {
   if (threadIdx.x == 0) __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -152,6 +181,34 @@ int main(int argc, char** argv) {
     check();
   });
   std::printf(" \"launch_signal_kernel_spin\": {\"med_us\": %.2f, \"p99_us\": %.2f},\n", d2.med, d2.p99);
+  {
+    Desc* hd = nullptr;  // coarse-grained mapped, as the library's pass table
+    CK(hipHostMalloc(reinterpret_cast<void**>(&hd), 64, hipHostMallocMapped | hipHostMallocNonCoherent));
+    Desc* ddv;
+    CK(hipHostGetDevicePointer(reinterpret_cast<void**>(&ddv), hd, 0));
+    hd->off = 0;
+    hd->len = 1504;
+    uint32_t w2 = 0;
+    for (uint32_t i = 0; i < 1504; ++i) w2 += in[i];
+    long bad2 = 0;
+    Stat x = time_calls(iters, [&] {
+      ++seq;
+      hipLaunchKernelGGL((desc_then_payload<false>), dim3(1), dim3(128), 0, s, din, ddv, Desc{}, dres, dflag, seq);
+      spin_flag(seq);
+      if (__atomic_load_n(res, __ATOMIC_ACQUIRE) != w2) ++bad2;
+    });
+    std::printf(" \"desc_in_host_memory_then_payload\": {\"med_us\": %.2f, \"p99_us\": %.2f},\n", x.med, x.p99);
+    Stat y = time_calls(iters, [&] {
+      ++seq;
+      hipLaunchKernelGGL((desc_then_payload<true>), dim3(1), dim3(128), 0, s, din, nullptr, *hd, dres, dflag, seq);
+      spin_flag(seq);
+      if (__atomic_load_n(res, __ATOMIC_ACQUIRE) != w2) ++bad2;
+    });
+    std::printf(" \"desc_by_value_then_payload\": {\"med_us\": %.2f, \"p99_us\": %.2f},\n", y.med, y.p99);
+    bad += bad2;
+    CK(hipStreamSynchronize(s));
+    CK(hipHostFree(hd));
+  }
   Stat d5 = time_calls(iters, [&] {
     ++seq;
     hipLaunchKernelGGL(tiny, dim3(1), dim3(256), 0, s, din, n, dres, nullptr, 0u);
