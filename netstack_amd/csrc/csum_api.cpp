@@ -379,11 +379,33 @@ int submit_small(ns_csum_ctx* ctx, SmallReq* req) {
 // 2.18, 256K 2.16, 512K 2.52 ms per call).
 constexpr uint32_t kHostChunkDesc = 1u << 17;
 
+// Whether [p, p + bytes) is page-locked host memory the DMA engines read
+// directly (hipHostMalloc, hipHostRegister, torch pin_memory).  A pageable
+// pointer makes hipPointerGetAttributes fail; that error is cleared so no
+// later hipGetLastError sees it.
+bool host_pinned(const void* p, uint64_t bytes) {
+  if (!p || !bytes) return false;
+  for (const void* q : {p, static_cast<const void*>(static_cast<const uint8_t*>(p) + bytes - 1)}) {
+    hipPointerAttribute_t a{};
+    if (hipPointerGetAttributes(&a, q) != hipSuccess) {
+      (void)hipGetLastError();
+      return false;
+    }
+    if (a.type != hipMemoryTypeHost) return false;
+  }
+  return true;
+}
+
 int run_host_batch(ns_csum_ctx* ctx, const uint8_t* h_arena, uint64_t arena_bytes,
                    const ns_pkt_desc* h_desc, uint32_t n, uint16_t* h_out,
                    bool chained) {
   if (n == 0) return NS_OK;
   const uint64_t budget = ctx->staging;
+  // A pinned table goes to the device straight from the caller's memory; a
+  // pageable one is copied into pinned staging chunk by chunk first (1M x
+  // 64 B: that copy, 16 MB per call on one core, was as long as the chunks'
+  // DMA).
+  const bool desc_pinned = host_pinned(h_desc, (uint64_t)n * sizeof(ns_pkt_desc));
   struct Pending {
     bool live = false;
     uint32_t first = 0, count = 0;
@@ -434,14 +456,18 @@ int run_host_batch(ns_csum_ctx* ctx, const uint8_t* h_arena, uint64_t arena_byte
       if ((rc = ctx->d_arena[slot].ensure(std::max<uint64_t>(span, 16))) != NS_OK) return rc;
       if ((rc = ctx->d_desc[slot].ensure(cnt)) != NS_OK) return rc;
       if ((rc = ctx->d_out[slot].ensure(cnt)) != NS_OK) return rc;
-      if ((rc = ctx->h_desc[slot].ensure(cnt)) != NS_OK) return rc;
+      if (!desc_pinned && (rc = ctx->h_desc[slot].ensure(cnt)) != NS_OK) return rc;
       if ((rc = ctx->h_out[slot].ensure(cnt)) != NS_OK) return rc;
       if (chained && (rc = ctx->d_chain[slot].ensure(cnt)) != NS_OK) return rc;
-      // The table goes over verbatim (one memcpy into pinned memory) and is
-      // rebased to the chunk on the device: a per-descriptor rewrite on the
-      // CPU was the limit of small-packet batches.
-      ns_pkt_desc* hd = ctx->h_desc[slot].p;
-      std::memcpy(hd, h_desc + k, (size_t)cnt * sizeof(ns_pkt_desc));
+      // The table goes over verbatim (from the caller's pinned table, or one
+      // memcpy into pinned staging) and is rebased to the chunk on the
+      // device: a per-descriptor rewrite on the CPU was the limit of
+      // small-packet batches.
+      const ns_pkt_desc* hd = h_desc + k;
+      if (!desc_pinned) {
+        std::memcpy(ctx->h_desc[slot].p, hd, (size_t)cnt * sizeof(ns_pkt_desc));
+        hd = ctx->h_desc[slot].p;
+      }
       hipStream_t s = ctx->stream[slot];
       if (span) HIP_TRY(hipMemcpyAsync(ctx->d_arena[slot].p, h_arena + cut_lo, span, hipMemcpyHostToDevice, s));
       HIP_TRY(hipMemcpyAsync(ctx->d_desc[slot].p, hd, cnt * sizeof(ns_pkt_desc), hipMemcpyHostToDevice, s));

@@ -1015,3 +1015,36 @@ def test_host_batch_out_of_range_is_erange_and_pipeline_recovers(engine, bad_at)
     assert ei.value.status == NS_ERANGE
     want, _ = O.c_batch(arena, d)
     assert np.array_equal(engine.batch_host(arena, d), want)
+
+
+@pytest.mark.parametrize("chained", [False, True])
+def test_host_batch_pinned_table_read_in_place(engine, chained):
+    """ns_csum_batch_host with a page-locked descriptor table (torch
+    pin_memory): the DMA pipeline sends each chunk's table straight from the
+    caller's memory instead of copying it into staging first.  A multi-chunk
+    batch (128K-descriptor chunks) with unaligned starts, odd flags and, with
+    `chained`, NS_DESC_CONT runs (never split across chunks), bit-exact
+    with the oracle and with the same table passed pageable."""
+    import oracle as O
+    from netstack_amd import workloads as W
+
+    torch = _torch()
+    rng = np.random.default_rng(404 + chained)
+    n = 300_001
+    lens = rng.integers(0, 200, n).astype(np.uint32)
+    d, end = W.make_desc(lens, rng.integers(0, 65536, n).astype(np.uint16), align=1)
+    d["flags"] |= rng.integers(0, 2, n).astype(np.uint16)  # NS_DESC_ODD
+    if chained:
+        d["flags"][1:] |= (rng.random(n - 1) < 0.6).astype(np.uint16) << 1  # NS_DESC_CONT
+    arena = rng.integers(0, 256, end, dtype=np.uint8)
+    pa = torch.empty(end, dtype=torch.uint8).pin_memory()
+    pa.numpy()[:] = arena
+    pt = torch.empty(d.nbytes, dtype=torch.uint8).pin_memory()
+    pt.numpy()[:] = d.view(np.uint8)
+    pd = pt.numpy().view(d.dtype)
+    want, nbad = O.c_batch(arena, d, chained=chained)
+    assert nbad == 0
+    got = engine.batch_host(pa.numpy(), pd, chained=chained)
+    assert np.array_equal(got, want)
+    assert np.array_equal(engine.batch_host(arena, d, chained=chained), want)
+    assert np.array_equal(pd, d)  # the caller's table is not rebased in place
