@@ -594,12 +594,12 @@ hipError_t launch_quad_direct(const uint8_t* arena, uint64_t arena_bytes, const 
 // quad_direct software-pipelined over K groups of 64 packets per wave: the
 // descriptors of group k + 2 and the payload of group k + 1 are in flight
 // while group k is summed and stored.
-template <int K, int AUX>
-__global__ __launch_bounds__(256) void quad_pipe(const uint8_t* __restrict__ arena, uint64_t arena_bytes,
+template <int K, int AUX, int WGQ = 256>
+__global__ __launch_bounds__(WGQ) void quad_pipe(const uint8_t* __restrict__ arena, uint64_t arena_bytes,
                                                  const uint4* __restrict__ desc, uint32_t n,
                                                  uint16_t* __restrict__ out, unsigned long long* __restrict__ err) {
   const uint32_t l = threadIdx.x & 63;
-  const uint64_t wb = ((uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 64 * K;
+  const uint64_t wb = ((uint64_t)blockIdx.x * (WGQ / 64) + (threadIdx.x >> 6)) * 64 * K;
   const uint64_t arena_abs = (uint64_t)(uintptr_t)arena;
   const uint64_t base = arena_abs & ~15ull;
   const Srd r = make_srd(base, arena_abs + arena_bytes - base);
@@ -668,10 +668,10 @@ __global__ __launch_bounds__(256) void quad_pipe(const uint8_t* __restrict__ are
     }
   }
 }
-template <int K, int AUX>
+template <int K, int AUX, int WGQ = 256>
 hipError_t launch_quad_pipe(const uint8_t* arena, uint64_t arena_bytes, const void* desc, uint32_t n,
                             uint16_t* out, unsigned long long* err, hipStream_t s) {
-  hipLaunchKernelGGL((quad_pipe<K, AUX>), dim3((n + 256 * K - 1) / (256 * K)), dim3(256), 0, s, arena, arena_bytes,
+  hipLaunchKernelGGL((quad_pipe<K, AUX, WGQ>), dim3((n + WGQ * K - 1) / (WGQ * K)), dim3(WGQ), 0, s, arena, arena_bytes,
                      reinterpret_cast<const uint4*>(desc), n, out, err);
   return hipGetLastError();
 }
@@ -806,6 +806,11 @@ static const Variant kVariants[] = {
     {"floor_quad_nt_wg64", launch_floor_quad<1, 2, 64>},
     {"quad_pipe4_nt", launch_quad_pipe<4, 2>},
     {"quad_pipe8_nt", launch_quad_pipe<8, 2>},
+    // one-wave workgroups, 2-4 groups of 64 packets per wave (cold tables)
+    {"quad_pipe2_nt_wg64", launch_quad_pipe<2, 2, 64>},
+    {"quad_pipe4_nt_wg64", launch_quad_pipe<4, 2, 64>},
+    {"quad_direct2_nt_wg64", launch_quad_direct<2, 2, 64>},
+    {"floor_quad_nt_wg64_k2", launch_floor_quad<2, 2, 64>},
     // the group kernel at smaller workgroups, production group threshold
     {"wg64_tp8_b40", launch_wg<64, 8, kBigChunks>},
     {"wg64_tp16_b40", launch_wg<64, 16, kBigChunks>},
