@@ -275,7 +275,10 @@ int run_zero_copy(ns_csum_ctx* ctx, SmallReq* const* reqs, size_t nreq) {
   int rc;
   if ((rc = ctx->z_buf.ensure(std::max<uint64_t>(kPassTableBytes, nd * sizeof(ns_pkt_desc)))) != NS_OK) return rc;
   if ((rc = ctx->z_res.ensure(std::max<uint64_t>(kPassTableBytes / 8, nd * 2))) != NS_OK) return rc;
-  if ((rc = ctx->z_done.ensure(64)) != NS_OK) return rc;
+  if (ctx->z_done.cap == 0) {  // zeroed once: no stale word may equal a pass's sequence number
+    if ((rc = ctx->z_done.ensure(64)) != NS_OK) return rc;
+    __atomic_store_n(reinterpret_cast<uint32_t*>(ctx->z_done.p), 0u, __ATOMIC_RELEASE);
+  }
   if (chained && (rc = ctx->d_chain[0].ensure(nd)) != NS_OK) return rc;
   uint8_t* z = ctx->z_buf.p;
   ns_pkt_desc* zd = reinterpret_cast<ns_pkt_desc*>(z);

@@ -209,6 +209,14 @@ int main(int argc, char** argv) {
     CK(hipStreamSynchronize(s));
     CK(hipHostFree(hd));
   }
+  Stat wv = time_calls(iters, [&] {
+    ++seq;
+    hipLaunchKernelGGL(tiny, dim3(1), dim3(256), 0, s, din, n, dres, nullptr, 0u);
+    CK(hipStreamWriteValue32(s, dflag, seq, 0));
+    spin_flag(seq);
+    check();
+  });
+  std::printf(" \"launch_streamwritevalue_spin\": {\"med_us\": %.2f, \"p99_us\": %.2f},\n", wv.med, wv.p99);
   Stat d5 = time_calls(iters, [&] {
     ++seq;
     hipLaunchKernelGGL(tiny, dim3(1), dim3(256), 0, s, din, n, dres, nullptr, 0u);
