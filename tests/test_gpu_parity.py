@@ -1048,3 +1048,34 @@ def test_host_batch_pinned_table_read_in_place(engine, chained):
     assert np.array_equal(got, want)
     assert np.array_equal(engine.batch_host(arena, d, chained=chained), want)
     assert np.array_equal(pd, d)  # the caller's table is not rebased in place
+
+
+@pytest.mark.parametrize("chained", [False, True])
+def test_zero_copy_pass_shapes(engine, chained):
+    """Small host batches (<= 1 MiB of bytes) run as zero-copy passes, which
+    launch in a PCIe-latency shape: packets below 32 KiB through per-lane
+    runs only, 16 KiB tiles, larger ones through the 8-lane groups
+    (csum_kernels.hip kZeroCopyBigChunks).  Lengths on both sides of that
+    threshold and of the W-only limit (8190 chunks), 1-byte and empty
+    packets, odd offsets and odd flags, every result against the oracle."""
+    import oracle as O
+    from netstack_amd import workloads as W
+
+    rng = np.random.default_rng(2048 + chained)
+    edge = [0, 1, 15, 16, 17, 1500, 32 * 1024 - 16, 32 * 1024 - 1, 32 * 1024, 32 * 1024 + 1,
+            32 * 1024 + 17, 65536, 131_040, 131_041, 200_000]
+    for trial in range(6):
+        lens = np.array(edge + list(rng.integers(0, 30_000, 10)), dtype=np.uint32)
+        rng.shuffle(lens)
+        d, end = W.make_desc(lens, rng.integers(0, 65536, len(lens)).astype(np.uint16), align=1,
+                             base=int(rng.integers(0, 7)))
+        d["flags"] |= rng.integers(0, 2, len(d)).astype(np.uint16)
+        if chained:
+            d["flags"][1:] |= (rng.random(len(d) - 1) < 0.5).astype(np.uint16) << 1
+        arena = rng.integers(0, 256, end + 8, dtype=np.uint8)
+        if trial % 2:
+            arena[: end // 2] = 0xFF  # long runs of 0xFF words: the wrap of large packets
+        assert end + 8 <= 1 << 20  # one zero-copy pass
+        want, nbad = O.c_batch(arena, d, chained=chained)
+        assert nbad == 0
+        assert np.array_equal(engine.batch_host(arena, d, chained=chained), want)
