@@ -658,11 +658,19 @@ __device__ __forceinline__ uint32_t hyb_scan_tile(HybLds<WG>& L, const Srd& r, c
 // as ^r (SetChecksum(^xsum): connect.go:663, ipv4.go:236) or, with
 // NS_DESC_STORE_RAW, as r (the CHECKSUM_PARTIAL pseudo-header sum,
 // connect.go:660).  One u16 store, or two byte stores at an odd address.
+//
+// The aligned store is a relaxed agent-scope store (global_store_short sc1:
+// written through, the line dropped from L2) rather than a plain one that
+// leaves a partially dirty line in L2 to be written back during the next
+// launch's stream: TX fill 285-286 vs 290-292 us (nontemporal: 292),
+// bench.py --config 8, two interleaved rounds on one box
+// (profiles/r02/tx_store_policy.txt).
 __device__ __forceinline__ void store_result(uint64_t addr, uint32_t r, uint32_t stw) {
   const uint32_t v = (stw & 2u) ? r : (~r & 0xFFFFu);
   uint8_t* p = reinterpret_cast<uint8_t*>((uintptr_t)addr);
   if (!(addr & 1u)) {
-    *reinterpret_cast<uint16_t*>(p) = (uint16_t)(((v & 0xFFu) << 8) | (v >> 8));
+    __hip_atomic_store(reinterpret_cast<uint16_t*>(p), (uint16_t)(((v & 0xFFu) << 8) | (v >> 8)), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
   } else {
     p[0] = (uint8_t)(v >> 8);
     p[1] = (uint8_t)v;
