@@ -128,6 +128,47 @@ using MappedPin = PinBuf<uint8_t, hipHostMallocMapped | hipHostMallocNonCoherent
 // kernel's last store (tools/sync_probe.hip).
 using CoherentPin = PinBuf<uint8_t, hipHostMallocMapped | hipHostMallocCoherent | hipHostMallocPortable>;
 
+// A zero-copy pass's descriptor table.  On a large-BAR part (the whole VRAM
+// mapped into the CPU's address space, hipDeviceAttributeIsLargeBar) it is
+// fine-grained device memory the host writes through the BAR at the same
+// address, so the kernel's first, dependent read is local instead of a PCIe
+// round trip; elsewhere mapped host memory.  The host only ever writes it
+// (reads through the BAR are uncached and slow).
+struct PassTable {
+  uint8_t* p = nullptr;    // host view
+  uint8_t* dev = nullptr;  // device view (the same address in VRAM)
+  size_t cap = 0;
+  bool vram = false;
+  MappedPin host;
+  int ensure(size_t n, bool want_vram) {
+    if (n <= cap) return NS_OK;
+    release();
+    if (want_vram) {
+      void* q = nullptr;
+      if (hipExtMallocWithFlags(&q, n, hipDeviceMallocFinegrained) == hipSuccess) {
+        p = dev = static_cast<uint8_t*>(q);
+        cap = n;
+        vram = true;
+        return NS_OK;
+      }
+      (void)hipGetLastError();
+    }
+    const int rc = host.ensure(n);
+    if (rc != NS_OK) return rc;
+    p = host.p;
+    dev = host.dev;
+    cap = n;
+    return NS_OK;
+  }
+  void release() {
+    if (vram && p) (void)hipFree(p);
+    host.release();
+    p = dev = nullptr;
+    cap = 0;
+    vram = false;
+  }
+};
+
 // Chained-batch scratch (csum_kernels.h ChainScratch): partials + flags, and
 // the fold statuses in a buffer of their own, zeroed once at allocation.
 struct ChainBuf {
@@ -203,7 +244,8 @@ struct ns_csum_ctx {
   PinBuf<uint16_t> h_out[2];
   // zero-copy pass buffers for small calls: the table (read by the kernel),
   // the results and the completion word (written by it)
-  MappedPin z_buf;
+  PassTable z_buf;
+  bool bar_table = false;  // large BAR: z_buf in device memory
   CoherentPin z_res;
   CoherentPin z_done;
   uint32_t z_seq = 0;
@@ -273,7 +315,9 @@ int run_zero_copy(ns_csum_ctx* ctx, SmallReq* const* reqs, size_t nreq) {
   }
   if (nd == 0) return NS_OK;
   int rc;
-  if ((rc = ctx->z_buf.ensure(std::max<uint64_t>(kPassTableBytes, nd * sizeof(ns_pkt_desc)))) != NS_OK) return rc;
+  if ((rc = ctx->z_buf.ensure(std::max<uint64_t>(kPassTableBytes, nd * sizeof(ns_pkt_desc)), ctx->bar_table)) !=
+      NS_OK)
+    return rc;
   if ((rc = ctx->z_res.ensure(std::max<uint64_t>(kPassTableBytes / 8, nd * 2))) != NS_OK) return rc;
   if (ctx->z_done.cap == 0) {  // zeroed once: no stale word may equal a pass's sequence number
     if ((rc = ctx->z_done.ensure(64)) != NS_OK) return rc;
@@ -287,18 +331,23 @@ int run_zero_copy(ns_csum_ctx* ctx, SmallReq* const* reqs, size_t nreq) {
     const SmallReq& q = *reqs[r];
     const uint64_t base = (uint64_t)(uintptr_t)q.dbytes;
     for (uint32_t i = 0; i < q.ndesc; ++i, ++k) {
-      zd[k] = q.desc[i];
-      zd[k].off = zd[k].len ? base + (zd[k].off - q.lo) : 0;
+      // built in a register and written once: the table may be device memory
+      // behind the BAR, which the host must never read back
+      ns_pkt_desc d = q.desc[i];
+      d.off = d.len ? base + (d.off - q.lo) : 0;
       if (!q.chained) {
-        zd[k].flags &= (uint16_t)~NS_DESC_CONT;  // independent in an unchained batch
-      } else if (i == 0 && (zd[k].flags & NS_DESC_CONT)) {
+        d.flags &= (uint16_t)~NS_DESC_CONT;  // independent in an unchained batch
+      } else if (i == 0 && (d.flags & NS_DESC_CONT)) {
         // A batch's first descriptor heads its run even when flagged CONT
         // (with initial 0, fold_scan): keep that inside a combined pass.
-        zd[k].flags &= (uint16_t)~NS_DESC_CONT;
-        zd[k].initial = 0;
+        d.flags &= (uint16_t)~NS_DESC_CONT;
+        d.initial = 0;
       }
+      zd[k] = d;
     }
   }
+  // BAR writes are write-combined: drain them before the launch's doorbell.
+  __builtin_ia32_sfence();
   hipStream_t s = ctx->stream[0];
   HIP_TRY(nsk::launch_batch(nullptr, kWholeSpace, ctx->z_buf.dev, (uint32_t)nd,
                             reinterpret_cast<uint16_t*>(ctx->z_res.dev),
@@ -724,6 +773,15 @@ int ns_csum_init(const ns_csum_opts* opts, ns_csum_ctx** out) {
     ns_csum_destroy(ctx);
     return rc;
   }
+  // Zero-copy pass tables in device memory written through the BAR when the
+  // whole VRAM is CPU-mapped (NS_CSUM_NO_BAR_TABLE=1: mapped host memory, for
+  // A/B diagnostics only).
+  int large_bar = 0;
+  if (hipDeviceGetAttribute(&large_bar, hipDeviceAttributeIsLargeBar, dev) != hipSuccess) {
+    large_bar = 0;
+    (void)hipGetLastError();
+  }
+  ctx->bar_table = large_bar != 0 && std::getenv("NS_CSUM_NO_BAR_TABLE") == nullptr;
   *out = ctx;
   return NS_OK;
 }

@@ -19,6 +19,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <functional>
 #include <vector>
 
@@ -208,6 +209,67 @@ int main(int argc, char** argv) {
     bad += bad2;
     CK(hipStreamSynchronize(s));
     CK(hipHostFree(hd));
+  }
+  {
+    // Fine-grained device memory the CPU writes through the BAR: the
+    // descriptor and the payload staged in HBM by host stores, read by the
+    // kernel from local memory (no PCIe read round trip).
+    uint8_t* vram = nullptr;
+    hipError_t e = hipExtMallocWithFlags(reinterpret_cast<void**>(&vram), 1 << 16, hipDeviceMallocFinegrained);
+    hipPointerAttribute_t at{};
+    // argv[3] == "direct": dereference the device address on the host (SVM
+    // over a large BAR); a fault ends only this process
+    const bool direct = argc > 3 && argv[3][0] == 'd';
+    const bool ok = e == hipSuccess && hipPointerGetAttributes(&at, vram) == hipSuccess && (at.hostPointer || direct);
+    std::printf(" \"vram_finegrained_host_ptr\": %s, \"direct\": %s,\n", at.hostPointer ? "true" : "false",
+                direct ? "true" : "false");
+    std::fflush(stdout);
+    if (ok) {
+      uint8_t* hv = at.hostPointer ? static_cast<uint8_t*>(at.hostPointer) : vram;
+      Desc* vd = reinterpret_cast<Desc*>(hv + 4096);
+      uint32_t w3 = 0;
+      for (uint32_t i = 0; i < 1504; ++i) w3 += in[i];
+      long bad3 = 0;
+      // freshness: every call stages different bytes (the previous call's
+      // lines may sit in the GPU's L2); the kernel must sum the new ones
+      std::vector<uint8_t> pat(1504);
+      Stat zf = time_calls(iters, [&] {
+        ++seq;
+        uint32_t w = 0;
+        for (uint32_t i = 0; i < 1504; ++i) w += (pat[i] = (uint8_t)(seq * 131u + i * 7u));
+        std::memcpy(hv, pat.data(), 1504);
+        vd->off = 0;
+        vd->len = 1504;
+        std::atomic_thread_fence(std::memory_order_seq_cst);
+        hipLaunchKernelGGL((desc_then_payload<false>), dim3(1), dim3(128), 0, s, vram,
+                           reinterpret_cast<const Desc*>(vram + 4096), Desc{}, dres, dflag, seq);
+        spin_flag(seq);
+        if (__atomic_load_n(res, __ATOMIC_ACQUIRE) != w) ++bad3;
+      });
+      std::printf(" \"vram_staged_fresh_bytes_each_call\": {\"med_us\": %.2f, \"wrong\": %ld},\n", zf.med, bad3);
+      Stat z = time_calls(iters, [&] {
+        ++seq;
+        std::memcpy(hv, in, 1504);  // the staging copy, into HBM
+        vd->off = 0;
+        vd->len = 1504;
+        std::atomic_thread_fence(std::memory_order_seq_cst);
+        hipLaunchKernelGGL((desc_then_payload<false>), dim3(1), dim3(128), 0, s, vram,
+                           reinterpret_cast<const Desc*>(vram + 4096), Desc{}, dres, dflag, seq);
+        spin_flag(seq);
+        if (__atomic_load_n(res, __ATOMIC_ACQUIRE) != w3) ++bad3;
+      });
+      std::printf(" \"vram_staged_desc_and_payload\": {\"med_us\": %.2f, \"p99_us\": %.2f, \"wrong\": %ld},\n",
+                  z.med, z.p99, bad3);
+      std::vector<uint8_t> big(1 << 16, 7);
+      const double tw0 = now_us();
+      for (int r = 0; r < 100; ++r) std::memcpy(hv, big.data(), 1 << 16);
+      std::atomic_thread_fence(std::memory_order_seq_cst);
+      std::printf(" \"cpu_write_to_vram_GBps\": %.2f,\n", 100.0 * 65536 / (now_us() - tw0) / 1e3);
+      CK(hipStreamSynchronize(s));
+      CK(hipFree(vram));
+    } else {
+      (void)hipGetLastError();
+    }
   }
   Stat wv = time_calls(iters, [&] {
     ++seq;
