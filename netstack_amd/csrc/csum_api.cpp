@@ -128,13 +128,15 @@ using MappedPin = PinBuf<uint8_t, hipHostMallocMapped | hipHostMallocNonCoherent
 // kernel's last store (tools/sync_probe.hip).
 using CoherentPin = PinBuf<uint8_t, hipHostMallocMapped | hipHostMallocCoherent | hipHostMallocPortable>;
 
-// A zero-copy pass's descriptor table.  On a large-BAR part (the whole VRAM
-// mapped into the CPU's address space, hipDeviceAttributeIsLargeBar) it is
-// fine-grained device memory the host writes through the BAR at the same
-// address, so the kernel's first, dependent read is local instead of a PCIe
-// round trip; elsewhere mapped host memory.  The host only ever writes it
-// (reads through the BAR are uncached and slow).
-struct PassTable {
+// What a zero-copy pass reads: its descriptor table and the bytes small
+// calls gather.  On a large-BAR part (the whole VRAM mapped into the CPU's
+// address space, hipDeviceAttributeIsLargeBar) they are fine-grained device
+// memory the host writes through the BAR at the same address, so the
+// kernel's dependent reads are local instead of PCIe round trips; elsewhere
+// mapped host memory.  The host only ever writes these buffers (reads
+// through the BAR are uncached and slow), and drains its write-combined
+// stores (sfence) before the work is launched.
+struct BarBuf {
   uint8_t* p = nullptr;    // host view
   uint8_t* dev = nullptr;  // device view (the same address in VRAM)
   size_t cap = 0;
@@ -244,15 +246,19 @@ struct ns_csum_ctx {
   PinBuf<uint16_t> h_out[2];
   // zero-copy pass buffers for small calls: the table (read by the kernel),
   // the results and the completion word (written by it)
-  PassTable z_buf;
+  BarBuf z_buf;
   bool bar_table = false;  // large BAR: z_buf in device memory
   CoherentPin z_res;
   CoherentPin z_done;
   uint32_t z_seq = 0;
   // flat combining of concurrent small calls (nsh::FlatCombiner)
   nsh::FlatCombiner<SmallReq> combiner{kPassTableBytes};
-  // the pool of mapped staging buffers small calls gather into; guarded by qmu
+  // the pool of staging buffers small calls gather into (BarBuf: device
+  // memory behind the BAR where possible), and the pool of mapped host
+  // buffers callers acquire (ns_csum_stage_acquire); guarded by qmu
   std::mutex qmu;
+  std::vector<BarBuf*> gstage_free;
+  std::vector<BarBuf*> gstage_all;
   std::vector<MappedPin*> stage_free;
   std::vector<MappedPin*> stage_all;
   std::vector<MappedPin*> big_free;  // pooled caller stages above kStageBytes
@@ -377,7 +383,8 @@ int run_zero_copy(ns_csum_ctx* ctx, SmallReq* const* reqs, size_t nreq) {
   return NS_OK;
 }
 
-// Lease / return a mapped staging buffer of kStageBytes from the context's pool.
+// Lease a mapped staging buffer of kStageBytes from the context's pool
+// (ns_csum_stage_acquire; ns_csum_stage_release returns it).
 MappedPin* lease_stage(ns_csum_ctx* ctx, int* rc) {
   {
     std::lock_guard<std::mutex> ql(ctx->qmu);
@@ -404,10 +411,38 @@ MappedPin* lease_stage(ns_csum_ctx* ctx, int* rc) {
   return b;
 }
 
-void return_stage(ns_csum_ctx* ctx, MappedPin* b) {
+// Lease / return a gather stage of kStageBytes (device memory behind the BAR
+// on large-BAR parts) from the context's pool.
+BarBuf* lease_gather_stage(ns_csum_ctx* ctx, int* rc) {
+  {
+    std::lock_guard<std::mutex> ql(ctx->qmu);
+    if (!ctx->gstage_free.empty()) {
+      BarBuf* b = ctx->gstage_free.back();
+      ctx->gstage_free.pop_back();
+      return b;
+    }
+  }
+  BarBuf* b = new (std::nothrow) BarBuf();
+  if (!b) {
+    *rc = NS_ENOMEM;
+    return nullptr;
+  }
+  {
+    DeviceGuard g(ctx->device);
+    if ((*rc = b->ensure(kStageBytes, ctx->bar_table)) != NS_OK) {
+      delete b;
+      return nullptr;
+    }
+  }
+  std::lock_guard<std::mutex> ql(ctx->qmu);
+  ctx->gstage_all.push_back(b);
+  return b;
+}
+
+void return_gather_stage(ns_csum_ctx* ctx, BarBuf* b) {
   if (!b) return;
   std::lock_guard<std::mutex> ql(ctx->qmu);
-  ctx->stage_free.push_back(b);
+  ctx->gstage_free.push_back(b);
 }
 
 // Flat combining of concurrent small synchronous calls (nsh::FlatCombiner):
@@ -417,6 +452,9 @@ void return_stage(ns_csum_ctx* ctx, MappedPin* b) {
 // to separate calls (descriptors are independent; chains never cross
 // requests).
 int submit_small(ns_csum_ctx* ctx, SmallReq* req) {
+  // This thread's gather may have gone to device memory through the BAR:
+  // drain its write-combined stores before another thread launches the pass.
+  __builtin_ia32_sfence();
   return ctx->combiner.submit(req, [ctx](SmallReq* const* reqs, size_t nreq) {
     std::lock_guard<std::mutex> lk(ctx->mu);
     DeviceGuard g(ctx->device);
@@ -612,17 +650,21 @@ struct SpanProbe {
 // address that stage (adopt mode).
 struct ByteSink {
   ns_csum_ctx* ctx;
-  MappedPin* stage = nullptr;    // leased from the pool (copy mode)
+  BarBuf* stage = nullptr;       // leased from the pool (copy mode)
   MappedPin* adopted = nullptr;  // the caller's acquired stage (adopt mode)
   std::unique_lock<std::mutex> big;  // held once the bytes live in ctx->g_arena
   uint64_t n = 0;  // copy: bytes appended; adopt: end of the highest byte used
   int rc = NS_OK;
+  // the pieces copied into the stage so far: a move to g_arena copies them
+  // again from their sources, never back out of the stage (device memory
+  // behind the BAR reads at PCIe-latency speed)
+  std::vector<std::pair<const uint8_t*, uint64_t>> staged;
   explicit ByteSink(ns_csum_ctx* c, MappedPin* adopt = nullptr) : ctx(c), adopted(adopt) {
     if (adopted) return;
-    if (zero_copy_enabled()) stage = lease_stage(ctx, &rc);
+    if (zero_copy_enabled()) stage = lease_gather_stage(ctx, &rc);
     if (!stage) rc = to_big(0);
   }
-  ~ByteSink() { return_stage(ctx, stage); }
+  ~ByteSink() { return_gather_stage(ctx, stage); }
   ByteSink(const ByteSink&) = delete;
   ByteSink& operator=(const ByteSink&) = delete;
   bool in_big() const { return big.owns_lock(); }
@@ -645,8 +687,14 @@ struct ByteSink {
   int to_big(uint64_t need) {
     big = std::unique_lock<std::mutex>(ctx->mu);
     const int r = reserve_big(std::max<uint64_t>(need, 1ull << 20), 0);
-    if (r == NS_OK && n) std::memcpy(ctx->g_arena.p, stage->p, n);
-    return r;
+    if (r != NS_OK) return r;
+    uint64_t at = 0;
+    for (const auto& pc : staged) {
+      std::memcpy(ctx->g_arena.p + at, pc.first, pc.second);
+      at += pc.second;
+    }
+    staged.clear();
+    return NS_OK;
   }
   // Makes bytes [p, p + len) part of the arena; returns their arena offset.
   uint64_t append(const uint8_t* p, uint64_t len) {
@@ -661,6 +709,7 @@ struct ByteSink {
     else if (in_big()) rc = reserve_big(n + len, n);
     if (rc != NS_OK) return at;
     std::memcpy(base() + n, p, len);
+    if (!in_big()) staged.emplace_back(p, len);
     n += len;
     return at;
   }
@@ -808,6 +857,12 @@ void ns_csum_destroy(ns_csum_ctx* ctx) {
     }
     ctx->stage_all.clear();
     ctx->stage_free.clear();
+    for (BarBuf* b : ctx->gstage_all) {
+      b->release();
+      delete b;
+    }
+    ctx->gstage_all.clear();
+    ctx->gstage_free.clear();
     for (int s = 0; s < 2; ++s) {
       ctx->d_arena[s].release();
       ctx->d_desc[s].release();
@@ -918,7 +973,7 @@ int ns_csum_batch_host(ns_csum_ctx* ctx, const uint8_t* h_arena, uint64_t arena_
   }
   if (maybe_small && hi - lo <= kStageBytes) {
     int rc = NS_OK;
-    MappedPin* st = lease_stage(ctx, &rc);
+    BarBuf* st = lease_gather_stage(ctx, &rc);
     if (!st) return rc;
     if (hi > lo) std::memcpy(st->p, h_arena + lo, hi - lo);
     SmallReq rq;
@@ -930,7 +985,7 @@ int ns_csum_batch_host(ns_csum_ctx* ctx, const uint8_t* h_arena, uint64_t arena_
     rq.res = h_out;
     rq.chained = (batch_flags & NS_BATCH_CHAINED) != 0;
     rc = submit_small(ctx, &rq);
-    return_stage(ctx, st);
+    return_gather_stage(ctx, st);
     return rc;
   }
   std::lock_guard<std::mutex> lk(ctx->mu);
