@@ -1079,3 +1079,55 @@ def test_zero_copy_pass_shapes(engine, chained):
         want, nbad = O.c_batch(arena, d, chained=chained)
         assert nbad == 0
         assert np.array_equal(engine.batch_host(arena, d, chained=chained), want)
+
+
+def _small_call_mix(eng, seed):
+    import oracle as O
+    from netstack_amd import workloads as W
+
+    rng = np.random.default_rng(seed)
+    for L in (0, 1, 1500, 65536, 200_000):
+        buf = rng.integers(0, 256, L, dtype=np.uint8)
+        ini = int(rng.integers(0, 65536))
+        assert eng.checksum(buf, ini) == O.c_checksum(bytes(buf), ini)
+    # 40 segments over ~1.2 MB of views: the gather outgrows its 1 MiB stage
+    views = [rng.integers(0, 256, int(k), dtype=np.uint8) for k in rng.integers(1, 400_000, 6)]
+    segs = [(int(o), int(s), int(i)) for o, s, i in zip(rng.integers(0, 900_000, 40),
+                                                        rng.integers(0, 300_000, 40),
+                                                        rng.integers(0, 65536, 40))]
+    vb = [bytes(v) for v in views]
+    assert eng.vv_batch(views, segs).tolist() == [O.c_checksum_vv_with_offset(vb, i, o, s) for o, s, i in segs]
+    n = 3000
+    d, end = W.make_desc(rng.integers(0, 300, n).astype(np.uint32), rng.integers(0, 65536, n).astype(np.uint16),
+                         align=1, flags=(rng.integers(0, 2, n) | (2 * (rng.random(n) < 0.5))).astype(np.uint16))
+    arena = rng.integers(0, 256, end, dtype=np.uint8)
+    for chained in (False, True):
+        want, _ = O.c_batch(arena, d, chained=chained)
+        assert np.array_equal(eng.batch_host(arena, d, chained=chained), want)
+
+
+def test_small_call_mix_default_staging(engine):
+    """Small synchronous calls through the default staging (device memory
+    written through the BAR on MI355X): single buffers up to 200 KB, a
+    VectorisedView batch whose gather outgrows its 1 MiB stage (re-copied
+    from its sources), chained and unchained host batches."""
+    _small_call_mix(engine, 77)
+
+
+def test_small_calls_with_host_memory_staging():
+    """NS_CSUM_NO_BAR_TABLE=1 (read at ns_csum_init): a context whose
+    zero-copy tables and gather stages stay in mapped host memory, as on parts
+    without a large BAR, gives the same bit-exact results."""
+    import os
+
+    from netstack_amd import Engine
+
+    os.environ["NS_CSUM_NO_BAR_TABLE"] = "1"
+    try:
+        eng = Engine(0)
+    finally:
+        del os.environ["NS_CSUM_NO_BAR_TABLE"]
+    try:
+        _small_call_mix(eng, 78)
+    finally:
+        eng.close()
