@@ -429,6 +429,12 @@ def main():
         },
         "bad_descriptors": bad,
     }
+    # per GPU: the whole-job value split evenly, and the
+    # spread of the ranks' own kernel averages (roofline above is rank 0's)
+    kmax = dist.max(kern_avg_s, dev)
+    kmin = -dist.max(-kern_avg_s, dev)
+    result["per_gpu"] = {"value": result["value"] / dist.world, "unit": "GiB/s",
+                         "kernel_avg_us_min": kmin * 1e6, "kernel_avg_us_max": kmax * 1e6}
 
     if not args.no_parity:
         # Every rank checks its own measured launch's results (the first and
