@@ -250,6 +250,7 @@ struct ns_csum_ctx {
   bool bar_table = false;  // large BAR: z_buf in device memory
   CoherentPin z_res;
   CoherentPin z_done;
+  DevBuf<uint32_t> z_ctr;  // a self-signalling pass's workgroup counter (zero between passes)
   uint32_t z_seq = 0;
   // flat combining of concurrent small calls (nsh::FlatCombiner)
   nsh::FlatCombiner<SmallReq> combiner{kPassTableBytes};
@@ -330,6 +331,7 @@ int run_zero_copy(ns_csum_ctx* ctx, SmallReq* const* reqs, size_t nreq) {
     __atomic_store_n(reinterpret_cast<uint32_t*>(ctx->z_done.p), 0u, __ATOMIC_RELEASE);
   }
   if (chained && (rc = ctx->d_chain[0].ensure(nd)) != NS_OK) return rc;
+  if ((rc = ctx->z_ctr.ensure(1, true)) != NS_OK) return rc;
   uint8_t* z = ctx->z_buf.p;
   ns_pkt_desc* zd = reinterpret_cast<ns_pkt_desc*>(z);
   uint64_t k = 0;
@@ -355,18 +357,26 @@ int run_zero_copy(ns_csum_ctx* ctx, SmallReq* const* reqs, size_t nreq) {
   // BAR writes are write-combined: drain them before the launch's doorbell.
   __builtin_ia32_sfence();
   hipStream_t s = ctx->stream[0];
-  HIP_TRY(nsk::launch_batch(nullptr, kWholeSpace, ctx->z_buf.dev, (uint32_t)nd,
-                            reinterpret_cast<uint16_t*>(ctx->z_res.dev),
-                            chained ? ctx->d_chain[0].get() : nsk::ChainScratch{}, ctx->d_err, s,
-                            std::max<uint64_t>(nb, 1)));
-  // Completion: the pass's last kernel is followed on the stream by a store of
-  // the pass's sequence number into coherent host memory; spin for it, and
-  // only if it is late (a fault, or a busy device) wait on the stream itself,
-  // which also reports a failed kernel.
+  // Completion: the pass's sequence number lands in coherent host memory once
+  // every result is there — stored by the checksum launch's last workgroup
+  // (unchained passes: the results are written through, nsk::ZcSignal) or by
+  // a one-wave kernel behind the fold pass (chained).  The caller spins for
+  // it, and only if it is late (a fault, or a busy device) waits on the
+  // stream itself, which also reports a failed kernel.
   uint32_t seq = ++ctx->z_seq;
   if (seq == 0) seq = ++ctx->z_seq;
   uint32_t* done = reinterpret_cast<uint32_t*>(ctx->z_done.p);
-  HIP_TRY(nsk::launch_signal(reinterpret_cast<uint32_t*>(ctx->z_done.dev), seq, s));
+  uint32_t* done_dev = reinterpret_cast<uint32_t*>(ctx->z_done.dev);
+  // NS_CSUM_SIGNAL_KERNEL=1: the signal kernel for unchained passes too (A/B only)
+  static const bool sig_kernel = std::getenv("NS_CSUM_SIGNAL_KERNEL") != nullptr;
+  const bool self = !chained && !sig_kernel;
+  nsk::ZcSignal zc{};
+  if (self) zc = nsk::ZcSignal{ctx->z_ctr.p, done_dev, seq};
+  HIP_TRY(nsk::launch_batch(nullptr, kWholeSpace, ctx->z_buf.dev, (uint32_t)nd,
+                            reinterpret_cast<uint16_t*>(ctx->z_res.dev),
+                            chained ? ctx->d_chain[0].get() : nsk::ChainScratch{}, ctx->d_err, s,
+                            std::max<uint64_t>(nb, 1), 0, nullptr, zc));
+  if (!self) HIP_TRY(nsk::launch_signal(done_dev, seq, s));
   const auto t0 = std::chrono::steady_clock::now();
   for (uint32_t spin = 0; __atomic_load_n(done, __ATOMIC_ACQUIRE) != seq; ++spin) {
     if ((spin & 255u) == 255u && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) {
@@ -851,6 +861,7 @@ void ns_csum_destroy(ns_csum_ctx* ctx) {
     ctx->z_buf.release();
     ctx->z_res.release();
     ctx->z_done.release();
+    ctx->z_ctr.release();
     for (MappedPin* b : ctx->stage_all) {
       b->release();
       delete b;

@@ -42,11 +42,23 @@ struct ChainScratch {
   uint64_t* status = nullptr;   // chain_blocks(n) u64, zeroed at allocation
 };
 
+// A self-signalling launch (`zc.flag` set; unchained checksum tiles only, no
+// `chain` and no `split`): results are written through to `out` (coherent
+// host memory) and the launch's last workgroup stores `zc.seq` into
+// `*zc.flag` (coherent host memory) once every result is complete; `zc.ctr`
+// is a device counter that is zero between launches (each launch leaves it
+// so).  The caller spins on the flag instead of launching a signal kernel.
+struct ZcSignal {
+  uint32_t* ctr = nullptr;
+  uint32_t* flag = nullptr;
+  uint32_t seq = 0;
+};
+
 hipError_t launch_batch(const uint8_t* arena, uint64_t arena_bytes,
                         const void* desc, uint32_t n, uint16_t* out,
                         ChainScratch chain, unsigned long long* err,
                         hipStream_t stream, uint64_t sizing_bytes = 0, uint32_t store = 0,
-                        uint32_t* split = nullptr);
+                        uint32_t* split = nullptr, ZcSignal zc = {});
 
 // *taken = the error count, which is reset to 0 in the same atomic exchange
 // (counts added by kernels still running on other streams are never lost).

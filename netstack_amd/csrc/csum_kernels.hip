@@ -704,7 +704,7 @@ __device__ __forceinline__ void park_store(HybLds<P>& L, uint32_t store, uint4 r
 template <int P, bool CH>
 __device__ __forceinline__ void finish_tile(HybLds<P>& L, uint32_t s, const Pkt& d, bool mine, uint64_t i,
                                             uint64_t n, uint16_t* __restrict__ out,
-                                            uint32_t* __restrict__ partial, uint32_t store) {
+                                            uint32_t* __restrict__ partial, uint32_t store, bool wt = false) {
   const int t = threadIdx.x;
   if constexpr (CH) {
     const bool head = !d.cont || i == 0;
@@ -722,10 +722,31 @@ __device__ __forceinline__ void finish_tile(HybLds<P>& L, uint32_t s, const Pkt&
   } else {
     if (!mine) return;
     const uint32_t r = fold1(d.init + s);
-    out[i] = (uint16_t)r;
+    if (wt)  // a self-signalling launch (zc_complete): results written through to the host
+      __hip_atomic_store(out + i, (uint16_t)r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    else
+      out[i] = (uint16_t)r;
     if (store) {
       const uint32_t stw = L.stw[t];
       if (stw) store_result(L.sat[t], r, stw);
+    }
+  }
+}
+
+// Completion word of a self-signalling launch (an unchained zero-copy pass,
+// csum_api.cpp run_zero_copy): every workgroup waits until its own result
+// stores — written through to coherent host memory (finish_tile `wt`) — are
+// complete, then counts itself done; the last one resets the counter for the
+// next launch and stores `seq` into the host's completion word, which the
+// caller spins on.  Saves the separate signal kernel's launch and dispatch.
+__device__ __forceinline__ void zc_complete(uint32_t* __restrict__ ctr, uint32_t* __restrict__ flag, uint32_t seq) {
+  __builtin_amdgcn_s_waitcnt(0);  // this wave's stores are acknowledged
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t prev = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (prev == gridDim.x - 1u) {
+      __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(flag, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
 }
@@ -743,9 +764,10 @@ __global__ __launch_bounds__(WG) void csum_hyb(
     const uint8_t* __restrict__ arena, uint64_t arena_bytes,
     const uint4* __restrict__ desc, uint32_t n, uint16_t* __restrict__ out,
     uint32_t* __restrict__ partial, unsigned long long* __restrict__ err, uint32_t big_chunks,
-    uint32_t store) {
+    uint32_t store, uint32_t* __restrict__ zc_ctr, uint32_t* __restrict__ zc_flag, uint32_t zc_seq) {
   static_assert((WG & (WG - 1)) == 0, "tile must be a power of two");
   __shared__ HybLds<WG> L;
+  const bool wt = zc_flag != nullptr;
   const int t = threadIdx.x;
   const uint64_t i = (uint64_t)blockIdx.x * TP + t;
   const bool mine = t < TP && i < n;
@@ -762,6 +784,7 @@ __global__ __launch_bounds__(WG) void csum_hyb(
     w.small = false;
   }
 
+  auto tile = [&]() {
   if constexpr (!WIN && UD > 0) {
     // Small-packet tiles, decided per wave: a wave whose packets all span
     // <= UD chunks sums them directly and finishes at once — the quad-lane
@@ -776,12 +799,12 @@ __global__ __launch_bounds__(WG) void csum_hyb(
     const bool small = __all(p.nch <= (uint32_t)UD) != 0;
     if (small) {
       const uint32_t s = (TP == WG && __all(p.nch <= 4u)) ? quad_sum(r, p) : direct_sum<UD ? UD : 1>(r, p);
-      finish_tile<WG, CH>(L, s, d, mine, i, n, out, partial, store);
+      finish_tile<WG, CH>(L, s, d, mine, i, n, out, partial, store, wt);
     }
     if (!__syncthreads_or(!small)) return;
     const uint32_t s =
         hyb_scan_tile<WG, TP, GB, UB, US, AUXB, false, SU, false, QS>(L, r, small ? PktInfo{} : p, big_chunks);
-    if (!small) finish_tile<WG, CH>(L, s, d, mine, i, n, out, partial, store);
+    if (!small) finish_tile<WG, CH>(L, s, d, mine, i, n, out, partial, store, wt);
     return;
   }
 
@@ -793,19 +816,22 @@ __global__ __launch_bounds__(WG) void csum_hyb(
       // (a full tile: lane t holds packet blockIdx.x * WG + t), else one lane
       // per packet
       const uint32_t s = (TP == WG && __all(p.nch <= 4u)) ? quad_sum(r, p) : direct_sum<UD ? UD : 1>(r, p);
-      finish_tile<WG, CH>(L, s, d, mine, i, n, out, partial, store);
+      finish_tile<WG, CH>(L, s, d, mine, i, n, out, partial, store, wt);
       return;
     }
     const uint32_t s = hyb_scan_tile<WG, TP, GB, UB, US, AUXB, false, SU, false, QS>(L, r, p, big_chunks);
-    finish_tile<WG, CH>(L, s, d, mine, i, n, out, partial, store);
+    finish_tile<WG, CH>(L, s, d, mine, i, n, out, partial, store, wt);
   } else if constexpr (WIN) {
     // The tile spans >= 4 GiB: 64-bit global loads, fewer in flight per lane
     // so this rarely taken path does not raise the kernel's register count.
     const Srd r = make_srd(0ull, 0ull);
     const PktInfo p = pkt_info(d, 0ull);
     const uint32_t s = hyb_scan_tile<WG, TP, 16, 4, 4, AUXB, true, 1>(L, r, p, big_chunks);
-    finish_tile<WG, CH>(L, s, d, mine, i, n, out, partial, store);
+    finish_tile<WG, CH>(L, s, d, mine, i, n, out, partial, store, wt);
   }
+  };
+  tile();
+  if (wt) zc_complete(zc_ctr, zc_flag, zc_seq);
 }
 
 // ---- descriptors far larger than a tile: csum_split -----------------------
@@ -1157,7 +1183,7 @@ template <int TP, int GB, int UB, int US, int AUXB, int UD, int SU = 1, bool QS 
 static hipError_t launch_hyb_tp(const uint8_t* arena, uint64_t arena_bytes, const void* desc,
                                 uint32_t n, uint16_t* out, uint32_t* partial,
                                 unsigned long long* err, hipStream_t stream, uint32_t big_chunks,
-                                uint32_t store = 0) {
+                                uint32_t store = 0, ZcSignal zc = {}) {
   static_assert(TP <= WG, "a tile holds at most one descriptor per thread");
   const uint32_t grid = (uint32_t)(((uint64_t)n + TP - 1) / TP);
   const uint4* d = reinterpret_cast<const uint4*>(desc);
@@ -1166,7 +1192,7 @@ static hipError_t launch_hyb_tp(const uint8_t* arena, uint64_t arena_bytes, cons
   const bool win = ((uintptr_t)arena & 15u) + arena_bytes + 64 >= kMaxSrdBytes;
 #define NSK_LAUNCH(W, C)                                                                              \
   hipLaunchKernelGGL((csum_hyb<WG, TP, GB, UB, US, AUXB, UD, W, SU, QS, C>), dim3(grid), dim3(WG), 0, \
-                     stream, arena, arena_bytes, d, n, out, partial, err, big_chunks, store)
+                     stream, arena, arena_bytes, d, n, out, partial, err, big_chunks, store, zc.ctr, zc.flag, zc.seq)
   if (partial) {
     if (win) NSK_LAUNCH(true, true);
     else NSK_LAUNCH(false, true);
@@ -1196,12 +1222,13 @@ template <int GB, int UB, int US, int AUXB, int UD = 0, int SU = 1, bool QS = fa
 static hipError_t launch_hyb(const uint8_t* arena, uint64_t arena_bytes, const void* desc,
                              uint32_t n, uint16_t* out, uint32_t* partial,
                              unsigned long long* err, hipStream_t stream, uint32_t big_chunks,
-                             uint64_t sizing_bytes = 0, uint64_t tile_bytes = kTileBytes, uint32_t store = 0) {
+                             uint64_t sizing_bytes = 0, uint64_t tile_bytes = kTileBytes, uint32_t store = 0,
+                             ZcSignal zc = {}) {
   const uint64_t avg = std::max<uint64_t>((sizing_bytes ? sizing_bytes : arena_bytes) / n, 1);
   const uint64_t want = tile_bytes / avg;
 #define NSK_TP(tp) \
   if (want >= tp)              \
-  return launch_hyb_tp<tp, GB, UB, US, AUXB, UD, SU, QS>(arena, arena_bytes, desc, n, out, partial, err, stream, big_chunks, store)
+  return launch_hyb_tp<tp, GB, UB, US, AUXB, UD, SU, QS>(arena, arena_bytes, desc, n, out, partial, err, stream, big_chunks, store, zc)
   if constexpr (UD > 0) {
     // The small-packet variant (launch_batch: < 256 B per descriptor) keeps
     // full tiles of one-wave workgroups: its direct path is one packet per
@@ -1211,7 +1238,7 @@ static hipError_t launch_hyb(const uint8_t* arena, uint64_t arena_bytes, const v
     // vs 16.7 us for 256-thread tiles (tools/tune.py --rot-desc,
     // profiles/r02/tune_small_wg_rotdesc.log; 128-B packets -1%, 192-B +2%).
     return launch_hyb_tp<64, GB, UB, US, AUXB, UD, SU, QS, 64>(arena, arena_bytes, desc, n, out, partial, err,
-                                                               stream, big_chunks, store);
+                                                               stream, big_chunks, store, zc);
   } else {
     NSK_TP(256);
     NSK_TP(128);
@@ -1222,7 +1249,7 @@ static hipError_t launch_hyb(const uint8_t* arena, uint64_t arena_bytes, const v
     NSK_TP(4);
     NSK_TP(2);
     return launch_hyb_tp<1, GB, UB, US, AUXB, UD, SU, QS>(arena, arena_bytes, desc, n, out, partial, err, stream,
-                                                          big_chunks, store);
+                                                          big_chunks, store, zc);
   }
 #undef NSK_TP
 }
@@ -1258,8 +1285,9 @@ hipError_t launch_batch(const uint8_t* arena, uint64_t arena_bytes,
                         const void* desc, uint32_t n, uint16_t* out,
                         ChainScratch chain, unsigned long long* err,
                         hipStream_t stream, uint64_t sizing_bytes, uint32_t store,
-                        uint32_t* split) {
+                        uint32_t* split, ZcSignal zc) {
   uint32_t* part = chain.partial;  // the chained scratch (layout: csum_kernels.h)
+  if (zc.flag && (part || split || !zc.ctr)) return hipErrorInvalidValue;  // unchained tiles only
   if (n == 0) return hipSuccess;
   hipError_t e;
   if (sizing_bytes == 0) sizing_bytes = arena_bytes;
@@ -1295,14 +1323,14 @@ hipError_t launch_batch(const uint8_t* arena, uint64_t arena_bytes,
     // 1 MiB of packets 44.7-45.3 vs 50.7-50.9 (profiles/r02/latency_zc_ab.txt).
     e = launch_hyb<8, 16, 4, 2, 0, 2>(arena, arena_bytes, desc, n, out, part, err, stream,
                                       arena ? kBigChunks : kZeroCopyBigChunks, sizing_bytes,
-                                      arena ? kTileBytes : kZeroCopyTileBytes, store);
+                                      arena ? kTileBytes : kZeroCopyTileBytes, store, zc);
   } else {
     // Small packets: the same kernel plus the direct path — a tile whose
     // packets all span <= 5 chunks (any <= 65-B packet) has each lane read its
     // own packet with no scan; 16 x 8 groups keep the register count (and the
     // occupancy this latency-bound case needs) lower.
     e = launch_hyb<16, 8, 4, 2, 5>(arena, arena_bytes, desc, n, out, part, err, stream, 64u, 0, kTileBytes,
-                                   store);
+                                   store, zc);
   }
   if (e != hipSuccess || part == nullptr) return e;
   // run folding: one pass over 6 B per descriptor, any run length

@@ -392,7 +392,8 @@ hipError_t launch_wg(const uint8_t* arena, uint64_t arena_bytes, const void* des
                      uint16_t* out, unsigned long long* err, hipStream_t s) {
   const uint32_t grid = (uint32_t)(((uint64_t)n + TP - 1) / TP);
   hipLaunchKernelGGL((csum_hyb<WG, TP, 8, 16, 4, 2, 0, false, 2, false, false>), dim3(grid), dim3(WG), 0, s, arena,
-                     arena_bytes, reinterpret_cast<const uint4*>(desc), n, out, nullptr, err, BIG, 0u);
+                     arena_bytes, reinterpret_cast<const uint4*>(desc), n, out, nullptr, err, BIG, 0u, nullptr, nullptr,
+                     0u);
   return hipGetLastError();
 }
 
