@@ -122,10 +122,11 @@ struct PinBuf {
 using MappedPin = PinBuf<uint8_t, hipHostMallocMapped | hipHostMallocNonCoherent | hipHostMallocPortable>;
 // Mapped, fine-grained (coherent) host memory: device stores reach it
 // uncached, in order, so the host may poll it while kernels run.  A zero-copy
-// pass writes its results here and then a completion word (nsk::launch_signal,
-// a system-scope release store), which the caller spins on instead of
-// hipStreamSynchronize: the stream's own completion arrives ~10 us after the
-// kernel's last store (tools/sync_probe.hip).
+// pass writes its results here and then a completion word (from the checksum
+// launch's last workgroup, nsk::ZcSignal, or a signal kernel behind a chained
+// pass's fold), which the caller spins on instead of hipStreamSynchronize:
+// the stream's own completion arrives ~10 us after the kernel's last store
+// (tools/sync_probe.hip).
 using CoherentPin = PinBuf<uint8_t, hipHostMallocMapped | hipHostMallocCoherent | hipHostMallocPortable>;
 
 // What a zero-copy pass reads: its descriptor table and the bytes small
