@@ -1034,15 +1034,26 @@ int ns_csum_vv_batch(ns_csum_ctx* ctx, const ns_view* views, uint32_t nviews,
                      const ns_seg* segs, uint32_t nsegs, uint16_t* out) {
   if (!ctx || (nsegs && (!segs || !out)) || (nviews && !views)) return NS_EINVAL;
   if (nsegs == 0) return NS_OK;
-  std::vector<std::vector<std::pair<const uint8_t*, uint64_t>>> clipped(nsegs);
+  // Every segment's clipped views as one flat list of chain pieces (a
+  // segment's first piece restarts, the others continue it), so a
+  // sendTCPBatch-sized call makes a few allocations, not two per segment.
+  std::vector<Piece> ps;
+  std::vector<uint32_t> start(nsegs + 1);
+  std::vector<std::pair<const uint8_t*, uint64_t>> clipped;
+  ps.reserve((size_t)nsegs * 2);
   SpanProbe pr;
   for (uint32_t q = 0; q < nsegs; ++q) {
-    int rc = clip_views(views, nviews, segs[q].off, segs[q].size, &clipped[q]);
+    int rc = clip_views(views, nviews, segs[q].off, segs[q].size, &clipped);
     if (rc != NS_OK) return rc;
-    for (const auto& pc : clipped[q]) pr.add(pc.first, pc.second);
+    start[q] = (uint32_t)ps.size();
+    for (size_t k = 0; k < clipped.size(); ++k) {
+      ps.push_back(Piece{clipped[k].first, clipped[k].second, k == 0});
+      pr.add(clipped[k].first, clipped[k].second);
+    }
   }
+  start[nsegs] = (uint32_t)ps.size();
   Gather gt(ctx, pr.stage(ctx));
-  for (uint32_t q = 0; q < nsegs; ++q) gt.segment(clipped[q], segs[q].initial);
+  for (uint32_t q = 0; q < nsegs; ++q) gt.chain(ps.data() + start[q], start[q + 1] - start[q], segs[q].initial);
   return gt.run(out);
 }
 
