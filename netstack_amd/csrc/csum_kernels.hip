@@ -414,12 +414,13 @@ __device__ __forceinline__ uint32_t quad_sum(const Srd& r, const PktInfo& p) {
 // Returns this thread's packet sum (finish_tile turns it into the result).
 // FX = always the exact (T, W) accumulator (csum_split: its pieces' sums are
 // added, so they must be exact mod 2^32, not W-only class values).
-// QS = quad-lane small runs (US = 4, SRD path only): a wave takes 64
+// QS = quad-lane small runs (US = 4, SRD path only; 1: nontemporal loads, 2:
+// the default policy): a wave takes 64
 // consecutive small runs per iteration, lane l looking up run l and quad q of
 // load instruction j loading run 16 j + q, one chunk per lane; consecutive
 // runs lie back to back in memory when packets are packed, so one
 // instruction reads ~1 KiB contiguous and the loads are nontemporal.
-template <int WG, int TP, int GB, int UB, int US, int AUXB, bool GL, int SU, bool FX = false, bool QS = false>
+template <int WG, int TP, int GB, int UB, int US, int AUXB, bool GL, int SU, bool FX = false, int QS = 0>
 __device__ __forceinline__ uint32_t hyb_scan_tile(HybLds<WG>& L, const Srd& r, const PktInfo& p,
                                                   uint32_t big_chunks) {
   constexpr int P = WG;
@@ -572,7 +573,7 @@ __device__ __forceinline__ uint32_t hyb_scan_tile(HybLds<WG>& L, const Srd& r, c
       if (li == 0) atomicAdd(&L.acc[pk], sg);
     }
 
-    if constexpr (QS && !GL) {
+    if constexpr (QS != 0 && !GL) {
       static_assert(US == 4, "quad-lane small runs are runs of 4 chunks");
       const uint32_t c = (uint32_t)lane & 3u;
       for (uint32_t qb = (uint32_t)wv * 64u; qb < RSt; qb += (uint32_t)NW * 64u) {
@@ -606,7 +607,7 @@ __device__ __forceinline__ uint32_t hyb_scan_tile(HybLds<WG>& L, const Srd& r, c
           const int src = (int)(16 * j + (lane >> 2));
           mj[j] = (uint32_t)__shfl((int)meta, src, 64);
           const uint32_t o = (uint32_t)__shfl((int)roff, src, 64);
-          v[j] = bload<2>(r.rsrc, c < (mj[j] & 7u) ? o + 16u * c : r.oob);
+          v[j] = bload<QS == 1 ? 2 : 0>(r.rsrc, c < (mj[j] & 7u) ? o + 16u * c : r.oob);
         }
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -759,7 +760,7 @@ __device__ __forceinline__ void zc_complete(uint32_t* __restrict__ ctr, uint32_t
 // SU = small runs issued per lane per iteration; CH = chained batch
 // (finish_tile writes partials and continuation flags for fold_scan).
 template <int WG, int TP, int GB, int UB, int US, int AUXB, int UD = 0, bool WIN = false,
-          int SU = 1, bool QS = false, bool CH = false>
+          int SU = 1, int QS = 0, bool CH = false>
 __global__ __launch_bounds__(WG) void csum_hyb(
     const uint8_t* __restrict__ arena, uint64_t arena_bytes,
     const uint4* __restrict__ desc, uint32_t n, uint16_t* __restrict__ out,
@@ -1179,7 +1180,7 @@ static void launch_fold(ChainScratch ch, uint32_t n, uint16_t* out, const void* 
                      reinterpret_cast<const uint4*>(desc), arena);
 }
 
-template <int TP, int GB, int UB, int US, int AUXB, int UD, int SU = 1, bool QS = false, int WG = 256>
+template <int TP, int GB, int UB, int US, int AUXB, int UD, int SU = 1, int QS = 0, int WG = 256>
 static hipError_t launch_hyb_tp(const uint8_t* arena, uint64_t arena_bytes, const void* desc,
                                 uint32_t n, uint16_t* out, uint32_t* partial,
                                 unsigned long long* err, hipStream_t stream, uint32_t big_chunks,
@@ -1218,7 +1219,7 @@ constexpr uint32_t kBigChunks = 40;  // packets of >= this many 16-B chunks take
 // way, 26.8 us through the lane runs)
 constexpr uint32_t kZeroCopyBigChunks = 2048;
 constexpr uint64_t kZeroCopyTileBytes = 16u << 10;  // ... and its tiles
-template <int GB, int UB, int US, int AUXB, int UD = 0, int SU = 1, bool QS = false>
+template <int GB, int UB, int US, int AUXB, int UD = 0, int SU = 1, int QS = 0>
 static hipError_t launch_hyb(const uint8_t* arena, uint64_t arena_bytes, const void* desc,
                              uint32_t n, uint16_t* out, uint32_t* partial,
                              unsigned long long* err, hipStream_t stream, uint32_t big_chunks,

@@ -220,7 +220,7 @@ __global__ __launch_bounds__(256) void calib_tile_x(const uint4* __restrict__ p,
   }
 }
 
-template <int GB, int UB, int US, int AUXB, uint32_t BIG, int UD = 0, int SU = 1, bool QS = false>
+template <int GB, int UB, int US, int AUXB, uint32_t BIG, int UD = 0, int SU = 1, int QS = 0>
 hipError_t launch_h(const uint8_t* arena, uint64_t arena_bytes, const void* desc, uint32_t n,
                     uint16_t* out, unsigned long long* err, hipStream_t s) {
   return launch_hyb<GB, UB, US, AUXB, UD, SU, QS>(arena, arena_bytes, desc, n, out, nullptr, err, s, BIG);
@@ -725,11 +725,11 @@ struct Variant {
 // and DESIGN.md §4.2.
 static const Variant kVariants[] = {
     {"prod", launch_h<8, 16, 4, 2, kBigChunks, 0, 2>},  // the production big-packet launch
-    {"qs_b40", launch_h<8, 16, 4, 2, kBigChunks, 0, 2, true>},   // quad-lane nt small runs
-    {"qs_b24", launch_h<8, 16, 4, 2, 24, 0, 2, true>},
-    {"qs_b64", launch_h<8, 16, 4, 2, 64, 0, 2, true>},
-    {"qs_b1000", launch_h<8, 16, 4, 2, 1000, 0, 2, true>},     // every packet below 16 KB through small runs
-    {"prod_small_qs", launch_h<16, 8, 4, 2, 64, 5, 1, true>},
+    {"qs_b40", launch_h<8, 16, 4, 2, kBigChunks, 0, 2, 1>},   // quad-lane nt small runs
+    {"qs_b24", launch_h<8, 16, 4, 2, 24, 0, 2, 1>},
+    {"qs_b64", launch_h<8, 16, 4, 2, 64, 0, 2, 1>},
+    {"qs_b1000", launch_h<8, 16, 4, 2, 1000, 0, 2, 1>},     // every packet below 16 KB through small runs
+    {"prod_small_qs", launch_h<16, 8, 4, 2, 64, 5, 1, 1>},
     {"prod_g8u16_b64", launch_h<8, 16, 4, 2, 64, 0, 2>},
     {"g8u16_su1", launch_h<8, 16, 4, 2, 64>},
     {"chained_main", launch_chained<false>},
@@ -807,6 +807,10 @@ static const Variant kVariants[] = {
     {"floor_quad_nt_wg64", launch_floor_quad<1, 2, 64>},
     {"quad_pipe4_nt", launch_quad_pipe<4, 2>},
     {"quad_pipe8_nt", launch_quad_pipe<8, 2>},
+    // quad-lane small runs with the default cache policy
+    {"qsd_b40", launch_h<8, 16, 4, 2, kBigChunks, 0, 2, 2>},
+    {"qsd_b64", launch_h<8, 16, 4, 2, 64, 0, 2, 2>},
+    {"prod_small_qsd", launch_h<16, 8, 4, 2, 64, 5, 1, 2>},
     // one-wave workgroups, 2-4 groups of 64 packets per wave (cold tables)
     {"quad_pipe2_nt_wg64", launch_quad_pipe<2, 2, 64>},
     {"quad_pipe4_nt_wg64", launch_quad_pipe<4, 2, 64>},

@@ -103,7 +103,8 @@ def main():
             arenas = [a7]
         elif cfg >= 100:  # uniform packets of `cfg` bytes, 1.5 GB of payload (TP-rule sweeps)
             b = W.uniform(f"uniform_{cfg}B", 9000 + cfg, nover.get(cfg, (1_572_864_000 // cfg)), cfg)
-            arenas = [b.arena_device(dev)]
+            arenas = [b.arena_device(dev)] + [W.random_bytes_torch(b.seed + 77 * r, b.arena_bytes, dev)
+                                              for r in range(1, rot)]
         else:
             b = W.config(cfg, nover.get(cfg))
             arenas = [b.arena_device(dev)] + [W.random_bytes_torch(b.seed + 77 * r, b.arena_bytes, dev)
