@@ -674,6 +674,7 @@ struct ByteSink {
     if (adopted) return;
     if (zero_copy_enabled()) stage = lease_gather_stage(ctx, &rc);
     if (!stage) rc = to_big(0);
+    else staged.reserve(64);
   }
   ~ByteSink() { return_gather_stage(ctx, stage); }
   ByteSink(const ByteSink&) = delete;
@@ -1156,6 +1157,8 @@ int ns_csum_packet_buffers(ns_csum_ctx* ctx, const ns_pkt_buf* pkts, uint32_t n,
     for (const auto& sg : pb[i].seg) pr.add(sg.first, sg.second);
   }
   Gather gt(ctx, pr.stage(ctx));
+  gt.desc.reserve((size_t)n * 4);  // IP header + transport chain pieces, typically
+  gt.result_at.reserve((size_t)n * 2);
   std::vector<nsh::PacketPlan> plan(n);
   for (uint32_t i = 0; i < n; ++i) {
     const int rc = nsh::plan_packet(gt, pb[i], op, &plan[i]);

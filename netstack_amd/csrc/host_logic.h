@@ -181,6 +181,8 @@ struct PacketBytes {
     if (pk.hdr_len && !pk.hdr) return NS_EINVAL;
     if (pk.ndata && !pk.data) return NS_EINVAL;
     hdr_len = pk.hdr_len;
+    seg.reserve((size_t)pk.ndata + 1);
+    at.reserve((size_t)pk.ndata + 1);
     add(pk.hdr, pk.hdr_len);
     uint64_t left = pk.data_size;
     for (uint32_t k = 0; k < pk.ndata && left; ++k) {
@@ -322,7 +324,8 @@ int plan_packet(Builder& g, const PacketBytes& pb, uint32_t op, PacketPlan* pp) 
     }
     return NS_EINVAL;
   }
-  std::vector<Piece> ps;
+  thread_local std::vector<Piece> ps;  // capacity kept across the packets of a batch
+  ps.clear();
   auto add_chain = [&](uint16_t init) {
     g.chain(ps.data(), ps.size(), init);
     ps.clear();

@@ -108,6 +108,55 @@ int main(int argc, char** argv) {
     });
     std::printf(" \"chains_45_tcp_segments\": {\"gpu_med_us\": %.2f, \"gpu_p99_us\": %.2f},\n", g.med, g.p99);
   }
+  {  // recvmmsg batches of received IPv4/TCP packets as PacketBuffers (NS_PKB_VERIFY):
+     // 1500-B packets in BufConfig views (128+256+256+512+348), valid checksums
+    const uint32_t cuts[5] = {128, 256, 256, 512, 348};
+    auto be16 = [](uint8_t* p, uint32_t v) { p[0] = (uint8_t)(v >> 8); p[1] = (uint8_t)v; };
+    std::printf(" \"packet_buffers_verify\": [");
+    const uint32_t counts[] = {8, 64};
+    for (int qi = 0; qi < 2; ++qi) {
+      const uint32_t n = counts[qi];
+      std::vector<uint8_t> pk((size_t)n * 1500);
+      std::vector<ns_view> views((size_t)n * 5);
+      std::vector<ns_pkt_buf> pb(n);
+      for (uint32_t i = 0; i < n; ++i) {
+        uint8_t* p = pk.data() + (size_t)i * 1500;
+        std::memcpy(p + 40, payload.data() + (size_t)i * 1460, 1460);
+        const uint8_t ip[20] = {0x45, 0, 0x05, 0xDC, (uint8_t)(i >> 8), (uint8_t)i, 0x40, 0, 64, 6, 0, 0,
+                                10, 0, 0, 1, 10, 0, 0, 2};
+        std::memcpy(p, ip, 20);
+        be16(p + 10, ~scalar(p, 20, 0) & 0xFFFF);
+        uint8_t* t = p + 20;
+        std::memset(t, 0, 20);
+        be16(t, 40000 + i);
+        be16(t + 2, 443);
+        t[12] = 5 << 4;
+        t[13] = 0x10;
+        be16(t + 14, 65535);
+        const uint8_t ph[12] = {10, 0, 0, 1, 10, 0, 0, 2, 0, 6, 0x05, 0xC8};  // pseudo-header, length 1480
+        uint16_t x = scalar(ph, 12, 0);
+        x = scalar(t, 20, x);
+        x = scalar(p + 40, 1460, x);
+        be16(t + 16, ~x & 0xFFFF);
+        uint32_t o = 0;
+        for (int k = 0; k < 5; ++k) {
+          views[(size_t)i * 5 + k] = ns_view{p + o, cuts[k]};
+          o += cuts[k];
+        }
+        pb[i] = ns_pkt_buf{nullptr, 0, &views[(size_t)i * 5], 5, 0, 1500};
+      }
+      std::vector<uint8_t> verdict(n);
+      check(ns_csum_packet_buffers(ctx, pb.data(), n, NS_PKB_VERIFY, nullptr, verdict.data()), "packet_buffers");
+      uint32_t valid = 0;
+      for (uint8_t v : verdict) valid += v == NS_PKB_VALID;
+      const Stat g = time_calls(std::max(20, iters / 2), [&] {
+        check(ns_csum_packet_buffers(ctx, pb.data(), n, NS_PKB_VERIFY, nullptr, verdict.data()), "packet_buffers");
+      });
+      std::printf("%s{\"packets\": %u, \"gpu_med_us\": %.2f, \"gpu_p99_us\": %.2f, \"valid\": %u}", qi ? ", " : "",
+                  n, g.med, g.p99, valid);
+    }
+    std::printf("],\n");
+  }
   {  // host batches of growing size: zero-copy below kStageBytes (1 MiB), DMA above
     std::printf(" \"batch_host_sizes\": [");
     const uint32_t ns[] = {43, 170, 680, 2720};
