@@ -875,8 +875,11 @@ __global__ __launch_bounds__(256) void csum_split(const uint8_t* __restrict__ ar
     d.len = (uint32_t)(r1 - r0);
     d.odd = (raw.w >> 16) & 1u;
   }
-  const uint64_t base = arena_abs & ~15ull;
-  const Srd r = make_srd(base, arena_abs + arena_bytes - base);
+  // The piece's own SRD window (uniform over the block: it depends only on
+  // the descriptor and blockIdx), so the arena may be any size; launch_batch
+  // keeps every piece below 2^31 + 128 bytes.
+  const uint64_t base = (arena_abs + off + r0) & ~15ull;
+  const Srd r = make_srd(base, r1 > r0 ? arena_abs + off + r1 - base : 0ull);
   const PktInfo p = pkt_info(d, base);
   const uint32_t s = hyb_scan_tile<256, 1, GB, UB, US, AUXB, false, SU, true>(L, r, p, big_chunks);
   if (t != 0) return;
@@ -1292,11 +1295,16 @@ hipError_t launch_batch(const uint8_t* arena, uint64_t arena_bytes,
   if (n == 0) return hipSuccess;
   hipError_t e;
   if (sizing_bytes == 0) sizing_bytes = arena_bytes;
-  if (split && sizing_bytes / n >= kSplitAvg && n < kSplitMaxN &&
-      ((uintptr_t)arena & 15u) + arena_bytes + 64 < kMaxSrdBytes) {
+  if (split && sizing_bytes / n >= kSplitAvg && n < kSplitMaxN) {
     // A few huge descriptors: spread each over many workgroups.  (`split`
-    // holds zeros between launches: csum_split leaves it so.)
-    const uint32_t per = std::max<uint32_t>(1, kSplitWGs / n);
+    // holds zeros between launches: csum_split leaves it so.)  Each piece
+    // reads through its own SRD window, so arenas of any size qualify; in one
+    // of 4 GiB or more, at least two pieces per descriptor keep a piece of a
+    // u32-length descriptor below the window limit.  (Before the windows such
+    // arenas took one workgroup per descriptor: 64-bit loads, ~0.1 s for a
+    // 4 GiB descriptor.)
+    const bool huge_arena = ((uintptr_t)arena & 15u) + arena_bytes + 64 >= kMaxSrdBytes;
+    const uint32_t per = std::max<uint32_t>(huge_arena ? 2u : 1u, kSplitWGs / n);
     hipLaunchKernelGGL((csum_split<8, 16, 4, 2, 2>), dim3(n * per), dim3(256), 0, stream, arena, arena_bytes,
                        reinterpret_cast<const uint4*>(desc), n, per, out, part, split, err, store, 64u);
     e = hipGetLastError();

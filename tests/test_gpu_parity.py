@@ -993,6 +993,50 @@ def test_huge_descriptors_split(engine, chained):
     assert np.array_equal(dt.cpu().numpy(), expect)
 
 
+@pytest.mark.parametrize("tiles", [False, True])
+@pytest.mark.parametrize("chained", [False, True])
+def test_maximum_length_descriptors(engine, chained, tiles):
+    """The largest descriptor the table can hold: len = 0xFFFFFFFF (the u32
+    maximum, 2^28 + 1 chunks from an unaligned start) at an odd offset, and a
+    second one of 2^32 - 7 bytes ending 4 bytes before the end of a 4 GiB +
+    4 MiB arena.  Go's uint32 accumulator wraps many times over such a buffer
+    (checksum.go:41-43); the oracle wraps the same way.  With a few
+    descriptors the batch takes csum_split; with `tiles`, 300 descriptors
+    (n >= kSplitMaxN) send them through the tile kernel, where a tile holding
+    one spans more than an SRD can address (the 64-bit global-load path)."""
+    import oracle as O
+
+    torch = _torch()
+    size = (1 << 32) + (1 << 22)
+    g = torch.Generator(device="cuda").manual_seed(77 + 2 * chained + tiles)
+    arena = torch.randint(0, 256, (size,), dtype=torch.uint8, device="cuda", generator=g)
+    host = arena.cpu().numpy()
+    rng = np.random.default_rng(77 + 2 * chained + tiles)
+    big = [(1, 0xFFFFFFFF), ((1 << 22) + 3, (1 << 32) - 7)]
+    small = [(size - 1, 1), (12345, 0)]
+    if tiles:
+        offs = rng.integers(0, size - 70000, 296)
+        small += [(int(o), int(rng.integers(0, 65536))) for o in offs]
+    rows = big[:1] + small[: len(small) // 2] + big[1:] + small[len(small) // 2:]
+    d = np.zeros(len(rows), dtype=O.DESC_DTYPE)
+    d["off"] = [o for o, _ in rows]
+    d["len"] = [L for _, L in rows]
+    d["initial"] = rng.integers(0, 65536, len(rows))
+    d["flags"] = rng.integers(0, 2, len(rows))
+    d["flags"][0] |= 1  # odd carry-in on the u32-max descriptor
+    if chained:
+        d["flags"][1::3] |= 2
+    want, bad = O.c_batch(host, d, chained=chained)
+    assert bad == 0
+    desc = torch.from_numpy(d.view(np.uint8).copy()).cuda()
+    engine.sync()
+    out = engine.batch_tensors(arena, desc, chained=chained)
+    torch.cuda.synchronize()
+    assert engine.sync() == 0
+    got = out.cpu().numpy().view(np.uint16)
+    assert np.array_equal(got, want), np.nonzero(got != want)
+
+
 @pytest.mark.parametrize("bad_at", [5, 300_000])
 def test_host_batch_out_of_range_is_erange_and_pipeline_recovers(engine, bad_at):
     """ns_csum_batch_host over a multi-chunk DMA pipeline (an arena above one
