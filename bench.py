@@ -74,21 +74,33 @@ def parse():
 # distributed plumbing (also exercised by tests/test_bench_dist.py on gloo)
 # ---------------------------------------------------------------------------
 class Dist:
-    def __init__(self, backend: str | None):
+    def __init__(self, backend: str | None, device_index: int | None = None):
+        """`device_index`: this rank's GPU, already made current; with nccl
+        (RCCL) it is bound to the process group, so the barrier runs on it
+        rather than on a device RCCL guesses from the rank."""
         import torch.distributed as dist
 
         self.dist = dist
         self.backend = backend
+        self.device_index = device_index if backend == "nccl" else None
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         self.local = int(os.environ.get("LOCAL_RANK", "0"))
         self.on = self.world > 1
         if self.on and not dist.is_initialized():
-            dist.init_process_group(backend=backend)
+            if self.device_index is not None:
+                import torch
+
+                dist.init_process_group(backend=backend, device_id=torch.device("cuda", self.device_index))
+            else:
+                dist.init_process_group(backend=backend)
 
     def barrier(self):
         if self.on:
-            self.dist.barrier()
+            if self.device_index is not None:
+                self.dist.barrier(device_ids=[self.device_index])
+            else:
+                self.dist.barrier()
 
     def max(self, x: float, device=None) -> float:
         if not self.on:
@@ -306,12 +318,13 @@ def main():
     from netstack_amd import Engine
 
     backend = args.dist_backend if args.dist_backend != "auto" else ("nccl" if torch.cuda.is_available() else "gloo")
-    dist = Dist(backend)
+    # one rank per GPU, made current before the process group exists; more
+    # ranks than GPUs share them (gloo control plane)
+    ordinal = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(ordinal)
+    dist = Dist(backend, ordinal)
     if dist.on and args.gpus != dist.world:
         print(f"warning: --gpus {args.gpus} != WORLD_SIZE {dist.world}", file=sys.stderr)
-    # one rank per GPU; more ranks than GPUs share them (gloo control plane)
-    ordinal = dist.local % max(1, torch.cuda.device_count())
-    torch.cuda.set_device(ordinal)
     dev = torch.device("cuda", ordinal)
     eng = Engine(ordinal)
 
