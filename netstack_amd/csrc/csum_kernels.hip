@@ -370,25 +370,21 @@ __device__ __forceinline__ uint32_t direct_sum(const Srd& r, const PktInfo& p) {
 // bytes, a quad DPP sum gives the packet's W, and the W-only class values
 // (s_class) shuffle back to one per lane.  1M x 64 B: 14.7 vs 16.3 us for the
 // lane-per-packet path (tools/tune.py, profiles/r02/tune_cfg3_quad.log).
-__device__ __forceinline__ uint32_t quad_sum(const Srd& r, const PktInfo& p) {
+__device__ __forceinline__ uint32_t quad_geo(const PktInfo& p) {  // nch (3 bits) | lo (4) | hiex (5) | phase (1)
+  return p.nch | ((p.ew & 15u) << 3) | (((p.ew >> 5) & 31u) << 7) | ((p.ew >> 31) << 12);
+}
+
+// The quad layout's sums: v[j] holds chunk l % 4 of packet 16 j + l / 4 and
+// g[j] that packet's geometry; a chunk past the packet's last is masked out
+// (it reads zeros in quad_sum, the next packet's bytes in a speculative load).
+__device__ __forceinline__ uint32_t quad_reduce(const uint4 (&v)[4], const uint32_t (&g)[4]) {
   const uint32_t l = threadIdx.x & 63u, c = l & 3u;
-  // nch (3 bits) | lo (4) | hiex (5) | phase (1)
-  const uint32_t geo = p.nch | ((p.ew & 15u) << 3) | (((p.ew >> 5) & 31u) << 7) | ((p.ew >> 31) << 12);
-  uint4 v[4];
-  uint32_t g[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int src = (int)(16 * j + (l >> 2));
-    g[j] = (uint32_t)__shfl((int)geo, src, 64);
-    const uint32_t f = (uint32_t)__shfl((int)p.first, src, 64);
-    v[j] = bload<2>(r.rsrc, c < (g[j] & 7u) ? f + 16u * c : r.oob);
-  }
   uint32_t sv[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const uint32_t gj = g[j];
+    const uint32_t gj = g[j], nc = gj & 7u;
     const int lo_b = c == 0 ? (int)((gj >> 3) & 15u) : 0;
-    const int hi_b = c + 1 == (gj & 7u) ? (int)((gj >> 7) & 31u) : 16;
+    const int hi_b = c + 1 == nc ? (int)((gj >> 7) & 31u) : (c < nc ? 16 : 0);
     uint4 w = v[j];
     w.x &= bytes_below(hi_b) & ~bytes_below(lo_b);
     w.y &= bytes_below(hi_b - 4) & ~bytes_below(lo_b - 4);
@@ -406,6 +402,50 @@ __device__ __forceinline__ uint32_t quad_sum(const Srd& r, const PktInfo& p) {
     me = (l >> 4) == (uint32_t)j ? x : me;
   }
   return me;
+}
+
+__device__ __forceinline__ uint32_t quad_sum(const Srd& r, const PktInfo& p) {
+  const uint32_t l = threadIdx.x & 63u, c = l & 3u;
+  const uint32_t geo = quad_geo(p);
+  uint4 v[4];
+  uint32_t g[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int src = (int)(16 * j + (l >> 2));
+    g[j] = (uint32_t)__shfl((int)geo, src, 64);
+    const uint32_t f = (uint32_t)__shfl((int)p.first, src, 64);
+    v[j] = bload<2>(r.rsrc, c < (g[j] & 7u) ? f + 16u * c : r.oob);
+  }
+  return quad_reduce(v, g);
+}
+
+// Speculative quad loads (one-wave small-packet tiles; launch_batch sets
+// `spec` only for a 16-B-aligned arena of exactly n * spec bytes, spec a
+// multiple of 16 up to 64): packet k predicted at arena byte k * spec, its 4
+// chunks loaded in quad_sum's layout together with the descriptors instead of
+// after them.  spec_check: every packet of the wave is where predicted and
+// spans <= 4 chunks (then the loaded chunks cover it), else the wave takes
+// quad_sum / direct_sum as without speculation.
+__device__ __forceinline__ void spec_load(const Srd& r, uint64_t tile0, uint32_t n, uint32_t spec, uint4 (&v)[4]) {
+  const uint32_t l = threadIdx.x & 63u, c = l & 3u;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const uint64_t k = tile0 + 16u * j + (l >> 2);
+    v[j] = bload<2>(r.rsrc, k < n ? (uint32_t)(k * spec) + 16u * c : r.oob);
+  }
+}
+
+__device__ __forceinline__ bool spec_check(const PktInfo& p, uint64_t i, uint32_t spec) {
+  return __all(p.nch == 0u || (p.nch <= 4u && (uint64_t)p.first == i * spec)) != 0;
+}
+
+__device__ __forceinline__ uint32_t spec_sum(const PktInfo& p, const uint4 (&v)[4]) {
+  const uint32_t l = threadIdx.x & 63u;
+  const uint32_t geo = quad_geo(p);
+  uint32_t g[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) g[j] = (uint32_t)__shfl((int)geo, (int)(16 * j + (l >> 2)), 64);
+  return quad_reduce(v, g);
 }
 
 // One tile through the scan path (thread t holds packet p of global index i).
@@ -765,15 +805,33 @@ __global__ __launch_bounds__(WG) void csum_hyb(
     const uint8_t* __restrict__ arena, uint64_t arena_bytes,
     const uint4* __restrict__ desc, uint32_t n, uint16_t* __restrict__ out,
     uint32_t* __restrict__ partial, unsigned long long* __restrict__ err, uint32_t big_chunks,
-    uint32_t store, uint32_t* __restrict__ zc_ctr, uint32_t* __restrict__ zc_flag, uint32_t zc_seq) {
+    uint32_t store, uint32_t* __restrict__ zc_ctr, uint32_t* __restrict__ zc_flag, uint32_t zc_seq,
+    uint32_t spec) {
   static_assert((WG & (WG - 1)) == 0, "tile must be a power of two");
   __shared__ HybLds<WG> L;
   const bool wt = zc_flag != nullptr;
   const int t = threadIdx.x;
   const uint64_t i = (uint64_t)blockIdx.x * TP + t;
   const bool mine = t < TP && i < n;
-  const uint4 raw = mine ? desc[i] : make_uint4(0, 0, 0, 0);
   const uint64_t arena_abs = (uint64_t)(uintptr_t)arena;
+  // Speculative payload loads beside the descriptor loads (spec_load), in
+  // the one-wave small-packet tiles.  There every lane loads its descriptor
+  // (the tail wave's spare lanes re-read the last one; the launcher never
+  // launches n = 0) and selects afterwards: a load behind a branch is waited
+  // for at the branch's end, before the speculative loads could be issued.
+  constexpr bool kSpec = !WIN && UD > 0 && WG == 64 && TP == WG;
+  [[maybe_unused]] uint4 sv[4];
+  uint4 raw;
+  if constexpr (kSpec) {
+    const uint4 rawl = desc[min(i, (uint64_t)n - 1u)];
+    // branch-free: with spec = 0 every slot is out of range (no memory access)
+    spec_load(make_srd(arena_abs & ~15ull, arena_abs + arena_bytes - (arena_abs & ~15ull)),
+              (uint64_t)blockIdx.x * TP, spec ? n : 0u, spec, sv);
+    __builtin_amdgcn_sched_barrier(0);  // all four issued before anything waits for the descriptor
+    raw = mine ? rawl : make_uint4(0, 0, 0, 0);
+  } else {
+    raw = mine ? desc[i] : make_uint4(0, 0, 0, 0);
+  }
   const Pkt d = decode(raw, mine, arena_abs, arena_bytes, err);
   park_store(L, store, raw, mine, arena_abs, arena_bytes, err);
   Win w;
@@ -799,7 +857,15 @@ __global__ __launch_bounds__(WG) void csum_hyb(
     const PktInfo p = pkt_info(d, w.base);
     const bool small = __all(p.nch <= (uint32_t)UD) != 0;
     if (small) {
-      const uint32_t s = (TP == WG && __all(p.nch <= 4u)) ? quad_sum(r, p) : direct_sum<UD ? UD : 1>(r, p);
+      bool done = false;
+      uint32_t s = 0;
+      if constexpr (kSpec) {
+        if (spec && spec_check(p, i, spec)) {
+          s = spec_sum(p, sv);
+          done = true;
+        }
+      }
+      if (!done) s = (TP == WG && __all(p.nch <= 4u)) ? quad_sum(r, p) : direct_sum<UD ? UD : 1>(r, p);
       finish_tile<WG, CH>(L, s, d, mine, i, n, out, partial, store, wt);
     }
     if (!__syncthreads_or(!small)) return;
@@ -1187,7 +1253,7 @@ template <int TP, int GB, int UB, int US, int AUXB, int UD, int SU = 1, int QS =
 static hipError_t launch_hyb_tp(const uint8_t* arena, uint64_t arena_bytes, const void* desc,
                                 uint32_t n, uint16_t* out, uint32_t* partial,
                                 unsigned long long* err, hipStream_t stream, uint32_t big_chunks,
-                                uint32_t store = 0, ZcSignal zc = {}) {
+                                uint32_t store = 0, ZcSignal zc = {}, uint32_t spec = 0) {
   static_assert(TP <= WG, "a tile holds at most one descriptor per thread");
   const uint32_t grid = (uint32_t)(((uint64_t)n + TP - 1) / TP);
   const uint4* d = reinterpret_cast<const uint4*>(desc);
@@ -1196,7 +1262,7 @@ static hipError_t launch_hyb_tp(const uint8_t* arena, uint64_t arena_bytes, cons
   const bool win = ((uintptr_t)arena & 15u) + arena_bytes + 64 >= kMaxSrdBytes;
 #define NSK_LAUNCH(W, C)                                                                              \
   hipLaunchKernelGGL((csum_hyb<WG, TP, GB, UB, US, AUXB, UD, W, SU, QS, C>), dim3(grid), dim3(WG), 0, \
-                     stream, arena, arena_bytes, d, n, out, partial, err, big_chunks, store, zc.ctr, zc.flag, zc.seq)
+                     stream, arena, arena_bytes, d, n, out, partial, err, big_chunks, store, zc.ctr, zc.flag, zc.seq, spec)
   if (partial) {
     if (win) NSK_LAUNCH(true, true);
     else NSK_LAUNCH(false, true);
@@ -1227,7 +1293,7 @@ static hipError_t launch_hyb(const uint8_t* arena, uint64_t arena_bytes, const v
                              uint32_t n, uint16_t* out, uint32_t* partial,
                              unsigned long long* err, hipStream_t stream, uint32_t big_chunks,
                              uint64_t sizing_bytes = 0, uint64_t tile_bytes = kTileBytes, uint32_t store = 0,
-                             ZcSignal zc = {}) {
+                             ZcSignal zc = {}, uint32_t spec = 0) {
   const uint64_t avg = std::max<uint64_t>((sizing_bytes ? sizing_bytes : arena_bytes) / n, 1);
   const uint64_t want = tile_bytes / avg;
 #define NSK_TP(tp) \
@@ -1242,7 +1308,7 @@ static hipError_t launch_hyb(const uint8_t* arena, uint64_t arena_bytes, const v
     // vs 16.7 us for 256-thread tiles (tools/tune.py --rot-desc,
     // profiles/r02/tune_small_wg_rotdesc.log; 128-B packets -1%, 192-B +2%).
     return launch_hyb_tp<64, GB, UB, US, AUXB, UD, SU, QS, 64>(arena, arena_bytes, desc, n, out, partial, err,
-                                                               stream, big_chunks, store, zc);
+                                                               stream, big_chunks, store, zc, spec);
   } else {
     NSK_TP(256);
     NSK_TP(128);
@@ -1338,8 +1404,19 @@ hipError_t launch_batch(const uint8_t* arena, uint64_t arena_bytes,
     // packets all span <= 5 chunks (any <= 65-B packet) has each lane read its
     // own packet with no scan; 16 x 8 groups keep the register count (and the
     // occupancy this latency-bound case needs) lower.
+    // Fixed-stride tables (every packet in a slot of `spec` bytes: an arena
+    // of exactly n slots, as a receive ring of fixed-size buffers) get the
+    // speculative payload loads (spec_load): the descriptor -> payload
+    // dependency is what this latency-bound case waits on.
+    // A table that only looks fixed-stride costs one wasted load round per
+    // wave; results never depend on the prediction.
+    uint32_t spec = 0;
+    if (arena && ((uintptr_t)arena & 15u) == 0 && arena_bytes % n == 0) {
+      const uint64_t st = arena_bytes / n;
+      if (st % 16 == 0 && st >= 16 && st <= 64) spec = (uint32_t)st;
+    }
     e = launch_hyb<16, 8, 4, 2, 5>(arena, arena_bytes, desc, n, out, part, err, stream, 64u, 0, kTileBytes,
-                                   store, zc);
+                                   store, zc, spec);
   }
   if (e != hipSuccess || part == nullptr) return e;
   // run folding: one pass over 6 B per descriptor, any run length

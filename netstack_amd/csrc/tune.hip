@@ -393,7 +393,7 @@ hipError_t launch_wg(const uint8_t* arena, uint64_t arena_bytes, const void* des
   const uint32_t grid = (uint32_t)(((uint64_t)n + TP - 1) / TP);
   hipLaunchKernelGGL((csum_hyb<WG, TP, 8, 16, 4, 2, 0, false, 2, false, false>), dim3(grid), dim3(WG), 0, s, arena,
                      arena_bytes, reinterpret_cast<const uint4*>(desc), n, out, nullptr, err, BIG, 0u, nullptr, nullptr,
-                     0u);
+                     0u, 0u);
   return hipGetLastError();
 }
 
@@ -714,6 +714,21 @@ hipError_t launch_small_wg(const uint8_t* arena, uint64_t arena_bytes, const voi
   return launch_hyb_tp<WGT, 16, 8, 4, 2, 5, 1, false, WGT>(arena, arena_bytes, desc, n, out, nullptr, err, s, 64u);
 }
 
+// ... and with the launcher's fixed-stride speculation (spec_load): an arena
+// of exactly n slots of 16-64 bytes gets its payload loads beside the
+// descriptor loads.
+template <int WGT>
+hipError_t launch_small_wg_spec(const uint8_t* arena, uint64_t arena_bytes, const void* desc, uint32_t n,
+                                uint16_t* out, unsigned long long* err, hipStream_t s) {
+  uint32_t spec = 0;
+  if (((uintptr_t)arena & 15u) == 0 && n && arena_bytes % n == 0) {
+    const uint64_t st = arena_bytes / n;
+    if (st % 16 == 0 && st >= 16 && st <= 64) spec = (uint32_t)st;
+  }
+  return launch_hyb_tp<WGT, 16, 8, 4, 2, 5, 1, false, WGT>(arena, arena_bytes, desc, n, out, nullptr, err, s, 64u, 0,
+                                                          ZcSignal{}, spec);
+}
+
 typedef hipError_t (*launch_fn)(const uint8_t*, uint64_t, const void*, uint32_t, uint16_t*,
                                 unsigned long long*, hipStream_t);
 struct Variant {
@@ -796,6 +811,7 @@ static const Variant kVariants[] = {
     {"quad_direct_nt_wg512", launch_quad_direct<1, 2, 512>},
     {"quad_pf0", launch_quad_prefetch<0xFFFFFFFFu>},
     {"small_wg64", launch_small_wg<64>},
+    {"small_wg64_spec", launch_small_wg_spec<64>},
     {"small_wg128", launch_small_wg<128>},
     {"quad_pf256k", launch_quad_prefetch<262144u>},
     {"quad_pf512k", launch_quad_prefetch<524288u>},

@@ -993,6 +993,55 @@ def test_huge_descriptors_split(engine, chained):
     assert np.array_equal(dt.cpu().numpy(), expect)
 
 
+@pytest.mark.parametrize("stride", [16, 32, 48, 64])
+@pytest.mark.parametrize("chained", [False, True])
+def test_fixed_stride_tables_speculative_loads(engine, stride, chained):
+    """Small-packet tables over an arena of exactly n slots of `stride` bytes
+    (16-B-aligned): the launcher predicts packet k at byte k * stride and
+    loads it beside its descriptor.  Waves where every prediction holds
+    (packets at their slot's start, any length up to the slot) use those
+    loads; waves with a packet elsewhere in its slot, spanning 5 chunks, or
+    out of order fall back.  Every result against the oracle, bit for bit,
+    including empties, odd carry-ins, an out-of-range descriptor, a permuted
+    table (every prediction wrong) and an unaligned arena (no speculation)."""
+    import oracle as O
+
+    torch = _torch()
+    rng = np.random.default_rng(stride * 7 + chained)
+    n = 64 * 40 + 17
+    arena = rng.integers(0, 256, n * stride, dtype=np.uint8)
+    d = np.zeros(n, dtype=O.DESC_DTYPE)
+    d["off"] = np.arange(n, dtype=np.uint64) * np.uint64(stride)
+    d["len"] = rng.integers(0, stride + 1, n)
+    d["len"][rng.random(n) < 0.05] = 0
+    d["initial"] = rng.integers(0, 65536, n)
+    d["flags"] = rng.integers(0, 2, n)
+    if chained:
+        d["flags"] |= (2 * (rng.random(n) < 0.3)).astype(np.uint16)
+    # waves 3, 9, ...: one packet moved inside its slot (prediction misses);
+    # waves 5, 11, ...: one packet spanning 5 chunks (past its slot)
+    for wv in range(3, n // 64, 6):
+        k = wv * 64 + int(rng.integers(0, 64))
+        d["off"][k] += np.uint64(int(rng.integers(1, 16)))
+        d["len"][k] = min(int(d["len"][k]), stride - int(d["off"][k]) % stride)
+    for wv in range(5, n // 64 - 1, 6):
+        k = wv * 64 + int(rng.integers(0, 63))
+        d["off"][k] += np.uint64(8)
+        d["len"][k] = 66
+    d["off"][100] = n * stride + 16  # out of range: counted, summed as empty
+
+    def check(table, arena_offset=0):
+        want, bad = O.c_batch(arena, table, chained=chained)
+        engine.sync()
+        got = dev_batch(engine, arena, table, chained=chained, arena_offset=arena_offset)
+        assert engine.sync() == bad
+        assert np.array_equal(got, want), np.flatnonzero(got != want)[:10]
+
+    check(d)
+    check(d, arena_offset=8)  # unaligned arena base: no speculation
+    check(d[rng.permutation(n)] if not chained else d[::-1].copy())  # every prediction wrong
+
+
 @pytest.mark.parametrize("tiles", [False, True])
 @pytest.mark.parametrize("chained", [False, True])
 def test_maximum_length_descriptors(engine, chained, tiles):
