@@ -155,7 +155,11 @@ int ns_csum_sync(ns_csum_ctx* ctx, void* stream, uint64_t* bad);
  * NS_BATCH_CHAINED, or when descriptors average >= 1 MiB (arena_bytes / n:
  * then each is spread over many workgroups), the call uses device scratch
  * that the context keeps per stream: calls on different streams of one
- * context run concurrently, calls on one stream are ordered by it.          */
+ * context run concurrently, calls on one stream are ordered by it.
+ * A 16-B-aligned arena of exactly n slots of 16, 32, 48 or 64 bytes (a ring
+ * of fixed-size receive buffers, packet k in slot k) lets the kernel load
+ * each packet beside its descriptor instead of after it; any other layout
+ * gives the same results.                                                    */
 int ns_csum_batch_dev(ns_csum_ctx* ctx, const uint8_t* d_arena,
                       uint64_t arena_bytes, const ns_pkt_desc* d_desc,
                       uint32_t n, uint16_t* d_out, uint32_t batch_flags,
