@@ -1110,6 +1110,26 @@ def test_host_batch_out_of_range_is_erange_and_pipeline_recovers(engine, bad_at)
     assert np.array_equal(engine.batch_host(arena, d), want)
 
 
+def test_host_batch_fixed_stride_chunks(engine):
+    """ns_csum_batch_host over 300,000 packets in cfg3's layout (64-B slots):
+    the pipeline's 128K-descriptor chunks, rebased to their own staging
+    arenas, are fixed-stride arenas of their own, so their launches take the
+    speculative payload loads; a corrupted slot start in the last chunk makes
+    its waves fall back.  Every result against the oracle."""
+    import oracle as O
+    from netstack_amd import workloads as W
+
+    b = W.config(3, 300_000)
+    arena = b.arena_host()
+    d = b.desc.copy()
+    d["off"][299_000] += np.uint64(3)
+    d["len"][299_000] = 61
+    want, bad = O.c_batch(arena, d)
+    assert bad == 0
+    got = engine.batch_host(arena, d)
+    assert np.array_equal(got, want)
+
+
 @pytest.mark.parametrize("chained", [False, True])
 def test_host_batch_pinned_table_read_in_place(engine, chained):
     """ns_csum_batch_host with a page-locked descriptor table (torch
