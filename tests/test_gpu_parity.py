@@ -1001,9 +1001,11 @@ def test_fixed_stride_tables_speculative_loads(engine, stride, chained):
     loads it beside its descriptor.  Waves where every prediction holds
     (packets at their slot's start, any length up to the slot) use those
     loads; waves with a packet elsewhere in its slot, spanning 5 chunks, or
-    out of order fall back.  Every result against the oracle, bit for bit,
-    including empties, odd carry-ins, an out-of-range descriptor, a permuted
-    table (every prediction wrong) and an unaligned arena (no speculation)."""
+    out of order fall back, and waves holding a packet over many slots (one
+    past the W-only limit) take the scan path.  Every result against the
+    oracle, bit for bit, including empties, odd carry-ins, an out-of-range
+    descriptor, a permuted table (every prediction wrong) and an unaligned
+    arena (no speculation)."""
     import oracle as O
 
     torch = _torch()
@@ -1029,6 +1031,10 @@ def test_fixed_stride_tables_speculative_loads(engine, stride, chained):
         d["off"][k] += np.uint64(8)
         d["len"][k] = 66
     d["off"][100] = n * stride + 16  # out of range: counted, summed as empty
+    # wave 7: a packet over many slots; wave 12: one past the W-only limit
+    # (> 8190 chunks, Go's uint32 wraps) — each lane then walks its packet
+    d["len"][7 * 64 + 5] = 3000
+    d["len"][12 * 64 + 9] = min(140_000, n * stride - int(d["off"][12 * 64 + 9]))
 
     def check(table, arena_offset=0):
         want, bad = O.c_batch(arena, table, chained=chained)
