@@ -128,6 +128,9 @@ func (s *csumStage) views(n int) (*C.ns_view, []C.ns_view) {
 	if n == 0 {
 		return nil, nil
 	}
+	if n > 1<<26 { // the array type below; a VectorisedView never gets near it
+		panic("netstack_csum: more than 1<<26 views in one packet")
+	}
 	p := unsafe.Pointer(&s.mem[s.used])
 	s.used += n * int(unsafe.Sizeof(C.ns_view{}))
 	return (*C.ns_view)(p), (*[1 << 26]C.ns_view)(p)[:n:n]

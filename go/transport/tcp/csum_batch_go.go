@@ -1,0 +1,27 @@
+// Copyright 2026 netstack-csum-mi355x authors.
+//
+// The default build's side of csum_batch_hip.go (see there): with
+// tcpBatchChecksums false, sendTCPBatch never defers, and buildTCPHdr
+// computes every segment's checksum itself exactly as the reference does
+// (connect.go:661-663).  finishTCPBatchChecksums is that same per-segment
+// computation, for completeness.
+
+// +build !hipcsum
+
+package tcp
+
+import (
+	"github.com/google/netstack/tcpip/buffer"
+	"github.com/google/netstack/tcpip/header"
+	"github.com/google/netstack/tcpip/stack"
+)
+
+const tcpBatchChecksums = false
+
+func finishTCPBatchChecksums(hdrs []stack.PacketDescriptor, data buffer.VectorisedView, pseudo []uint16) {
+	for i := range hdrs {
+		xsum := header.ChecksumVVWithOffset(data, pseudo[i], hdrs[i].Off, hdrs[i].Size)
+		tcp := header.TCP(hdrs[i].Hdr.View())
+		tcp.SetChecksum(^tcp.CalculateChecksum(xsum))
+	}
+}

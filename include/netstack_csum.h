@@ -263,15 +263,22 @@ typedef struct ns_pkt_buf {
  *   ICMPv6: ICMPv6Checksum(first view, src, dst, the other views) == the
  *     field (network/ipv6/icmp.go:76-84).
  * verdict[i]: NS_PKB_VALID / NS_PKB_INVALID; NS_PKB_UNCHECKED where the
- * reference verifies nothing on receive (UDP, other protocols, IPv4
- * fragments before reassembly, ICMPv4 other than echo); NS_PKB_MALFORMED
- * where IsValid or the transport's length checks drop the packet first.
+ * reference verifies nothing on receive (UDP, other protocols, ICMPv4 other
+ * than echo) and for IPv4 fragments, whose transport checksum can only be
+ * checked after reassembly (ipv4.go:375-385; the receive contract in
+ * INTEGRATION.md §2 says who checks it then); NS_PKB_MALFORMED where IsValid,
+ * HandlePacket's fragment checks (no payload, or a uint16
+ * FragmentOffset() + size - 1 that wraps: ipv4.go:357-373) or the
+ * transport's length checks drop the packet first.
  * NS_PKB_FILL — a batch to transmit: Header holds the IP header and the
  * transport header (Data the payload); writes ^sum into the transport
  * checksum field — TCP buildTCPHdr (connect.go:653-663), UDP sendUDP
  * (udp/endpoint.go:808-815), ICMPv4 echo reply (icmp.go:96-100), ICMPv6
  * ICMPv6Checksum — and into the IPv4 header checksum (addIPHeader,
- * ipv4.go:236).  NS_EINVAL if a field to write lies outside Header.
+ * ipv4.go:236).  An IPv4 fragment (MF set or a fragment offset) gets only
+ * its IP header checksum, as writePacketFragments writes it (ipv4.go:159-160).
+ * NS_EINVAL if a field to write lies outside Header (for IPv4, the whole IP
+ * header must lie in Header).
  * sums (2n, or NULL): [2i] the IPv4 header sum (0 for IPv6), [2i+1] the
  * transport chain's un-complemented sum (0 when there is none).
  * All sums of the batch are one device pass.                                */

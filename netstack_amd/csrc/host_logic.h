@@ -266,6 +266,7 @@ struct IpInfo {
   uint64_t hlen = 0, tbeg = 0, tend = 0, addr = 0, addr_len = 0;
   uint8_t proto = 0;
   bool fragment = false;
+  uint16_t frag_off = 0;  // IPv4 FragmentOffset() in bytes (header/ipv4.go:167-169)
 };
 
 inline bool parse_ip(const PacketBytes& pb, bool rx, IpInfo* ip) {
@@ -290,7 +291,8 @@ inline bool parse_ip(const PacketBytes& pb, bool rx, IpInfo* ip) {
     ip->proto = h[9];
     ip->addr = 12;
     ip->addr_len = 8;
-    ip->fragment = (h[6] & 0x20) || (((h[6] & 0x1F) << 8) | h[7]);  // MF or a fragment offset
+    ip->frag_off = (uint16_t)((((h[6] & 0x1F) << 8) | h[7]) << 3);
+    ip->fragment = (h[6] & 0x20) || ip->frag_off;  // MF or a fragment offset (ipv4.go:355-356)
   } else if (ver == 6) {
     if ((rx && first < 40) || !pb.read(0, h, 40)) return false;
     ip->hlen = 40;
@@ -332,6 +334,10 @@ int plan_packet(Builder& g, const PacketBytes& pb, uint32_t op, PacketPlan* pp) 
     return (int)g.result_at.size() - 1;
   };
   if (ip.v4) {
+    // TX: the IPv4 checksum field is written into Header, so the whole IP
+    // header must lie there (addIPHeader prepends it, ipv4.go:217-238); a
+    // header reaching into Data (borrowed, read-only bytes) is NS_EINVAL.
+    if (!rx && ip.hlen > pb.hdr_len) return NS_EINVAL;
     // TX: addIPHeader's ip.SetChecksum(^ip.CalculateChecksum()) (ipv4.go:236),
     // CalculateChecksum = Checksum(b[:HeaderLength()], 0) (ipv4.go:251-253).
     // RX: not verified on receive in the reference; reported for the caller.
@@ -353,7 +359,16 @@ int plan_packet(Builder& g, const PacketBytes& pb, uint32_t op, PacketPlan* pp) 
     return combine((uint16_t)len, proto);
   };
   if (rx) {
-    if (ip.fragment) return NS_OK;  // reassembled before the transport layer sees it
+    if (ip.fragment) {
+      // ipv4.go:357-373: a fragment with no payload, or whose uint16
+      // `last = FragmentOffset() + size - 1` wraps below its offset, is
+      // dropped as malformed.  Any other fragment is reassembled before the
+      // transport layer sees it (:375-385): UNCHECKED, its checksum is
+      // verified after reassembly (receive contract).
+      const uint16_t last = (uint16_t)(ip.frag_off + (uint16_t)tl - 1);
+      if (tl == 0 || last < ip.frag_off) pp->verdict = NS_PKB_MALFORMED;
+      return NS_OK;
+    }
     if (ip.proto == kProtoTCP) {
       // stack.DeliverTransportPacket: First() >= TCPMinimumSize; segment.parse
       // (segment.go:145-181): offset in [20, len(First())]
@@ -404,6 +419,11 @@ int plan_packet(Builder& g, const PacketBytes& pb, uint32_t op, PacketPlan* pp) 
     }
     return NS_OK;
   }
+  // TX of an IPv4 fragment: writePacketFragments (ipv4.go:119-212) writes only
+  // each fragment's IP header checksum (:159-160); the transport checksum was
+  // computed over the whole segment before it was cut, and a later fragment
+  // carries no transport header at all.
+  if (ip.fragment) return NS_OK;
   // TX: the transport header follows the IP header in Header; its checksum
   // field must lie in Header (it is written there).
   const uint64_t hdr_end = pb.hdr_len;

@@ -46,10 +46,13 @@ class PacketBuffer:
     LinkHeader: View | None = None
     NetworkHeader: View | None = None
     TransportHeader: View | None = None
+    # New with the receive contract (netstack_amd/rx.py):
+    # the link's verdict on the transport checksum, 0 = not verified.
+    RXChecksum: int = 0
 
     def Clone(self) -> "PacketBuffer":  # packet_buffer.go:55-58
         return PacketBuffer(self.Data.Clone(None), self.Header, self.LinkHeader, self.NetworkHeader,
-                            self.TransportHeader)
+                            self.TransportHeader, self.RXChecksum)
 
 
 def _marshal(pkts):

@@ -85,9 +85,17 @@ def verify(hdr: bytes, views, size: int):
             return MALFORMED, 0, 0
         net = c_checksum(first[:hlen], 0)  # IPv4.CalculateChecksum (ipv4.go:251-253), reported only
         src, dst, proto = first[12:16], first[16:20], first[9]
-        frag = (first[6] & 0x20) or (((first[6] & 0x1F) << 8) | first[7])
+        more = first[6] & 0x20
+        foff = ((((first[6] & 0x1F) << 8) | first[7]) << 3) & 0xFFFF  # FragmentOffset() (header/ipv4.go:167-169)
         data = _cap(_trim_front(data, hlen), tlen - hlen)
-        if frag:
+        if more or foff:
+            # ipv4.go:355-373: a fragment without payload, or one whose
+            # uint16 `last = offset + size - 1` wraps below its offset, is
+            # dropped as malformed; any other goes to reassembly (:375-385),
+            # and its transport checksum is checked only after that.
+            size = _size(data)
+            if size == 0 or ((foff + (size & 0xFFFF) - 1) & 0xFFFF) < foff:
+                return MALFORMED, net, 0
             return UNCHECKED, net, 0
     elif ver == 6:
         # IPv6 HandlePacket (network/ipv6/ipv6.go:168-177) + IsValid (header/ipv6.go:207-222)
@@ -154,7 +162,12 @@ def fill(hdr: bytes, views, size: int):
     t0, tl = hlen, total - hlen
     rest = [bytes(h[t0:])] + data  # everything after the IP header, as views
     tr = 0
-    if proto == 6:
+    # an IPv4 fragment (MF or an offset) gets only its IP header checksum, as
+    # writePacketFragments writes it (network/ipv4/ipv4.go:159-160)
+    frag = ver == 4 and ((h[6] & 0x20) or (((h[6] & 0x1F) << 8) | h[7]))
+    if frag:
+        pass
+    elif proto == 6:
         # buildTCPHdr (transport/tcp/connect.go:653-663)
         thl = (h[t0 + 12] >> 4) * 4
         xsum = c_pseudo_header(6, src, dst, tl & 0xFFFF)

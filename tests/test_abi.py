@@ -214,3 +214,91 @@ def test_go_shim_names_do_not_collide_with_the_reference_package():
         mine |= set(re.findall(r"^\s*(\w+)\s*=", blk, flags=re.M))
     mine |= set(re.findall(r"^const (\w+)", code, flags=re.M))
     assert mine and not (mine & ref), mine & ref
+
+
+GO_CALLERS = {  # file -> (package, build tag)
+    "go/transport/tcp/csum_batch_hip.go": ("tcp", "hipcsum"),
+    "go/transport/tcp/csum_batch_go.go": ("tcp", "!hipcsum"),
+    "go/link/fdbased/csum_rx_hip.go": ("fdbased", "linux,hipcsum"),
+    "go/link/fdbased/csum_rx_go.go": ("fdbased", "linux,!hipcsum"),
+}
+GO_PATCH = os.path.join(ROOT, "go", "netstack-hipcsum.patch")
+
+
+def _top_level(code):
+    names = set(re.findall(r"^func (\w+)\(", code, flags=re.M)) | set(re.findall(r"^type (\w+)\b", code, flags=re.M))
+    names |= set(re.findall(r"^(?:var|const)\s+(\w+)", code, flags=re.M))
+    for blk in re.findall(r"^(?:const|var) \((.*?)^\)", code, flags=re.M | re.S):
+        names |= set(re.findall(r"^\s*(\w+)", blk, flags=re.M))
+    return names
+
+
+def _signatures(code):
+    return dict(re.findall(r"^func (\w+)(\(.*?\)[^{]*)\{", code, flags=re.M))
+
+
+def test_go_caller_files_pair_up_and_use_only_what_exists():
+    """The build-tagged caller files: Go <= 1.14 forms,
+    the tag before the package clause, each hipcsum file paired with a
+    default-build file declaring the same functions with the same
+    signatures; every header.X they call exists in the shim or the reference
+    package, and every tcpip.RXChecksum* they use is declared by the patch."""
+    shim = _top_level(_go_code(open(GO_SHIM).read()))
+    patch = open(GO_PATCH).read()
+    added = "\n".join(l[1:] for l in patch.splitlines() if l.startswith("+") and not l.startswith("+++"))
+    by_pkg = {}
+    for rel, (pkg, tag) in GO_CALLERS.items():
+        raw = open(os.path.join(ROOT, rel)).read()
+        code = _go_code(raw)
+        for pat in POST_GO114:
+            assert not re.search(pat, code), (rel, pat)
+        assert f"\n\n// +build {tag}\n\npackage {pkg}\n" in raw, rel
+        by_pkg.setdefault(pkg, []).append((tag, _signatures(code), code))
+        for name in set(re.findall(r"\bheader\.(\w+)", code)):
+            assert name in shim or name in REF_HEADER_NAMES or not os.path.isdir("/root/reference"), (rel, name)
+        for name in set(re.findall(r"\btcpip\.(RXChecksum\w*)", code)):
+            assert re.search(rf"\b{name}\b", added), (rel, name)
+    for pkg, files in by_pkg.items():
+        (t1, s1, c1), (t2, s2, c2) = files
+        assert t1.replace("!", "") == t2.replace("!", "") and t1 != t2
+        # what the patch calls in this package is declared by both variants, alike
+        for name in ("tcpBatchChecksums", "finishTCPBatchChecksums") if pkg == "tcp" else ("verifyRXChecksums",):
+            assert re.search(rf"\b{name}\b", added)
+            assert s1.get(name) == s2.get(name), (pkg, name)
+            assert re.search(rf"^(?:func|const) {name}\b", c1, flags=re.M) and \
+                re.search(rf"^(?:func|const) {name}\b", c2, flags=re.M), (pkg, name)
+
+
+def _ref_names(d):
+    out = set()
+    for fn in os.listdir(d):
+        if fn.endswith(".go") and not fn.endswith("_test.go"):
+            out |= _top_level(_go_code(open(os.path.join(d, fn)).read()))
+    return out
+
+
+REF_HEADER_NAMES = _ref_names("/root/reference/tcpip/header") if os.path.isdir("/root/reference/tcpip/header") \
+    else set()
+
+
+def test_go_patch_applies_to_the_reference_and_adds_no_colliding_names(tmp_path):
+    """go/netstack-hipcsum.patch applies cleanly to the reference's files
+    (patch --dry-run on a copy), and the caller files' top-level names are
+    new in their packages."""
+    if not os.path.isdir("/root/reference/tcpip"):
+        pytest.skip("reference tree absent")
+    import shutil
+
+    files = re.findall(r"^\+\+\+ b/(\S+)", open(GO_PATCH).read(), flags=re.M)
+    assert set(files) == {"tcpip/packet_buffer.go", "tcpip/transport/tcp/segment.go",
+                          "tcpip/transport/tcp/connect.go", "tcpip/network/ipv4/ipv4.go",
+                          "tcpip/link/fdbased/packet_dispatchers.go"}
+    for f in files:
+        os.makedirs(tmp_path / os.path.dirname(f), exist_ok=True)
+        shutil.copy(os.path.join("/root/reference", f), tmp_path / f)
+    r = subprocess.run(["patch", "-p1", "--dry-run", "-i", GO_PATCH], cwd=tmp_path, capture_output=True, text=True)
+    assert r.returncode == 0 and "FAILED" not in r.stdout and "fuzz" not in r.stdout, r.stdout + r.stderr
+    for rel, (pkg, _) in GO_CALLERS.items():
+        d = {"tcp": "tcpip/transport/tcp", "fdbased": "tcpip/link/fdbased"}[pkg]
+        mine = _top_level(_go_code(open(os.path.join(ROOT, rel)).read()))
+        assert mine and not (mine & _ref_names(os.path.join("/root/reference", d))), (rel, mine)

@@ -102,6 +102,33 @@ def _valid_packet(rng, kind, plen):
     return bytearray(hdr + payload)
 
 
+def _frag_packet(rng, how, plen):
+    """IPv4 fragments of every kind HandlePacket tells apart
+    (network/ipv4/ipv4.go:355-385; FragmentOffset() = field << 3 in a uint16):
+    0 MF with a TCP header and payload (reassembled: UNCHECKED); 1 the last
+    fragment (no MF, an offset; UNCHECKED); 2 MF and no payload (MALFORMED,
+    :357-363); 3 an offset with no payload (MALFORMED); 4 the highest offset
+    with `last = offset + size - 1` wrapping past 0xffff (MALFORMED,
+    :365-373); 5 the same offset with exactly 8 bytes, last = 0xffff (no wrap:
+    UNCHECKED)."""
+    if how in (0, 1):
+        p = _valid_packet(rng, "tcp4", plen)
+        struct.pack_into(">H", p, 6, 0x2000 if how == 0 else int(rng.integers(1, 0x2000)))
+        return p
+    src, dst = bytes(rng.integers(0, 256, 4, dtype=np.uint8)), bytes(rng.integers(0, 256, 4, dtype=np.uint8))
+    size = 0 if how in (2, 3) else int(rng.integers(9, 3000)) if how == 4 else 8
+    frag = {2: 0x2000 | int(rng.integers(0, 0x2000)), 3: int(rng.integers(1, 0x2000)),
+            4: 0x1FFF | (0x2000 if rng.random() < 0.5 else 0), 5: 0x1FFF}[how]
+    p = _ip4(6, src, dst, size, int(rng.integers(0, 65536)), frag=frag)
+    p += bytes(rng.integers(0, 256, size, dtype=np.uint8))
+    # the IPv4 header checksum as addIPHeader writes it (the reference does not check it on receive)
+    import oracle as O
+
+    struct.pack_into(">H", p, 10, 0)
+    struct.pack_into(">H", p, 10, (~O.c_checksum(bytes(p[:20]), 0)) & 0xFFFF)
+    return p
+
+
 def _rx_batch(rng, n):
     """A recvmmsg-like batch: mostly TCP (v4/v6) of 0..9000-B payloads,
     plus ICMPv4/v6, UDP, fragments, malformed packets; ~1/7 of the valid ones
@@ -115,8 +142,7 @@ def _rx_batch(rng, n):
             "icmp6" if r < 0.79 else "udp4" if r < 0.85 else "frag" if r < 0.88 else "bad"
         plen = int(rng.choice([0, 1, 7, int(rng.integers(0, 1460)), int(rng.integers(0, 9000))]))
         if kind == "frag":
-            p = _valid_packet(rng, "tcp4", plen)
-            struct.pack_into(">H", p, 6, 0x2000)  # MF
+            p = _frag_packet(rng, int(rng.integers(0, 6)), plen)
         elif kind == "bad":
             p = _valid_packet(rng, "tcp4", plen)
             how = int(rng.integers(0, 4))

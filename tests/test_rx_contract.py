@@ -1,0 +1,187 @@
+"""CPU: the receive path's packet-level semantics against the reference's own
+test fixtures (tests/golden/rx_fixtures.json): the oracle's per-packet
+verdicts (oracle/packets.py) and the receive-contract mirror
+(netstack_amd/rx.py) on IsValid, HandlePacket's fragment checks, reassembly
+and the transmit-side fragmenter.  The checksum sums themselves are GPU work
+(tests/test_gpu_rx_contract.py); nothing here calls the engine."""
+import struct
+
+import pytest
+
+import rxcases as R
+
+
+@pytest.fixture(scope="module")
+def fx(oracle_mod):
+    return R.fixtures()
+
+
+def _pk(b: bytes):
+    from netstack_amd.buffer import NewVectorisedView, View
+    from netstack_amd.packet import PacketBuffer
+
+    return PacketBuffer(Data=NewVectorisedView(len(b), [View(bytearray(b))]))
+
+
+def test_invalid_fragments_counts_match_the_reference(fx):
+    """TestInvalidFragments (ipv4_test.go:360-481): every case's packets,
+    injected in order, give the reference's MalformedPacketsReceived and
+    MalformedFragmentsReceived counts through the mirror's network layer."""
+    from netstack_amd.rx import ReceivePath
+
+    for case in fx["invalid_fragments"]:
+        rp = ReceivePath(engine=object())  # the network layer never calls the engine
+        for p in case["packets"]:
+            assert rp.network(_pk(bytes.fromhex(p))) is None
+        assert rp.stats.IPMalformedPacketsReceived == case["malformed_ip"], case["name"]
+        assert rp.stats.IPMalformedFragmentsReceived == case["malformed_fragments"], case["name"]
+
+
+def test_invalid_fragments_per_packet_verdicts(fx):
+    """The per-packet checks (what one device pass can decide) agree with the
+    mirror: a packet is MALFORMED in oracle/packets.py iff, arriving alone,
+    HandlePacket drops it as malformed; a valid fragment is UNCHECKED."""
+    import packets as P
+
+    from netstack_amd.rx import ReceivePath
+
+    seen = set()
+    for case in fx["invalid_fragments"]:
+        for p in case["packets"]:
+            b = bytes.fromhex(p)
+            rp = ReceivePath(engine=object())
+            rp.network(_pk(b))
+            v, _, _ = P.verify(b"", [b], len(b))
+            assert (v == P.MALFORMED) == (rp.stats.IPMalformedPacketsReceived == 1), (case["name"], p)
+            if v != P.MALFORMED:
+                assert v == P.UNCHECKED, case["name"]  # fragments and a truncated-TCP-less packet
+            seen.add(v)
+    assert seen == {P.MALFORMED, P.UNCHECKED}
+
+
+def test_fragment_edge_verdicts():
+    """ipv4.go:355-373 on the edges: no payload with MF or an offset is
+    malformed; at the highest offset (65528) 8 bytes end at 0xffff (kept),
+    9 bytes wrap (malformed); a last fragment (offset, no MF) is kept."""
+    import packets as P
+
+    def frag(field, size, mf=False):
+        h = bytearray(20)
+        struct.pack_into(">BBHHHBBH4s4s", h, 0, 0x45, 0, 20 + size, 7, (0x2000 if mf else 0) | field, 64, 6, 0,
+                         b"\x0a\0\0\1", b"\x0a\0\0\2")
+        return bytes(h) + bytes(range(size))
+
+    cases = [(frag(0, 0, True), P.MALFORMED), (frag(5, 0), P.MALFORMED), (frag(0x1FFF, 8), P.UNCHECKED),
+             (frag(0x1FFF, 9), P.MALFORMED), (frag(0x1FFF, 9, True), P.MALFORMED), (frag(3, 100), P.UNCHECKED),
+             (frag(0, 100, True), P.UNCHECKED), (frag(0x1FFE, 16), P.UNCHECKED), (frag(0x1FFE, 17), P.MALFORMED)]
+    for b, want in cases:
+        assert P.verify(b"", [b], len(b))[0] == want, b[:8].hex()
+
+
+def test_reassembler_holes_and_process(fx):
+    """TestUpdateHoles (reassembler_test.go:28-111) and
+    TestFragmentationProcess (fragmentation_test.go:50-98) on the mirror's
+    reassembler."""
+    from netstack_amd.buffer import NewVectorisedView, View
+    from netstack_amd.rx import _Reassembler
+
+    for c in fx["holes"]:
+        r = _Reassembler()
+        for first, last, more in c["in"]:
+            r.process(first, last, more, NewVectorisedView(0, []))
+        assert [list(h) for h in r.holes] == c["want"]
+    for c in fx["process"]:
+        rs = {}
+        for (ident, first, last, more, pieces), (done, want) in zip(c["in"], c["out"]):
+            views = [View(bytearray(p.encode())) for p in pieces]
+            r = rs.setdefault(ident, _Reassembler())
+            vv, ok = r.process(first, last, more, NewVectorisedView(sum(map(len, views)), views))
+            assert ok
+            assert (vv is not None) == done
+            if done:
+                del rs[ident]
+                assert [bytes(v).decode() for v in vv.Views()] == want and vv.Size() == sum(map(len, want))
+
+
+def test_fragmentation_table_shapes(fx):
+    """TestFragmentation's table (ipv4_test.go:257-320): the restated
+    writePacketFragments gives the reference's fragment counts, every
+    fragment a valid IPv4 header summing to 0xffff within the MTU, and the
+    fragments reassemble (through the mirror) to the source payload."""
+    import random
+
+    import oracle as O
+
+    from netstack_amd.buffer import NewVectorisedView, View
+    from netstack_amd.packet import PacketBuffer
+    from netstack_amd.rx import ReceivePath
+
+    rnd = random.Random(257)
+    for row in fx["fragmentation"]:
+        sizes = R.view_sizes(row["views"])
+        rest = bytes(rnd.getrandbits(8) for _ in range(row["hdr_length"]))
+        views = [bytes(rnd.getrandbits(8) for _ in range(s)) for s in sizes]
+        total = 20 + len(rest) + sum(sizes)
+        ip = bytearray(20)
+        struct.pack_into(">BBHHHBBH4s4s", ip, 0, 0x45, 0, total, 1, 0, 42, 6, 0, b"\x10\0\0\1", b"\x10\0\0\2")
+        frags = R.write_packet_fragments(bytes(ip) + rest, views, row["mtu"])
+        assert len(frags) == row["expected_frags"], row["name"]
+        rp = ReceivePath(engine=object())
+        got = None
+        for h, d in frags:
+            wire = h + b"".join(d)
+            assert len(wire) <= row["mtu"] and O.c_checksum(h[:20], 0) == 0xFFFF, row["name"]
+            pk = PacketBuffer(Data=NewVectorisedView(len(wire), [View(bytearray(wire))]))
+            r = rp._ipv4(pk)
+            if r is not None:
+                got = b"".join(bytes(v) for v in r[3].Data.Views())[:r[3].Data.Size()]
+        assert got == rest + b"".join(views), row["name"]
+        assert rp.stats.IPMalformedPacketsReceived == 0
+
+
+def test_fill_writes_only_the_ip_checksum_of_a_fragment():
+    """A fragment on transmit gets its IPv4 header checksum only
+    (writePacketFragments, ipv4.go:159-160): oracle.fill leaves the
+    transport bytes as they are."""
+    import packets as P
+
+    seg = R.build_segment(b"\x0a\0\0\2", b"\x0a\0\0\1", 4096, 1235, 790, 1, 0x10, 30000, bytes(range(256)) * 8)
+    frags = R.write_packet_fragments(bytes(seg[:20]), [bytes(seg[20:])], 800, set_checksums=False)
+    for h, d in frags:
+        out, net, tr = P.fill(h, d, sum(map(len, d)))
+        assert tr == 0 and out[:10] == h[:10] and out[12:] == h[12:]
+        assert (~net) & 0xFFFF == struct.unpack_from(">H", out, 10)[0]
+
+
+def test_transport_step_trusts_the_link_verdict():
+    """Contract step 3 without the engine: VALID and INVALID verdicts decide
+    csumValid with no sum taken, and INVALID is counted where tcp
+    HandlePacket counts it (endpoint.go:2108-2114), at every level."""
+    from netstack_amd.rx import RX_CHECKSUM_INVALID, RX_CHECKSUM_VALID, ReceivePath
+
+    seg = R.build_segment(b"\x0a\0\0\2", b"\x0a\0\0\1", 4096, 1235, 790, 1, 0x10, 30000, b"\x01\x02\x03")
+    good, bad = _pk(bytes(seg)), _pk(bytes(seg))
+    good.RXChecksum, bad.RXChecksum = RX_CHECKSUM_VALID, RX_CHECKSUM_INVALID
+    rp = ReceivePath(engine=object())
+    segs = [rp.network(good), rp.network(bad)]
+    out = rp.transport(segs)
+    assert [o[2] for o in out] == [bytes(seg[20:])]
+    s = rp.stats
+    assert (s.TCPChecksumErrors, s.EndpointChecksumErrors, s.TCPValidSegmentsReceived) == (1, 1, 1)
+
+
+def test_reassembly_clears_a_fragment_verdict():
+    """Contract step 2: a reassembled packet never carries a fragment's
+    verdict (were a link to mark a fragment VALID, the reassembled segment
+    would still be verified)."""
+    from netstack_amd.rx import RX_CHECKSUM_UNKNOWN, RX_CHECKSUM_VALID, ReceivePath
+
+    seg = R.build_segment(b"\x0a\0\0\2", b"\x0a\0\0\1", 4096, 1235, 790, 1, 0x10, 30000, bytes(2000))
+    frags = R.write_packet_fragments(bytes(seg[:20]), [bytes(seg[20:])], 600)
+    rp = ReceivePath(engine=object())
+    last = None
+    for h, d in frags:
+        pk = _pk(h + b"".join(d))
+        pk.RXChecksum = RX_CHECKSUM_VALID
+        last = rp.network(pk)
+    assert last is not None and last[2].RXChecksum == RX_CHECKSUM_UNKNOWN
