@@ -382,7 +382,17 @@ int run_zero_copy(ns_csum_ctx* ctx, SmallReq* const* reqs, size_t nreq) {
   for (uint32_t spin = 0; __atomic_load_n(done, __ATOMIC_ACQUIRE) != seq; ++spin) {
     if ((spin & 255u) == 255u && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) {
       HIP_TRY(hipStreamSynchronize(s));
-      if (__atomic_load_n(done, __ATOMIC_ACQUIRE) != seq) return NS_EHIP;
+      if (__atomic_load_n(done, __ATOMIC_ACQUIRE) != seq) {
+        // The pass ended without its last workgroup's word: its counter may
+        // be left nonzero, which would keep every later pass from
+        // signalling.  Reset it before the next pass can run.
+        if (self) {
+          HIP_TRY(hipMemsetAsync(ctx->z_ctr.p, 0, sizeof(uint32_t), s));
+          HIP_TRY(hipStreamSynchronize(s));
+        }
+        if (std::getenv("NS_CSUM_DEBUG")) std::fprintf(stderr, "netstack_csum: pass %u signalled no completion\n", seq);
+        return NS_EHIP;
+      }
       break;
     }
   }

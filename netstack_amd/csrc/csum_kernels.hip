@@ -775,18 +775,39 @@ __device__ __forceinline__ void finish_tile(HybLds<P>& L, uint32_t s, const Pkt&
 }
 
 // Completion word of a self-signalling launch (an unchained zero-copy pass,
-// csum_api.cpp run_zero_copy): every workgroup waits until its own result
-// stores — written through to coherent host memory (finish_tile `wt`) — are
-// complete, then counts itself done; the last one resets the counter for the
-// next launch and stores `seq` into the host's completion word, which the
-// caller spins on.  Saves the separate signal kernel's launch and dispatch.
+// csum_api.cpp run_zero_copy).  The caller, a CPU thread, spins on `flag` in
+// coherent host memory and then reads the results; what makes a host reader
+// that sees `seq` also see every result is the memory model's release/acquire
+// chain (HSA / LLVM AMDGPU scoped model), not the hardware's store order:
+//   1. every wave waits for its own result stores (vmcnt 0; MI355X_MICROARCH
+//      "Valid forms": every storing wave, then the workgroup barrier);
+//   2. lane 0: a SYSTEM-scope release fence (the host is a system-scope
+//      observer), then the count on the device counter — release fence +
+//      relaxed RMW = a release of everything this workgroup stored;
+//   3. the workgroup whose add returns gridDim.x - 1 read the value written by
+//      the RMW chain every other workgroup's release heads, so an acquire
+//      fence (agent scope: all workgroups share the agent) makes their results
+//      happen-before what it does next;
+//   4. it resets the counter for the next pass, then a SYSTEM-scope release
+//      fence and the store of `seq`: the host's acquire load of `flag`
+//      (csum_api.cpp) synchronizes with it, so by transitivity it sees every
+//      workgroup's results.
+// Each fence is followed by an explicit `s_waitcnt vmcnt(0)`: ROCm 7.2 can
+// drop a release fence's own wait when the wave's counter is provably empty
+// (here: after a returned atomic), letting the next store overtake the L2
+// write-back (MI355X_MICROARCH.md "Compiler hazard").
 __device__ __forceinline__ void zc_complete(uint32_t* __restrict__ ctr, uint32_t* __restrict__ flag, uint32_t seq) {
-  __builtin_amdgcn_s_waitcnt(0);  // this wave's stores are acknowledged
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // 1
   __syncthreads();
   if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // 2: system scope
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const uint32_t prev = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (prev == gridDim.x - 1u) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // 3
       __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // 4: system scope
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __hip_atomic_store(flag, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }

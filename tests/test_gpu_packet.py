@@ -286,6 +286,16 @@ def test_fill_rejects_a_field_outside_header(engine):
     with pytest.raises(ValueError):
         fill_packet_buffers([pk], engine)
     assert bytes(pk.Header.View()) == before
+    # the IPv4 header itself (its checksum field) reaching into Data: Header
+    # holds only its first 10 bytes, or nothing at all
+    for cut in (10, 0):
+        wire = bytes(ip) + bytes(tcp) + bytes(10)
+        data = bytearray(wire[cut:])
+        pk = PacketBuffer(Data=NewVectorisedView(len(data), [View(data)]),
+                          Header=NewPrependableFromView(View(bytearray(wire[:cut]))))
+        with pytest.raises(ValueError):
+            fill_packet_buffers([pk], engine)
+        assert bytes(data) == wire[cut:]
 
 
 @pytest.mark.parametrize("big", [False, True])
