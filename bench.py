@@ -311,6 +311,37 @@ def kernel_name(arena_bytes: int, n: int, chained: bool = False) -> str:
     return f"nsk::csum_hyb<64,64,16,8,4,2,5,{win},1,{ch}>"
 
 
+def usable_cpus() -> dict:
+    """The CPUs this process may run on: its affinity set (what `nproc`
+    reports without OMP_NUM_THREADS), capped by the cgroup's CPU quota where
+    one is set (a GPU box gives each GPU's jobs a share of a larger
+    machine: there the affinity set is the whole machine)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()
+        if q != "max":
+            quota = -(-int(q) // int(period))
+    except (OSError, ValueError):
+        pass
+    return {"affinity": aff, "cgroup_quota_cpus": quota, "usable": min(aff, quota) if quota else aff}
+
+
+def device_ordinal(backend: str, local_rank: int, ndev: int, local_world: int) -> int:
+    """This rank's GPU: one per rank.  With nccl (RCCL) a node must have a GPU
+    for every local rank — RCCL rejects two ranks on one device, and mapping
+    ranks modulo the count would hide a launch with too many ranks — so that
+    is refused with a message.  With gloo (the control plane only) ranks
+    beyond the GPU count share them, which the one-GPU box's multi-rank tests
+    use."""
+    if backend == "nccl" and (local_world > ndev or local_rank >= ndev):
+        raise SystemExit(f"bench.py: {max(local_world, local_rank + 1)} ranks on this node but {ndev} GPU(s): "
+                         f"the nccl (RCCL) backend needs one GPU per rank; launch at most {ndev} ranks, "
+                         f"or pass --dist-backend gloo to share GPUs")
+    return local_rank % max(1, ndev)
+
+
 def main():
     args = parse()
     import torch
@@ -318,9 +349,9 @@ def main():
     from netstack_amd import Engine
 
     backend = args.dist_backend if args.dist_backend != "auto" else ("nccl" if torch.cuda.is_available() else "gloo")
-    # one rank per GPU, made current before the process group exists; more
-    # ranks than GPUs share them (gloo control plane)
-    ordinal = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
+    # one rank per GPU, made current before the process group exists
+    ordinal = device_ordinal(backend, int(os.environ.get("LOCAL_RANK", "0")),
+                             torch.cuda.device_count(), int(os.environ.get("LOCAL_WORLD_SIZE", "1")))
     torch.cuda.set_device(ordinal)
     dist = Dist(backend, ordinal)
     if dist.on and args.gpus != dist.world:
@@ -465,8 +496,10 @@ def main():
         # The CPU leg (rank 0): the oracle timed as the scalar baseline.
         cb, _ = cpu_baseline(batch, args.cpu_seconds, 1)
         result["cpu_baseline"] = cb
-        th = args.cpu_threads or min(16, os.cpu_count() or 1)
+        cpus = usable_cpus()
+        th = args.cpu_threads or cpus["usable"]
         cbm, _ = cpu_baseline(batch, max(2.0, args.cpu_seconds / 4), th)
+        cbm["host_cpus"] = cpus
         result["cpu_baseline_multicore"] = cbm
 
     if dist.rank == 0:

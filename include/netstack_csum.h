@@ -56,8 +56,9 @@
 extern "C" {
 #endif
 
-#define NS_CSUM_ABI_VERSION 3  /* 2: ns_csum_batch_dev_store, NS_DESC_STORE*;
-                                  3: ns_csum_stage_*, ns_csum_packet_buffers */
+#define NS_CSUM_ABI_VERSION 4  /* 2: ns_csum_batch_dev_store, NS_DESC_STORE*;
+                                  3: ns_csum_stage_*, ns_csum_packet_buffers;
+                                  4: ns_csum_stream_release, _scratch_count */
 
 /* ---- status codes ------------------------------------------------------- */
 #define NS_OK 0
@@ -155,7 +156,10 @@ int ns_csum_sync(ns_csum_ctx* ctx, void* stream, uint64_t* bad);
  * NS_BATCH_CHAINED, or when descriptors average >= 1 MiB (arena_bytes / n:
  * then each is spread over many workgroups), the call uses device scratch
  * that the context keeps per stream: calls on different streams of one
- * context run concurrently, calls on one stream are ordered by it.
+ * context run concurrently, calls on one stream are ordered by it.  (For
+ * hipStreamPerThread the scratch is per calling thread as well.)  Growing it
+ * is stream-ordered and never waits for the device; at most 64 streams keep
+ * scratch, the least recently used giving it up when another needs it.
  * A 16-B-aligned arena of exactly n slots of 16, 32, 48 or 64 bytes (a ring
  * of fixed-size receive buffers, packet k in slot k) lets the kernel load
  * each packet beside its descriptor instead of after it; any other layout
@@ -173,6 +177,15 @@ int ns_csum_batch_dev_store(ns_csum_ctx* ctx, uint8_t* d_arena,
                             uint64_t arena_bytes, const ns_pkt_desc* d_desc,
                             uint32_t n, uint16_t* d_out, uint32_t batch_flags,
                             void* stream);
+
+/* Frees the scratch the context keeps for `stream` (see ns_csum_batch_dev),
+ * after the stream's last launch that used it; nothing waits.  Call it
+ * before destroying a stream that ran chained or huge-descriptor batches
+ * (otherwise the scratch is reclaimed only when 64 other streams need some).
+ * NS_EINVAL if another thread is launching on that stream right now; NS_OK
+ * if the stream has no scratch.  ns_csum_scratch_count: streams holding some. */
+int ns_csum_stream_release(ns_csum_ctx* ctx, void* stream);
+int ns_csum_scratch_count(ns_csum_ctx* ctx, uint32_t* count);
 
 /* Host-memory batch: H2D of arena and table, kernels, D2H of results,
  * pipelined over two streams in chunks; synchronous.  Pageable host memory is

@@ -17,7 +17,7 @@ CSRC = os.path.join(_HERE, "csrc")
 
 # The NS_CSUM_ABI_VERSION this binding is written against; lib() refuses a
 # library that reports another (a stale build).
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 NS_OK = 0
 NS_EINVAL = -1
@@ -41,6 +41,7 @@ EXPORTED = (
     "ns_csum_vv_batch", "ns_csum_views_restart", "ns_csum_pseudo_header",
     "ns_csum_combine", "ns_csum_shard_plan", "ns_csum_batch_multi", "ns_csum_chains",
     "ns_csum_stage_acquire", "ns_csum_stage_release", "ns_csum_packet_buffers",
+    "ns_csum_stream_release", "ns_csum_scratch_count",
 )
 NS_PIECE_RESTART = 0x1
 NS_PIECE_END = 0x2
@@ -137,6 +138,8 @@ def _declare(lib):
         "ns_csum_stage_release": (c.c_int, [vp, vp]),
         "ns_csum_packet_buffers": (c.c_int, [vp, c.POINTER(NsPktBuf), c.c_uint32, c.c_uint32, u16p,
                                              c.POINTER(c.c_uint8)]),
+        "ns_csum_stream_release": (c.c_int, [vp, vp]),
+        "ns_csum_scratch_count": (c.c_int, [vp, c.POINTER(c.c_uint32)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

@@ -87,6 +87,26 @@ struct DevBuf {
     p = nullptr;
     cap = 0;
   }
+  // Stream-ordered growth for per-stream scratch: the old buffer is freed
+  // after the work already queued on `s` (hipFreeAsync), the new one is
+  // allocated and cleared in stream order.  Unlike hipFree, nothing waits for
+  // the device, so a growing batch on one stream never stalls another.
+  int ensure_async(size_t n, bool zero, hipStream_t s) {
+    if (n <= cap) return NS_OK;
+    if (p) (void)hipFreeAsync(p, s);
+    p = nullptr;
+    cap = 0;
+    size_t want = std::max<size_t>(n, 1);
+    HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&p), want * sizeof(T), s));
+    if (zero) HIP_TRY(hipMemsetAsync(p, 0, want * sizeof(T), s));
+    cap = want;
+    return NS_OK;
+  }
+  void release_async(hipStream_t s) {
+    if (p) (void)hipFreeAsync(p, s);
+    p = nullptr;
+    cap = 0;
+  }
 };
 
 template <typename T, unsigned FLAGS = hipHostMallocDefault>
@@ -182,21 +202,36 @@ struct ChainBuf {
     if (rc == NS_OK) rc = status.ensure((size_t)nsk::chain_blocks(n), true);
     return rc;
   }
+  int ensure_async(uint64_t n, hipStream_t s) {
+    int rc = part.ensure_async((size_t)nsk::chain_scratch_words(n), false, s);
+    if (rc == NS_OK) rc = status.ensure_async((size_t)nsk::chain_blocks(n), true, s);
+    return rc;
+  }
   nsk::ChainScratch get() const { return nsk::ChainScratch{part.p, status.p}; }
   void release() {
     part.release();
     status.release();
+  }
+  void release_async(hipStream_t s) {
+    part.release_async(s);
+    status.release_async(s);
   }
 };
 
 // Scratch of the device-resident API for one caller stream: chained batches
 // and huge-descriptor splits on different streams of one context run
 // concurrently, each on its own scratch (the same stream orders its own).
-struct StreamScratch {
-  hipStream_t stream = nullptr;
+// The bookkeeping (keys, pins, LRU bound, release) is nsh::ScratchRegistry.
+// `last` marks the stream's last launch that used the scratch, so the
+// buffers can be freed after it even once the stream itself is gone
+// (retire_scratch).
+struct StreamScratch : nsh::ScratchSlot {
   ChainBuf chain;
   DevBuf<uint32_t> split;  // csum_split accumulators (zero between launches)
+  hipEvent_t last = nullptr;
+  std::mutex mu;  // held while growing it and launching with it
 };
+constexpr size_t kMaxStreamScratch = 64;
 
 // One small synchronous call's batch: `ndesc` descriptors over bytes
 // [lo, lo + nbytes) of the caller's arena, staged in mapped memory whose
@@ -234,8 +269,11 @@ struct ns_csum_ctx {
   unsigned long long* d_err = nullptr;
   std::mutex mu;  // guards everything below
 
-  // device-resident API scratch, one per caller stream (allocated on first use)
-  std::vector<StreamScratch*> scratch;
+  // device-resident API scratch, one per caller stream (allocated on first
+  // use), under its own lock: growing one never holds up synchronous calls
+  nsh::ScratchRegistry<StreamScratch> scratch{kMaxStreamScratch};
+  std::mutex rmu;                // guards retire
+  hipStream_t retire = nullptr;  // frees retired scratch after its last use
   // ns_csum_sync's exchanged error count (mapped: written by take_err)
   MappedPin err_taken;
   // host-path slots (double-buffered)
@@ -271,6 +309,43 @@ struct ns_csum_ctx {
 };
 
 namespace {
+
+// Frees a scratch entry the registry dropped: its buffers are freed on the
+// context's retire stream after the last launch that used them (its event),
+// so neither the host nor the device waits, and the entry's own stream may
+// already be destroyed.
+void retire_scratch(ns_csum_ctx* ctx, StreamScratch* sc) {
+  std::lock_guard<std::mutex> lk(ctx->rmu);
+  if (!ctx->retire && hipStreamCreateWithFlags(&ctx->retire, hipStreamNonBlocking) != hipSuccess) ctx->retire = nullptr;
+  if (ctx->retire && hipStreamWaitEvent(ctx->retire, sc->last, 0) == hipSuccess) {
+    sc->chain.release_async(ctx->retire);
+    sc->split.release_async(ctx->retire);
+  } else {  // no retire stream: free once its last launch is done
+    (void)hipGetLastError();
+    (void)hipEventSynchronize(sc->last);
+    sc->chain.release();
+    sc->split.release();
+  }
+  (void)hipEventDestroy(sc->last);
+  delete sc;
+}
+
+StreamScratch* make_scratch() {
+  StreamScratch* sc = new (std::nothrow) StreamScratch();
+  if (sc && hipEventCreateWithFlags(&sc->last, hipEventDisableTiming) != hipSuccess) {
+    (void)hipGetLastError();
+    delete sc;
+    sc = nullptr;
+  }
+  return sc;
+}
+
+nsh::ScratchKey scratch_key(hipStream_t s) {
+  nsh::ScratchKey k;
+  k.stream = (const void*)s;
+  if (s == hipStreamPerThread) k.thread = std::this_thread::get_id();
+  return k;
+}
 
 struct DeviceGuard {
   int prev = -1;
@@ -863,12 +938,11 @@ void ns_csum_destroy(ns_csum_ctx* ctx) {
     DeviceGuard g(ctx->device);
     for (int s = 0; s < 2; ++s)
       if (ctx->stream[s]) (void)hipStreamSynchronize(ctx->stream[s]);
-    for (StreamScratch* sc : ctx->scratch) {
-      sc->chain.release();
-      sc->split.release();
-      delete sc;
+    ctx->scratch.clear([&](StreamScratch* sc) { retire_scratch(ctx, sc); });
+    if (ctx->retire) {
+      (void)hipStreamSynchronize(ctx->retire);
+      (void)hipStreamDestroy(ctx->retire);
     }
-    ctx->scratch.clear();
     ctx->err_taken.release();
     ctx->z_buf.release();
     ctx->z_res.release();
@@ -926,46 +1000,55 @@ int ns_csum_sync(ns_csum_ctx* ctx, void* stream, uint64_t* bad) {
 }
 
 namespace {
-// The scratch of `s` (caller holds ctx->mu).  Growing a buffer frees the old
-// one with hipFree, which waits for the device, so no launch still uses it.
-StreamScratch* stream_scratch(ns_csum_ctx* ctx, hipStream_t s) {
-  for (StreamScratch* sc : ctx->scratch)
-    if (sc->stream == s) return sc;
-  StreamScratch* sc = new (std::nothrow) StreamScratch();
-  if (!sc) return nullptr;
-  sc->stream = s;
-  ctx->scratch.push_back(sc);
-  return sc;
-}
-
 int batch_dev(ns_csum_ctx* ctx, const uint8_t* d_arena, uint64_t arena_bytes, const ns_pkt_desc* d_desc,
               uint32_t n, uint16_t* d_out, uint32_t batch_flags, void* stream, bool store) {
   if (!ctx || (n && (!d_desc || !d_out)) || (arena_bytes && !d_arena)) return NS_EINVAL;
   if (n == 0) return NS_OK;
   DeviceGuard g(ctx->device);
   hipStream_t s = (hipStream_t)stream;  // NULL = the HIP null stream
-  nsk::ChainScratch chain{};
-  uint32_t* split = nullptr;
-  if ((batch_flags & NS_BATCH_CHAINED) || arena_bytes / n >= nsk::split_min_avg()) {
-    std::lock_guard<std::mutex> lk(ctx->mu);
-    StreamScratch* sc = stream_scratch(ctx, s);
-    if (!sc) return NS_ENOMEM;
-    if (batch_flags & NS_BATCH_CHAINED) {
-      int rc = sc->chain.ensure(n);
-      if (rc != NS_OK) return rc;
-      chain = sc->chain.get();
-    }
-    if (arena_bytes / n >= nsk::split_min_avg()) {
-      int rc = sc->split.ensure(nsk::split_words(n), true);  // zero once; the kernel keeps it so
-      if (rc != NS_OK) return rc;
+  const bool need_chain = (batch_flags & NS_BATCH_CHAINED) != 0;
+  const bool need_split = arena_bytes / n >= nsk::split_min_avg();
+  if (!need_chain && !need_split) {
+    HIP_TRY(nsk::launch_batch(d_arena, arena_bytes, d_desc, n, d_out, nsk::ChainScratch{}, ctx->d_err, s, 0,
+                              store ? 1u : 0u, nullptr));
+    return NS_OK;
+  }
+  StreamScratch* sc = ctx->scratch.pin(scratch_key(s), make_scratch,
+                                       [&](StreamScratch* old) { retire_scratch(ctx, old); });
+  if (!sc) return NS_ENOMEM;
+  int rc = NS_OK;
+  {
+    std::lock_guard<std::mutex> lk(sc->mu);
+    nsk::ChainScratch chain{};
+    uint32_t* split = nullptr;
+    if (need_chain && (rc = sc->chain.ensure_async(n, s)) == NS_OK) chain = sc->chain.get();
+    // split accumulators: zero once, the kernel leaves them so
+    if (rc == NS_OK && need_split && (rc = sc->split.ensure_async(nsk::split_words(n), true, s)) == NS_OK)
       split = sc->split.p;
+    if (rc == NS_OK) {
+      hipError_t e = nsk::launch_batch(d_arena, arena_bytes, d_desc, n, d_out, chain, ctx->d_err, s, 0,
+                                       store ? 1u : 0u, split);
+      if (e == hipSuccess) e = hipEventRecord(sc->last, s);
+      if (e != hipSuccess) rc = report_hip(e, "launch_batch", __FILE__, __LINE__);
     }
   }
-  HIP_TRY(nsk::launch_batch(d_arena, arena_bytes, d_desc, n, d_out, chain, ctx->d_err, s, 0, store ? 1u : 0u,
-                            split));
-  return NS_OK;
+  ctx->scratch.unpin(sc);
+  return rc;
 }
 }  // namespace
+
+int ns_csum_stream_release(ns_csum_ctx* ctx, void* stream) {
+  if (!ctx) return NS_EINVAL;
+  DeviceGuard g(ctx->device);
+  return ctx->scratch.release(scratch_key((hipStream_t)stream),
+                              [&](StreamScratch* sc) { retire_scratch(ctx, sc); });
+}
+
+int ns_csum_scratch_count(ns_csum_ctx* ctx, uint32_t* count) {
+  if (!ctx || !count) return NS_EINVAL;
+  *count = (uint32_t)ctx->scratch.size();
+  return NS_OK;
+}
 
 int ns_csum_batch_dev(ns_csum_ctx* ctx, const uint8_t* d_arena, uint64_t arena_bytes,
                       const ns_pkt_desc* d_desc, uint32_t n, uint16_t* d_out,

@@ -7,6 +7,7 @@
 //   - PacketBytes / plan_packet: tcpip.PacketBuffer checksum steps;
 //   - cut_chunk: the host pipeline's chunking of a descriptor table;
 //   - shard_plan: byte-balanced contiguous shards;
+//   - ScratchRegistry: per-stream scratch bookkeeping (LRU, pins, release);
 //   - FlatCombiner: flat combining of concurrent small synchronous calls.
 // Plumbing only: no checksum arithmetic happens here (pseudo-header length
 // and protocol words are folded with the reference's ChecksumCombine).
@@ -566,6 +567,97 @@ inline void shard_plan(const ns_pkt_desc* d, uint32_t n, uint32_t parts, uint32_
   }
   first[parts] = n;
 }
+
+// ---- per-stream scratch registry (ns_csum_batch_dev, ns_csum_stream_release)
+// The device-resident API keeps scratch per caller stream (csum_api.cpp
+// StreamScratch).  This is its bookkeeping, HIP-free so the sanitizer tests
+// cover it: entries keyed by (stream handle, thread — hipStreamPerThread
+// names a different stream in every thread), pinned while a call grows or
+// launches with one, at most `max` kept (a new key evicts the least recently
+// used unpinned entry), released on request.  `make()` builds an entry
+// (nullptr on failure); `retire(e)` frees one and is called with the
+// registry lock held, never for a pinned entry.
+struct ScratchKey {
+  const void* stream = nullptr;
+  std::thread::id thread{};
+  bool operator==(const ScratchKey& o) const { return stream == o.stream && thread == o.thread; }
+};
+struct ScratchSlot {
+  ScratchKey key;
+  int pins = 0;
+  uint64_t tick = 0;
+};
+
+template <class Entry>
+class ScratchRegistry {
+ public:
+  explicit ScratchRegistry(size_t max) : max_(max) {}
+
+  template <class Make, class Retire>
+  Entry* pin(const ScratchKey& k, Make&& make, Retire&& retire) {
+    std::lock_guard<std::mutex> lk(mu_);
+    Entry* e = nullptr;
+    for (Entry* x : v_)
+      if (x->key == k) e = x;
+    if (!e) {
+      if (v_.size() >= max_) {
+        size_t lru = SIZE_MAX;
+        for (size_t i = 0; i < v_.size(); ++i)
+          if (v_[i]->pins == 0 && (lru == SIZE_MAX || v_[i]->tick < v_[lru]->tick)) lru = i;
+        if (lru != SIZE_MAX) {
+          Entry* old = v_[lru];
+          v_.erase(v_.begin() + (long)lru);
+          retire(old);
+        }
+      }
+      e = make();
+      if (!e) return nullptr;
+      e->key = k;
+      v_.push_back(e);
+    }
+    e->pins++;
+    e->tick = ++tick_;
+    return e;
+  }
+
+  void unpin(Entry* e) {
+    std::lock_guard<std::mutex> lk(mu_);
+    e->pins--;
+  }
+
+  // NS_EINVAL if the key's entry is pinned (a call on it is running).
+  template <class Retire>
+  int release(const ScratchKey& k, Retire&& retire) {
+    std::lock_guard<std::mutex> lk(mu_);
+    for (size_t i = 0; i < v_.size(); ++i) {
+      if (!(v_[i]->key == k)) continue;
+      if (v_[i]->pins) return NS_EINVAL;
+      Entry* old = v_[i];
+      v_.erase(v_.begin() + (long)i);
+      retire(old);
+      break;
+    }
+    return NS_OK;
+  }
+
+  template <class Retire>
+  void clear(Retire&& retire) {
+    std::lock_guard<std::mutex> lk(mu_);
+    for (Entry* e : v_) retire(e);
+    v_.clear();
+  }
+
+  size_t size() {
+    std::lock_guard<std::mutex> lk(mu_);
+    return v_.size();
+  }
+
+ private:
+  const size_t max_;
+  std::mutex mu_;
+  std::vector<Entry*> v_;
+  uint64_t tick_ = 0;
+};
 
 // ---- flat combining of concurrent small synchronous calls ------------------
 // netstack calls the checksum from every endpoint's goroutine at once

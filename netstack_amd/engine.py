@@ -112,6 +112,19 @@ class Engine:
                        out.data_ptr(), chained, stream.cuda_stream, store)
         return out
 
+    def stream_release(self, stream) -> None:
+        """Free the scratch this context keeps for `stream` (a torch.cuda.Stream
+        or a raw hipStream_t) after its last launch (ns_csum_stream_release);
+        call before destroying a stream that ran chained batches."""
+        h = getattr(stream, "cuda_stream", stream)
+        check(lib().ns_csum_stream_release(self._h, h), "ns_csum_stream_release")
+
+    def scratch_count(self) -> int:
+        """Streams currently holding device-resident scratch on this context."""
+        c = ctypes.c_uint32(0)
+        check(lib().ns_csum_scratch_count(self._h, ctypes.byref(c)), "ns_csum_scratch_count")
+        return int(c.value)
+
     def sync(self, stream: int | None = None) -> int:
         """Wait for `stream`; return the number of out-of-range descriptors."""
         bad = ctypes.c_uint64(0)

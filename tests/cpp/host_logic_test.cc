@@ -29,7 +29,7 @@
 #include "csum_oracle.h"
 #include "host_logic.h"
 
-static int g_fail = 0, g_run = 0;
+static std::atomic<int> g_fail{0}, g_run{0};  // CHECK runs in worker threads too
 #define CHECK(cond, ...)                                         \
   do {                                                           \
     ++g_run;                                                     \
@@ -427,6 +427,71 @@ static void TestCombiner(int threads, int per_thread) {
               (unsigned long long)passes.load(), max_batch.load());
 }
 
+// ScratchRegistry (per-stream scratch of ns_csum_batch_dev): `threads`
+// threads each pin, use and unpin scratch for random streams out of
+// `streams` handles (half of them through a per-thread key, as
+// hipStreamPerThread is), releasing some; checks that an entry is never
+// retired while pinned, that one key maps to one live entry, that at most
+// `max` entries live, and that every entry made is retired exactly once.
+struct FakeScratch : nsh::ScratchSlot {
+  std::atomic<int> users{0};
+  bool retired = false;
+};
+
+static void TestScratchRegistry(int threads, int streams, int per_thread) {
+  const size_t kMax = 64;
+  nsh::ScratchRegistry<FakeScratch> reg(kMax);
+  std::atomic<uint64_t> made{0}, retired{0}, busy_release{0};
+  std::mutex gm;
+  std::vector<FakeScratch*> graveyard;  // retired entries, deleted at the end
+  auto make = [&]() {
+    made++;
+    return new FakeScratch();
+  };
+  auto retire = [&](FakeScratch* e) {
+    CHECK(e->pins == 0 && e->users.load() == 0, "retired while in use");
+    CHECK(!e->retired, "retired twice");
+    e->retired = true;
+    retired++;
+    std::lock_guard<std::mutex> lk(gm);
+    graveyard.push_back(e);
+  };
+  std::vector<std::thread> th;
+  for (int t = 0; t < threads; ++t) {
+    th.emplace_back([&, t]() {
+      Rng r((uint64_t)t * 7919 + 1);
+      for (int i = 0; i < per_thread; ++i) {
+        const uintptr_t h = 0x1000 + 16 * (uintptr_t)(r() % (uint64_t)streams);
+        nsh::ScratchKey k;
+        k.stream = reinterpret_cast<const void*>(h);
+        if (h & 16) k.thread = std::this_thread::get_id();  // a per-thread stream handle
+        if (r() % 8 == 0) {
+          if (reg.release(k, retire) == NS_EINVAL) busy_release++;
+          continue;
+        }
+        FakeScratch* e = reg.pin(k, make, retire);
+        CHECK(e != nullptr, "pin");
+        if (!e) continue;
+        CHECK(!e->retired && e->key == k, "pinned entry");
+        e->users++;
+        if (r() % 4 == 0) std::this_thread::yield();
+        CHECK(!e->retired, "retired during use");
+        e->users--;
+        reg.unpin(e);
+        CHECK(reg.size() <= kMax + (size_t)threads, "registry size");
+      }
+    });
+  }
+  for (auto& x : th) x.join();
+  CHECK(reg.size() <= kMax, "registry above its bound when idle");
+  reg.clear(retire);
+  CHECK(made.load() == retired.load(), "made %llu retired %llu", (unsigned long long)made.load(),
+        (unsigned long long)retired.load());
+  for (FakeScratch* e : graveyard) delete e;
+  std::printf("scratch registry: %d threads, %d streams, %llu entries made and retired, %llu busy releases\n",
+              threads, streams, (unsigned long long)made.load(), (unsigned long long)busy_release.load());
+}
+
 int main(int argc, char** argv) {
   const bool quick = argc > 1 && std::strcmp(argv[1], "--quick") == 0;
   Rng rng(20261016);
@@ -437,6 +502,7 @@ int main(int argc, char** argv) {
   TestCutChunk(rng, r);
   TestShardPlan(rng, r);
   TestCombiner(16, quick ? 200 : 2000);
-  std::printf("%d checks, %d failed\n", g_run, g_fail);
+  TestScratchRegistry(8, 1000, quick ? 2000 : 20000);
+  std::printf("%d checks, %d failed\n", g_run.load(), g_fail.load());
   return g_fail ? 1 : 0;
 }

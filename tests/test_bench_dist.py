@@ -121,3 +121,19 @@ def test_cfg5_strong_scaling_shards_reproduce_the_whole_batch():
     assert "true" in bench.kernel_name(12_583_000_000, 8 << 20)
     assert bench.kernel_name(1_577_058_304, 1 << 20) == "nsk::csum_hyb<256,32,8,16,4,2,0,false,2,false>"
     assert bench.kernel_name(67_108_864, 1 << 20) == "nsk::csum_hyb<64,64,16,8,4,2,5,false,1,false>"
+
+
+def test_nccl_refuses_more_ranks_than_gpus():
+    """Under nccl (RCCL) every local rank needs its own GPU: bench.py refuses
+    a launch with more ranks on the node than GPUs, with a message, instead
+    of mapping ranks modulo the device count.  gloo may share GPUs (the
+    one-GPU box's multi-rank tests)."""
+    import bench
+
+    assert [bench.device_ordinal("nccl", r, 8, 8) for r in range(8)] == list(range(8))
+    for local_rank, ndev, world in ((1, 1, 2), (0, 1, 2), (7, 4, 8), (2, 2, 1)):
+        with pytest.raises(SystemExit) as e:
+            bench.device_ordinal("nccl", local_rank, ndev, world)
+        assert "one GPU per rank" in str(e.value)
+    assert [bench.device_ordinal("gloo", r, 1, 8) for r in range(8)] == [0] * 8
+    assert bench.device_ordinal("gloo", 5, 2, 8) == 1

@@ -73,25 +73,29 @@ def _free_port():
 
 
 @pytest.mark.slow
-@pytest.mark.parametrize("config", [5, 2])
-def test_bench_world_size_2_with_the_hip_engine(config):
-    """bench.py under torch.distributed.run with two ranks, each running the
-    HIP engine on its own batch (cfg2: weak scaling) or shard (cfg5: strong
-    scaling) — both on this box's one GPU.  The JSON line reports both ranks,
-    the summed payload and every rank's parity sample bit-exact."""
+@pytest.mark.parametrize("config,world", [(5, 2), (2, 2), (5, 4), (5, 8), (2, 8)])
+def test_bench_multi_rank_with_the_hip_engine(config, world):
+    """bench.py under torch.distributed.run with 2, 4 and 8 ranks, each
+    running the HIP engine on its own batch (cfg2: weak scaling, 8 ranks =
+    BASELINE configs[4]'s 8M x 1500 B) or shard (cfg5: strong scaling, 8
+    shards of 1.6 GB) — all on this box's one GPU, with the gloo control
+    plane (RCCL refuses two ranks on one device; bench.py refuses that under
+    nccl, tests/test_bench_dist.py).  The JSON line reports every rank, the
+    summed payload and every rank's parity sample bit-exact.  The 8-GPU
+    scaling curve itself is the driver's (SCALE_rNN.json)."""
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", PYTHONUNBUFFERED="1")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
-           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--config", str(config), "--steps", "3",
+           os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--config", str(config), "--steps", "3",
            "--warmup", "1", "--no-cpu", "--dist-backend", "gloo"]
-    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, r.stdout  # rank 0 prints one line
     res = json.loads(lines[0])
-    assert res["n_gpus"] == 2 and res["value"] > 0
+    assert res["n_gpus"] == world and res["value"] > 0
     assert res["scaling"] == ("strong" if config == 5 else "weak")
-    assert res["config"]["global_packets"] == (8 << 20 if config == 5 else 2 << 20)
+    assert res["config"]["global_packets"] == (8 << 20 if config == 5 else world << 20)
     ps = res["parity_sample"]
-    assert ps["bit_exact"] and ps["ranks_checked"] == 2 and ps["ranks_failed"] == 0
+    assert ps["bit_exact"] and ps["ranks_checked"] == world and ps["ranks_failed"] == 0
     assert res["bad_descriptors"] == 0
