@@ -42,6 +42,26 @@
 
 namespace nsk {
 
+// Per-workgroup finish stamps, in the tuning library only (tune.hip defines
+// NSK_TIMELINE before including this file; tools/timeline.py): the low word
+// of s_memrealtime (100 MHz) when a workgroup's thread 0 ends, stored when a
+// buffer is set.  The product library compiles them out.  Nothing more: a
+// start stamp, or the counter's high word, or the XCD id, each made the
+// compiler hold uniform values in VGPRs (72 -> 86 VGPRs, 7 -> 5 waves per
+// SIMD), which would time a different kernel.
+#ifdef NSK_TIMELINE
+__device__ uint32_t* nsk_timeline = nullptr;
+#define NSK_TL_BEGIN
+#define NSK_TL_END                                                                                      \
+  {                                                                                                     \
+    uint32_t* nsk_p = *(uint32_t* volatile*)&nsk_timeline;                                              \
+    if (nsk_p != nullptr && threadIdx.x == 0) nsk_p[blockIdx.x] = (uint32_t)__builtin_amdgcn_s_memrealtime(); \
+  }
+#else
+#define NSK_TL_BEGIN
+#define NSK_TL_END
+#endif
+
 // ChecksumCombine(uint16(v), uint16(v>>16)) — checksum.go:45, :104-107.
 __device__ __forceinline__ uint32_t fold1(uint32_t v) {
   const uint32_t s = (v & 0xFFFFu) + (v >> 16);
@@ -829,6 +849,7 @@ __global__ __launch_bounds__(WG) void csum_hyb(
     uint32_t store, uint32_t* __restrict__ zc_ctr, uint32_t* __restrict__ zc_flag, uint32_t zc_seq,
     uint32_t spec) {
   static_assert((WG & (WG - 1)) == 0, "tile must be a power of two");
+  NSK_TL_BEGIN
   __shared__ HybLds<WG> L;
   const bool wt = zc_flag != nullptr;
   const int t = threadIdx.x;
@@ -920,6 +941,7 @@ __global__ __launch_bounds__(WG) void csum_hyb(
   };
   tile();
   if (wt) zc_complete(zc_ctr, zc_flag, zc_seq);
+  NSK_TL_END
 }
 
 // ---- descriptors far larger than a tile: csum_split -----------------------

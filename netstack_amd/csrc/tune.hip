@@ -3,6 +3,7 @@
 // calibration kernels, so tools/tune.py can A/B them in one process
 // (cdna_hip_programming.md §5.4 rule 24) and bench.py can report the roofline
 // against a same-run calibration.
+#define NSK_TIMELINE  // per-workgroup stamps in this library's kernels (tools/timeline.py)
 #include "csum_kernels.hip"
 
 namespace nsk {
@@ -846,6 +847,12 @@ static const Variant kVariants[] = {
 extern "C" {
 
 int nsk_tune_count(void) { return (int)(sizeof(nsk::kVariants) / sizeof(nsk::kVariants[0])); }
+
+// Device buffer of one uint4 per workgroup for the timeline stamps of the
+// csum_hyb variants launched next (nullptr: off).
+int nsk_tune_timeline(void* buf) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(nsk::nsk_timeline), &buf, sizeof(buf)) == hipSuccess ? 0 : -5;
+}
 
 const char* nsk_tune_name(int v) {
   return (v >= 0 && v < nsk_tune_count()) ? nsk::kVariants[v].name : "";
