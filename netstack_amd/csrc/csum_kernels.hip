@@ -387,41 +387,58 @@ __device__ __forceinline__ uint32_t direct_sum(const Srd& r, const PktInfo& p) {
 // lines per instruction and the loads are nontemporal (cdna: a line split
 // across instructions must stay cached).  Each packet's
 // geometry reaches its quad by __shfl, a lane masks only its own chunk's edge
-// bytes, a quad DPP sum gives the packet's W, and the W-only class values
-// (s_class) shuffle back to one per lane.  1M x 64 B: 14.7 vs 16.3 us for the
-// lane-per-packet path (tools/tune.py, profiles/r02/tune_cfg3_quad.log).
-__device__ __forceinline__ uint32_t quad_geo(const PktInfo& p) {  // nch (3 bits) | lo (4) | hiex (5) | phase (1)
-  return p.nch | ((p.ew & 15u) << 3) | (((p.ew >> 5) & 31u) << 7) | ((p.ew >> 31) << 12);
+// bytes, a quad DPP sum gives the packet's W, and the W totals shuffle back to
+// one per lane.  1M x 64 B: 14.7 vs 16.3 us for the lane-per-packet path
+// (tools/tune.py, profiles/r02/tune_cfg3_quad.log).
+//
+// This path is VALU-bound, not memory-bound, at 1M x 64 B: with 8 one-wave
+// tiles per SIMD each issuing ~420 VALU instructions, every wave was issuing
+// VALU for 14.8% of its life (SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES,
+// profiles/r03/sq_summary.json): 8 waves x 14.8% fills the SIMD; the floor
+// kernel issues 72 per wave.  So a chunk is masked only when it needs it —
+// the packet's first chunk with a partial start, its last with a partial
+// end, a chunk past its last (the "need" bits, computed once by the packet's
+// own lane) — in a branch the lanes of whole aligned chunks skip, and the
+// W-only class value (s_class) is taken once per packet by its own lane after
+// one shuffle back, not by all four lanes of its quad before four.
+__device__ __forceinline__ uint32_t quad_geo(const PktInfo& p) {
+  // nch (3 bits) | lo (4) | hiex (5) | phase (1) | need (4: bit c = chunk c is masked)
+  const uint32_t nc = p.nch, lo = p.ew & 15u, hx = (p.ew >> 5) & 31u;
+  uint32_t need = 0xFu & ~((1u << min(nc, 4u)) - 1u);  // past the last chunk
+  if (lo != 0u) need |= 1u;
+  if (nc != 0u && hx != 16u) need |= 1u << ((nc - 1u) & 3u);
+  return nc | (lo << 3) | (hx << 7) | ((p.ew >> 31) << 12) | (need << 13);
 }
 
 // The quad layout's sums: v[j] holds chunk l % 4 of packet 16 j + l / 4 and
 // g[j] that packet's geometry; a chunk past the packet's last is masked out
 // (it reads zeros in quad_sum, the next packet's bytes in a speculative load).
-__device__ __forceinline__ uint32_t quad_reduce(const uint4 (&v)[4], const uint32_t (&g)[4]) {
+// `phase` is the lane's own packet's byte phase (pkt_info's edge word).
+__device__ __forceinline__ uint32_t quad_reduce(const uint4 (&v)[4], const uint32_t (&g)[4], uint32_t phase) {
   const uint32_t l = threadIdx.x & 63u, c = l & 3u;
   uint32_t sv[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const uint32_t gj = g[j], nc = gj & 7u;
-    const int lo_b = c == 0 ? (int)((gj >> 3) & 15u) : 0;
-    const int hi_b = c + 1 == nc ? (int)((gj >> 7) & 31u) : (c < nc ? 16 : 0);
+    const uint32_t gj = g[j];
     uint4 w = v[j];
-    w.x &= bytes_below(hi_b) & ~bytes_below(lo_b);
-    w.y &= bytes_below(hi_b - 4) & ~bytes_below(lo_b - 4);
-    w.z &= bytes_below(hi_b - 8) & ~bytes_below(lo_b - 8);
-    w.w &= bytes_below(hi_b - 12) & ~bytes_below(lo_b - 12);
+    if ((gj >> (13u + c)) & 1u) {  // an edge chunk, or one past the packet
+      const uint32_t nc = gj & 7u;
+      const int lo_b = c == 0 ? (int)((gj >> 3) & 15u) : 0;
+      const int hi_b = c + 1 == nc ? (int)((gj >> 7) & 31u) : (c < nc ? 16 : 0);
+      w.x &= bytes_below(hi_b) & ~bytes_below(lo_b);
+      w.y &= bytes_below(hi_b - 4) & ~bytes_below(lo_b - 4);
+      w.z &= bytes_below(hi_b - 8) & ~bytes_below(lo_b - 8);
+      w.w &= bytes_below(hi_b - 12) & ~bytes_below(lo_b - 12);
+    }
     uint32_t T = 0, W = 0;
     acc_chunk<false>(w, T, W);
-    sv[j] = s_class(group_sum<4>(W), (gj >> 12) & 1u);
+    sv[j] = group_sum<4>(W);  // the packet's W, in all four lanes of its quad
   }
-  const int src = (int)(4u * (l & 15u));
-  uint32_t me = 0;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const uint32_t x = (uint32_t)__shfl((int)sv[j], src, 64);
-    me = (l >> 4) == (uint32_t)j ? x : me;
-  }
-  return me;
+  // lane 4k + c keeps packet 16 c + k's total; lane l reads its own packet
+  // (16 (l >> 4) + (l & 15)) from lane 4 (l & 15) + (l >> 4): one shuffle
+  const uint32_t mine = c == 0u ? sv[0] : c == 1u ? sv[1] : c == 2u ? sv[2] : sv[3];
+  const uint32_t W = (uint32_t)__shfl((int)mine, (int)(4u * (l & 15u) + (l >> 4)), 64);
+  return s_class(W, phase);
 }
 
 __device__ __forceinline__ uint32_t quad_sum(const Srd& r, const PktInfo& p) {
@@ -436,7 +453,7 @@ __device__ __forceinline__ uint32_t quad_sum(const Srd& r, const PktInfo& p) {
     const uint32_t f = (uint32_t)__shfl((int)p.first, src, 64);
     v[j] = bload<2>(r.rsrc, c < (g[j] & 7u) ? f + 16u * c : r.oob);
   }
-  return quad_reduce(v, g);
+  return quad_reduce(v, g, p.ew >> 31);
 }
 
 // Speculative quad loads (one-wave small-packet tiles; launch_batch sets
@@ -465,7 +482,7 @@ __device__ __forceinline__ uint32_t spec_sum(const PktInfo& p, const uint4 (&v)[
   uint32_t g[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) g[j] = (uint32_t)__shfl((int)geo, (int)(16 * j + (l >> 2)), 64);
-  return quad_reduce(v, g);
+  return quad_reduce(v, g, p.ew >> 31);
 }
 
 // One tile through the scan path (thread t holds packet p of global index i).

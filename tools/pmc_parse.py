@@ -45,7 +45,7 @@ def main():
         k = int(r["Dispatch_Id"])
         disp[k][r["Counter_Name"]] = disp[k].get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
         names[k] = r["Kernel_Name"]
-    ours = [k for k in sorted(disp) if ("calib_" in names[k] or "nsk::csum_" in names[k])]
+    ours = [k for k in sorted(disp) if ("calib_" in names[k] or "nsk::" in names[k])]
     out = {}
     for i, (lab, meta) in enumerate(labels):
         ks = ours[i * REPS:(i + 1) * REPS]
@@ -59,21 +59,22 @@ def main():
     for m in ("calib800", "calib400", "calib102", "calib2164"):
         if m in out and "FETCH_SIZE" in out[m]["avg"]:
             cal[m] = float(out[m]["meta"]["bytes"]) / (out[m]["avg"]["FETCH_SIZE"] * 1024.0)
-    for lab in ("cfg2", "cfg3", "cfg4"):
-        if lab in out and "FETCH_SIZE" in out[lab]["avg"]:
-            raw = out[lab]["avg"]["FETCH_SIZE"] * 1024.0
-            # cfg3's 64-B packets take the quad-lane direct path: nontemporal
-            # whole-line loads, the 16-lane-group shape (calib2164)
-            big = float(out[lab]["meta"].get("big_share", 0.0)) if lab != "cfg3" else 1.0
-            shape = {"calib2164": big, "calib400": 1.0 - big}
-            f = None
-            if all(cal.get(m) for m, w in shape.items() if w > 0):
-                f = sum(w * cal[m] for m, w in shape.items() if w > 0)
-            out[lab]["hbm_read_bytes_raw"] = raw
-            out[lab]["fetch_calibration"] = {"shape": shape, "factor": f}
-            out[lab]["hbm_bytes_per_launch"] = raw * f if f else None
-            if "WRITE_SIZE" in out[lab]["avg"]:
-                out[lab]["hbm_write_bytes"] = out[lab]["avg"]["WRITE_SIZE"] * 1024.0
+    for lab in list(out):
+        if "algorithmic_bytes" not in out[lab]["meta"] or "FETCH_SIZE" not in out[lab]["avg"]:
+            continue
+        raw = out[lab]["avg"]["FETCH_SIZE"] * 1024.0
+        # the quad-lane small-packet paths (cfg3 and its probes) load whole
+        # lines nontemporally: the 16-lane-group shape (calib2164)
+        big = float(out[lab]["meta"].get("big_share", 1.0)) if lab != "cfg3" else 1.0
+        shape = {"calib2164": big, "calib400": 1.0 - big}
+        f = None
+        if all(cal.get(m) for m, w in shape.items() if w > 0):
+            f = sum(w * cal[m] for m, w in shape.items() if w > 0)
+        out[lab]["hbm_read_bytes_raw"] = raw
+        out[lab]["fetch_calibration"] = {"shape": shape, "factor": f}
+        out[lab]["hbm_bytes_per_launch"] = raw * f if f else None
+        if "WRITE_SIZE" in out[lab]["avg"]:
+            out[lab]["hbm_write_bytes"] = out[lab]["avg"]["WRITE_SIZE"] * 1024.0
     json.dump(out, sys.stdout, indent=1)
 
 

@@ -1,9 +1,20 @@
 #!/usr/bin/env python3
-"""Workload for rocprofv3 --pmc passes (tools/profile.sh): calibration reads
-of a known byte count in the product kernel's access shapes, then the product
-kernel (ns_csum_batch_dev) on BASELINE configs 2, 3, 4.  Each launch is
-repeated REPS times; tools/pmc_parse.py maps dispatches back to labels in the
-order printed here."""
+"""Workload for rocprofv3 --pmc passes (tools/profile.sh).
+
+--set main (default): calibration reads of a known byte count in the product
+kernel's access shapes, then the product kernel (ns_csum_batch_dev) on every
+bench.py config: 2, 3, 4, 5, 7 (RX, fused table) and 8 (TX fill).  cfg3's
+82 MB batch fits the 256 MiB MALL, so it runs as bench.py runs it: 4
+batches with 4 descriptor tables, the measured launches each on a batch last
+touched three launches earlier (over 256 MiB of other data), so FETCH_SIZE
+counts HBM reads; a label `cfg3warm` covers the launches that cycle the
+batches in.
+--set cfg3probe: cfg3 rotated through the product's small-packet instance and
+the floor kernels of tools/tune.py (libns_tune.so), for the SQ counters.
+
+Each label covers REPS launches; tools/pmc_parse.py maps dispatches to labels
+in the order printed here."""
+import argparse
 import ctypes
 import os
 import sys
@@ -21,11 +32,21 @@ REPS = 3
 CAL_BYTES = (1 << 31) - 4096
 
 
-def main():
-    L = ctypes.CDLL(os.path.join(ROOT, "netstack_amd", "lib", "libns_tune.so"))
-    L.nsk_calib_launch.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
-                                   ctypes.c_uint32, ctypes.c_void_p]
-    dev = torch.device("cuda", 0)
+def big_share(desc) -> float:
+    """Share of payload in packets csum_hyb sends to the 8-lane groups (>= 40 chunks)."""
+    ln = desc["len"].astype(np.float64)
+    return float(ln[desc["len"] >= 40 * 16 - 15].sum() / max(ln.sum(), 1.0))
+
+
+def cfg3_rotated(dev):
+    b = W.config(3)
+    arenas = [b.arena_device(dev)] + [W.random_bytes_torch(b.seed + 77 * r, b.arena_bytes, dev) for r in range(1, 4)]
+    t = torch.from_numpy(b.desc.view(np.uint8).copy()).to(dev)
+    descs = [t] + [t.clone() for _ in range(3)]
+    return b, arenas, descs
+
+
+def main_set(dev, L):
     sp = torch.cuda.current_stream(dev).cuda_stream
     buf = torch.ones(CAL_BYTES, dtype=torch.uint8, device=dev)
     outb = torch.zeros(65536, dtype=torch.int32, device=dev)
@@ -37,7 +58,7 @@ def main():
         print(f"LABEL calib{mode} bytes={CAL_BYTES}", flush=True)
     del buf
     eng = Engine(0)
-    for cfg in (2, 3, 4):
+    for cfg in (2, 4, 5):
         b = W.config(cfg)
         arena = b.arena_device(dev)
         desc = torch.from_numpy(b.desc.view(np.uint8).copy()).to(dev)
@@ -45,11 +66,77 @@ def main():
         for _ in range(REPS):
             eng.batch_tensors(arena, desc, out)
         torch.cuda.synchronize()
-        # share of payload in packets csum_hyb sends to 16-lane groups (>= 64 chunks)
-        big = float(b.desc["len"][b.desc["len"] >= 1024 - 15].sum()) / max(b.payload_bytes, 1)
         print(f"LABEL cfg{cfg} algorithmic_bytes={b.algorithmic_bytes} payload={b.payload_bytes} "
-              f"arena={b.arena_bytes} n={b.n} big_share={big:.4f}", flush=True)
+              f"arena={b.arena_bytes} n={b.n} big_share={big_share(b.desc):.4f}", flush=True)
         del arena, desc, out
+        torch.cuda.empty_cache()
+    b, arenas, descs = cfg3_rotated(dev)
+    out = torch.empty(b.n, dtype=torch.int16, device=dev)
+    for k in (1, 2, 3):  # cycle the other batches in: batch 0 is now 3 launches (>256 MiB) old
+        eng.batch_tensors(arenas[k], descs[k], out)
+    torch.cuda.synchronize()
+    print(f"LABEL cfg3warm n={b.n}", flush=True)
+    for k in (0, 1, 2):
+        eng.batch_tensors(arenas[k], descs[k], out)
+    torch.cuda.synchronize()
+    print(f"LABEL cfg3 algorithmic_bytes={b.algorithmic_bytes} payload={b.payload_bytes} arena={b.arena_bytes} "
+          f"n={b.n} big_share=0 rotated=4", flush=True)
+    del arenas, descs, out
+    torch.cuda.empty_cache()
+    for cfg, tx in ((7, False), (8, True)):
+        n = 1 << 20
+        if tx:
+            arena, d = W.tx_batch(n, 7000, dev, fused=True)
+        else:
+            arena, d, _ = W.rx_batch(n, 7000, dev, corrupt_every=1000, fused=True)
+        desc = torch.from_numpy(d.view(np.uint8).copy()).to(dev)
+        out = torch.empty(len(d), dtype=torch.int16, device=dev)
+        for _ in range(REPS):
+            eng.batch_tensors(arena, desc, out, store=tx)
+        torch.cuda.synchronize()
+        algo = n * W.RX_PKT + 8 * n + len(d) * 18 + (4 * n if tx else 0)  # bench.py packet_mode
+        print(f"LABEL cfg{cfg} algorithmic_bytes={algo} payload={n * W.RX_PKT} arena={arena.numel()} n={len(d)} "
+              f"big_share={big_share(d):.4f}", flush=True)
+        del arena, desc, out
+        torch.cuda.empty_cache()
+
+
+def cfg3probe_set(dev, L):
+    names = [L.nsk_tune_name(v).decode() for v in range(L.nsk_tune_count())]
+    sp = torch.cuda.current_stream(dev).cuda_stream
+    b, arenas, descs = cfg3_rotated(dev)
+    out = torch.empty(b.n, dtype=torch.int16, device=dev)
+    err = torch.zeros(1, dtype=torch.int64, device=dev)
+    for name in ("small_wg64_spec", "small_wg64", "floor_quad_nt_wg64", "floor_quad_nt", "quad_direct_nt_wg64"):
+        v = names.index(name)
+        for k in (1, 2, 3, 0, 1, 2):  # three to cycle in, three measured (see cfg3warm above)
+            assert L.nsk_tune_launch(v, arenas[k].data_ptr(), b.arena_bytes, descs[k].data_ptr(), b.n,
+                                     out.data_ptr(), err.data_ptr(), sp) == 0
+            if k == 3:
+                torch.cuda.synchronize()
+                print(f"LABEL {name}_warm n={b.n}", flush=True)
+        torch.cuda.synchronize()
+        print(f"LABEL {name} algorithmic_bytes={b.algorithmic_bytes} n={b.n} rotated=4", flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--set", default="main", choices=("main", "cfg3probe"))
+    args = ap.parse_args()
+    L = ctypes.CDLL(os.path.join(ROOT, "netstack_amd", "lib", "libns_tune.so"))
+    L.nsk_calib_launch.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                   ctypes.c_uint32, ctypes.c_void_p]
+    L.nsk_tune_count.restype = ctypes.c_int
+    L.nsk_tune_name.restype = ctypes.c_char_p
+    L.nsk_tune_name.argtypes = [ctypes.c_int]
+    L.nsk_tune_launch.restype = ctypes.c_int
+    L.nsk_tune_launch.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                  ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    dev = torch.device("cuda", 0)
+    if args.set == "main":
+        main_set(dev, L)
+    else:
+        cfg3probe_set(dev, L)
 
 
 if __name__ == "__main__":
