@@ -1,6 +1,6 @@
 set -e
 # Every bench line of a round, on the GPU box: tools/final_round.sh TAG
-TAG=${1:-r02}
+TAG=${1:-r03}
 OUT=gpurun_out/final_$TAG
 mkdir -p $OUT
 for c in 1 2 3 4 5 7 8; do
