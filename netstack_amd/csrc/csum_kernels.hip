@@ -297,6 +297,7 @@ struct HybLds {
   uint32_t acc[P];
   uint32_t wsmall[P / 64];
   uint32_t wex[P / 64];
+  uint32_t wsch[P / 64];  // QS & 8: each wave's small-run chunks
   // NS_DESC_STORE launches only: each lane's validated store word and
   // address (written at decode, read back by the same lane after the scan).
   uint64_t sat[P];
@@ -492,7 +493,9 @@ __device__ __forceinline__ uint32_t spec_sum(const PktInfo& p, const uint4 (&v)[
 // FX = always the exact (T, W) accumulator (csum_split: its pieces' sums are
 // added, so they must be exact mod 2^32, not W-only class values).
 // QS = quad-lane small runs (US = 4, SRD path only; 1: nontemporal loads, 2:
-// the default policy): a wave takes 64
+// the default policy; | 4: two sets of 64 runs per iteration; | 8: only in
+// tiles whose small runs fill >= 7/8 of their quads, the others take the
+// lane runs): a wave takes 64
 // consecutive small runs per iteration, lane l looking up run l and quad q of
 // load instruction j loading run 16 j + q, one chunk per lane; consecutive
 // runs lie back to back in memory when packets are packed, so one
@@ -537,17 +540,26 @@ __device__ __forceinline__ uint32_t hyb_scan_tile(HybLds<WG>& L, const Srd& r, c
     if (lane >= d) incl += y;
   }
   const int wex = FX || __any(nch > kWOnlyMaxChunks);
+  uint32_t sch = 0u;  // QS & 8: chunks in small runs (the quads they fill)
+  if constexpr ((QS & 8) != 0) {
+    sch = split ? h + nch - ts : nch;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) sch += __shfl_xor(sch, d, 64);
+  }
   if (lane == 63) {
     L.wtot[wv] = incl;
     L.wex[wv] = (uint32_t)wex;
+    if constexpr ((QS & 8) != 0) L.wsch[wv] = sch;
   }
   __syncthreads();
   uint64_t excl = incl - nr;
   bool exact = false;
+  uint32_t scht = 0u;
 #pragma unroll
   for (int w = 0; w < NW; ++w) {
     if (w < wv) excl += L.wtot[w];
     exact = exact || L.wex[w];
+    if constexpr ((QS & 8) != 0) scht += L.wsch[w];
   }
   L.rb[t] = (uint32_t)excl;
   L.rs[t] = (uint32_t)(excl >> 32);
@@ -652,50 +664,60 @@ __device__ __forceinline__ uint32_t hyb_scan_tile(HybLds<WG>& L, const Srd& r, c
 
     if constexpr (QS != 0 && !GL) {
       static_assert(US == 4, "quad-lane small runs are runs of 4 chunks");
+      if ((QS & 8) && scht * 8u < RSt * 28u) goto lane_runs;  // | 8: only when the quads are >= 7/8 full
+      constexpr int QN = (QS & 4) ? 2 : 1;  // sets of 64 runs per wave per iteration
+      constexpr int QP = (QS & 3) == 1 ? 2 : 0;  // load policy: nontemporal or default
       const uint32_t c = (uint32_t)lane & 3u;
-      for (uint32_t qb = (uint32_t)wv * 64u; qb < RSt; qb += (uint32_t)NW * 64u) {
-        // lane l describes run qb + l: SRD offset of its first chunk and a
-        // meta word nvalid (3 bits) | lo (4) | last chunk in run (1) | its
-        // index (2) | hiex (5) | phase (1) | packet (8)
-        const uint32_t q = qb + (uint32_t)lane;
-        uint32_t roff = r.oob, meta = 0u;
-        if (q < RSt) {
-          const int pk = search(L.rs, q);
-          const uint32_t k = q - L.rs[pk];
-          const uint4 inf = L.info[pk];
-          uint32_t ci0 = k * 4u, cend = inf.y;
-          if (inf.z & kSplitBit) {  // head runs cover [0, h), tail runs [ts, nch)
-            const uint32_t hh = (inf.z >> 10) & 15u, nh = (hh + 3u) / 4u;
-            if (k < nh) cend = hh;
-            else ci0 = inf.w + (k - nh) * 4u;
+      for (uint32_t qb = (uint32_t)wv * 64u * QN; qb < RSt; qb += (uint32_t)NW * 64u * QN) {
+        // lane l describes run qb + 64 s + l: SRD offset of its first chunk
+        // and a meta word nvalid (3 bits) | lo (4) | last chunk in run (1) |
+        // its index (2) | hiex (5) | phase (1) | packet (8)
+        uint32_t roff[QN], meta[QN];
+#pragma unroll
+        for (int s = 0; s < QN; ++s) {
+          const uint32_t q = qb + 64u * s + (uint32_t)lane;
+          roff[s] = r.oob;
+          meta[s] = 0u;
+          if (q < RSt) {
+            const int pk = search(L.rs, q);
+            const uint32_t k = q - L.rs[pk];
+            const uint4 inf = L.info[pk];
+            uint32_t ci0 = k * 4u, cend = inf.y;
+            if (inf.z & kSplitBit) {  // head runs cover [0, h), tail runs [ts, nch)
+              const uint32_t hh = (inf.z >> 10) & 15u, nh = (hh + 3u) / 4u;
+              if (k < nh) cend = hh;
+              else ci0 = inf.w + (k - nh) * 4u;
+            }
+            const uint32_t nv = min(cend - ci0, 4u);
+            const uint32_t lo = ci0 == 0u ? (inf.z & 15u) : 0u;
+            const uint32_t jl = inf.y - 1u - ci0;
+            const uint32_t has_last = jl < nv ? 1u : 0u;
+            meta[s] = nv | (lo << 3) | (has_last << 7) | ((jl & 3u) << 8) | (((inf.z >> 5) & 31u) << 10) |
+                      ((inf.z >> 31) << 15) | ((uint32_t)pk << 16);
+            roff[s] = inf.x + ci0 * 16u;
           }
-          const uint32_t nv = min(cend - ci0, 4u);
-          const uint32_t lo = ci0 == 0u ? (inf.z & 15u) : 0u;
-          const uint32_t jl = inf.y - 1u - ci0;
-          const uint32_t has_last = jl < nv ? 1u : 0u;
-          meta = nv | (lo << 3) | (has_last << 7) | ((jl & 3u) << 8) | (((inf.z >> 5) & 31u) << 10) |
-                 ((inf.z >> 31) << 15) | ((uint32_t)pk << 16);
-          roff = inf.x + ci0 * 16u;
         }
-        uint4 v[4];
-        uint32_t mj[4];
+        uint4 v[4 * QN];
+        uint32_t mj[4 * QN];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int src = (int)(16 * j + (lane >> 2));
-          mj[j] = (uint32_t)__shfl((int)meta, src, 64);
-          const uint32_t o = (uint32_t)__shfl((int)roff, src, 64);
-          v[j] = bload<QS == 1 ? 2 : 0>(r.rsrc, c < (mj[j] & 7u) ? o + 16u * c : r.oob);
+        for (int j = 0; j < 4 * QN; ++j) {
+          const int src = (int)(16 * (j & 3) + (lane >> 2));
+          mj[j] = (uint32_t)__shfl((int)meta[j >> 2], src, 64);
+          const uint32_t o = (uint32_t)__shfl((int)roff[j >> 2], src, 64);
+          v[j] = bload<QP>(r.rsrc, c < (mj[j] & 7u) ? o + 16u * c : r.oob);
         }
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
+        for (int j = 0; j < 4 * QN; ++j) {
           const uint32_t m = mj[j];
           const int lo_b = c == 0u ? (int)((m >> 3) & 15u) : 0;
           const int hi_b = ((m >> 7) & 1u) && c == ((m >> 8) & 3u) ? (int)((m >> 10) & 31u) : 16;
           uint4 w = v[j];
-          w.x &= bytes_below(hi_b) & ~bytes_below(lo_b);
-          w.y &= bytes_below(hi_b - 4) & ~bytes_below(lo_b - 4);
-          w.z &= bytes_below(hi_b - 8) & ~bytes_below(lo_b - 8);
-          w.w &= bytes_below(hi_b - 12) & ~bytes_below(lo_b - 12);
+          if (lo_b != 0 || hi_b != 16) {  // an edge chunk (slots past the run read zeros)
+            w.x &= bytes_below(hi_b) & ~bytes_below(lo_b);
+            w.y &= bytes_below(hi_b - 4) & ~bytes_below(lo_b - 4);
+            w.z &= bytes_below(hi_b - 8) & ~bytes_below(lo_b - 8);
+            w.w &= bytes_below(hi_b - 12) & ~bytes_below(lo_b - 12);
+          }
           uint32_t T = 0, W = 0;
           acc_chunk<EX>(w, T, W);
           const uint32_t val = group_sum<4>(run_value<EX>(T, W, (m >> 15) & 1u));
@@ -704,6 +726,7 @@ __device__ __forceinline__ uint32_t hyb_scan_tile(HybLds<WG>& L, const Srd& r, c
       }
       return;
     }
+  lane_runs:
     static_assert(SU == 1 || SU == 2, "the small loop issues one or two runs per iteration");
     for (uint32_t q = (uint32_t)t; q < RSt; q += SU * WG) {
       uint4 va[US];

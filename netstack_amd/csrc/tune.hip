@@ -826,6 +826,9 @@ static const Variant kVariants[] = {
     {"quad_pipe8_nt", launch_quad_pipe<8, 2>},
     // quad-lane small runs with the default cache policy
     {"qsd_b40", launch_h<8, 16, 4, 2, kBigChunks, 0, 2, 2>},
+    {"qsa_b40", launch_h<8, 16, 4, 2, kBigChunks, 0, 2, 9>},   // quad-lane nt runs in tiles without big packets
+    {"qs2_b40", launch_h<8, 16, 4, 2, kBigChunks, 0, 2, 5>},   // two sets of 64 runs per wave iteration
+    {"qsd2_b40", launch_h<8, 16, 4, 2, kBigChunks, 0, 2, 6>},
     {"qsd_b64", launch_h<8, 16, 4, 2, 64, 0, 2, 2>},
     {"prod_small_qsd", launch_h<16, 8, 4, 2, 64, 5, 1, 2>},
     // one-wave workgroups, 2-4 groups of 64 packets per wave (cold tables)

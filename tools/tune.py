@@ -101,6 +101,31 @@ def main():
             a7, d7, _ = W.rx_batch(nover.get(7, 1 << 20), 7000, dev)
             b = W.Batch("rx_1Mx1500_3desc", 7000, d7, a7.numel())
             arenas = [a7]
+        elif cfg in (10, 11, 12):  # mixed shapes: Zipf 64-600 B; half 64-B ACKs, half 1460-B segments (by
+            # count); Zipf 200-1000 B
+            n = nover.get(cfg, {10: 1 << 22, 11: 1 << 21, 12: 1 << 22}[cfg])
+            if cfg == 10:
+                ln = W.zipf_lengths(10, n, 64, 600)
+            elif cfg == 12:
+                ln = W.zipf_lengths(12, n, 200, 1000)
+            else:
+                ln = np.where(W.splitmix64(11, n) & np.uint64(1), 1460, 64).astype(np.uint32)
+            d, end = W.make_desc(ln, W._initials(cfg, n), 16)
+            b = W.Batch(f"mix{cfg}", cfg, d, ((end + 15) // 16) * 16)
+            arenas = [b.arena_device(dev)] + [W.random_bytes_torch(b.seed + 77 * r, b.arena_bytes, dev)
+                                              for r in range(1, rot)]
+        elif cfg in (13, 14):  # receive rings: 512-B slots holding Zipf 64-512 B; 256-B slots, 128-256 B
+            slot = 512 if cfg == 13 else 256
+            n = nover.get(cfg, 1_572_864_000 // slot)
+            ln = W.zipf_lengths(cfg, n, 64, 512) if cfg == 13 else \
+                (128 + (W.splitmix64(cfg, n) % np.uint64(129))).astype(np.uint32)
+            d = np.zeros(n, dtype=W.DESC_DTYPE)
+            d["off"] = np.arange(n, dtype=np.uint64) * np.uint64(slot)
+            d["len"] = ln
+            d["initial"] = W._initials(cfg, n)
+            b = W.Batch(f"ring{slot}", cfg, d, n * slot)
+            arenas = [b.arena_device(dev)] + [W.random_bytes_torch(b.seed + 77 * r, b.arena_bytes, dev)
+                                              for r in range(1, rot)]
         elif cfg >= 100:  # uniform packets of `cfg` bytes, 1.5 GB of payload (TP-rule sweeps)
             b = W.uniform(f"uniform_{cfg}B", 9000 + cfg, nover.get(cfg, (1_572_864_000 // cfg)), cfg)
             arenas = [b.arena_device(dev)] + [W.random_bytes_torch(b.seed + 77 * r, b.arena_bytes, dev)
