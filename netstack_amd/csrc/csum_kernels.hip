@@ -893,7 +893,16 @@ __global__ __launch_bounds__(WG) void csum_hyb(
   __shared__ HybLds<WG> L;
   const bool wt = zc_flag != nullptr;
   const int t = threadIdx.x;
-  const uint64_t i = (uint64_t)blockIdx.x * TP + t;
+  // QS & 16: XCD-aware tiles — the blocks one XCD runs (b, b + 8, ...) take
+  // consecutive tiles, so the line two neighbouring tiles share is read
+  // through one L2 (bijective for any grid).
+  uint32_t tid = blockIdx.x;
+  if constexpr ((QS & 16) != 0) {
+    const uint32_t g = gridDim.x, q = g >> 3, r = g & 7u, x = blockIdx.x & 7u, k = blockIdx.x >> 3;
+    tid = x < r ? x * (q + 1u) + k : r * (q + 1u) + (x - r) * q + k;
+  }
+  constexpr int QL = QS & 15;
+  const uint64_t i = (uint64_t)tid * TP + t;
   const bool mine = t < TP && i < n;
   const uint64_t arena_abs = (uint64_t)(uintptr_t)arena;
   // Speculative payload loads beside the descriptor loads (spec_load), in
@@ -908,7 +917,7 @@ __global__ __launch_bounds__(WG) void csum_hyb(
     const uint4 rawl = desc[min(i, (uint64_t)n - 1u)];
     // branch-free: with spec = 0 every slot is out of range (no memory access)
     spec_load(make_srd(arena_abs & ~15ull, arena_abs + arena_bytes - (arena_abs & ~15ull)),
-              (uint64_t)blockIdx.x * TP, spec ? n : 0u, spec, sv);
+              (uint64_t)tid * TP, spec ? n : 0u, spec, sv);
     __builtin_amdgcn_sched_barrier(0);  // all four issued before anything waits for the descriptor
     raw = mine ? rawl : make_uint4(0, 0, 0, 0);
   } else {
@@ -952,7 +961,7 @@ __global__ __launch_bounds__(WG) void csum_hyb(
     }
     if (!__syncthreads_or(!small)) return;
     const uint32_t s =
-        hyb_scan_tile<WG, TP, GB, UB, US, AUXB, false, SU, false, QS>(L, r, small ? PktInfo{} : p, big_chunks);
+        hyb_scan_tile<WG, TP, GB, UB, US, AUXB, false, SU, false, QL>(L, r, small ? PktInfo{} : p, big_chunks);
     if (!small) finish_tile<WG, CH>(L, s, d, mine, i, n, out, partial, store, wt);
     return;
   }
@@ -968,7 +977,7 @@ __global__ __launch_bounds__(WG) void csum_hyb(
       finish_tile<WG, CH>(L, s, d, mine, i, n, out, partial, store, wt);
       return;
     }
-    const uint32_t s = hyb_scan_tile<WG, TP, GB, UB, US, AUXB, false, SU, false, QS>(L, r, p, big_chunks);
+    const uint32_t s = hyb_scan_tile<WG, TP, GB, UB, US, AUXB, false, SU, false, QL>(L, r, p, big_chunks);
     finish_tile<WG, CH>(L, s, d, mine, i, n, out, partial, store, wt);
   } else if constexpr (WIN) {
     // The tile spans >= 4 GiB: 64-bit global loads, fewer in flight per lane

@@ -718,7 +718,7 @@ hipError_t launch_small_wg(const uint8_t* arena, uint64_t arena_bytes, const voi
 // ... and with the launcher's fixed-stride speculation (spec_load): an arena
 // of exactly n slots of 16-64 bytes gets its payload loads beside the
 // descriptor loads.
-template <int WGT>
+template <int WGT, int QSX = 0>
 hipError_t launch_small_wg_spec(const uint8_t* arena, uint64_t arena_bytes, const void* desc, uint32_t n,
                                 uint16_t* out, unsigned long long* err, hipStream_t s) {
   uint32_t spec = 0;
@@ -726,8 +726,8 @@ hipError_t launch_small_wg_spec(const uint8_t* arena, uint64_t arena_bytes, cons
     const uint64_t st = arena_bytes / n;
     if (st % 16 == 0 && st >= 16 && st <= 64) spec = (uint32_t)st;
   }
-  return launch_hyb_tp<WGT, 16, 8, 4, 2, 5, 1, false, WGT>(arena, arena_bytes, desc, n, out, nullptr, err, s, 64u, 0,
-                                                          ZcSignal{}, spec);
+  return launch_hyb_tp<WGT, 16, 8, 4, 2, 5, 1, QSX, WGT>(arena, arena_bytes, desc, n, out, nullptr, err, s, 64u, 0,
+                                                        ZcSignal{}, spec);
 }
 
 typedef hipError_t (*launch_fn)(const uint8_t*, uint64_t, const void*, uint32_t, uint16_t*,
@@ -742,6 +742,7 @@ struct Variant {
 static const Variant kVariants[] = {
     {"prod", launch_h<8, 16, 4, 2, kBigChunks, 0, 2>},  // the production big-packet launch
     {"qs_b40", launch_h<8, 16, 4, 2, kBigChunks, 0, 2, 1>},   // quad-lane nt small runs
+    {"prod_xcd", launch_h<8, 16, 4, 2, kBigChunks, 0, 2, 16>},  // prod with XCD-aware tiles
     {"qs_b24", launch_h<8, 16, 4, 2, 24, 0, 2, 1>},
     {"qs_b64", launch_h<8, 16, 4, 2, 64, 0, 2, 1>},
     {"qs_b1000", launch_h<8, 16, 4, 2, 1000, 0, 2, 1>},     // every packet below 16 KB through small runs
@@ -813,6 +814,7 @@ static const Variant kVariants[] = {
     {"quad_pf0", launch_quad_prefetch<0xFFFFFFFFu>},
     {"small_wg64", launch_small_wg<64>},
     {"small_wg64_spec", launch_small_wg_spec<64>},
+    {"small_wg64_spec_xcd", launch_small_wg_spec<64, 16>},
     {"small_wg128", launch_small_wg<128>},
     {"quad_pf256k", launch_quad_prefetch<262144u>},
     {"quad_pf512k", launch_quad_prefetch<524288u>},
@@ -845,9 +847,37 @@ static const Variant kVariants[] = {
     {"wg256_tp64_b40", launch_wg<256, 64, kBigChunks>},
 };
 
+// TX probe: the stores of an NS_DESC_STORE table as a pass of their own,
+// after a read-only launch wrote the results to `out` (the descriptor
+// re-read is this pass's only read).  Same validation and store as the
+// product's park_store / store_result.
+__global__ __launch_bounds__(256) void store_pass(const uint8_t* __restrict__ arena, uint64_t arena_bytes,
+                                                  const uint4* __restrict__ desc, uint32_t n,
+                                                  const uint16_t* __restrict__ out, unsigned long long* err) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const uint4 raw = desc[i];
+  const uint32_t stw = (raw.w >> 18) & 0x3FFFu;
+  if (!(stw & 1u)) return;
+  const uint64_t at = ((uint64_t)raw.x | ((uint64_t)raw.y << 32)) + (stw >> 2);
+  if (at > arena_bytes || arena_bytes - at < 2) {
+    atomicAdd(err, 1ull);
+    return;
+  }
+  store_result((uint64_t)(uintptr_t)arena + at, out[i], stw);
+}
+
 }  // namespace nsk
 
 extern "C" {
+
+int nsk_store_pass_launch(const uint8_t* arena, uint64_t arena_bytes, const void* desc, uint32_t n,
+                          const uint16_t* out, unsigned long long* err, void* stream) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(nsk::store_pass, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, arena, arena_bytes,
+                     reinterpret_cast<const uint4*>(desc), n, out, err);
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}
 
 int nsk_tune_count(void) { return (int)(sizeof(nsk::kVariants) / sizeof(nsk::kVariants[0])); }
 
