@@ -139,6 +139,29 @@ def test_icmpv6_checksums(engine):
     assert proto.icmpv6_checksums(items) == want
 
 
+def test_icmpv6_reference_validation_cases(engine):
+    """icmp_test.go:367-899 (tests/icmpv6cases.py): the engine's ICMPv6Checksum
+    equals the oracle's for the transmit split, the receive split of the
+    message with the field set gives the same value (received), and no value
+    is 0 (the unset field is Invalid)."""
+    import icmpv6cases as C
+    import oracle as O
+    from netstack_amd import proto
+    from netstack_amd.buffer import NewVectorisedView, View
+
+    def vv(views):
+        return NewVectorisedView(sum(map(len, views)), [View(bytearray(v)) for v in views])
+
+    cs = C.cases()
+    tx = proto.icmpv6_checksums([(bytearray(h), C.LLADDR1, C.LLADDR0, vv(v)) for _, h, v, _, _ in cs])
+    want = [C.oracle_checksum(O, h, C.LLADDR1, C.LLADDR0, v) for _, h, v, _, _ in cs]
+    assert tx == want
+    assert all(c != 0 for c in tx)
+    rx = proto.icmpv6_checksums([(bytearray(C.with_checksum(h, c)), C.LLADDR1, C.LLADDR0, vv(v))
+                                 for (_, _, _, h, v), c in zip(cs, tx)])
+    assert rx == tx
+
+
 def test_tcp_encode_partial(engine):
     """tcp.go:295-314: the incremental update must equal a full recompute of
     the segment checksum when `partial` covers everything else."""
