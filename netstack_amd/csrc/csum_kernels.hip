@@ -882,7 +882,8 @@ __device__ __forceinline__ void zc_complete(uint32_t* __restrict__ ctr, uint32_t
 // (finish_tile writes partials and continuation flags for fold_scan).
 template <int WG, int TP, int GB, int UB, int US, int AUXB, int UD = 0, bool WIN = false,
           int SU = 1, int QS = 0, bool CH = false>
-__global__ __launch_bounds__(WG) void csum_hyb(
+// QS & 32 (tuning only): at least 8 waves per SIMD (<= 64 VGPRs).
+__global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu((QS & 32) ? 8 : 1))) void csum_hyb(
     const uint8_t* __restrict__ arena, uint64_t arena_bytes,
     const uint4* __restrict__ desc, uint32_t n, uint16_t* __restrict__ out,
     uint32_t* __restrict__ partial, unsigned long long* __restrict__ err, uint32_t big_chunks,

@@ -221,6 +221,142 @@ __global__ __launch_bounds__(256) void calib_tile_x(const uint4* __restrict__ p,
   }
 }
 
+// ---- probe: one coalesced stream over a tile's byte span ------------------
+// For tables whose descriptors are sorted by offset and do not overlap (packed
+// batches).  Groups of 8 lanes read the tile's span line by line (one whole
+// 128-B line per group per load, nontemporal, 16 lines per lane in flight),
+// and each lane attributes its chunks to packets with a cursor over the
+// tile's chunk ranges: W-only sums (packets <= kWOnlyMaxChunks), flushed to
+// the packet's LDS accumulator when the lane moves on to another packet.
+// Chunks in gaps between packets are read and dropped.  Probe only: no
+// sortedness check, no exact path, arenas < 4 GiB.
+template <int TP>
+__global__ __launch_bounds__(256) void stream_tile(const uint8_t* __restrict__ arena, uint64_t arena_bytes,
+                                                   const uint4* __restrict__ desc, uint32_t n,
+                                                   uint16_t* __restrict__ out, unsigned long long* err) {
+  constexpr int WG = 256, NG = WG / 8, NW = WG / 64;
+  __shared__ uint32_t s_c0[TP], s_c1[TP], s_ew[TP], s_pe[TP], s_acc[TP];
+  __shared__ uint32_t s_lo[NW], s_hi[NW];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const uint64_t i = (uint64_t)blockIdx.x * TP + t;
+  const bool mine = t < TP && i < n;
+  const uint64_t arena_abs = (uint64_t)(uintptr_t)arena;
+  const uint4 raw = mine ? desc[i] : make_uint4(0, 0, 0, 0);
+  const Pkt d = decode(raw, mine, arena_abs, arena_bytes, err);
+  const uint64_t wbase = arena_abs & ~15ull;
+  const PktInfo p = pkt_info(d, wbase);
+  const uint32_t c0 = p.first >> 4, c1 = p.nch ? c0 + p.nch : 0u;
+  // prefix max of the chunk ends (monotone, for the cursor search)
+  uint32_t pe = c1;
+#pragma unroll
+  for (int k = 1; k < 64; k <<= 1) {
+    const uint32_t y = __shfl_up(pe, k, 64);
+    if (lane >= k) pe = max(pe, y);
+  }
+  const uint32_t lo = (uint32_t)__ockl_wfred_min_u64(p.nch ? c0 : 0xFFFFFFFFull);
+  const uint32_t hi = (uint32_t)__ockl_wfred_max_u64(c1);
+  if (lane == 63) {
+    s_lo[wv] = lo;
+    s_hi[wv] = pe;
+  }
+  __syncthreads();
+  uint32_t tlo = 0xFFFFFFFFu, thi = 0u, pre = 0u;
+#pragma unroll
+  for (int w = 0; w < NW; ++w) {
+    tlo = min(tlo, s_lo[w]);
+    thi = max(thi, s_hi[w]);
+    if (w < wv) pre = max(pre, s_hi[w]);
+  }
+  (void)hi;
+  if (t < TP) {
+    s_c0[t] = c0;
+    s_c1[t] = c1;
+    s_ew[t] = p.ew;
+    s_pe[t] = max(pe, pre);
+    s_acc[t] = 0u;
+  }
+  __syncthreads();
+  const Srd r = make_srd(wbase, arena_abs + arena_bytes - wbase);
+  if (tlo < thi) {
+    const uint32_t L0 = tlo >> 3, L1 = (thi + 7u) >> 3;
+    const uint32_t li = (uint32_t)t & 7u;
+    for (uint32_t sl = L0 + 16u * (uint32_t)(t >> 3); sl < L1; sl += 16u * NG) {
+      uint4 v[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const uint32_t line = sl + (uint32_t)j;
+        v[j] = bload<2>(r.rsrc, line < L1 ? (line * 8u + li) * 16u : r.oob);
+      }
+      // cursor: the first packet whose prefix end passes this lane's first chunk
+      const uint32_t cfirst = sl * 8u + li;
+      int q = 0;
+#pragma unroll
+      for (int step = TP / 2; step >= 1; step >>= 1)
+        q = (s_pe[q + step - 1] <= cfirst) ? q + step : q;
+      // packet q's chunk range and edge word stay in registers; LDS is read
+      // only when the cursor moves on
+      uint32_t qa = 0u, qb = 0u, qe = 0u;
+      if (q < TP) {
+        qa = s_c0[q];
+        qb = s_c1[q];
+        qe = s_ew[q];
+      }
+      uint32_t cur = 0xFFFFFFFFu, W = 0u;
+      auto take = [&](uint4 w, uint32_t c, uint32_t a, uint32_t b, uint32_t e, uint32_t pk) {
+        const int lo_b = c == a ? (int)(e & 31u) : 0;
+        const int hi_b = c + 1u == b ? (int)((e >> 5) & 31u) : 16;
+        if (lo_b != 0 || hi_b != 16) {
+          w.x &= bytes_below(hi_b) & ~bytes_below(lo_b);
+          w.y &= bytes_below(hi_b - 4) & ~bytes_below(lo_b - 4);
+          w.z &= bytes_below(hi_b - 8) & ~bytes_below(lo_b - 8);
+          w.w &= bytes_below(hi_b - 12) & ~bytes_below(lo_b - 12);
+        }
+        if (pk != cur) {
+          if (cur != 0xFFFFFFFFu) atomicAdd(&s_acc[cur], W);
+          cur = pk;
+          W = 0u;
+        }
+        acc_chunk<false>(w, W, W);
+      };
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const uint32_t c = cfirst + 8u * (uint32_t)j;
+        while (q < TP && qb <= c) {  // packets that ended before c (empty ones too)
+          ++q;
+          if (q < TP) {
+            qa = s_c0[q];
+            qb = s_c1[q];
+            qe = s_ew[q];
+          }
+        }
+        if (q < TP && qa <= c) {
+          take(v[j], c, qa, qb, qe, (uint32_t)q);
+          if (qb == c + 1u) {  // q ends in this chunk: the next packets may start in it
+            for (int qq = q + 1; qq < TP; ++qq) {
+              const uint32_t a = s_c0[qq], b = s_c1[qq];
+              if (b == 0u) continue;  // empty
+              if (a > c) break;
+              take(v[j], c, a, b, s_ew[qq], (uint32_t)qq);
+              if (b > c + 1u) break;
+            }
+          }
+        }
+      }
+      if (cur != 0xFFFFFFFFu) atomicAdd(&s_acc[cur], W);
+    }
+  }
+  __syncthreads();
+  if (mine) out[i] = (uint16_t)fold1(d.init + s_class(s_acc[t], p.ew >> 31));
+}
+
+template <int TP>
+hipError_t launch_stream(const uint8_t* arena, uint64_t arena_bytes, const void* desc, uint32_t n,
+                         uint16_t* out, unsigned long long* err, hipStream_t s) {
+  hipLaunchKernelGGL(stream_tile<TP>, dim3((n + TP - 1) / TP), dim3(256), 0, s, arena, arena_bytes,
+                     reinterpret_cast<const uint4*>(desc), n, out, err);
+  return hipGetLastError();
+}
+
 template <int GB, int UB, int US, int AUXB, uint32_t BIG, int UD = 0, int SU = 1, int QS = 0>
 hipError_t launch_h(const uint8_t* arena, uint64_t arena_bytes, const void* desc, uint32_t n,
                     uint16_t* out, unsigned long long* err, hipStream_t s) {
@@ -743,6 +879,11 @@ static const Variant kVariants[] = {
     {"prod", launch_h<8, 16, 4, 2, kBigChunks, 0, 2>},  // the production big-packet launch
     {"qs_b40", launch_h<8, 16, 4, 2, kBigChunks, 0, 2, 1>},   // quad-lane nt small runs
     {"prod_xcd", launch_h<8, 16, 4, 2, kBigChunks, 0, 2, 16>},  // prod with XCD-aware tiles
+    {"prod_o8", launch_h<8, 16, 4, 2, kBigChunks, 0, 2, 32>},  // prod at >= 8 waves per SIMD
+    {"stream_tp64", launch_stream<64>},   // one coalesced stream over each tile's span
+    {"stream_tp128", launch_stream<128>},
+    {"stream_tp256", launch_stream<256>},
+    {"g8u8_b40_o8", launch_h<8, 8, 4, 2, kBigChunks, 0, 2, 32>},
     {"qs_b24", launch_h<8, 16, 4, 2, 24, 0, 2, 1>},
     {"qs_b64", launch_h<8, 16, 4, 2, 64, 0, 2, 1>},
     {"qs_b1000", launch_h<8, 16, 4, 2, 1000, 0, 2, 1>},     // every packet below 16 KB through small runs
