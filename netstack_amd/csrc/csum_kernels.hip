@@ -495,7 +495,7 @@ __device__ __forceinline__ uint32_t spec_sum(const PktInfo& p, const uint4 (&v)[
 // QS = quad-lane small runs (US = 4, SRD path only; 1: nontemporal loads, 2:
 // the default policy; | 4: two sets of 64 runs per iteration; | 8: only in
 // tiles whose small runs fill >= 7/8 of their quads, the others take the
-// lane runs): a wave takes 64
+// lane runs; | 64, without the quad loop: lean load addressing): a wave takes 64
 // consecutive small runs per iteration, lane l looking up run l and quad q of
 // load instruction j loading run 16 j + q, one chunk per lane; consecutive
 // runs lie back to back in memory when packets are packed, so one
@@ -619,11 +619,19 @@ __device__ __forceinline__ uint32_t hyb_scan_tile(HybLds<WG>& L, const Srd& r, c
         if constexpr (GL) gb = L.g[sr.pk] + (uint64_t)sr.ci0 * 16u;
         else base = inf.x + sr.ci0 * 16u;
       }
+      if constexpr ((QS & 64) != 0 && !GL) {
+        // QS & 64: the valid slots counted once, each load's select on the
+        // base alone (the chunk step folds into the instruction's offset)
+        const uint32_t kv = sr.ci0 < cend ? min(cend - sr.ci0, (uint32_t)US) : 0u;
 #pragma unroll
-      for (int j = 0; j < US; ++j) {
-        const bool valid = sr.ci0 + (uint32_t)j < cend;
-        if constexpr (GL) v[j] = valid ? gload<false>(gb + 16u * j) : make_uint4(0, 0, 0, 0);
-        else v[j] = bload(r.rsrc, valid ? base + 16u * j : r.oob);
+        for (int j = 0; j < US; ++j) v[j] = bload(r.rsrc, ((uint32_t)j < kv ? base : r.oob) + 16u * j);
+      } else {
+#pragma unroll
+        for (int j = 0; j < US; ++j) {
+          const bool valid = sr.ci0 + (uint32_t)j < cend;
+          if constexpr (GL) v[j] = valid ? gload<false>(gb + 16u * j) : make_uint4(0, 0, 0, 0);
+          else v[j] = bload(r.rsrc, valid ? base + 16u * j : r.oob);
+        }
       }
       return sr;
     };
@@ -650,9 +658,15 @@ __device__ __forceinline__ uint32_t hyb_scan_tile(HybLds<WG>& L, const Srd& r, c
           v[j] = ci0 + (uint32_t)(GB * j) < cend ? gload<AUXB != 0>(g0 + 16u * GB * j) : make_uint4(0, 0, 0, 0);
       } else {
         const uint32_t b0 = inf.x + ci0 * 16u;
+        if constexpr ((QS & 64) != 0) {
+          const uint32_t kv = ci0 < cend ? min((cend - ci0 + GB - 1u) / GB, (uint32_t)UB) : 0u;
 #pragma unroll
-        for (int j = 0; j < UB; ++j)
-          v[j] = bload<AUXB>(r.rsrc, ci0 + (uint32_t)(GB * j) < cend ? b0 + 16u * GB * j : r.oob);
+          for (int j = 0; j < UB; ++j) v[j] = bload<AUXB>(r.rsrc, ((uint32_t)j < kv ? b0 : r.oob) + 16u * GB * j);
+        } else {
+#pragma unroll
+          for (int j = 0; j < UB; ++j)
+            v[j] = bload<AUXB>(r.rsrc, ci0 + (uint32_t)(GB * j) < cend ? b0 + 16u * GB * j : r.oob);
+        }
       }
       uint32_t T = 0, W = 0;
 #pragma unroll
@@ -662,7 +676,7 @@ __device__ __forceinline__ uint32_t hyb_scan_tile(HybLds<WG>& L, const Srd& r, c
       if (li == 0) atomicAdd(&L.acc[pk], sg);
     }
 
-    if constexpr (QS != 0 && !GL) {
+    if constexpr ((QS & 3) != 0 && !GL) {
       static_assert(US == 4, "quad-lane small runs are runs of 4 chunks");
       if ((QS & 8) && scht * 8u < RSt * 28u) goto lane_runs;  // | 8: only when the quads are >= 7/8 full
       constexpr int QN = (QS & 4) ? 2 : 1;  // sets of 64 runs per wave per iteration
@@ -902,7 +916,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu((QS & 32) ? 
     const uint32_t g = gridDim.x, q = g >> 3, r = g & 7u, x = blockIdx.x & 7u, k = blockIdx.x >> 3;
     tid = x < r ? x * (q + 1u) + k : r * (q + 1u) + (x - r) * q + k;
   }
-  constexpr int QL = QS & 15;
+  constexpr int QL = QS & ~(16 | 32);
   const uint64_t i = (uint64_t)tid * TP + t;
   const bool mine = t < TP && i < n;
   const uint64_t arena_abs = (uint64_t)(uintptr_t)arena;

@@ -880,6 +880,7 @@ static const Variant kVariants[] = {
     {"qs_b40", launch_h<8, 16, 4, 2, kBigChunks, 0, 2, 1>},   // quad-lane nt small runs
     {"prod_xcd", launch_h<8, 16, 4, 2, kBigChunks, 0, 2, 16>},  // prod with XCD-aware tiles
     {"prod_o8", launch_h<8, 16, 4, 2, kBigChunks, 0, 2, 32>},  // prod at >= 8 waves per SIMD
+    {"prod_lean", launch_h<8, 16, 4, 2, kBigChunks, 0, 2, 64>},  // lean load addressing
     {"stream_tp64", launch_stream<64>},   // one coalesced stream over each tile's span
     {"stream_tp128", launch_stream<128>},
     {"stream_tp256", launch_stream<256>},
