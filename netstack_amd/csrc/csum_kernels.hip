@@ -117,6 +117,17 @@ __device__ __forceinline__ uint32_t s_of(uint32_t T, uint32_t W, uint32_t phase)
   return phase ? W : (257u * T - W);
 }
 
+// Lane jj of each quad, broadcast to the quad (DPP quad_perm; jj folds to a
+// constant once the caller's loop is unrolled).
+__device__ __forceinline__ uint32_t quad_bcast(uint32_t x, int jj) {
+  switch (jj & 3) {
+    case 0: return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x00, 0xF, 0xF, false);
+    case 1: return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x55, 0xF, 0xF, false);
+    case 2: return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xAA, 0xF, 0xF, false);
+    default: return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xFF, 0xF, 0xF, false);
+  }
+}
+
 // Sum over an aligned group of G lanes (DPP; every lane gets the total).
 template <int G>
 __device__ __forceinline__ uint32_t group_sum(uint32_t s) {
@@ -495,7 +506,8 @@ __device__ __forceinline__ uint32_t spec_sum(const PktInfo& p, const uint4 (&v)[
 // QS = quad-lane small runs (US = 4, SRD path only; 1: nontemporal loads, 2:
 // the default policy; | 4: two sets of 64 runs per iteration; | 8: only in
 // tiles whose small runs fill >= 7/8 of their quads, the others take the
-// lane runs; | 64, without the quad loop: lean load addressing): a wave takes 64
+// lane runs; | 64, without the quad loop: lean load addressing; | 128: the
+// run words exchanged within quads by DPP): a wave takes 64
 // consecutive small runs per iteration, lane l looking up run l and quad q of
 // load instruction j loading run 16 j + q, one chunk per lane; consecutive
 // runs lie back to back in memory when packets are packed, so one
@@ -689,7 +701,10 @@ __device__ __forceinline__ uint32_t hyb_scan_tile(HybLds<WG>& L, const Srd& r, c
         uint32_t roff[QN], meta[QN];
 #pragma unroll
         for (int s = 0; s < QN; ++s) {
-          const uint32_t q = qb + 64u * s + (uint32_t)lane;
+          // | 128: lane 4 q + c describes run 16 c + q, so that quad q finds
+          // instruction j's run in its own lane j (a DPP broadcast)
+          const uint32_t q = qb + 64u * s +
+                             ((QS & 128) ? 16u * ((uint32_t)lane & 3u) + ((uint32_t)lane >> 2) : (uint32_t)lane);
           roff[s] = r.oob;
           meta[s] = 0u;
           if (q < RSt) {
@@ -715,9 +730,15 @@ __device__ __forceinline__ uint32_t hyb_scan_tile(HybLds<WG>& L, const Srd& r, c
         uint32_t mj[4 * QN];
 #pragma unroll
         for (int j = 0; j < 4 * QN; ++j) {
-          const int src = (int)(16 * (j & 3) + (lane >> 2));
-          mj[j] = (uint32_t)__shfl((int)meta[j >> 2], src, 64);
-          const uint32_t o = (uint32_t)__shfl((int)roff[j >> 2], src, 64);
+          uint32_t o;
+          if constexpr ((QS & 128) != 0) {
+            mj[j] = quad_bcast(meta[j >> 2], j & 3);
+            o = quad_bcast(roff[j >> 2], j & 3);
+          } else {
+            const int src = (int)(16 * (j & 3) + (lane >> 2));
+            mj[j] = (uint32_t)__shfl((int)meta[j >> 2], src, 64);
+            o = (uint32_t)__shfl((int)roff[j >> 2], src, 64);
+          }
           v[j] = bload<QP>(r.rsrc, c < (mj[j] & 7u) ? o + 16u * c : r.oob);
         }
 #pragma unroll

@@ -881,6 +881,8 @@ static const Variant kVariants[] = {
     {"prod_xcd", launch_h<8, 16, 4, 2, kBigChunks, 0, 2, 16>},  // prod with XCD-aware tiles
     {"prod_o8", launch_h<8, 16, 4, 2, kBigChunks, 0, 2, 32>},  // prod at >= 8 waves per SIMD
     {"prod_lean", launch_h<8, 16, 4, 2, kBigChunks, 0, 2, 64>},  // lean load addressing
+    {"qs_dpp", launch_h<8, 16, 4, 2, kBigChunks, 0, 2, 129>},  // quad runs, run words by DPP
+    {"qsd_dpp", launch_h<8, 16, 4, 2, kBigChunks, 0, 2, 130>},
     {"stream_tp64", launch_stream<64>},   // one coalesced stream over each tile's span
     {"stream_tp128", launch_stream<128>},
     {"stream_tp256", launch_stream<256>},
