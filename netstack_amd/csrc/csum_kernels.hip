@@ -512,6 +512,24 @@ __device__ __forceinline__ uint32_t spec_sum(const PktInfo& p, const uint4 (&v)[
 // load instruction j loading run 16 j + q, one chunk per lane; consecutive
 // runs lie back to back in memory when packets are packed, so one
 // instruction reads ~1 KiB contiguous and the loads are nontemporal.
+// Staged small runs (QS & 256, SRD path): the 128-B lines the tile's small
+// runs read are fetched whole, nontemporal, by LDS-DMA into a line buffer of
+// SLN lines, and the lane runs sum from LDS.  Per packet, its small-run lines
+// (every line of a small packet; the head and tail line of a split one) take
+// consecutive slots, a line equal to the previous packet's last one sharing
+// its slot, so a packet's chunk ci sits at LDS chunk lb + ci (lb: its first
+// slot * 8 + line position; the tail of a split packet has its own base).
+template <int N>
+struct SlLds {
+  uint4 line[N * 8];  // N staged 128-B lines
+  uint32_t la[N];     // SRD offset of each staged line
+  uint32_t nlt;       // lines the tile stages
+};
+template <>
+struct SlLds<0> {
+  uint32_t nlt;
+};
+
 template <int WG, int TP, int GB, int UB, int US, int AUXB, bool GL, int SU, bool FX = false, int QS = 0>
 __device__ __forceinline__ uint32_t hyb_scan_tile(HybLds<WG>& L, const Srd& r, const PktInfo& p,
                                                   uint32_t big_chunks) {
@@ -519,6 +537,10 @@ __device__ __forceinline__ uint32_t hyb_scan_tile(HybLds<WG>& L, const Srd& r, c
   constexpr int NW = WG / 64;
   constexpr int NG = WG / GB;
   constexpr uint32_t RB = GB * UB;
+  constexpr bool SL = (QS & 256) != 0 && !GL && !FX;
+  constexpr int SAUX = (QS >> 10) & 31;  // tuning only: the lane runs' cache-policy bits (0 = default)
+  constexpr uint32_t SLN = (QS & 512) ? 96u : 80u;
+  __shared__ SlLds<SL ? (int)SLN : 0> S;
   const int t = threadIdx.x;
   const int lane = t & 63;
   const int wv = t >> 6;
@@ -541,10 +563,29 @@ __device__ __forceinline__ uint32_t hyb_scan_tile(HybLds<WG>& L, const Srd& r, c
   // At most 2^28 chunks per packet (len is a u32), so a tile's big-run total
   // stays below 2^32 with RB >= 16; small runs per packet are bounded by
   // big_chunks / US + 4.
-  const uint64_t nr = nch == 0 ? 0ull
-                      : split ? ((uint64_t)((ts - h + RB - 1) / RB) |
-                                 ((uint64_t)((h + US - 1) / US + (nch - ts + US - 1) / US) << 32))
-                              : ((uint64_t)((nch + US - 1) / US) << 32);
+  uint64_t nr = nch == 0 ? 0ull
+                : split ? ((uint64_t)((ts - h + RB - 1) / RB) |
+                           ((uint64_t)((h + US - 1) / US + (nch - ts + US - 1) / US) << 32))
+                        : ((uint64_t)((nch + US - 1) / US) << 32);
+  // SL: the packet's staged lines (nl, the first of them deduplicated against
+  // the previous lane's last) ride in bits 48-63 of the scan; small runs stay
+  // below 2^16 per tile (<= big_chunks / US + 4 per packet).
+  [[maybe_unused]] uint32_t sl_nl = 0u, sl_dup = 0u, sl_span = 0u;
+  if constexpr (SL) {
+    uint32_t fl = 0u, ll = 0u;
+    if (nch) {
+      const uint32_t l0 = (uint32_t)(p.g >> 7), ln = (uint32_t)((p.g + 16ull * (nch - 1u)) >> 7);
+      const bool hh = h > 0u, ht = ts < nch;
+      sl_span = ln - l0;
+      sl_nl = split ? (uint32_t)hh + (uint32_t)ht : sl_span + 1u;
+      fl = (split && !hh) ? ln : l0;
+      ll = (split && !ht) ? l0 : ln;
+    }
+    const uint32_t pnl = (uint32_t)__shfl_up((int)sl_nl, 1, 64);
+    const uint32_t pll = (uint32_t)__shfl_up((int)ll, 1, 64);
+    sl_dup = (lane > 0 && sl_nl && pnl && pll == fl) ? 1u : 0u;
+    nr |= (uint64_t)(sl_nl - sl_dup) << 48;
+  }
   uint64_t incl = nr;
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
@@ -573,14 +614,28 @@ __device__ __forceinline__ uint32_t hyb_scan_tile(HybLds<WG>& L, const Srd& r, c
     exact = exact || L.wex[w];
     if constexpr ((QS & 8) != 0) scht += L.wsch[w];
   }
+  constexpr uint32_t kRsMask = SL ? 0xFFFFu : 0xFFFFFFFFu;
   L.rb[t] = (uint32_t)excl;
-  L.rs[t] = (uint32_t)(excl >> 32);
+  L.rs[t] = (uint32_t)(excl >> 32) & kRsMask;
   if constexpr (GL) L.g[t] = p.g;
   L.info[t] = make_uint4(p.first, nch, p.ew | (split ? (kSplitBit | (h << 10)) : 0u), ts);
   L.acc[t] = 0u;
   if (t == WG - 1) {
     L.rb[P] = (uint32_t)(excl + nr);
-    L.rs[P] = (uint32_t)((excl + nr) >> 32);
+    L.rs[P] = (uint32_t)((excl + nr) >> 32) & kRsMask;
+    if constexpr (SL) S.nlt = (uint32_t)((excl + nr) >> 48);
+  }
+  if constexpr (SL) {
+    // this packet's line slots and the LDS chunk bases of its runs (in L.g,
+    // which only the 64-bit path uses otherwise)
+    const uint32_t hh = (split && h > 0u) ? 1u : 0u;
+    const uint32_t base = (uint32_t)(excl >> 48) - sl_dup;
+    const uint32_t lof = p.first - 16u * p.lp;  // SRD offset of the first line (may wrap below 0)
+    for (uint32_t j = sl_dup; j < sl_nl; ++j) {
+      const uint32_t rel = split ? ((j == 0u && hh) ? 0u : sl_span) : j;
+      if (base + j < SLN) S.la[base + j] = lof + 128u * rel;
+    }
+    L.g[t] = (uint64_t)(base * 8u + p.lp) | ((uint64_t)((base + hh) * 8u - ts) << 32);
   }
   __syncthreads();
 
@@ -595,6 +650,23 @@ __device__ __forceinline__ uint32_t hyb_scan_tile(HybLds<WG>& L, const Srd& r, c
   };
   const uint32_t RBt = L.rb[P];
   const uint32_t RSt = L.rs[P];
+  // SL: issue the staging loads before the big loop's, 8 lanes per line (one
+  // wave instruction = 8 whole lines = 1 KiB of LDS, lane-linear); a tile
+  // with more than SLN lines takes the lane runs from memory.
+  [[maybe_unused]] bool staged = false;
+  if constexpr (SL) {
+    const uint32_t nlt = S.nlt;
+    staged = nlt <= SLN;
+    if (staged) {
+      const uint32_t l8 = (uint32_t)t & 7u;
+      for (uint32_t s0 = (uint32_t)wv * 8u; s0 < nlt; s0 += (uint32_t)WG / 8u) {
+        const uint32_t s = s0 + ((uint32_t)lane >> 3);
+        const uint32_t o = s < nlt ? S.la[s] + 16u * l8 : r.oob;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(r.rsrc, (__attribute__((address_space(3))) void*)&S.line[s0 * 8u],
+                                                 16, o < r.oob ? o : r.oob, 0, 0, 2);
+      }
+    }
+  }
 
   // The loops, with the exact (T, W) or the W-only accumulator for the whole
   // tile.  Every load offset is a select (out-of-range slots read r.oob, which
@@ -642,7 +714,7 @@ __device__ __forceinline__ uint32_t hyb_scan_tile(HybLds<WG>& L, const Srd& r, c
         for (int j = 0; j < US; ++j) {
           const bool valid = sr.ci0 + (uint32_t)j < cend;
           if constexpr (GL) v[j] = valid ? gload<false>(gb + 16u * j) : make_uint4(0, 0, 0, 0);
-          else v[j] = bload(r.rsrc, valid ? base + 16u * j : r.oob);
+          else v[j] = bload<SAUX>(r.rsrc, valid ? base + 16u * j : r.oob);
         }
       }
       return sr;
@@ -763,6 +835,53 @@ __device__ __forceinline__ uint32_t hyb_scan_tile(HybLds<WG>& L, const Srd& r, c
     }
   lane_runs:
     static_assert(SU == 1 || SU == 2, "the small loop issues one or two runs per iteration");
+    if constexpr (SL) {
+      if (staged) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's staging loads have landed
+        __syncthreads();                                   // ... and every other wave's
+        auto sl_issue = [&](uint32_t q, uint4 (&v)[US]) -> SRun {
+          SRun sr{0, 0u, 0u, 0u, q < RSt};
+          uint32_t cend = 0u, lb = 0u;
+          if (sr.act) {
+            sr.pk = search(L.rs, q);
+            const uint32_t k = q - L.rs[sr.pk];
+            const uint4 inf = L.info[sr.pk];
+            const uint64_t lbs = L.g[sr.pk];
+            sr.ci0 = k * US;
+            sr.lastc = inf.y - 1u;
+            sr.ew = inf.z;
+            cend = inf.y;
+            lb = (uint32_t)lbs;
+            if (inf.z & kSplitBit) {
+              const uint32_t hh = (inf.z >> 10) & 15u, nh = (hh + US - 1) / US;
+              if (k < nh) {
+                cend = hh;
+              } else {
+                sr.ci0 = inf.w + (k - nh) * US;
+                lb = (uint32_t)(lbs >> 32);
+              }
+            }
+          }
+#pragma unroll
+          for (int j = 0; j < US; ++j)
+            v[j] = sr.ci0 + (uint32_t)j < cend ? S.line[lb + sr.ci0 + (uint32_t)j] : make_uint4(0, 0, 0, 0);
+          return sr;
+        };
+        for (uint32_t q = (uint32_t)t; q < RSt; q += SU * WG) {
+          uint4 va[US];
+          const SRun ra = sl_issue(q, va);
+          if constexpr (SU == 2) {
+            uint4 vb[US];
+            const SRun rb = sl_issue(q + WG, vb);
+            small_sum(ra, va);
+            small_sum(rb, vb);
+          } else {
+            small_sum(ra, va);
+          }
+        }
+        return;
+      }
+    }
     for (uint32_t q = (uint32_t)t; q < RSt; q += SU * WG) {
       uint4 va[US];
       const SRun ra = small_issue(q, va);
@@ -918,7 +1037,7 @@ __device__ __forceinline__ void zc_complete(uint32_t* __restrict__ ctr, uint32_t
 template <int WG, int TP, int GB, int UB, int US, int AUXB, int UD = 0, bool WIN = false,
           int SU = 1, int QS = 0, bool CH = false>
 // QS & 32 (tuning only): at least 8 waves per SIMD (<= 64 VGPRs).
-__global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu((QS & 32) ? 8 : 1))) void csum_hyb(
+__global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu((QS & 32) ? 8 : (QS & 256) ? 7 : 1))) void csum_hyb(
     const uint8_t* __restrict__ arena, uint64_t arena_bytes,
     const uint4* __restrict__ desc, uint32_t n, uint16_t* __restrict__ out,
     uint32_t* __restrict__ partial, unsigned long long* __restrict__ err, uint32_t big_chunks,

@@ -27,14 +27,16 @@ from netstack_amd import workloads as W  # noqa: E402
 TUNE = os.path.join(ROOT, "netstack_amd", "lib", "libns_tune.so")
 
 
-def load():
-    L = ctypes.CDLL(TUNE)
+def load(path=TUNE):
+    L = ctypes.CDLL(path)
     L.nsk_tune_count.restype = ctypes.c_int
     L.nsk_tune_name.restype = ctypes.c_char_p
     L.nsk_tune_name.argtypes = [ctypes.c_int]
     L.nsk_tune_launch.restype = ctypes.c_int
     L.nsk_tune_launch.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
                                   ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    if not hasattr(L, "nsk_calib_launch"):  # the small A/B library (tune_ab.hip)
+        return L
     L.nsk_calib_launch.restype = ctypes.c_int
     L.nsk_calib_launch.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
                                    ctypes.c_uint32, ctypes.c_void_p]
@@ -75,6 +77,7 @@ def main():
     ap.add_argument("--calib-modes", default="2,4,5,6")
     ap.add_argument("--calib-blocks", default="4096,8192,16384")
     ap.add_argument("--json", default="")
+    ap.add_argument("--lib", default=TUNE, help="tuning library (e.g. netstack_amd/lib/libns_tune_ab.so)")
     ap.add_argument("--b2b", action="store_true", help="time back-to-back launches (as bench.py does)")
     ap.add_argument("--rot", type=int, default=0, help="distinct arenas cycled (0: 4 for cfg3, else 1)")
     ap.add_argument("--rot-desc", action="store_true",
@@ -82,7 +85,7 @@ def main():
     ap.add_argument("--n", default="", help="packet counts per config, e.g. 2:2097152")
     args = ap.parse_args()
 
-    L = load()
+    L = load(args.lib)
     B2B["on"] = args.b2b
     names = [L.nsk_tune_name(v).decode() for v in range(L.nsk_tune_count())]
     sel = list(range(len(names))) if args.variants == "all" else \
