@@ -555,8 +555,10 @@ def main():
         ps["ranks_failed"] = int(failed)
         ps["bit_exact"] = ps["bit_exact"] and failed == 0
         result["parity_sample"] = ps
-    if dist.rank == 0 and not args.no_cpu:
-        # The CPU leg (rank 0): the oracle timed as the scalar baseline.
+    if dist.rank == 0 and dist.world > 1:
+        result["cpu_baseline_note"] = "timed at N=1 only (bench.py --gpus 1), not beside a multi-GPU run"
+    elif dist.rank == 0 and not args.no_cpu:
+        # The CPU leg (rank 0 at N=1): the oracle timed as the scalar baseline.
         cb, _ = cpu_baseline(batch, args.cpu_seconds, 1)
         result["cpu_baseline"] = cb
         cpus = usable_cpus()
