@@ -392,6 +392,42 @@ def test_on_side_stream(engine):
     assert np.array_equal(got, want)
 
 
+@pytest.mark.parametrize("chained", [False, True])
+def test_pipelined_batches_over_two_streams(engine, chained):
+    """INTEGRATION.md §4's stream of batches (bench.py `pipelined`): distinct
+    batches launched back to back round-robin over two streams, each stream
+    with its own results, the next batch's ramp overlapping the previous
+    one's tail; every batch's results against the oracle.  Chained batches
+    also run their fold pass on their stream's own scratch."""
+    torch = _torch()
+    import oracle as O
+    from netstack_amd import workloads as W
+
+    rng = np.random.default_rng(31)
+    batches = []
+    for k in range(6):
+        ln = W.zipf_lengths(40 + k, 3000 + 500 * k)
+        d, end = W.make_desc(ln, rng.integers(0, 65536, len(ln)).astype(np.uint16), 16 if k % 2 else 1)
+        if chained:
+            d["flags"] = rng.integers(0, 4, len(d)).astype(np.uint16)
+        arena = W.random_bytes(900 + k, end + 32)
+        batches.append((arena, d, O.c_batch(arena, d, chained)[0]))
+    ss = [torch.cuda.current_stream(), torch.cuda.Stream()]
+    dev = [(torch.from_numpy(a).cuda(), torch.from_numpy(d.view(np.uint8).copy()).cuda()) for a, d, _ in batches]
+    outs = [torch.empty(len(d), dtype=torch.int16, device="cuda") for _, d, _ in batches]
+    torch.cuda.synchronize()
+    for rnd in range(3):
+        for o in outs:
+            o.fill_(0x5A5A)
+        torch.cuda.synchronize()
+        for k, (a, d) in enumerate(dev):
+            engine.batch_tensors(a, d, outs[k], chained=chained, stream=ss[k % 2])
+        torch.cuda.synchronize()
+        for k, (_, _, want) in enumerate(batches):
+            assert np.array_equal(outs[k].cpu().numpy().view(np.uint16), want), (rnd, k)
+    engine.stream_release(ss[1])
+
+
 def test_fuzz_small(engine):
     import oracle as O
 
