@@ -290,6 +290,8 @@ typedef struct ns_pkt_buf {
  * ICMPv6Checksum — and into the IPv4 header checksum (addIPHeader,
  * ipv4.go:236).  An IPv4 fragment (MF set or a fragment offset) gets only
  * its IP header checksum, as writePacketFragments writes it (ipv4.go:159-160).
+ * NS_EINVAL for a Header or a clipped Data view of 4 GiB or more (one
+ * descriptor's length is a u32, as for every view-taking entry point).
  * NS_EINVAL if a field to write lies outside Header (for IPv4, the whole IP
  * header must lie in Header).
  * sums (2n, or NULL): [2i] the IPv4 header sum (0 for IPv6), [2i+1] the

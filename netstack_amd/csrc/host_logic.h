@@ -181,6 +181,8 @@ struct PacketBytes {
   int init(const ns_pkt_buf& pk) {
     if (pk.hdr_len && !pk.hdr) return NS_EINVAL;
     if (pk.ndata && !pk.data) return NS_EINVAL;
+    // A piece is one descriptor (u32 length), as in every other entry point.
+    if (pk.hdr_len > 0xFFFFFFFFull) return NS_EINVAL;
     hdr_len = pk.hdr_len;
     seg.reserve((size_t)pk.ndata + 1);
     at.reserve((size_t)pk.ndata + 1);
@@ -189,6 +191,7 @@ struct PacketBytes {
     for (uint32_t k = 0; k < pk.ndata && left; ++k) {
       const uint64_t l = std::min<uint64_t>(pk.data[k].len, left);
       if (l && !pk.data[k].data) return NS_EINVAL;
+      if (l > 0xFFFFFFFFull) return NS_EINVAL;
       add(pk.data[k].data, l);
       left -= l;
     }

@@ -300,6 +300,26 @@ static void TestPackets(Rng& rng, int rounds) {
     }
   }
   CHECK(valid_tcp > 0 || rounds < 50, "no filled TCP packet was checked");
+  // A Header or Data view of 4 GiB or more is NS_EINVAL (a descriptor's length
+  // is a u32); init reads no bytes, so no such buffer is needed.
+  {
+    uint8_t b[64] = {0x45};
+    ns_view big{b, 1ull << 32};
+    ns_pkt_buf pk{};
+    pk.data = &big;
+    pk.ndata = 1;
+    pk.data_size = 1ull << 32;
+    nsh::PacketBytes pb;
+    CHECK(pb.init(pk) == NS_EINVAL, "a 4 GiB data view");
+    pk.data_size = 64;
+    nsh::PacketBytes pc;
+    CHECK(pc.init(pk) == NS_OK, "the same view clipped to 64 bytes");
+    ns_pkt_buf ph{};
+    ph.hdr = b;
+    ph.hdr_len = 1ull << 32;
+    nsh::PacketBytes pd;
+    CHECK(pd.init(ph) == NS_EINVAL, "a 4 GiB header");
+  }
 }
 
 static void TestCutChunk(Rng& rng, int rounds) {
