@@ -878,7 +878,6 @@ struct Variant {
 static const Variant kVariants[] = {
     {"prod", launch_h<8, 16, 4, 2, kBigChunks, 0, 2>},  // the production big-packet launch
     {"sl80", launch_h<8, 16, 4, 2, kBigChunks, 0, 2, 256>},  // small runs from LDS-staged lines (80)
-    {"sl96", launch_h<8, 16, 4, 2, kBigChunks, 0, 2, 768>},  // ... 96 lines
     {"qs_b40", launch_h<8, 16, 4, 2, kBigChunks, 0, 2, 1>},   // quad-lane nt small runs
     {"prod_xcd", launch_h<8, 16, 4, 2, kBigChunks, 0, 2, 16>},  // prod with XCD-aware tiles
     {"prod_o8", launch_h<8, 16, 4, 2, kBigChunks, 0, 2, 32>},  // prod at >= 8 waves per SIMD
