@@ -56,9 +56,10 @@
 extern "C" {
 #endif
 
-#define NS_CSUM_ABI_VERSION 4  /* 2: ns_csum_batch_dev_store, NS_DESC_STORE*;
+#define NS_CSUM_ABI_VERSION 5  /* 2: ns_csum_batch_dev_store, NS_DESC_STORE*;
                                   3: ns_csum_stage_*, ns_csum_packet_buffers;
-                                  4: ns_csum_stream_release, _scratch_count */
+                                  4: ns_csum_stream_release, _scratch_count;
+                                  5: ns_csum_get_stats */
 
 /* ---- status codes ------------------------------------------------------- */
 #define NS_OK 0
@@ -326,6 +327,32 @@ int ns_csum_batch_multi(ns_csum_ctx* const* ctxs, uint32_t nctx,
  * first descriptor of part p; first[parts] = n.  Pure host arithmetic.      */
 int ns_csum_shard_plan(const ns_pkt_desc* h_desc, uint32_t n, uint32_t parts,
                        uint32_t* first);
+
+/* ---- diagnostics ----------------------------------------------------------
+ * Where a context's host time went, so a slow synchronous call can be placed
+ * on one path (no reference counterpart: instrumentation of this boundary).
+ * Times are host wall-clock nanoseconds.  ns_csum_get_stats copies the
+ * counters; with reset != 0 it also zeroes them.                            */
+typedef struct ns_csum_stats {
+  uint64_t calls;            /* synchronous calls returned (ns_csum_checksum,
+                                _vv_*, _views_restart, _pseudo_header, _chains,
+                                _packet_buffers, _batch_host)                  */
+  uint64_t call_ns_max;      /* the longest of them, entry to return          */
+  uint64_t lock_ns_max;      /* longest wait for the context lock by a pass   */
+  uint64_t zc_passes;        /* zero-copy passes run                          */
+  uint64_t zc_late;          /* ...whose completion word was not in after
+                                2 ms (the caller then waited on the stream)   */
+  uint64_t zc_pass_ns_max;   /* longest pass, launch to results               */
+  uint64_t growths;          /* stream-ordered scratch growths (batch_dev)    */
+  uint64_t growth_ns_total;  /* host time in hipFreeAsync/hipMallocAsync/
+                                hipMemsetAsync for them                       */
+  uint64_t growth_ns_max;
+  uint64_t retires;          /* scratch entries retired (LRU bound, release)  */
+  uint64_t retire_ns_max;    /* longest retire, incl. creating its stream     */
+  uint64_t stage_allocs;     /* staging buffers allocated (pool was empty)    */
+  uint64_t stage_alloc_ns_max;
+} ns_csum_stats;
+int ns_csum_get_stats(ns_csum_ctx* ctx, ns_csum_stats* out, int reset);
 
 #ifdef __cplusplus
 }

@@ -17,7 +17,7 @@ CSRC = os.path.join(_HERE, "csrc")
 
 # The NS_CSUM_ABI_VERSION this binding is written against; lib() refuses a
 # library that reports another (a stale build).
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 NS_OK = 0
 NS_EINVAL = -1
@@ -41,7 +41,7 @@ EXPORTED = (
     "ns_csum_vv_batch", "ns_csum_views_restart", "ns_csum_pseudo_header",
     "ns_csum_combine", "ns_csum_shard_plan", "ns_csum_batch_multi", "ns_csum_chains",
     "ns_csum_stage_acquire", "ns_csum_stage_release", "ns_csum_packet_buffers",
-    "ns_csum_stream_release", "ns_csum_scratch_count",
+    "ns_csum_stream_release", "ns_csum_scratch_count", "ns_csum_get_stats",
 )
 NS_PIECE_RESTART = 0x1
 NS_PIECE_END = 0x2
@@ -94,13 +94,21 @@ class NsPktBuf(ctypes.Structure):
                 ("ndata", ctypes.c_uint32), ("flags", ctypes.c_uint32), ("data_size", ctypes.c_uint64)]
 
 
+class NsStats(ctypes.Structure):
+    """ns_csum_stats: where a context's host time went (diagnostics)."""
+    _fields_ = [(f, ctypes.c_uint64) for f in (
+        "calls", "call_ns_max", "lock_ns_max", "zc_passes", "zc_late", "zc_pass_ns_max",
+        "growths", "growth_ns_total", "growth_ns_max", "retires", "retire_ns_max",
+        "stage_allocs", "stage_alloc_ns_max")]
+
+
 class NsOpts(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int32), ("flags", ctypes.c_uint32),
                 ("staging_bytes", ctypes.c_uint64)]
 
 
 assert ctypes.sizeof(NsPktDesc) == 16 and ctypes.sizeof(NsSeg) == 24 and ctypes.sizeof(NsPiece) == 24
-assert ctypes.sizeof(NsPktBuf) == 40
+assert ctypes.sizeof(NsPktBuf) == 40 and ctypes.sizeof(NsStats) == 13 * 8
 
 _lock = threading.Lock()
 _lib = None
@@ -140,6 +148,7 @@ def _declare(lib):
                                              c.POINTER(c.c_uint8)]),
         "ns_csum_stream_release": (c.c_int, [vp, vp]),
         "ns_csum_scratch_count": (c.c_int, [vp, c.POINTER(c.c_uint32)]),
+        "ns_csum_get_stats": (c.c_int, [vp, c.POINTER(NsStats), c.c_int]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

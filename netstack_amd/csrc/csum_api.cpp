@@ -259,6 +259,25 @@ constexpr uint64_t kPassTableBytes = 1ull << 20;
 // absolute device addresses (the kernel's per-tile windows take it from there).
 constexpr uint64_t kWholeSpace = 1ull << 60;
 
+// Diagnostic counters of one context (ns_csum_get_stats), updated lock-free.
+struct StatCounters {
+  std::atomic<uint64_t> calls{0}, call_ns_max{0}, lock_ns_max{0}, zc_passes{0}, zc_late{0}, zc_pass_ns_max{0},
+      growths{0}, growth_ns_total{0}, growth_ns_max{0}, retires{0}, retire_ns_max{0}, stage_allocs{0},
+      stage_alloc_ns_max{0};
+};
+
+uint64_t now_ns() {
+  return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+             std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
+void bump_max(std::atomic<uint64_t>& m, uint64_t v) {
+  uint64_t c = m.load(std::memory_order_relaxed);
+  while (v > c && !m.compare_exchange_weak(c, v, std::memory_order_relaxed)) {
+  }
+}
+
 }  // namespace
 
 struct ns_csum_ctx {
@@ -306,6 +325,7 @@ struct ns_csum_ctx {
   // gather staging for the VectorisedView entry points
   PinBuf<uint8_t> g_arena;
   std::vector<ns_pkt_desc> g_desc;
+  StatCounters st;
 };
 
 namespace {
@@ -315,6 +335,7 @@ namespace {
 // so neither the host nor the device waits, and the entry's own stream may
 // already be destroyed.
 void retire_scratch(ns_csum_ctx* ctx, StreamScratch* sc) {
+  const uint64_t t0 = now_ns();
   std::lock_guard<std::mutex> lk(ctx->rmu);
   if (!ctx->retire && hipStreamCreateWithFlags(&ctx->retire, hipStreamNonBlocking) != hipSuccess) ctx->retire = nullptr;
   if (ctx->retire && hipStreamWaitEvent(ctx->retire, sc->last, 0) == hipSuccess) {
@@ -328,7 +349,34 @@ void retire_scratch(ns_csum_ctx* ctx, StreamScratch* sc) {
   }
   (void)hipEventDestroy(sc->last);
   delete sc;
+  ctx->st.retires.fetch_add(1, std::memory_order_relaxed);
+  bump_max(ctx->st.retire_ns_max, now_ns() - t0);
 }
+
+// Times one synchronous entry point, entry to return (ns_csum_stats.calls,
+// call_ns_max).
+struct CallClock {
+  ns_csum_ctx* ctx;
+  uint64_t t0;
+  explicit CallClock(ns_csum_ctx* c) : ctx(c), t0(now_ns()) {}
+  ~CallClock() {
+    ctx->st.calls.fetch_add(1, std::memory_order_relaxed);
+    bump_max(ctx->st.call_ns_max, now_ns() - t0);
+  }
+  CallClock(const CallClock&) = delete;
+  CallClock& operator=(const CallClock&) = delete;
+};
+
+// Times a staging allocation (a pool was empty).
+struct AllocClock {
+  ns_csum_ctx* ctx;
+  uint64_t t0;
+  explicit AllocClock(ns_csum_ctx* c) : ctx(c), t0(now_ns()) {}
+  ~AllocClock() {
+    ctx->st.stage_allocs.fetch_add(1, std::memory_order_relaxed);
+    bump_max(ctx->st.stage_alloc_ns_max, now_ns() - t0);
+  }
+};
 
 StreamScratch* make_scratch() {
   StreamScratch* sc = new (std::nothrow) StreamScratch();
@@ -453,9 +501,12 @@ int run_zero_copy(ns_csum_ctx* ctx, SmallReq* const* reqs, size_t nreq) {
                             chained ? ctx->d_chain[0].get() : nsk::ChainScratch{}, ctx->d_err, s,
                             std::max<uint64_t>(nb, 1), 0, nullptr, zc));
   if (!self) HIP_TRY(nsk::launch_signal(done_dev, seq, s));
+  ctx->st.zc_passes.fetch_add(1, std::memory_order_relaxed);
+  const uint64_t pass_t0 = now_ns();
   const auto t0 = std::chrono::steady_clock::now();
   for (uint32_t spin = 0; __atomic_load_n(done, __ATOMIC_ACQUIRE) != seq; ++spin) {
     if ((spin & 255u) == 255u && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) {
+      ctx->st.zc_late.fetch_add(1, std::memory_order_relaxed);
       HIP_TRY(hipStreamSynchronize(s));
       if (__atomic_load_n(done, __ATOMIC_ACQUIRE) != seq) {
         // The pass ended without its last workgroup's word: its counter may
@@ -471,6 +522,7 @@ int run_zero_copy(ns_csum_ctx* ctx, SmallReq* const* reqs, size_t nreq) {
       break;
     }
   }
+  bump_max(ctx->st.zc_pass_ns_max, now_ns() - pass_t0);
   const uint16_t* res = reinterpret_cast<const uint16_t*>(ctx->z_res.p);
   for (size_t r = 0; r < nreq; ++r) {
     std::memcpy(reqs[r]->res, res, (size_t)reqs[r]->ndesc * 2);
@@ -490,6 +542,7 @@ MappedPin* lease_stage(ns_csum_ctx* ctx, int* rc) {
       return b;
     }
   }
+  AllocClock clk(ctx);
   MappedPin* b = new (std::nothrow) MappedPin();
   if (!b) {
     *rc = NS_ENOMEM;
@@ -518,6 +571,7 @@ BarBuf* lease_gather_stage(ns_csum_ctx* ctx, int* rc) {
       return b;
     }
   }
+  AllocClock clk(ctx);
   BarBuf* b = new (std::nothrow) BarBuf();
   if (!b) {
     *rc = NS_ENOMEM;
@@ -552,7 +606,9 @@ int submit_small(ns_csum_ctx* ctx, SmallReq* req) {
   // drain its write-combined stores before another thread launches the pass.
   __builtin_ia32_sfence();
   return ctx->combiner.submit(req, [ctx](SmallReq* const* reqs, size_t nreq) {
+    const uint64_t t0 = now_ns();
     std::lock_guard<std::mutex> lk(ctx->mu);
+    bump_max(ctx->st.lock_ns_max, now_ns() - t0);
     DeviceGuard g(ctx->device);
     return run_zero_copy(ctx, reqs, nreq);
   });
@@ -695,6 +751,7 @@ MappedPin* lease_big(ns_csum_ctx* ctx, uint64_t bytes, int* rc) {
       }
     }
   }
+  AllocClock clk(ctx);
   MappedPin* b = new (std::nothrow) MappedPin();
   if (!b) {
     *rc = NS_ENOMEM;
@@ -904,9 +961,24 @@ int ns_csum_init(const ns_csum_opts* opts, ns_csum_ctx** out) {
   ctx->device = dev;
   if (opts && opts->staging_bytes) ctx->staging = opts->staging_bytes;
   DeviceGuard g(dev);
+  // The context's own streams serve synchronous callers only (zero-copy
+  // passes, the DMA pipeline, ns_csum_sync), so they take the device's
+  // greatest priority.  HIP pools hardware queues per priority
+  // (GPU_MAX_HW_QUEUES=4 each): at normal priority a pass could share a
+  // queue with a caller's stream and wait behind its whole backlog (round 3's
+  // 21-43 ms stalls, every one a pass whose completion was late; DESIGN.md
+  // §4.4).  NS_CSUM_NORMAL_PRIORITY=1 creates them at normal priority (A/B
+  // diagnostics only).
+  int least = 0, greatest = 0;
+  if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) {
+    least = greatest = 0;
+    (void)hipGetLastError();
+  }
+  (void)least;
+  if (std::getenv("NS_CSUM_NORMAL_PRIORITY")) greatest = 0;
   hipError_t e = hipSuccess;
   for (int s = 0; s < 2 && e == hipSuccess; ++s) {
-    e = hipStreamCreateWithFlags(&ctx->stream[s], hipStreamNonBlocking);
+    e = hipStreamCreateWithPriority(&ctx->stream[s], hipStreamNonBlocking, greatest);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->done[s], hipEventDisableTiming);
   }
   if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&ctx->d_err), sizeof(unsigned long long));
@@ -1021,10 +1093,18 @@ int batch_dev(ns_csum_ctx* ctx, const uint8_t* d_arena, uint64_t arena_bytes, co
     std::lock_guard<std::mutex> lk(sc->mu);
     nsk::ChainScratch chain{};
     uint32_t* split = nullptr;
+    const size_t caps = sc->chain.part.cap + sc->chain.status.cap + sc->split.cap;
+    const uint64_t t0 = now_ns();
     if (need_chain && (rc = sc->chain.ensure_async(n, s)) == NS_OK) chain = sc->chain.get();
     // split accumulators: zero once, the kernel leaves them so
     if (rc == NS_OK && need_split && (rc = sc->split.ensure_async(nsk::split_words(n), true, s)) == NS_OK)
       split = sc->split.p;
+    if (sc->chain.part.cap + sc->chain.status.cap + sc->split.cap != caps) {
+      const uint64_t dt = now_ns() - t0;
+      ctx->st.growths.fetch_add(1, std::memory_order_relaxed);
+      ctx->st.growth_ns_total.fetch_add(dt, std::memory_order_relaxed);
+      bump_max(ctx->st.growth_ns_max, dt);
+    }
     if (rc == NS_OK) {
       hipError_t e = nsk::launch_batch(d_arena, arena_bytes, d_desc, n, d_out, chain, ctx->d_err, s, 0,
                                        store ? 1u : 0u, split);
@@ -1066,6 +1146,7 @@ int ns_csum_batch_host(ns_csum_ctx* ctx, const uint8_t* h_arena, uint64_t arena_
                        const ns_pkt_desc* h_desc, uint32_t n, uint16_t* h_out,
                        uint32_t batch_flags) {
   if (!ctx || (n && (!h_desc || !h_out)) || (arena_bytes && !h_arena)) return NS_EINVAL;
+  CallClock clk(ctx);
   if (n == 0) return NS_OK;
   // The zero-copy pass needs the table's byte span first; an arena larger
   // than one staging buffer goes straight to the DMA pipeline, which checks
@@ -1103,6 +1184,7 @@ int ns_csum_batch_host(ns_csum_ctx* ctx, const uint8_t* h_arena, uint64_t arena_
 int ns_csum_checksum(ns_csum_ctx* ctx, const uint8_t* buf, uint64_t len, uint16_t initial,
                      uint16_t* out) {
   if (!ctx || !out || (len && !buf) || len > 0xFFFFFFFFull) return NS_EINVAL;
+  CallClock clk(ctx);
   SpanProbe pr;
   pr.add(buf, len);
   Gather gt(ctx, pr.stage(ctx));
@@ -1114,6 +1196,7 @@ int ns_csum_checksum(ns_csum_ctx* ctx, const uint8_t* buf, uint64_t len, uint16_
 int ns_csum_vv_with_offset(ns_csum_ctx* ctx, const ns_view* views, uint32_t nviews,
                            uint16_t initial, int64_t off, int64_t size, uint16_t* out) {
   if (!ctx || !out || (nviews && !views)) return NS_EINVAL;
+  CallClock clk(ctx);
   std::vector<std::pair<const uint8_t*, uint64_t>> pieces;
   int rc = clip_views(views, nviews, off, size, &pieces);
   if (rc != NS_OK) return rc;
@@ -1127,6 +1210,7 @@ int ns_csum_vv_with_offset(ns_csum_ctx* ctx, const ns_view* views, uint32_t nvie
 int ns_csum_vv_batch(ns_csum_ctx* ctx, const ns_view* views, uint32_t nviews,
                      const ns_seg* segs, uint32_t nsegs, uint16_t* out) {
   if (!ctx || (nsegs && (!segs || !out)) || (nviews && !views)) return NS_EINVAL;
+  CallClock clk(ctx);
   if (nsegs == 0) return NS_OK;
   // Every segment's clipped views as one flat list of chain pieces (a
   // segment's first piece restarts, the others continue it), so a
@@ -1154,6 +1238,7 @@ int ns_csum_vv_batch(ns_csum_ctx* ctx, const ns_view* views, uint32_t nviews,
 int ns_csum_views_restart(ns_csum_ctx* ctx, const ns_view* views, uint32_t nviews,
                           uint16_t initial, uint16_t* out) {
   if (!ctx || !out || (nviews && !views)) return NS_EINVAL;
+  CallClock clk(ctx);
   std::vector<std::pair<const uint8_t*, uint64_t>> pieces;
   SpanProbe pr;
   for (uint32_t k = 0; k < nviews; ++k) {
@@ -1170,6 +1255,7 @@ int ns_csum_views_restart(ns_csum_ctx* ctx, const ns_view* views, uint32_t nview
 int ns_csum_chains(ns_csum_ctx* ctx, const ns_piece* pieces, uint32_t npieces, uint16_t* out,
                    uint32_t nout) {
   if (!ctx || (npieces && !pieces)) return NS_EINVAL;
+  CallClock clk(ctx);
   uint32_t chains = 0;
   SpanProbe pr;
   for (uint32_t k = 0; k < npieces; ++k) {
@@ -1200,6 +1286,7 @@ int ns_csum_pseudo_header(ns_csum_ctx* ctx, uint32_t protocol, const uint8_t* sr
                           uint32_t src_len, const uint8_t* dst, uint32_t dst_len,
                           uint16_t total_len, uint16_t* out) {
   if (!ctx || !out || (src_len && !src) || (dst_len && !dst)) return NS_EINVAL;
+  CallClock clk(ctx);
   // checksum.go:112-122: four chained Checksum calls, each restarting alignment.
   const uint8_t lenbe[2] = {(uint8_t)(total_len >> 8), (uint8_t)total_len};
   const uint8_t proto[2] = {0, (uint8_t)protocol};
@@ -1241,6 +1328,7 @@ int ns_csum_stage_release(ns_csum_ctx* ctx, uint8_t* base) {
 int ns_csum_packet_buffers(ns_csum_ctx* ctx, const ns_pkt_buf* pkts, uint32_t n, uint32_t op,
                            uint16_t* sums, uint8_t* verdict) {
   if (!ctx || (n && !pkts) || (op != NS_PKB_VERIFY && op != NS_PKB_FILL)) return NS_EINVAL;
+  CallClock clk(ctx);
   if (n == 0) return NS_OK;
   std::vector<nsh::PacketBytes> pb(n);
   SpanProbe pr;
@@ -1296,6 +1384,19 @@ int ns_csum_batch_multi(ns_csum_ctx* const* ctxs, uint32_t nctx, const uint8_t* 
   for (auto& t : th) t.join();
   for (uint32_t c = 0; c < nctx; ++c)
     if (status[c] != NS_OK) return status[c];
+  return NS_OK;
+}
+
+int ns_csum_get_stats(ns_csum_ctx* ctx, ns_csum_stats* out, int reset) {
+  if (!ctx || !out) return NS_EINVAL;
+  StatCounters& c = ctx->st;
+  std::atomic<uint64_t>* src[] = {&c.calls,          &c.call_ns_max,   &c.lock_ns_max,    &c.zc_passes, &c.zc_late,
+                                  &c.zc_pass_ns_max, &c.growths,       &c.growth_ns_total, &c.growth_ns_max,
+                                  &c.retires,        &c.retire_ns_max, &c.stage_allocs,   &c.stage_alloc_ns_max};
+  static_assert(sizeof(ns_csum_stats) == sizeof(src) / sizeof(src[0]) * sizeof(uint64_t), "ns_csum_stats fields");
+  uint64_t* dst = reinterpret_cast<uint64_t*>(out);
+  for (size_t i = 0; i < sizeof(src) / sizeof(src[0]); ++i)
+    dst[i] = reset ? src[i]->exchange(0, std::memory_order_relaxed) : src[i]->load(std::memory_order_relaxed);
   return NS_OK;
 }
 

@@ -125,6 +125,13 @@ class Engine:
         check(lib().ns_csum_scratch_count(self._h, ctypes.byref(c)), "ns_csum_scratch_count")
         return int(c.value)
 
+    def stats(self, reset: bool = False) -> dict:
+        """The context's diagnostic counters (ns_csum_get_stats) as a dict;
+        reset=True zeroes them after reading."""
+        st = _lib.NsStats()
+        check(lib().ns_csum_get_stats(self._h, ctypes.byref(st), 1 if reset else 0), "ns_csum_get_stats")
+        return {name: int(getattr(st, name)) for name, _ in st._fields_}
+
     def sync(self, stream: int | None = None) -> int:
         """Wait for `stream`; return the number of out-of-range descriptors."""
         bad = ctypes.c_uint64(0)

@@ -14,6 +14,13 @@ for p in (ROOT, os.path.join(ROOT, "oracle"), GOLDEN):
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs through the HIP engine)")
     config.addinivalue_line("markers", "slow: full BASELINE.json sizes")
+    config.addinivalue_line("markers", "latency: wall-clock bounds on a shared GPU (collected after every other test)")
+
+
+def pytest_collection_modifyitems(session, config, items):
+    """Wall-clock latency bounds run last: a timing outlier on a loaded GPU
+    must not stop (-x) the run before the parity tests have reported."""
+    items.sort(key=lambda it: it.get_closest_marker("latency") is not None)  # stable
 
 
 @pytest.fixture(scope="session")

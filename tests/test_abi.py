@@ -43,7 +43,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_strerror():
     L = _lib.lib()
-    assert L.ns_csum_abi_version() == _lib.ABI_VERSION == 4
+    assert L.ns_csum_abi_version() == _lib.ABI_VERSION == 5
     for code in (0, -1, -2, -3, -4, -5):
         assert L.ns_csum_strerror(code)
 
@@ -302,3 +302,19 @@ def test_go_patch_applies_to_the_reference_and_adds_no_colliding_names(tmp_path)
         d = {"tcp": "tcpip/transport/tcp", "fdbased": "tcpip/link/fdbased"}[pkg]
         mine = _top_level(_go_code(open(os.path.join(ROOT, rel)).read()))
         assert mine and not (mine & _ref_names(os.path.join("/root/reference", d))), (rel, mine)
+
+
+def test_latency_bounds_are_collected_after_every_parity_test():
+    """A wall-clock bound (@pytest.mark.latency) is collected after every
+    other GPU test, so under -x a timing outlier cannot hide parity results."""
+    import subprocess
+    import sys
+
+    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "--collect-only", "-m", "gpu", "-p", "no:cacheprovider",
+                        os.path.join(ROOT, "tests")], capture_output=True, text=True, cwd=ROOT, timeout=300)
+    ids = [l for l in r.stdout.splitlines() if "::" in l]
+    assert len(ids) > 100, r.stdout[-2000:]
+    lat = [i for i, l in enumerate(ids) if "test_growing_scratch_does_not_hold_up_synchronous_calls" in l]
+    assert lat and lat[0] == len(ids) - len(lat), ids[-5:]
+    par = [i for i, l in enumerate(ids) if "test_gpu_tcp.py" in l or "test_gpu_sync.py" in l]
+    assert par and max(par) < lat[0]

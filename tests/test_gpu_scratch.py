@@ -54,14 +54,41 @@ def test_many_streams_bounded_scratch_and_release(engine):
     assert engine.scratch_count() <= max(n_kept, base)
 
 
+def _gc_clock():
+    """Records every garbage-collector pause of this process as (start, end,
+    generation) in perf_counter seconds; call the returned stop() to detach."""
+    import gc
+
+    pauses, t0 = [], {}
+
+    def cb(phase, info):
+        if phase == "start":
+            t0["t"] = time.perf_counter()
+        elif "t" in t0:
+            pauses.append((t0.pop("t"), time.perf_counter(), info.get("generation")))
+
+    gc.callbacks.append(cb)
+    return pauses, lambda: gc.callbacks.remove(cb)
+
+
+@pytest.mark.latency
 def test_growing_scratch_does_not_hold_up_synchronous_calls(engine):
-    """Thread A queues ~50 ms of device-resident work on its stream, then a
+    """Thread A queues ~50 ms of device-resident work on its streams, then a
     chained batch twice as large as any before on the same stream (its
     scratch grows), repeatedly; thread B meanwhile makes synchronous
     Checksum calls on the same context.  Every result is checked; B's calls
     must not wait for A's queued work (round 2 freed the old scratch with
     hipFree, a device-wide wait, under the context lock that B's calls
-    take)."""
+    take); nor may they queue behind it on a shared hardware queue (round 3:
+    the context's streams were normal priority; they are now the device's
+    highest).
+
+    Each call is timed twice: by the library itself (ns_csum_get_stats:
+    entry to return, plus the zero-copy passes that fell back to waiting on
+    the stream, the scratch growths and retires) and from Python around the
+    ctypes call.  A Python-side stall that the library did not see is the
+    interpreter's: the GC pauses are recorded and every such stall must lie
+    inside one (round 3's two 21-31 ms outliers)."""
     import torch
 
     import oracle as O
@@ -75,6 +102,10 @@ def test_growing_scratch_does_not_hold_up_synchronous_calls(engine):
     big_desc = torch.from_numpy(bd.view(np.uint8).copy()).cuda()
     big_out = torch.empty(n_big, dtype=torch.int16, device="cuda")
     sA = torch.cuda.Stream()
+    # A's backlog goes over 8 normal-priority streams (sA and 7 more), so
+    # with GPU_MAX_HW_QUEUES=4 every normal-priority hardware queue holds
+    # some of it, whichever queue a stream of the library's would share.
+    load = [sA] + [torch.cuda.Stream() for _ in range(7)]
     errors, lat = [], []
     stop = threading.Event()
 
@@ -88,8 +119,10 @@ def test_growing_scratch_does_not_hold_up_synchronous_calls(engine):
     def a_thread():
         try:
             for g, (arena, desc, want) in enumerate(gens):
-                for _ in range(200):  # ~250 us each
-                    engine.batch_tensors(big_arena, big_desc, big_out, stream=sA)
+                for k in range(200):  # ~250 us each
+                    engine.batch_tensors(big_arena, big_desc, big_out, stream=load[k % len(load)])
+                for s in load[1:]:
+                    sA.wait_stream(s)
                 out = engine.batch_tensors(arena, desc, chained=True, stream=sA)  # its scratch grows
                 sA.synchronize()
                 if not np.array_equal(out.cpu().numpy().view(np.uint16), want):
@@ -105,24 +138,49 @@ def test_growing_scratch_does_not_hold_up_synchronous_calls(engine):
             buf = r.integers(0, 256, int(r.integers(1, 3000)), dtype=np.uint8)
             t0 = time.perf_counter()
             got = engine.checksum(buf, 0)
-            lat.append(time.perf_counter() - t0)
+            t1 = time.perf_counter()
+            lat.append((t1 - t0, t0, t1))
             if got != O.c_checksum(bytes(buf), 0):
                 errors.append("checksum")
 
+    engine.stats(reset=True)
+    pauses, gc_off = _gc_clock()
     ta, tb = threading.Thread(target=a_thread), threading.Thread(target=b_thread)
-    tb.start()
-    ta.start()
-    ta.join()
-    tb.join()
+    try:
+        tb.start()
+        ta.start()
+        ta.join()
+        tb.join()
+    finally:
+        gc_off()
+    st = engine.stats()
     engine.stream_release(sA)
     assert not errors, errors[:5]
-    lat.sort()
-    print(f"synchronous calls during growth: {len(lat)}, median {lat[len(lat) // 2] * 1e6:.1f} us, "
-          f"p99 {lat[int(len(lat) * 0.99)] * 1e6:.1f} us, max {lat[-1] * 1e6:.1f} us, "
-          f"over 1 ms {sum(x > 1e-3 for x in lat)}, over 10 ms {sum(x > 1e-2 for x in lat)}, "
-          f"over 30 ms {sum(x > 3e-2 for x in lat)}")
-    assert len(lat) > 100
+
+    def in_gc(t0, t1):
+        return any(p0 < t1 and p1 > t0 for p0, p1, _ in pauses)
+
+    slow = [(d, t0, t1) for d, t0, t1 in lat if d > 1e-3]
+    unexplained = [d for d, t0, t1 in slow if not in_gc(t0, t1)]
+    lat_s = sorted(d for d, _, _ in lat)
+    gc_ms = sorted((p1 - p0) * 1e3 for p0, p1, _ in pauses)
+    print(f"synchronous calls during growth: {len(lat_s)}, median {lat_s[len(lat_s) // 2] * 1e6:.1f} us, "
+          f"p99 {lat_s[int(len(lat_s) * 0.99)] * 1e6:.1f} us, max {lat_s[-1] * 1e6:.1f} us, "
+          f"over 1 ms {len(slow)} (inside a GC pause {len(slow) - len(unexplained)}), "
+          f"over 10 ms {sum(d > 1e-2 for d in lat_s)}")
+    print(f"library: calls {st['calls']}, longest call {st['call_ns_max'] / 1e3:.1f} us, "
+          f"longest lock wait {st['lock_ns_max'] / 1e3:.1f} us, passes {st['zc_passes']} "
+          f"(late {st['zc_late']}, longest {st['zc_pass_ns_max'] / 1e3:.1f} us), "
+          f"growths {st['growths']} ({st['growth_ns_total'] / 1e3:.1f} us, longest {st['growth_ns_max'] / 1e3:.1f} us), "
+          f"retires {st['retires']} (longest {st['retire_ns_max'] / 1e3:.1f} us), "
+          f"stage allocs {st['stage_allocs']} (longest {st['stage_alloc_ns_max'] / 1e3:.1f} us)")
+    print(f"gc pauses: {len(gc_ms)}, gen2 {sum(g == 2 for _, _, g in pauses)}, "
+          f"longest {gc_ms[-1] if gc_ms else 0:.2f} ms")
+    assert len(lat_s) > 100
+    assert st["growths"] >= 5  # every generation grew A's scratch
     # Each growth lands behind ~50 ms of queued work; a device-wide wait under
     # the context lock would hold some call up that long at every growth.
-    # Measured: max 0.6 ms (profiles/r03/gputest_scratch.log).
-    assert sum(x > 1e-2 for x in lat) == 0, lat[-5:]
+    assert st["call_ns_max"] < 10e6, st
+    assert st["zc_late"] == 0, st
+    # Every Python-side stall over 1 ms is the interpreter's own GC pause.
+    assert not unexplained, sorted(unexplained)[-5:]
