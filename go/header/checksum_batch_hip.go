@@ -302,6 +302,23 @@ const (
 	PacketMalformed         = 3 // dropped by IsValid / the length checks first
 )
 
+// Offload thresholds.  A synchronous engine call costs one GPU round trip
+// (~11 us) plus its bytes; below these sizes one core running the
+// reference's own loop (checksum.go:26-46) on the same bytes finishes first
+// (tools/crossover.cc on MI355X, profiles/r04/crossover.json; INTEGRATION.md
+// §2 "When offload pays").  The build-tagged callers offload only calls at
+// or above them; smaller calls take the reference's unmodified Go code.
+const (
+	// ChainsOffloadMinBytes is the payload of one sendTCPBatch
+	// (ChecksumChains): at 64 KiB the engine took 1.55x one core's time,
+	// at 128 KiB 0.59x.
+	ChainsOffloadMinBytes = 128 << 10
+	// VerifyOffloadMinBytes is the Data bytes of one recvmmsg batch
+	// (VerifyPacketBuffers): 128 x 1500 B took 1.05x one core's time,
+	// 256 x 1500 B 0.85x.
+	VerifyOffloadMinBytes = 256 << 10
+)
+
 // VerifyPacketBuffers runs the receive path's checksum checks over a batch
 // of packets as the link layer delivers them (recvMMsgDispatcher,
 // link/fdbased/packet_dispatchers.go:258-317: Data holds the IP packet over

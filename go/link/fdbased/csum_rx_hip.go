@@ -12,7 +12,8 @@
 // verified before reassembly (ipv4.go:355-385).  Fragments and anything the
 // pass does not check stay RXChecksumUnknown and are verified by the stack
 // as usual; invalid packets are delivered too, so the stack drops and counts
-// them where the reference does (tcp/endpoint.go:2108-2114).
+// them where the reference does (tcp/endpoint.go:2108-2114).  Only batches
+// of at least header.VerifyOffloadMinBytes go to the engine (see below).
 
 // +build linux,hipcsum
 
@@ -27,6 +28,18 @@ import (
 func verifyRXChecksums(e *endpoint, pkts []tcpip.PacketBuffer) {
 	if len(pkts) == 0 || e.Capabilities()&stack.CapabilityRXChecksumOffload != 0 {
 		return // the NIC / host kernel verified them already
+	}
+	// Below header.VerifyOffloadMinBytes one core verifies the batch sooner
+	// than one engine call (INTEGRATION.md §2): leave every packet
+	// RXChecksumUnknown, and segment.parse verifies it as the reference does.
+	// With MaxMsgsPerRecv = 8 that takes packets of ~32 KiB on average (a
+	// large-MTU link); 8 x 1500 B never reaches it.
+	total := 0
+	for i := range pkts {
+		total += pkts[i].Data.Size()
+	}
+	if total < header.VerifyOffloadMinBytes {
+		return
 	}
 	var verdict [MaxMsgsPerRecv]uint8
 	header.VerifyPacketBuffers(pkts, verdict[:len(pkts)])

@@ -1,7 +1,7 @@
 // Copyright 2026 netstack-csum-mi355x authors.
 //
 // The default build's side of csum_batch_hip.go (see there): with
-// tcpBatchChecksums false, sendTCPBatch never defers, and buildTCPHdr
+// deferTCPBatchChecksums false, sendTCPBatch never defers, and buildTCPHdr
 // computes every segment's checksum itself exactly as the reference does
 // (connect.go:661-663).  finishTCPBatchChecksums is that same per-segment
 // computation, for completeness.
@@ -16,7 +16,9 @@ import (
 	"github.com/google/netstack/tcpip/stack"
 )
 
-const tcpBatchChecksums = false
+func deferTCPBatchChecksums(payload int) bool {
+	return false
+}
 
 func finishTCPBatchChecksums(hdrs []stack.PacketDescriptor, data buffer.VectorisedView, pseudo []uint16) {
 	for i := range hdrs {

@@ -17,8 +17,15 @@ import (
 	"github.com/google/netstack/tcpip/stack"
 )
 
-// tcpBatchChecksums tells sendTCPBatch to defer its checksums here.
-const tcpBatchChecksums = true
+// deferTCPBatchChecksums tells sendTCPBatch whether to defer its checksums
+// here: only for a payload of at least header.ChainsOffloadMinBytes, where
+// one engine call beats one core doing the segments' sums (INTEGRATION.md
+// §2).  The reference's own sendTCPBatch payload is one GSO packet of at
+// most 64 KiB (stack/registration.go:522-524), so with its settings this
+// never defers and buildTCPHdr sums every segment as before.
+func deferTCPBatchChecksums(payload int) bool {
+	return payload >= header.ChainsOffloadMinBytes
+}
 
 // finishTCPBatchChecksums writes every segment's checksum into its TCP
 // header: for segment i, buildTCPHdr's

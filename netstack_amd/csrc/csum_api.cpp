@@ -253,6 +253,13 @@ struct SmallReq {
 // the context's pool for the duration of the call, so concurrent callers
 // gather in parallel straight into memory the kernel reads.
 constexpr uint64_t kStageBytes = 1ull << 20;
+// A gather that outgrows its stage moves to a larger one leased from a second
+// pool (powers of two up to kZeroCopyMax) and stays zero-copy; only beyond
+// that does it take the DMA pipeline.  On MI355X (large BAR) a gather stage is
+// device memory the host writes through the BAR at ~23 GB/s, where the DMA
+// pipeline first gathers into pinned memory and then copies it: 2-4 MiB calls
+// ran at 13-15 GB/s there (tools/crossover.cc, profiles/r04/crossover.json).
+constexpr uint64_t kZeroCopyMax = 16ull << 20;
 // A pass's [table | results] buffer; a pass takes queued requests while they fit.
 constexpr uint64_t kPassTableBytes = 1ull << 20;
 // The "arena" of a zero-copy pass is the address space: descriptors hold
@@ -318,6 +325,7 @@ struct ns_csum_ctx {
   std::mutex qmu;
   std::vector<BarBuf*> gstage_free;
   std::vector<BarBuf*> gstage_all;
+  std::vector<BarBuf*> gbig_free;  // gather stages above kStageBytes (in gstage_all too)
   std::vector<MappedPin*> stage_free;
   std::vector<MappedPin*> stage_all;
   std::vector<MappedPin*> big_free;  // pooled caller stages above kStageBytes
@@ -560,15 +568,30 @@ MappedPin* lease_stage(ns_csum_ctx* ctx, int* rc) {
   return b;
 }
 
-// Lease / return a gather stage of kStageBytes (device memory behind the BAR
-// on large-BAR parts) from the context's pool.
-BarBuf* lease_gather_stage(ns_csum_ctx* ctx, int* rc) {
+// Lease / return a gather stage (device memory behind the BAR on large-BAR
+// parts) of at least `bytes`: kStageBytes from the context's pool, or above
+// that the smallest pooled big stage that fits (new ones are powers of two).
+BarBuf* lease_gather_stage(ns_csum_ctx* ctx, int* rc, uint64_t bytes = kStageBytes) {
+  uint64_t cap = kStageBytes;
   {
     std::lock_guard<std::mutex> ql(ctx->qmu);
-    if (!ctx->gstage_free.empty()) {
-      BarBuf* b = ctx->gstage_free.back();
-      ctx->gstage_free.pop_back();
-      return b;
+    if (bytes <= kStageBytes) {
+      if (!ctx->gstage_free.empty()) {
+        BarBuf* b = ctx->gstage_free.back();
+        ctx->gstage_free.pop_back();
+        return b;
+      }
+    } else {
+      size_t best = ctx->gbig_free.size();
+      for (size_t i = 0; i < ctx->gbig_free.size(); ++i)
+        if (ctx->gbig_free[i]->cap >= bytes && (best == ctx->gbig_free.size() || ctx->gbig_free[i]->cap < ctx->gbig_free[best]->cap))
+          best = i;
+      if (best < ctx->gbig_free.size()) {
+        BarBuf* b = ctx->gbig_free[best];
+        ctx->gbig_free.erase(ctx->gbig_free.begin() + (long)best);
+        return b;
+      }
+      while (cap < bytes) cap *= 2;
     }
   }
   AllocClock clk(ctx);
@@ -579,7 +602,7 @@ BarBuf* lease_gather_stage(ns_csum_ctx* ctx, int* rc) {
   }
   {
     DeviceGuard g(ctx->device);
-    if ((*rc = b->ensure(kStageBytes, ctx->bar_table)) != NS_OK) {
+    if ((*rc = b->ensure(cap, ctx->bar_table)) != NS_OK) {
       delete b;
       return nullptr;
     }
@@ -592,7 +615,7 @@ BarBuf* lease_gather_stage(ns_csum_ctx* ctx, int* rc) {
 void return_gather_stage(ns_csum_ctx* ctx, BarBuf* b) {
   if (!b) return;
   std::lock_guard<std::mutex> ql(ctx->qmu);
-  ctx->gstage_free.push_back(b);
+  (b->cap == kStageBytes ? ctx->gstage_free : ctx->gbig_free).push_back(b);
 }
 
 // Flat combining of concurrent small synchronous calls (nsh::FlatCombiner):
@@ -837,6 +860,21 @@ struct ByteSink {
     g = fresh;
     return NS_OK;
   }
+  // Move to a larger gather stage with room for `need` bytes (<=
+  // kZeroCopyMax), copying what is staged again from its sources.
+  int grow_stage(uint64_t need) {
+    int r = NS_OK;
+    BarBuf* nb = lease_gather_stage(ctx, &r, std::max<uint64_t>(need, 2 * stage->cap));
+    if (!nb) return r != NS_OK ? r : NS_ENOMEM;
+    uint64_t at = 0;
+    for (const auto& pc : staged) {
+      std::memcpy(nb->p + at, pc.first, pc.second);
+      at += pc.second;
+    }
+    return_gather_stage(ctx, stage);
+    stage = nb;
+    return NS_OK;
+  }
   // Move to g_arena (taking the context lock) with room for `need` bytes.
   int to_big(uint64_t need) {
     big = std::unique_lock<std::mutex>(ctx->mu);
@@ -859,7 +897,7 @@ struct ByteSink {
     }
     const uint64_t at = n;
     if (!len || rc != NS_OK) return at;
-    if (!in_big() && n + len > stage->cap) rc = to_big(n + len);
+    if (!in_big() && n + len > stage->cap) rc = n + len <= kZeroCopyMax ? grow_stage(n + len) : to_big(n + len);
     else if (in_big()) rc = reserve_big(n + len, n);
     if (rc != NS_OK) return at;
     std::memcpy(base() + n, p, len);

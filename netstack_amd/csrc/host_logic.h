@@ -286,6 +286,9 @@ inline bool parse_ip(const PacketBytes& pb, bool rx, IpInfo* ip) {
     ip->hlen = (uint64_t)(h[0] & 0xF) * 4;
     const uint64_t tlen = ((uint64_t)h[2] << 8) | h[3];
     if (rx) {
+      // IsValid (header/ipv4.go:280-296), plus `hlen > first`: where the
+      // reference reslices past the first view or panics (ipv4.go:348), the
+      // packet is MALFORMED (tests/golden/rx_choices.json).
       if (ip->hlen < 20 || ip->hlen > tlen || tlen > pb.size || ip->hlen > first) return false;
       ip->tend = tlen;  // Data.CapLength(tlen - hlen), ipv4.go:353
     } else {

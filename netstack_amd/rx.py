@@ -145,7 +145,10 @@ class ReceivePath:
         size = pk.Data.Size()
         hlen = (h[0] & 0xF) * 4 if h else 0
         tlen = struct.unpack_from(">H", h, 2)[0] if len(h) >= 4 else 0
-        if len(h) < 20 or hlen < 20 or hlen > tlen or tlen > size or hlen > len(h):  # IsValid
+        # IsValid (header/ipv4.go:280-296); `hlen > len(h)` is this repo's choice
+        # where ipv4.go:348 reslices past the view or panics (DESIGN.md §7,
+        # tests/golden/rx_choices.json)
+        if len(h) < 20 or hlen < 20 or hlen > tlen or tlen > size or hlen > len(h):
             self.stats.IPMalformedPacketsReceived += 1
             return None
         src, dst, proto, ident = h[12:16], h[16:20], h[9], struct.unpack_from(">H", h, 4)[0]

@@ -81,6 +81,10 @@ def verify(hdr: bytes, views, size: int):
             return MALFORMED, 0, 0
         hlen = (first[0] & 0xF) * 4
         tlen = (first[2] << 8) | first[3]
+        # `hlen > len(first)` is not in IsValid: there ipv4.go:348 reslices
+        # headerView past its length (spare capacity) or panics.  This repo
+        # makes it MALFORMED, i.e. RXChecksumUnknown for the stack (DESIGN.md
+        # §7; pinned by tests/golden/rx_choices.json).
         if hlen < 20 or hlen > tlen or tlen > _size(data) or hlen > len(first):
             return MALFORMED, 0, 0
         net = c_checksum(first[:hlen], 0)  # IPv4.CalculateChecksum (ipv4.go:251-253), reported only

@@ -262,7 +262,7 @@ def test_go_caller_files_pair_up_and_use_only_what_exists():
         (t1, s1, c1), (t2, s2, c2) = files
         assert t1.replace("!", "") == t2.replace("!", "") and t1 != t2
         # what the patch calls in this package is declared by both variants, alike
-        for name in ("tcpBatchChecksums", "finishTCPBatchChecksums") if pkg == "tcp" else ("verifyRXChecksums",):
+        for name in ("deferTCPBatchChecksums", "finishTCPBatchChecksums") if pkg == "tcp" else ("verifyRXChecksums",):
             assert re.search(rf"\b{name}\b", added)
             assert s1.get(name) == s2.get(name), (pkg, name)
             assert re.search(rf"^(?:func|const) {name}\b", c1, flags=re.M) and \

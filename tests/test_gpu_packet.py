@@ -206,6 +206,31 @@ def test_verify_single_corrupted_byte_fails(engine):
     assert verdict[0] == VALID and (verdict[1:] == INVALID).all()
 
 
+def test_ipv4_header_past_the_first_view(engine):
+    """tests/golden/rx_choices.json: an IPv4 header longer than
+    Data.First() is MALFORMED with no sums taken (the reference reslices past
+    the view or panics, network/ipv4/ipv4.go:348); a header within its view
+    verifies.  The fixture, the oracle and the engine agree."""
+    import json
+    import os
+
+    import packets as P
+
+    from netstack_amd.buffer import NewVectorisedView, View
+    from netstack_amd.packet import PacketBuffer, verify_packet_buffers
+
+    with open(os.path.join(os.path.dirname(__file__), "golden", "rx_choices.json")) as f:
+        cases = json.load(f)["ipv4_header_past_first_view"]
+    pkts = [PacketBuffer(Data=NewVectorisedView(c["size"], [View(bytearray.fromhex(v)) for v in c["views"]]))
+            for c in cases]
+    verdict, sums = verify_packet_buffers(pkts, engine)
+    for i, c in enumerate(cases):
+        want = (c["verdict"], c["ipv4_sum"], c["transport_sum"])
+        assert (int(verdict[i]), int(sums[2 * i]), int(sums[2 * i + 1])) == want, c["name"]
+        assert _oracle_rx(pkts[i]) == want, c["name"]
+    assert [int(v) for v in verdict] == [P.MALFORMED, P.MALFORMED, P.VALID, P.VALID]
+
+
 def _tx_batch(rng, n):
     """Outbound PacketBuffers: Header = a Prependable into which the
     transport header and then the IP header were prepended (checksum fields

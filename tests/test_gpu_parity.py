@@ -1286,3 +1286,28 @@ def test_small_calls_with_host_memory_staging():
         _small_call_mix(eng, 78)
     finally:
         eng.close()
+
+
+@pytest.mark.parametrize("total", [900_000, 1_500_000, 3_300_000, 9_000_000, 15_000_000, 40_000_000])
+def test_gathers_across_stage_sizes(engine, total):
+    """A VectorisedView batch and a single-buffer Checksum whose gathers end
+    in every staging regime: the 1 MiB stage, a larger zero-copy stage it
+    grows into (re-copied from the sources each time, up to 16 MiB:
+    csum_api.cpp grow_stage), and past 16 MiB the pinned arena and the DMA
+    pipeline.  Every result against the oracle."""
+    import oracle as O
+
+    rng = np.random.default_rng(total)
+    sizes = rng.integers(1, max(2, total // 6), 12)
+    sizes = (sizes * (total / sizes.sum())).astype(np.int64) + 1
+    views = [rng.integers(0, 256, int(k), dtype=np.uint8) for k in sizes]
+    vb = [bytes(v) for v in views]
+    tot = int(sum(len(v) for v in vb))
+    cuts = np.unique(np.concatenate([[0, tot], rng.integers(0, tot, 40)]))
+    # consecutive segments over the whole view (as sendTCPBatch cuts its
+    # payload), so the gather holds ~total bytes; one reaches past the end
+    segs = [(int(a), int(b - a), int(rng.integers(0, 65536))) for a, b in zip(cuts[:-1], cuts[1:])]
+    segs[-1] = (segs[-1][0], segs[-1][1] + 100, segs[-1][2])
+    assert engine.vv_batch(views, segs).tolist() == [O.c_checksum_vv_with_offset(vb, i, o, s) for o, s, i in segs]
+    buf = np.concatenate(views)
+    assert engine.checksum(buf, 0xBEEF) == O.c_checksum(buf.tobytes(), 0xBEEF)

@@ -185,3 +185,25 @@ def test_reassembly_clears_a_fragment_verdict():
         pk.RXChecksum = RX_CHECKSUM_VALID
         last = rp.network(pk)
     assert last is not None and last[2].RXChecksum == RX_CHECKSUM_UNKNOWN
+
+
+def _choices():
+    import json
+    import os
+
+    with open(os.path.join(os.path.dirname(__file__), "golden", "rx_choices.json")) as f:
+        return json.load(f)["ipv4_header_past_first_view"]
+
+
+def test_ipv4_header_past_the_first_view_is_malformed():
+    """tests/golden/rx_choices.json: an IPv4 header longer than
+    Data.First() — where the reference reslices into the view's spare
+    capacity or panics (network/ipv4/ipv4.go:348) — is MALFORMED in the
+    oracle, with no sums; the same header within its view verifies."""
+    import packets as P
+
+    cases = _choices()
+    assert len(cases) == 4
+    for c in cases:
+        views = [bytes.fromhex(v) for v in c["views"]]
+        assert P.verify(b"", views, c["size"]) == (c["verdict"], c["ipv4_sum"], c["transport_sum"]), c["name"]
