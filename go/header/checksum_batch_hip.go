@@ -8,7 +8,7 @@
 // which stays untouched: the single-buffer functions (Checksum, ChecksumVV,
 // ChecksumVVWithOffset, ChecksumCombine, PseudoHeaderChecksum,
 // checksum.go:52-122) remain the reference's own Go code, because one GPU
-// round trip (~18 us) costs far more than a 20-60-B header sum.  The callers'
+// round trip (~11 us) costs far more than a 20-60-B header sum.  The callers'
 // batches come here instead (SURVEY.md §8(b)): sendTCPBatch's n segments
 // (tcp/connect.go:668-702), a recvmmsg batch of packet buffers
 // (link/fdbased/packet_dispatchers.go:258-317), WritePackets' headers
@@ -310,13 +310,13 @@ const (
 // or above them; smaller calls take the reference's unmodified Go code.
 const (
 	// ChainsOffloadMinBytes is the payload of one sendTCPBatch
-	// (ChecksumChains): at 64 KiB the engine took 1.55x one core's time,
-	// at 128 KiB 0.59x.
+	// (ChecksumChains): at 64 KiB the engine took 1.61x one core's time,
+	// at 128 KiB 0.98x, at 256 KiB 0.60x.
 	ChainsOffloadMinBytes = 128 << 10
 	// VerifyOffloadMinBytes is the Data bytes of one recvmmsg batch
-	// (VerifyPacketBuffers): 128 x 1500 B took 1.05x one core's time,
-	// 256 x 1500 B 0.85x.
-	VerifyOffloadMinBytes = 256 << 10
+	// (VerifyPacketBuffers): 128 x 1500 B took 1.08x one core's time,
+	// 256 x 1500 B 0.89x, 512 x 1500 B 0.81x.
+	VerifyOffloadMinBytes = 256 * 1500
 )
 
 // VerifyPacketBuffers runs the receive path's checksum checks over a batch

@@ -318,3 +318,35 @@ def test_latency_bounds_are_collected_after_every_parity_test():
     assert lat and lat[0] == len(ids) - len(lat), ids[-5:]
     par = [i for i, l in enumerate(ids) if "test_gpu_tcp.py" in l or "test_gpu_sync.py" in l]
     assert par and max(par) < lat[0]
+
+
+def test_go_offload_gates_sit_at_the_measured_crossover():
+    """The build-tagged callers offload only calls at or above the sizes
+    where one engine call beat one core (tools/crossover.cc on MI355X,
+    profiles/r04/crossover.json); below them the reference's own Go code runs
+    (INTEGRATION.md §2).  Each gate is a measured point no smaller than the
+    measured crossover and no more than 2x it, and each caller tests it
+    before calling the engine."""
+    import json
+
+    code = _go_code(open(GO_SHIM).read())
+    env = {}
+    for name in ("ChainsOffloadMinBytes", "VerifyOffloadMinBytes"):
+        m = re.search(rf"^\s*{name}\s*=\s*([0-9<>* ]+)$", code, flags=re.M)
+        assert m, name
+        env[name] = int(eval(m.group(1), {}))  # a constant expression of integers
+    with open(os.path.join(ROOT, "profiles", "r04", "crossover.json")) as f:
+        xo = json.load(f)
+    for gate, shape in (("ChainsOffloadMinBytes", "chains"), ("ChainsOffloadMinBytes", "vv_batch"),
+                        ("VerifyOffloadMinBytes", "verify")):
+        x = xo[shape]["crossover"]
+        assert x is not None, shape
+        assert x["bytes"] <= env[gate] <= 2 * x["bytes"], (gate, shape, x, env[gate])
+        assert env[gate] in {p["bytes"] for p in xo[shape]["points"]}, (gate, shape)
+    tx = _go_code(open(os.path.join(ROOT, "go/transport/tcp/csum_batch_hip.go")).read())
+    assert re.search(r"return payload >= header\.ChainsOffloadMinBytes", tx)
+    rx = _go_code(open(os.path.join(ROOT, "go/link/fdbased/csum_rx_hip.go")).read())
+    assert re.search(r"if total < header\.VerifyOffloadMinBytes \{\s*return\s*\}", rx)
+    assert rx.index("VerifyOffloadMinBytes") < rx.index("header.VerifyPacketBuffers(")
+    patch = open(GO_PATCH).read()
+    assert "+\tdeferCsum := deferTCPBatchChecksums(data.Size()) &&" in patch

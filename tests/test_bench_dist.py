@@ -137,3 +137,65 @@ def test_nccl_refuses_more_ranks_than_gpus():
         assert "one GPU per rank" in str(e.value)
     assert [bench.device_ordinal("gloo", r, 1, 8) for r in range(8)] == [0] * 8
     assert bench.device_ordinal("gloo", 5, 2, 8) == 1
+
+
+def test_nccl_process_group_is_bound_to_the_rank_device(monkeypatch):
+    """What a one-GPU box cannot show about the 8-GPU nccl (RCCL) run,
+    pinned on CPU: bench.Dist hands init_process_group this rank's device
+    (eager communicator on the right GPU) and its barrier names that device,
+    while gloo passes neither; main() makes the device current before the
+    process group exists, builds the engine on the same ordinal, and times
+    the CPU leg only at N=1 (no rank waits on rank 0's CPU work)."""
+    import inspect
+
+    import torch
+    import torch.distributed as tdist
+
+    import bench
+
+    calls = []
+    monkeypatch.setattr(tdist, "is_initialized", lambda: False)
+    monkeypatch.setattr(tdist, "init_process_group", lambda **kw: calls.append(("init", kw)))
+    monkeypatch.setattr(tdist, "barrier", lambda **kw: calls.append(("barrier", kw)))
+    monkeypatch.setenv("WORLD_SIZE", "8")
+    monkeypatch.setenv("RANK", "5")
+    monkeypatch.setenv("LOCAL_RANK", "5")
+    d = bench.Dist("nccl", 5)
+    d.barrier()
+    assert calls[0] == ("init", {"backend": "nccl", "device_id": torch.device("cuda", 5)})
+    assert calls[1] == ("barrier", {"device_ids": [5]})
+    calls.clear()
+    g = bench.Dist("gloo", 5)
+    g.barrier()
+    assert calls == [("init", {"backend": "gloo"}), ("barrier", {})]
+
+    src = inspect.getsource(bench.main)
+    i_dev, i_pg, i_eng = src.index("torch.cuda.set_device(ordinal)"), src.index("Dist(backend, ordinal)"), \
+        src.index("Engine(ordinal)")
+    assert i_dev < i_pg < i_eng
+    assert 'elif dist.rank == 0 and not args.no_cpu' in src and "dist.world > 1" in src
+
+
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
+def test_per_rank_device_footprint(world):
+    """Per-rank HBM of the driver's scaling runs: the default
+    cfg2 (weak: every rank its own 1M x 1500 B batch, distinct seeds, 2
+    rotating batches + tables + results) and cfg5 (strong: 1/N of the one 8M x
+    1500 B batch, 12.6 / 6.3 / 3.2 / 1.6 GB shards that tile it exactly).
+    Both sit far below a 288 GB MI355X; nothing scales with N per rank except
+    the cfg5 shard, which shrinks."""
+    import bench
+    from netstack_amd import workloads as W
+
+    b2 = [bench.rank_batch(2, r, world) for r in range(world)]
+    assert len({b.seed for b in b2}) == world and {b.n for b in b2} == {1 << 20}
+    per_rank = 2 * (b2[0].arena_bytes + 16 * b2[0].n) + 2 * b2[0].n
+    assert 3.1e9 < per_rank < 3.3e9
+    whole = W.config(5)
+    shards = [whole.shard(r, world) for r in range(world)]
+    assert sum(s.n for s in shards) == 8 << 20 and {s.n for s in shards} == {(8 << 20) // world}
+    total = sum(int(s.desc["len"].sum()) for s in shards)
+    assert total == int(whole.desc["len"].sum())
+    for s in shards:
+        assert abs(s.arena_bytes - whole.arena_bytes / world) < 64
+        assert s.arena_bytes + 18 * s.n < 13e9 / world
