@@ -108,6 +108,16 @@ typedef struct ns_pkt_desc {
 /* batch_flags for ns_csum_batch_*: the table contains NS_DESC_CONT entries.
  * Without it CONT bits are an error-free no-op (each entry is independent). */
 #define NS_BATCH_CHAINED 0x1u
+/* batch_flags for ns_csum_batch_dev / _dev_store only: runs are pairs.  An
+ * odd-indexed NS_DESC_CONT descriptor continues the descriptor before it (its
+ * initial := that one's result, checksum.go:89), exactly as NS_BATCH_CHAINED
+ * would fold it; NS_DESC_CONT on an even-indexed descriptor is ignored.  The
+ * pair is folded inside the checksum kernel: no scratch, no fold pass.  Meant
+ * for two-piece sums whose pieces are not contiguous, e.g. a TCP segment whose
+ * header lies in sendTCPBatch's header slots and whose payload lies in its
+ * payload view (workloads.tx_split_desc).  NS_EINVAL together
+ * with NS_BATCH_CHAINED, and on the host-memory entry points.               */
+#define NS_BATCH_PAIRED 0x2u
 
 /* A borrowed host byte range: one buffer.View (tcpip/buffer/view.go:19). */
 typedef struct ns_view {

@@ -1114,13 +1114,23 @@ int batch_dev(ns_csum_ctx* ctx, const uint8_t* d_arena, uint64_t arena_bytes, co
               uint32_t n, uint16_t* d_out, uint32_t batch_flags, void* stream, bool store) {
   if (!ctx || (n && (!d_desc || !d_out)) || (arena_bytes && !d_arena)) return NS_EINVAL;
   if (n == 0) return NS_OK;
+  const bool need_chain = (batch_flags & NS_BATCH_CHAINED) != 0;
+  const bool paired = (batch_flags & NS_BATCH_PAIRED) != 0;
+  if (paired && need_chain) return NS_EINVAL;
   DeviceGuard g(ctx->device);
   hipStream_t s = (hipStream_t)stream;  // NULL = the HIP null stream
-  const bool need_chain = (batch_flags & NS_BATCH_CHAINED) != 0;
+  // NS_CSUM_STORE_WB=1: in-place stores of unchained tiles as plain
+  // write-back stores (A/B diagnostics only)
+  static const uint32_t wb = std::getenv("NS_CSUM_STORE_WB") ? 4u : 0u;
+  if (paired) {  // plain tiles, pairs folded in the kernel (no scratch)
+    HIP_TRY(nsk::launch_batch(d_arena, arena_bytes, d_desc, n, d_out, nsk::ChainScratch{}, ctx->d_err, s, 0,
+                              (store ? 1u | wb : 0u) | 2u, nullptr));
+    return NS_OK;
+  }
   const bool need_split = arena_bytes / n >= nsk::split_min_avg();
   if (!need_chain && !need_split) {
     HIP_TRY(nsk::launch_batch(d_arena, arena_bytes, d_desc, n, d_out, nsk::ChainScratch{}, ctx->d_err, s, 0,
-                              store ? 1u : 0u, nullptr));
+                              store ? 1u | wb : 0u, nullptr));
     return NS_OK;
   }
   StreamScratch* sc = ctx->scratch.pin(scratch_key(s), make_scratch,
@@ -1184,6 +1194,7 @@ int ns_csum_batch_host(ns_csum_ctx* ctx, const uint8_t* h_arena, uint64_t arena_
                        const ns_pkt_desc* h_desc, uint32_t n, uint16_t* h_out,
                        uint32_t batch_flags) {
   if (!ctx || (n && (!h_desc || !h_out)) || (arena_bytes && !h_arena)) return NS_EINVAL;
+  if (batch_flags & NS_BATCH_PAIRED) return NS_EINVAL;  // device-resident batches only
   CallClock clk(ctx);
   if (n == 0) return NS_OK;
   // The zero-copy pass needs the table's byte span first; an arena larger

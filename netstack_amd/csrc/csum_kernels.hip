@@ -920,10 +920,12 @@ __device__ __forceinline__ uint32_t hyb_scan_tile(HybLds<WG>& L, const Srd& r, c
 // launch's stream: TX fill 285-286 vs 290-292 us (nontemporal: 292),
 // bench.py --config 8, two interleaved rounds on one box
 // (profiles/r02/tx_store_policy.txt).
-__device__ __forceinline__ void store_result(uint64_t addr, uint32_t r, uint32_t stw) {
+__device__ __forceinline__ void store_result(uint64_t addr, uint32_t r, uint32_t stw, bool wb = false) {
   const uint32_t v = (stw & 2u) ? r : (~r & 0xFFFFu);
   uint8_t* p = reinterpret_cast<uint8_t*>((uintptr_t)addr);
-  if (!(addr & 1u)) {
+  if (wb && !(addr & 1u)) {  // A/B (store bit 2): a plain, write-back store
+    *reinterpret_cast<uint16_t*>(p) = (uint16_t)(((v & 0xFFu) << 8) | (v >> 8));
+  } else if (!(addr & 1u)) {
     __hip_atomic_store(reinterpret_cast<uint16_t*>(p), (uint16_t)(((v & 0xFFu) << 8) | (v >> 8)), __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
   } else {
@@ -944,7 +946,7 @@ __device__ __forceinline__ void park_store(HybLds<P>& L, uint32_t store, uint4 r
                                            uint64_t arena_abs, uint64_t arena_bytes,
                                            unsigned long long* err) {
   if (!store) return;
-  uint32_t stw = mine ? (raw.w >> 18) & 0x3FFFu : 0u;
+  uint32_t stw = (mine && (store & 1u)) ? (raw.w >> 18) & 0x3FFFu : 0u;
   const uint64_t at = ((uint64_t)raw.x | ((uint64_t)raw.y << 32)) + (stw >> 2);
   if (!(stw & 1u)) {  // NS_DESC_STORE_RAW counts only with NS_DESC_STORE
     stw = 0;
@@ -952,6 +954,9 @@ __device__ __forceinline__ void park_store(HybLds<P>& L, uint32_t store, uint4 r
     atomicAdd(err, 1ull);
     stw = 0;
   }
+  // NS_BATCH_PAIRED: the descriptor's CONT bit rides along at bit 14, so the
+  // decoded flag need not stay live in a register through the scan.
+  if (store & 2u) stw |= ((raw.w >> 17) & 1u) << 14;
   L.stw[threadIdx.x] = stw;
   L.sat[threadIdx.x] = arena_abs + at;
 }
@@ -970,20 +975,30 @@ __device__ __forceinline__ void finish_tile(HybLds<P>& L, uint32_t s, const Pkt&
     // the TX batch: 2M scattered 2-byte stores cost the same ~50 us of HBM
     // read-modify-write wherever they are issued, and issuing them here
     // holds every workgroup until its stores drain.)
-    const uint32_t stw = (store && mine) ? L.stw[t] : 0u;
+    const uint32_t stw = ((store & 1u) && mine) ? L.stw[t] : 0u;
     if (!mine) return;
     partial[i] = v;
     reinterpret_cast<uint16_t*>(partial + chain_flag_word(n))[i] = (uint16_t)((head ? 0u : 1u) | (stw << 1));
   } else {
+    uint32_t r = fold1(d.init + s);
+    if (store & 2u) {
+      // NS_BATCH_PAIRED: an odd-indexed NS_DESC_CONT descriptor continues the
+      // one before it — Go's `Checksum(v, xsum)` chaining, exactly: the uint32
+      // add wraps as Go's accumulator does, and a W-only class value (s_class)
+      // behaves as S does.  Tiles hold an even number of descriptors, so lane
+      // t - 1 of this wave holds it; every lane of the wave is here.
+      // row_shr:1 — lane t takes lane t - 1's value (odd lanes never start a DPP row)
+      const uint32_t prev = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)r, 0x111, 0xF, 0xF, false);
+      if ((t & 1) && (L.stw[t] >> 14)) r = fold1(prev + s);
+    }
     if (!mine) return;
-    const uint32_t r = fold1(d.init + s);
     if (wt)  // a self-signalling launch (zc_complete): results written through to the host
       __hip_atomic_store(out + i, (uint16_t)r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     else
       out[i] = (uint16_t)r;
-    if (store) {
-      const uint32_t stw = L.stw[t];
-      if (stw) store_result(L.sat[t], r, stw);
+    if (store & 1u) {
+      const uint32_t stw = L.stw[t] & 0x3FFFu;
+      if (stw) store_result(L.sat[t], r, stw, (store & 4u) != 0);
     }
   }
 }
@@ -1565,6 +1580,9 @@ static hipError_t launch_hyb(const uint8_t* arena, uint64_t arena_bytes, const v
     NSK_TP(8);
     NSK_TP(4);
     NSK_TP(2);
+    if (store & 2u)  // NS_BATCH_PAIRED: a pair never straddles two tiles
+      return launch_hyb_tp<2, GB, UB, US, AUXB, UD, SU, QS>(arena, arena_bytes, desc, n, out, partial, err, stream,
+                                                            big_chunks, store, zc);
     return launch_hyb_tp<1, GB, UB, US, AUXB, UD, SU, QS>(arena, arena_bytes, desc, n, out, partial, err, stream,
                                                           big_chunks, store, zc);
   }
@@ -1608,6 +1626,7 @@ hipError_t launch_batch(const uint8_t* arena, uint64_t arena_bytes,
   if (n == 0) return hipSuccess;
   hipError_t e;
   if (sizing_bytes == 0) sizing_bytes = arena_bytes;
+  if ((store & 2u) && (part || split || zc.flag)) return hipErrorInvalidValue;  // pairs: plain tiles only
   if (split && sizing_bytes / n >= kSplitAvg && n < kSplitMaxN) {
     // A few huge descriptors: spread each over many workgroups.  (`split`
     // holds zeros between launches: csum_split leaves it so.)  Each piece

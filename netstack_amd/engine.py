@@ -80,16 +80,19 @@ class Engine:
     # -- device-resident batch (the hot path) ------------------------------
     def batch_dev(self, arena_ptr: int, arena_bytes: int, desc_ptr: int, n: int,
                   out_ptr: int, chained: bool = False, stream: int | None = None,
-                  store: bool = False) -> None:
+                  store: bool = False, paired: bool = False) -> None:
         """Enqueue (asynchronously) the batch on `stream` (hipStream_t as int).
         With store=True (ns_csum_batch_dev_store) descriptors flagged
-        NS_DESC_STORE also write their result into the arena."""
+        NS_DESC_STORE also write their result into the arena; paired=True is
+        NS_BATCH_PAIRED (runs of two: an odd-indexed NS_DESC_CONT descriptor
+        continues the one before it)."""
         fn, name = (lib().ns_csum_batch_dev_store, "ns_csum_batch_dev_store") if store else \
             (lib().ns_csum_batch_dev, "ns_csum_batch_dev")
-        check(fn(self._h, arena_ptr, arena_bytes, desc_ptr, n, out_ptr,
-                 _lib.NS_BATCH_CHAINED if chained else 0, stream), name)
+        flags = (_lib.NS_BATCH_CHAINED if chained else 0) | (_lib.NS_BATCH_PAIRED if paired else 0)
+        check(fn(self._h, arena_ptr, arena_bytes, desc_ptr, n, out_ptr, flags, stream), name)
 
-    def batch_tensors(self, arena, desc, out=None, chained: bool = False, stream=None, store: bool = False):
+    def batch_tensors(self, arena, desc, out=None, chained: bool = False, stream=None, store: bool = False,
+                      paired: bool = False):
         """torch front end: `arena` uint8 CUDA tensor, `desc` CUDA tensor whose
         bytes are the 16-byte ns_pkt_desc table, `out` int16/uint16 CUDA tensor
         of n elements (allocated if None).  Launches on `stream` (a
@@ -109,7 +112,7 @@ class Engine:
         if stream is None:
             stream = torch.cuda.current_stream(arena.device)
         self.batch_dev(arena.data_ptr(), arena.numel() * arena.element_size(), desc.data_ptr(), n,
-                       out.data_ptr(), chained, stream.cuda_stream, store)
+                       out.data_ptr(), chained, stream.cuda_stream, store, paired)
         return out
 
     def stream_release(self, stream) -> None:

@@ -346,3 +346,140 @@ def tx_batch(n: int, seed: int, device, fused: bool = True):
     (arena, desc)."""
     arena, _ = _tcp_packets(n, seed, device)
     return arena, tx_desc(n, fused)
+
+
+# ---------------------------------------------------------------------------
+# Transmit batches laid out as sendTCPBatch builds them (transport/tcp/
+# connect.go:668-702).  stack.NewPacketDescriptors(n, hdrSize) allocates ONE
+# buffer of n * hdrSize bytes and gives segment i a Prependable over slot i
+# (stack/route.go:181-188); buildTCPHdr prepends the TCP header at the slot's
+# end, addIPHeader the IPv4 header before it (the link header's room comes
+# first); the payload is one VectorisedView, segment i at Off = i * MSS.  In
+# HBM: [n header slots | payload], one arena.  Per packet (3 descriptors,
+# NS_BATCH_CHAINED):
+#   3i    the IPv4 header [slot+14, +20)                       store ^sum at +10
+#   3i+1  the payload [P + i*MSS, +MSS), initial = ChecksumCombine(1480, 6)
+#   3i+2  src+dst addresses and the TCP header [slot+26, +28), NS_DESC_CONT:
+#         the run's final value (PseudoHeaderChecksum, ChecksumVVWithOffset,
+#         CalculateChecksum: restarts at even offsets, no uint32 wrap, so the
+#         order of the pieces does not change the folded sum; DESIGN.md §2)
+#                                                              store ^sum at +24
+# = TCP byte 16.  The checksum fields are dense (two per 54-B slot), where in
+# the wire layout (tx_batch) they sit one packet stride apart.
+# ---------------------------------------------------------------------------
+TX_HDR = 54     # TCPMinimumSize + MaxHeaderLength (IPv4 20 + Ethernet 14), no options
+TX_MSS = RX_TCP - 20  # 1460
+TX_IP_AT = 14   # the IPv4 header's offset in a slot
+TX_TCP_AT = 34  # the TCP header's offset in a slot
+
+
+def tx_split_layout(n: int) -> tuple[int, int]:
+    """(payload region offset, arena bytes) of the sendTCPBatch layout."""
+    pay = (n * TX_HDR + 4095) // 4096 * 4096
+    return pay, pay + n * TX_MSS
+
+
+def tx_split_desc(n: int, store: bool = True, paired: bool = False) -> np.ndarray:
+    """The table over the sendTCPBatch layout.  Chained (NS_BATCH_CHAINED):
+    per packet [IPv4 header, payload, addresses + TCP header (CONT)].  Paired
+    (NS_BATCH_PAIRED, n even): per two packets 2k, 2k+1
+        6k    payload of 2k       6k+1  addresses + TCP header of 2k (CONT)
+        6k+2  IPv4 header of 2k   6k+3  IPv4 header of 2k+1
+        6k+4  payload of 2k+1     6k+5  addresses + TCP header of 2k+1 (CONT)
+    so every pair starts at an even index and each packet's descriptors stay
+    together.  tx_split_order(n, paired) maps packets to their results."""
+    d = _tx_split_chained(n, store)
+    if not paired:
+        return d
+    if n % 2:
+        raise ValueError("the paired table needs an even packet count")
+    ip, pay_, tcp = d[0::3].reshape(-1, 2), d[1::3].reshape(-1, 2), d[2::3].reshape(-1, 2)
+    p = np.zeros(3 * n, dtype=DESC_DTYPE).reshape(-1, 6)
+    p[:, 0], p[:, 1] = pay_[:, 0], tcp[:, 0]
+    p[:, 2], p[:, 3] = ip[:, 0], ip[:, 1]
+    p[:, 4], p[:, 5] = pay_[:, 1], tcp[:, 1]
+    return p.reshape(-1)
+
+
+def tx_split_order(n: int, paired: bool) -> tuple[np.ndarray, np.ndarray]:
+    """(index of each packet's IPv4 result, index of its TCP result) in the
+    results of tx_split_desc(n, paired=...)."""
+    i = np.arange(n)
+    if not paired:
+        return 3 * i, 3 * i + 2
+    k, odd = i // 2, i % 2
+    return 6 * k + 2 + odd, 6 * k + 1 + 4 * odd
+
+
+def _tx_split_chained(n: int, store: bool) -> np.ndarray:
+    pay, _ = tx_split_layout(n)
+    slot = np.arange(n, dtype=np.uint64) * np.uint64(TX_HDR)
+    d = np.zeros(3 * n, dtype=DESC_DTYPE)
+    d["off"][0::3] = slot + np.uint64(TX_IP_AT)
+    d["len"][0::3] = RX_IHL
+    d["off"][1::3] = np.uint64(pay) + np.arange(n, dtype=np.uint64) * np.uint64(TX_MSS)
+    d["len"][1::3] = TX_MSS
+    d["initial"][1::3] = RX_TCP + 6  # ChecksumCombine(1480, 6): no carry
+    d["off"][2::3] = slot + np.uint64(TX_IP_AT + 12)
+    d["len"][2::3] = 8 + 20
+    d["flags"][2::3] = 2  # NS_DESC_CONT
+    if store:
+        d["flags"][0::3] |= 0x4 | (TX_IP_CSUM << 4)
+        d["flags"][2::3] |= 0x4 | ((TX_TCP_AT - (TX_IP_AT + 12) + TX_TCP_CSUM) << 4)
+    return d
+
+
+def _split_packets(n: int, seed: int, device):
+    """The sendTCPBatch-layout arena (splitmix64 bytes with fixed header
+    fields, both checksum fields zero) and views of its header slots and
+    payloads."""
+    pay, total = tx_split_layout(n)
+    arena = random_bytes_torch(seed, total, device)
+    h = arena[:n * TX_HDR].view(n, TX_HDR)
+    ip = h[:, TX_IP_AT:TX_IP_AT + RX_IHL]
+    ip[:, 0] = 0x45
+    ip[:, 1] = 0
+    ip[:, 2] = RX_PKT >> 8
+    ip[:, 3] = RX_PKT & 0xFF
+    ip[:, 6] = 0x40
+    ip[:, 7] = 0
+    ip[:, 8] = 64
+    ip[:, 9] = 6
+    ip[:, 10:12] = 0
+    t = h[:, TX_TCP_AT:TX_TCP_AT + 20]
+    t[:, 12] = 0x50
+    t[:, 13] = 0x18
+    t[:, 16:20] = 0
+    return arena, h, arena[pay:pay + n * TX_MSS].view(n, TX_MSS)
+
+
+def tx_split_batch(n: int, seed: int, device):
+    """n outbound IPv4/TCP segments in the sendTCPBatch layout with both
+    checksum fields zero, and tx_split_desc(n).  One ns_csum_batch_dev_store
+    launch with NS_BATCH_CHAINED fills them; afterwards the arena equals
+    tx_split_expected(n, seed)'s.  Returns (arena, desc)."""
+    arena, _, _ = _split_packets(n, seed, device)
+    return arena, tx_split_desc(n)
+
+
+def tx_split_expected(n: int, seed: int, device, chunk: int = 1 << 16):
+    """The same arena with both checksum fields written (RFC 1071 sums with
+    torch integer ops, as plain data generation, per chunk of packets)."""
+    import torch
+
+    arena, h, p = _split_packets(n, seed, device)
+
+    def be_sum(x):
+        w = x.to(torch.int64)
+        return (w[:, 0::2] * 256 + w[:, 1::2]).sum(dim=1)
+
+    for a in range(0, n, chunk):
+        b = min(n, a + chunk)
+        hh, pp = h[a:b], p[a:b]
+        ip = (~_fold_np(be_sum(hh[:, TX_IP_AT:TX_IP_AT + RX_IHL]))) & 0xFFFF
+        hh[:, TX_IP_AT + 10] = (ip >> 8).to(torch.uint8)
+        hh[:, TX_IP_AT + 11] = (ip & 0xFF).to(torch.uint8)
+        tcp = (~_fold_np(be_sum(hh[:, TX_IP_AT + 12:TX_TCP_AT + 20]) + be_sum(pp) + RX_TCP + 6)) & 0xFFFF
+        hh[:, TX_TCP_AT + 16] = (tcp >> 8).to(torch.uint8)
+        hh[:, TX_TCP_AT + 17] = (tcp & 0xFF).to(torch.uint8)
+    return arena

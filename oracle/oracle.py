@@ -266,6 +266,17 @@ def c_batch(arena: np.ndarray, desc: np.ndarray, chained: bool = False) -> tuple
     return out, int(bad)
 
 
+def c_batch_paired(arena: np.ndarray, desc: np.ndarray) -> tuple[np.ndarray, int]:
+    """NS_BATCH_PAIRED (include/netstack_csum.h): runs of at most two.  An
+    odd-indexed NS_DESC_CONT descriptor continues the one before it (Go's
+    `xsum = Checksum(v, xsum)` chaining, checksum.go:89); a CONT flag on an
+    even-indexed one is ignored.  That is the chained semantics on the table
+    with its even-indexed CONT bits cleared."""
+    d = np.array(desc, dtype=DESC_DTYPE, copy=True)
+    d["flags"][0::2] &= ~np.uint16(CONT)
+    return c_batch(arena, d, chained=True)
+
+
 def c_batch_mt(arena: np.ndarray, desc: np.ndarray, nthreads: int, out: np.ndarray | None = None) -> np.ndarray:
     """Packet-parallel scalar port over `nthreads` pthreads (independent
     descriptors only).  This is the timed CPU baseline."""

@@ -1311,3 +1311,117 @@ def test_gathers_across_stage_sizes(engine, total):
     assert engine.vv_batch(views, segs).tolist() == [O.c_checksum_vv_with_offset(vb, i, o, s) for o, s, i in segs]
     buf = np.concatenate(views)
     assert engine.checksum(buf, 0xBEEF) == O.c_checksum(buf.tobytes(), 0xBEEF)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_paired_batches_match_the_oracle(engine, seed):
+    """NS_BATCH_PAIRED (include/netstack_csum.h): an odd-indexed CONT
+    descriptor continues the one before it, a CONT bit on an even-indexed one
+    is ignored; the pair is folded inside the tile.  Random tables with CONT
+    bits anywhere, ODD bits, small packets (64-wide one-wave tiles) and big
+    ones (tiles of 2 to 256 descriptors, the 2-descriptor floor included),
+    with and without stores, against oracle.c_batch_paired and
+    oracle.apply_stores."""
+    import oracle as O
+
+    torch = _torch()
+    rng = np.random.default_rng(1700 + seed)
+    arena, d = _store_batch(rng, int(rng.integers(1, 4000)), True, seed >= 3)
+    want, bad = O.c_batch_paired(arena, d)
+    assert bad == 0
+    expect, dropped = O.apply_stores(arena, d, want)
+    assert dropped == 0
+    dt = torch.from_numpy(arena).cuda()
+    desc = torch.from_numpy(d.view(np.uint8).copy()).cuda()
+    out = engine.batch_tensors(dt, desc, paired=True)
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy().view(np.uint16), want)
+    assert np.array_equal(dt.cpu().numpy(), arena)
+    out = engine.batch_tensors(dt, desc, paired=True, store=True)
+    torch.cuda.synchronize()
+    assert engine.sync() == 0
+    assert np.array_equal(out.cpu().numpy().view(np.uint16), want)
+    got = dt.cpu().numpy()
+    assert np.array_equal(got, expect), np.flatnonzero(got != expect)[:8]
+
+
+def test_paired_continuation_wraps_as_go_does(engine):
+    """A pair whose continuation's word sum reaches 2^32 - 1 (131,074 bytes of
+    0xFF: Go's uint32 accumulator wraps once the initial is added) and pieces
+    of up to 3 MB (exact accumulation, and 1 MiB+ averages that unpaired
+    batches send to csum_split): the in-tile fold reproduces Go's wrap."""
+    import oracle as O
+
+    torch = _torch()
+    rng = np.random.default_rng(1777)
+    lens = [100, 131074, 7, 131074, 131073, 131074, 3_000_001, 200_000, 0, 131074, 65536, 2_500_000]
+    init = rng.integers(0, 65536, len(lens)).astype(np.uint16)
+    flags = np.array([0, 2, 2, 2, 1, 2, 0, 3, 0, 2, 2, 2], np.uint16)
+    from netstack_amd import workloads as W
+
+    d, end = W.make_desc(np.array(lens, np.uint32), init, align=2, flags=flags)
+    arena = np.full(end + 16, 0xFF, np.uint8)
+    arena[: end // 3] = rng.integers(0, 256, end // 3, dtype=np.uint8)
+    want, _ = O.c_batch_paired(arena, d)
+    out = engine.batch_tensors(torch.from_numpy(arena).cuda(), torch.from_numpy(d.view(np.uint8).copy()).cuda(),
+                               paired=True)
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy().view(np.uint16), want)
+
+
+@pytest.mark.parametrize("paired", [False, True])
+def test_tx_split_layout_fill(engine, paired):
+    """The transmit side in the layout sendTCPBatch builds
+    (stack.NewPacketDescriptors' one buffer of header slots, the payload in a
+    separate view; workloads.tx_split_*): chained (fold pass) or paired
+    (in-tile) tables fill every IPv4 and TCP checksum field.  Results match the
+    oracle over the pre-store bytes, the arena equals the one whose checksums
+    torch integer ops computed independently, and every filled segment
+    verifies."""
+    import oracle as O
+    from netstack_amd import workloads as W
+
+    torch = _torch()
+    n = 20000
+    arena, _ = W.tx_split_batch(n, 77, "cuda")
+    d = W.tx_split_desc(n, True, paired)
+    before = arena.cpu().numpy()
+    want, nbad = O.c_batch_paired(before, d) if paired else O.c_batch(before, d, chained=True)
+    assert nbad == 0
+    desc = torch.from_numpy(d.view(np.uint8).copy()).cuda()
+    out = engine.batch_tensors(arena, desc, chained=not paired, paired=paired, store=True)
+    torch.cuda.synchronize()
+    assert engine.sync() == 0
+    assert np.array_equal(out.cpu().numpy().view(np.uint16), want)
+    assert torch.equal(arena, W.tx_split_expected(n, 77, "cuda"))
+    vd = torch.from_numpy(W.tx_split_desc(n, False, paired).view(np.uint8).copy()).cuda()
+    chk = engine.batch_tensors(arena, vd, chained=not paired, paired=paired).cpu().numpy().view(np.uint16)
+    ip, tcp = W.tx_split_order(n, paired)
+    assert (chk[ip] == 0xFFFF).all() and (chk[tcp] == 0xFFFF).all()
+
+
+def test_paired_flag_is_device_resident_only(engine):
+    """NS_BATCH_PAIRED with NS_BATCH_CHAINED, or on the host-memory entry
+    point, is NS_EINVAL."""
+    import ctypes
+
+    from netstack_amd import _lib
+
+    torch = _torch()
+    a = torch.zeros(64, dtype=torch.uint8, device="cuda")
+    d = np.zeros(2, dtype=_lib_desc_dtype())
+    d["len"] = 8
+    desc = torch.from_numpy(d.view(np.uint8).copy()).cuda()
+    with pytest.raises(ValueError):
+        engine.batch_tensors(a, desc, chained=True, paired=True)
+    ha = np.zeros(64, np.uint8)
+    out = np.zeros(2, np.uint16)
+    rc = _lib.lib().ns_csum_batch_host(engine._h, ha.ctypes.data, ha.size, d.ctypes.data, 2,
+                                       out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint16)), _lib.NS_BATCH_PAIRED)
+    assert rc == _lib.NS_EINVAL
+
+
+def _lib_desc_dtype():
+    from netstack_amd.engine import DESC_DTYPE
+
+    return DESC_DTYPE
