@@ -53,7 +53,11 @@ def parse():
                          "8 = device-resident TX checksum fill (SURVEY §8(f) ranks 2 and 1)")
     ap.add_argument("--mode", default="dev", choices=("dev", "host"))
     ap.add_argument("--rx-layout", default="fused", choices=("fused", "chained"),
-                    help="--config 7/8 descriptor table: 2 independent descriptors per packet, or 3 chained")
+                    help="--config 7 (and 8 with --tx-layout wire) descriptor table: 2 independent descriptors "
+                         "per packet, or 3 chained")
+    ap.add_argument("--tx-layout", default="split", choices=("split", "wire"),
+                    help="--config 8 packets: as sendTCPBatch builds them (header slots + payload view, "
+                         "NS_BATCH_PAIRED), or wire-contiguous like config 7")
     ap.add_argument("--rotate", type=int, default=0,
                     help="distinct batches cycled per step (0 = auto: enough to exceed the 256 MiB MALL)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline time budget")
@@ -643,11 +647,17 @@ def packet_mode(args, dist, eng, dev, tx: bool):
     checker.go:51-53) — a size-independent property over all 1M packets.
 
     TX (config 8, rank 1: buildTCPHdr + addIPHeader for a whole batch): the
-    same packets with zeroed checksum fields, ns_csum_batch_dev_store writes
+    same segments with zeroed checksum fields, ns_csum_batch_dev_store writes
     ^sum into both fields of every packet (connect.go:662-663, ipv4.go:236).
-    The fields are re-zeroed after the timed region and filled by one more
-    launch; the check requires the whole arena to equal rx_batch's, whose
-    checksums torch integer ops computed independently.
+    By default (`--tx-layout split`) the segments are laid out as
+    sendTCPBatch builds them: stack.NewPacketDescriptors' one buffer of 54-B
+    header slots (route.go:181-188) and the payload in a view of its own
+    (workloads.tx_split_*), three descriptors per packet with the payload +
+    TCP header pair folded in the tile (NS_BATCH_PAIRED).  `--tx-layout wire`
+    keeps config 7's wire-contiguous packets.  The fields are re-zeroed after
+    the timed region and filled by one more launch; the check requires the
+    whole arena to equal one whose checksums torch integer ops computed
+    independently, and every filled segment to verify.
 
     value = packet bytes / s (GiB/s)."""
     import torch
@@ -655,10 +665,17 @@ def packet_mode(args, dist, eng, dev, tx: bool):
     from netstack_amd import workloads as W
 
     seed = 7000 + dist.rank
+    split = tx and args.tx_layout == "split"
     fused = args.rx_layout == "fused"
-    chained = not fused
+    chained = not fused and not split
     k = W.per_packet(fused)
-    if tx:
+    if split:
+        arena, _ = W.tx_split_batch(RX_N, seed, dev)
+        d = W.tx_split_desc(RX_N, True, paired=True)
+        ip_at, tcp_at = W.tx_split_order(RX_N, True)
+        k = 3
+        bad_idx = np.zeros(0, np.int64)
+    elif tx:
         arena, d = W.tx_batch(RX_N, seed, dev, fused=fused)
         bad_idx = np.zeros(0, np.int64)
     else:
@@ -673,7 +690,7 @@ def packet_mode(args, dist, eng, dev, tx: bool):
         k = state["i"]
         if k == args.warmup:
             ev[0].record(stream)
-        eng.batch_tensors(arena, desc, out, chained=chained, stream=stream, store=tx)
+        eng.batch_tensors(arena, desc, out, chained=chained, stream=stream, store=tx, paired=split)
         state["i"] = k + 1
         if state["i"] == args.warmup + args.steps:
             ev[1].record(stream)
@@ -682,24 +699,30 @@ def packet_mode(args, dist, eng, dev, tx: bool):
     bad = eng.sync()
     kern_avg_s = ev[0].elapsed_time(ev[1]) / 1e3 / args.steps
     k_cpu = k * 65536
-    span = int(d["off"][k_cpu - 1] + d["len"][k_cpu - 1])
+    span = int((d["off"][:k_cpu] + d["len"][:k_cpu].astype(np.uint64)).max())
     if tx:
         # untimed: re-zero both fields, fill them with one launch, check
-        p = arena.view(RX_N, W.RX_STRIDE)
-        p[:, 10:12] = 0
-        p[:, 36:38] = 0
+        if split:
+            h = arena[:RX_N * W.TX_HDR].view(RX_N, W.TX_HDR)
+            h[:, W.TX_IP_AT + 10:W.TX_IP_AT + 12] = 0
+            h[:, W.TX_TCP_AT + 16:W.TX_TCP_AT + 18] = 0
+        else:
+            p = arena.view(RX_N, W.RX_STRIDE)
+            p[:, 10:12] = 0
+            p[:, 36:38] = 0
         before = arena[:span].cpu().numpy() if dist.rank == 0 and not args.no_cpu else None
-        eng.batch_tensors(arena, desc, out, chained=chained, stream=stream, store=True)
+        eng.batch_tensors(arena, desc, out, chained=chained, stream=stream, store=True, paired=split)
         torch.cuda.synchronize()
         bad += eng.sync()
-        rx, _, _ = W.rx_batch(RX_N, seed, dev)
+        rx = W.tx_split_expected(RX_N, seed, dev) if split else W.rx_batch(RX_N, seed, dev)[0]
         arena_ok = bool(torch.equal(arena, rx))
         del rx
-        chk = torch.from_numpy(W._tcp_desc(RX_N, fused).view(np.uint8).copy()).to(dev)
-        vres = eng.batch_tensors(arena, chk, chained=chained, stream=stream).cpu().numpy().view(np.uint16)
+        vd = W.tx_split_desc(RX_N, False, paired=True) if split else W._tcp_desc(RX_N, fused)
+        chk = torch.from_numpy(vd.view(np.uint8).copy()).to(dev)
+        vres = eng.batch_tensors(arena, chk, chained=chained, stream=stream, paired=split).cpu().numpy().view(np.uint16)
         res = out.cpu().numpy().view(np.uint16)
-        ip_ok = vres[0::k] == 0xFFFF
-        tcp_fail = np.flatnonzero(vres[k - 1::k] != 0xFFFF)
+        ip_ok = vres[ip_at if split else slice(0, None, k)] == 0xFFFF
+        tcp_fail = np.flatnonzero(vres[tcp_at if split else slice(k - 1, None, k)] != 0xFFFF)
         prop_ok = arena_ok and bool(ip_ok.all()) and tcp_fail.size == 0
     else:
         before = None
@@ -716,7 +739,7 @@ def packet_mode(args, dist, eng, dev, tx: bool):
     # then read back); TX adds the two 2-B field stores per packet
     algo = pkt_bytes + 8 * RX_N + n_desc * (16 + 2 + (12 if chained else 0)) + (4 * RX_N if tx else 0)
     achieved = algo / kern_avg_s / 1e9
-    traffic, traffic_src = pmc_traffic(args.pmc_json, 8 if tx else 7) if fused else (None, None)
+    traffic, traffic_src = pmc_traffic(args.pmc_json, 8 if tx else 7) if fused and not split else (None, None)
     check = {"ipv4_all_valid": bool(ip_ok.all()), "tcp_failures": int(tcp_fail.size),
              "expected_failures": int(bad_idx.size), "ok": prop_ok, "ranks_failed": int(fails)}
     if tx:
@@ -730,12 +753,15 @@ def packet_mode(args, dist, eng, dev, tx: bool):
         "data": ("synthetic packets to send (checksum fields zero), resident in HBM" if tx else
                  "synthetic received packets (valid IPv4/TCP checksums, 1 in 1000 corrupted), resident in HBM"),
         "config": {"workload": ("tx" if tx else "rx") + ": 1,048,576 x 1500-B IPv4/TCP packets per GPU, "
-                   + ("2 descriptors each (IPv4 header; pseudo-header addresses + TCP segment)" if fused
+                   + ("in sendTCPBatch's layout (54-B header slots + a payload view), 3 descriptors each "
+                      "(IPv4 header; payload + pseudo-header addresses and TCP header, NS_BATCH_PAIRED)" if split
+                      else "2 descriptors each (IPv4 header; pseudo-header addresses + TCP segment)" if fused
                       else "3 chained descriptors each") + (", 2 checksum stores" if tx else ""),
                    "packets_per_gpu": RX_N, "descriptors_per_gpu": n_desc},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                      "kernel": kernel_name(arena.numel(), n_desc, chained=chained) + (" + nsk::fold_scan" if chained else ""),
+                     "layout": "split (sendTCPBatch: header slots + payload view)" if split else "wire",
                      "algorithmic_bytes_per_launch": algo, "avg_launch_us": kern_avg_s * 1e6},
         "bad_descriptors": bad,
         "property_check": check,
@@ -746,7 +772,7 @@ def packet_mode(args, dist, eng, dev, tx: bool):
         # CPU leg: the oracle on the first 65,536 packets' descriptors, same
         # bytes (TX: the bytes before the checked launch, and its stores)
         src = before if tx else arena[:span].cpu().numpy()
-        want, _ = O.c_batch(src, d[:k_cpu], chained=chained)
+        want, _ = O.c_batch_paired(src, d[:k_cpu]) if split else O.c_batch(src, d[:k_cpu], chained=chained)
         ps = {"packets": k_cpu // k, "bit_exact": bool(np.array_equal(res[:k_cpu], want))}
         if tx:
             stored, _ = O.apply_stores(src, d[:k_cpu], want)

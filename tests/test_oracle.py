@@ -286,3 +286,54 @@ def test_packet_oracle_fill_then_verify(oracle_mod):
     struct.pack_into(">BBHHHBBH", ip, 0, 0x45, 0, 20 + 8 + 5, 7, 0, 64, 1, 0)
     hdr, _, _ = P.fill(bytes(ip + icmp), [b"hello"], 5)
     assert P.verify(b"", [hdr + b"hello"], len(hdr) + 5)[0] == P.VALID
+
+
+def test_paired_oracle_is_go_chaining_on_runs_of_two(oracle_mod):
+    """oracle.c_batch_paired (NS_BATCH_PAIRED): each odd-indexed CONT
+    descriptor takes the previous descriptor's result as its initial —
+    checked against the pure-Python restatement of checksum.go run descriptor
+    by descriptor — and an even-indexed CONT bit changes nothing."""
+    import oracle as O
+
+    rng = np.random.default_rng(4242)
+    n = 301
+    arena = rng.integers(0, 256, 20000, dtype=np.uint8)
+    d = np.zeros(n, dtype=O.DESC_DTYPE)
+    d["off"] = rng.integers(0, 19000, n)
+    d["len"] = rng.integers(0, 900, n)
+    d["initial"] = rng.integers(0, 65536, n)
+    d["flags"] = rng.integers(0, 4, n)  # ODD and CONT anywhere
+    got, bad = O.c_batch_paired(arena, d)
+    assert bad == 0
+    want, prev = [], 0
+    for i in range(n):
+        o, ln, f = int(d["off"][i]), int(d["len"][i]), int(d["flags"][i])
+        init = prev if (i % 2 == 1 and f & O.CONT) else int(d["initial"][i])
+        s, _ = O.py_calculate_checksum(bytes(arena[o:o + ln]), bool(f & O.ODD), init)
+        want.append(s)
+        prev = s
+    assert got.tolist() == want
+
+
+def test_tx_split_layout_is_the_wire_segments_checksummed(oracle_mod):
+    """workloads.tx_split_*: the sendTCPBatch layout (54-B header slots, a
+    payload view).  The oracle's chained and paired fills equal the
+    independently computed arena, and the filled segments verify."""
+    import oracle as O
+    from netstack_amd import workloads as W
+
+    n = 1000
+    arena, _ = W.tx_split_batch(n, 5, "cpu")
+    exp = W.tx_split_expected(n, 5, "cpu", chunk=300).numpy()
+    a = arena.numpy()
+    for paired in (False, True):
+        d = W.tx_split_desc(n, True, paired)
+        want, bad = O.c_batch_paired(a, d) if paired else O.c_batch(a, d, chained=True)
+        st, dropped = O.apply_stores(a, d, want)
+        assert bad == 0 and dropped == 0 and np.array_equal(st, exp)
+        vd = W.tx_split_desc(n, False, paired)
+        res, _ = O.c_batch_paired(exp, vd) if paired else O.c_batch(exp, vd, chained=True)
+        ip, tcp = W.tx_split_order(n, paired)
+        assert (res[ip] == 0xFFFF).all() and (res[tcp] == 0xFFFF).all()
+    with pytest.raises(ValueError):
+        W.tx_split_desc(3, True, paired=True)
