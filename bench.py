@@ -327,7 +327,7 @@ def floor_calibration(arenas, descs, batch, stream, reps: int = 40):
             "variants": variants, "best": best, "GBps": variants[best]["GBps"]}
 
 
-def pmc_traffic(path: str, cfg: int):
+def pmc_traffic(path: str, cfg):
     """roofline.traffic: HBM bytes per launch (reads + writes) of this config's
     kernel from the committed rocprofv3 --pmc summary (tools/make_traffic.py),
     and where they come from — counters are taken in passes of their own,
@@ -739,7 +739,8 @@ def packet_mode(args, dist, eng, dev, tx: bool):
     # then read back); TX adds the two 2-B field stores per packet
     algo = pkt_bytes + 8 * RX_N + n_desc * (16 + 2 + (12 if chained else 0)) + (4 * RX_N if tx else 0)
     achieved = algo / kern_avg_s / 1e9
-    traffic, traffic_src = pmc_traffic(args.pmc_json, 8 if tx else 7) if fused and not split else (None, None)
+    traffic, traffic_src = (pmc_traffic(args.pmc_json, "8split") if split else
+                            pmc_traffic(args.pmc_json, 8 if tx else 7) if fused else (None, None))
     check = {"ipv4_all_valid": bool(ip_ok.all()), "tcp_failures": int(tcp_fail.size),
              "expected_failures": int(bad_idx.size), "ok": prop_ok, "ranks_failed": int(fails)}
     if tx:

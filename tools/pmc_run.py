@@ -99,6 +99,20 @@ def main_set(dev, L):
               f"big_share={big_share(d):.4f}", flush=True)
         del arena, desc, out
         torch.cuda.empty_cache()
+    # cfg 8 as bench.py runs it by default: sendTCPBatch's layout, NS_BATCH_PAIRED
+    n = 1 << 20
+    arena, _ = W.tx_split_batch(n, 7000, dev)
+    d = W.tx_split_desc(n, True, paired=True)
+    desc = torch.from_numpy(d.view(np.uint8).copy()).to(dev)
+    out = torch.empty(len(d), dtype=torch.int16, device=dev)
+    for _ in range(REPS):
+        eng.batch_tensors(arena, desc, out, store=True, paired=True)
+    torch.cuda.synchronize()
+    algo = n * W.RX_PKT + 8 * n + len(d) * 18 + 4 * n
+    print(f"LABEL cfg8split algorithmic_bytes={algo} payload={n * W.RX_PKT} arena={arena.numel()} n={len(d)} "
+          f"big_share={big_share(d):.4f}", flush=True)
+    del arena, desc, out
+    torch.cuda.empty_cache()
 
 
 def cfg3probe_set(dev, L):

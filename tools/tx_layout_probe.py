@@ -16,6 +16,9 @@ Variants, each over 2 rotating batches, median of `--rounds` rounds of
   split_rx / split_tx      the sendTCPBatch layout, 3 chained descriptors
   paired_rx / paired_tx    the sendTCPBatch layout, NS_BATCH_PAIRED (the
                            payload + TCP header pair folded in the tile)
+  paired_two_pass          paired_rx, then libns_tune.so's store pass (the
+                           table re-read, the results from `out`)
+  store_pass_only          that store pass alone, repeated
 The store cost of a layout is tx - rx.  Every TX fill is checked byte for
 byte against independently computed arenas.
 
@@ -24,6 +27,7 @@ byte against independently computed arenas.
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -50,6 +54,10 @@ def main():
     stream = torch.cuda.current_stream(dev)
     eng = Engine(0)
     out = torch.empty(3 * n, dtype=torch.int16, device=dev)
+    L = ctypes.CDLL(os.path.join(ROOT, "netstack_amd", "lib", "libns_tune.so"))
+    L.nsk_store_pass_launch.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint32,
+                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    err = torch.zeros(1, dtype=torch.int64, device=dev)
 
     def tdesc(d):
         return torch.from_numpy(d.view(np.uint8).copy()).to(dev)
@@ -75,9 +83,18 @@ def main():
         "paired_rx": lambda r: eng.batch_tensors(batches[r][1], pd[1], out, paired=True, stream=stream),
         "paired_tx": lambda r: eng.batch_tensors(batches[r][1], pd[0], out, paired=True, stream=stream, store=True),
     }
+
+    def store_pass(r):
+        a = batches[r][1]
+        assert L.nsk_store_pass_launch(a.data_ptr(), a.numel(), pd[0].data_ptr(), 3 * n, out.data_ptr(),
+                                       err.data_ptr(), stream.cuda_stream) == 0
+
+    variants["paired_two_pass"] = lambda r: (eng.batch_tensors(batches[r][1], pd[0], out, paired=True,
+                                                               stream=stream), store_pass(r))
+    variants["store_pass_only"] = store_pass
     # correctness of every TX fill (checked after one launch on batch 0)
     checks = {}
-    for name in ("wire_fused_tx", "wire_chained_tx", "split_tx", "paired_tx"):
+    for name in ("wire_fused_tx", "wire_chained_tx", "split_tx", "paired_tx", "paired_two_pass"):
         if name.startswith("wire"):  # the fields back to zero (a fill sums them)
             p = batches[0][0].view(n, W.RX_STRIDE)
             p[:, 10:12] = 0
@@ -92,7 +109,7 @@ def main():
         got = batches[0][0] if name.startswith("wire") else batches[0][1]
         checks[name] = bool(torch.equal(got, want))
         del want
-    assert eng.sync() == 0
+    assert eng.sync() == 0 and int(err.item()) == 0
     times = {k: [] for k in variants}
     for _ in range(args.rounds):
         for name, f in variants.items():
@@ -110,7 +127,8 @@ def main():
            "store_cost_us": {"wire_fused": med["wire_fused_tx"] - med["wire_fused_rx"],
                              "wire_chained": med["wire_chained_tx"] - med["wire_chained_rx"],
                              "split": med["split_tx"] - med["split_rx"],
-                             "paired": med["paired_tx"] - med["paired_rx"]}}
+                             "paired": med["paired_tx"] - med["paired_rx"],
+                             "paired_two_pass": med["paired_two_pass"] - med["paired_rx"]}}
     print(json.dumps(res, indent=1))
 
 
