@@ -166,6 +166,37 @@ struct ChainBuilder {
   }
 };
 
+// A vector whose first N elements live inline: a packet of a handful of views
+// needs no heap allocation (two per packet were ~a third of the planning
+// time of a recvmmsg batch; tools/plan_cost.cc).
+template <class T, size_t N>
+class InlineVec {
+ public:
+  void reserve(size_t) {}
+  void push_back(const T& v) {
+    if (n_ < N) {
+      inl_[n_] = v;
+    } else {
+      if (n_ == N) heap_.assign(inl_, inl_ + N);
+      heap_.push_back(v);
+    }
+    ++n_;
+  }
+  template <class... A>
+  void emplace_back(A&&... a) {
+    push_back(T{std::forward<A>(a)...});
+  }
+  size_t size() const { return n_; }
+  const T& operator[](size_t i) const { return n_ <= N ? inl_[i] : heap_[i]; }
+  const T* begin() const { return n_ <= N ? inl_ : heap_.data(); }
+  const T* end() const { return begin() + n_; }
+
+ private:
+  T inl_[N];
+  std::vector<T> heap_;
+  size_t n_ = 0;
+};
+
 // ---- tcpip.PacketBuffer batches (ns_csum_packet_buffers) -------------------
 // A packet as one byte stream: its Header bytes, then its Data views clipped
 // to Data.Size() (packet_buffer.go:25-50).  The host reads header fields from
@@ -173,8 +204,8 @@ struct ChainBuilder {
 // cuts it into the pieces of each reference call sequence; every sum is
 // computed by the kernel.
 struct PacketBytes {
-  std::vector<std::pair<const uint8_t*, uint64_t>> seg;  // non-empty segments in order
-  std::vector<uint64_t> at;                             // byte offset of each segment
+  InlineVec<std::pair<const uint8_t*, uint64_t>, 8> seg;  // non-empty segments in order
+  InlineVec<uint64_t, 8> at;                              // byte offset of each segment
   uint64_t size = 0;
   uint64_t hdr_len = 0;  // bytes [0, hdr_len) are the Header's (writable)
 
