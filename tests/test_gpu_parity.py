@@ -1425,3 +1425,28 @@ def _lib_desc_dtype():
     from netstack_amd.engine import DESC_DTYPE
 
     return DESC_DTYPE
+
+
+def test_paired_ring_of_fixed_slots(engine):
+    """NS_BATCH_PAIRED on a receive ring of fixed 64-B slots (the one-wave
+    small-packet tiles with speculative payload loads, csum_kernels.hip
+    spec_load): pairs of slots chained, odd and even CONT bits, against the
+    oracle."""
+    import oracle as O
+
+    torch = _torch()
+    rng = np.random.default_rng(1811)
+    n = 50_001
+    arena = rng.integers(0, 256, n * 64, dtype=np.uint8)
+    from netstack_amd.engine import DESC_DTYPE
+
+    d = np.zeros(n, dtype=DESC_DTYPE)
+    d["off"] = np.arange(n, dtype=np.uint64) * np.uint64(64)
+    d["len"] = rng.integers(0, 65, n)
+    d["initial"] = rng.integers(0, 65536, n)
+    d["flags"] = rng.integers(0, 4, n)
+    want, _ = O.c_batch_paired(arena, d)
+    out = engine.batch_tensors(torch.from_numpy(arena).cuda(), torch.from_numpy(d.view(np.uint8).copy()).cuda(),
+                               paired=True)
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy().view(np.uint16), want)

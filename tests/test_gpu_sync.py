@@ -76,3 +76,36 @@ def test_small_calls_under_uneven_load(engine):
     k = np.arange(0, n, 97)
     want, _ = O.c_batch(host, d[k])
     assert np.array_equal(out.cpu().numpy().view(np.uint16)[k], want)
+
+
+def test_stats_count_calls_passes_and_reset():
+    """ns_csum_get_stats (a fresh context): every synchronous call is counted
+    and timed, small calls run as zero-copy passes (none late on an idle
+    device), a chained device-resident batch on a new stream grows its
+    scratch once, ns_csum_stream_release retires it, and reset zeroes every
+    counter."""
+    import torch
+
+    from netstack_amd import Engine
+    from netstack_amd import workloads as W
+
+    eng = Engine(0)
+    try:
+        st = eng.stats(reset=True)
+        for _ in range(20):
+            eng.checksum(np.arange(1500, dtype=np.uint8), 7)
+        st = eng.stats()
+        assert st["calls"] == 20 and 20 >= st["zc_passes"] >= 1 and st["zc_late"] == 0, st
+        assert 0 < st["call_ns_max"] < 1e9 and st["zc_pass_ns_max"] <= st["call_ns_max"], st
+        lengths = np.full(1000, 100, np.uint32)
+        d, end = W.make_desc(lengths, np.zeros(1000, np.uint16), align=1, flags=np.full(1000, 2, np.uint16))
+        s = torch.cuda.Stream()
+        eng.batch_tensors(torch.zeros(end, dtype=torch.uint8, device="cuda"),
+                          torch.from_numpy(d.view(np.uint8).copy()).cuda(), chained=True, stream=s)
+        s.synchronize()
+        eng.stream_release(s)
+        st = eng.stats(reset=True)
+        assert st["growths"] >= 1 and st["retires"] == 1, st
+        assert all(v == 0 for v in eng.stats().values())
+    finally:
+        eng.close()
