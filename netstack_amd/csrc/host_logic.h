@@ -236,7 +236,8 @@ struct PacketBytes {
   }
   // Segment holding byte k (k < size).
   size_t seg_of(uint64_t k) const {
-    size_t lo = 0, hi = seg.size();
+    if (seg.size() < 2 || k < at[1]) return 0;  // the headers: nearly every lookup
+    size_t lo = 1, hi = seg.size();
     while (hi - lo > 1) {
       const size_t mid = (lo + hi) / 2;
       if (at[mid] <= k) lo = mid;
