@@ -89,6 +89,7 @@ struct ChainBuilder {
   Sink& bytes;
   std::vector<ns_pkt_desc> desc;
   std::vector<uint32_t> result_at;  // index of the descriptor holding each chain's result
+  std::vector<Piece> scratch;       // plan_packet's piece list, its capacity kept across packets
   explicit ChainBuilder(Sink& s) : bytes(s) {}
 
   // One chain (include/netstack_csum.h, ns_csum_chains): sum = initial,
@@ -365,7 +366,7 @@ int plan_packet(Builder& g, const PacketBytes& pb, uint32_t op, PacketPlan* pp) 
     }
     return NS_EINVAL;
   }
-  thread_local std::vector<Piece> ps;  // capacity kept across the packets of a batch
+  std::vector<Piece>& ps = g.scratch;  // capacity kept across the packets of a batch
   ps.clear();
   auto add_chain = [&](uint16_t init) {
     g.chain(ps.data(), ps.size(), init);
