@@ -1,12 +1,14 @@
 set -e
 # Every bench line of a round, on the GPU box: tools/final_round.sh TAG
-TAG=${1:-r03}
+TAG=${1:-r04}
 OUT=gpurun_out/final_$TAG
 mkdir -p $OUT
 for c in 1 2 3 4 5 7 8; do
   echo "bench cfg$c"
   timeout -k 10 300 python bench.py --config $c > $OUT/bench_cfg$c.json 2> $OUT/bench_cfg$c.err
 done
+echo "bench cfg8 wire layout"
+timeout -k 10 300 python bench.py --config 8 --tx-layout wire > $OUT/bench_cfg8_wire.json 2> $OUT/bench_cfg8_wire.err
 echo "host modes"
 for c in 2 3 4; do
   timeout -k 10 200 python bench.py --mode host --config $c --no-cpu --no-parity > $OUT/bench_host$c.json 2>/dev/null
