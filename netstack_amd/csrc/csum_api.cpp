@@ -1122,12 +1122,9 @@ int batch_dev(ns_csum_ctx* ctx, const uint8_t* d_arena, uint64_t arena_bytes, co
   // NS_CSUM_STORE_WB=1: in-place stores of unchained tiles as plain
   // write-back stores (A/B diagnostics only)
   static const uint32_t wb = std::getenv("NS_CSUM_STORE_WB") ? 4u : 0u;
-  // NS_CSUM_PAIRED_STORE_PASS=1: a paired batch's stores in a pass of their
-  // own after the sums (A/B diagnostics only)
-  static const uint32_t pass = std::getenv("NS_CSUM_PAIRED_STORE_PASS") ? 8u : 0u;
   if (paired) {  // plain tiles, pairs folded in the kernel (no scratch)
     HIP_TRY(nsk::launch_batch(d_arena, arena_bytes, d_desc, n, d_out, nsk::ChainScratch{}, ctx->d_err, s, 0,
-                              (store ? 1u | wb | pass : 0u) | 2u, nullptr));
+                              (store ? 1u | wb : 0u) | 2u, nullptr));
     return NS_OK;
   }
   const bool need_split = arena_bytes / n >= nsk::split_min_avg();

@@ -57,8 +57,7 @@ struct ZcSignal {
 // `store`: bit 0 = honour NS_DESC_STORE (ns_csum_batch_dev_store); bit 1 =
 // NS_BATCH_PAIRED (an odd-indexed NS_DESC_CONT descriptor continues the one
 // before it, folded inside the tile; not with `chain`, `split` or `zc`);
-// bit 2 = plain write-back stores (A/B); bit 3 (with bits 0 and 1) = the
-// stores in a pass of their own after the sums.
+// bit 2 = plain write-back stores (A/B diagnostics).
 hipError_t launch_batch(const uint8_t* arena, uint64_t arena_bytes,
                         const void* desc, uint32_t n, uint16_t* out,
                         ChainScratch chain, unsigned long long* err,

@@ -1606,27 +1606,6 @@ __global__ void signal_host(uint32_t* __restrict__ flag, uint32_t seq) {
   if (threadIdx.x == 0) __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// In-place stores in a pass of their own, after every sum of the batch
-// (launch_batch, store bit 3): one thread per descriptor re-reads its table
-// entry, validates the store as park_store does, and writes out[i] into the
-// packet as finish_tile would.
-__global__ __launch_bounds__(256) void store_results(const uint8_t* __restrict__ arena, uint64_t arena_bytes,
-                                                     const uint4* __restrict__ desc, uint32_t n,
-                                                     const uint16_t* __restrict__ out,
-                                                     unsigned long long* __restrict__ err) {
-  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= n) return;
-  const uint4 raw = desc[i];
-  const uint32_t stw = (raw.w >> 18) & 0x3FFFu;
-  if (!(stw & 1u)) return;
-  const uint64_t at = ((uint64_t)raw.x | ((uint64_t)raw.y << 32)) + (stw >> 2);
-  if (at > arena_bytes || arena_bytes - at < 2) {
-    atomicAdd(err, 1ull);
-    return;
-  }
-  store_result((uint64_t)(uintptr_t)arena + at, out[i], stw);
-}
-
 hipError_t launch_signal(uint32_t* flag, uint32_t seq, hipStream_t stream) {
   hipLaunchKernelGGL(signal_host, dim3(1), dim3(64), 0, stream, flag, seq);
   return hipGetLastError();
@@ -1648,14 +1627,6 @@ hipError_t launch_batch(const uint8_t* arena, uint64_t arena_bytes,
   hipError_t e;
   if (sizing_bytes == 0) sizing_bytes = arena_bytes;
   if ((store & 2u) && (part || split || zc.flag)) return hipErrorInvalidValue;  // pairs: plain tiles only
-  if (store & 8u) {  // the stores in a pass of their own, after the sums (pairs only)
-    if (!(store & 2u) || !(store & 1u)) return hipErrorInvalidValue;
-    e = launch_batch(arena, arena_bytes, desc, n, out, chain, err, stream, sizing_bytes, 2u, split, zc);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(store_results, dim3((n + 255) / 256), dim3(256), 0, stream, arena, arena_bytes,
-                       reinterpret_cast<const uint4*>(desc), n, out, err);
-    return hipGetLastError();
-  }
   if (split && sizing_bytes / n >= kSplitAvg && n < kSplitMaxN) {
     // A few huge descriptors: spread each over many workgroups.  (`split`
     // holds zeros between launches: csum_split leaves it so.)  Each piece
