@@ -310,13 +310,13 @@ const (
 // or above them; smaller calls take the reference's unmodified Go code.
 const (
 	// ChainsOffloadMinBytes is the payload of one sendTCPBatch
-	// (ChecksumChains): at 64 KiB the engine took 1.61x one core's time,
-	// at 128 KiB 0.98x, at 256 KiB 0.60x.
+	// (ChecksumChains): at 64 KiB the engine took 1.57x one core's time,
+	// at 128 KiB 0.91x, at 256 KiB 0.57x.
 	ChainsOffloadMinBytes = 128 << 10
 	// VerifyOffloadMinBytes is the Data bytes of one recvmmsg batch
-	// (VerifyPacketBuffers): 128 x 1500 B took 1.08x one core's time,
-	// 256 x 1500 B 0.89x, 512 x 1500 B 0.81x.
-	VerifyOffloadMinBytes = 256 * 1500
+	// (VerifyPacketBuffers): 64 x 1500 B took 1.31x one core's time,
+	// 128 x 1500 B 0.88x, 256 x 1500 B 0.70x.
+	VerifyOffloadMinBytes = 128 * 1500
 )
 
 // VerifyPacketBuffers runs the receive path's checksum checks over a batch

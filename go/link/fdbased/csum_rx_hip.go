@@ -32,7 +32,7 @@ func verifyRXChecksums(e *endpoint, pkts []tcpip.PacketBuffer) {
 	// Below header.VerifyOffloadMinBytes one core verifies the batch sooner
 	// than one engine call (INTEGRATION.md §2): leave every packet
 	// RXChecksumUnknown, and segment.parse verifies it as the reference does.
-	// With MaxMsgsPerRecv = 8 that takes packets of 48,000 B on average (a
+	// With MaxMsgsPerRecv = 8 that takes packets of 24,000 B on average (a
 	// large-MTU link); 8 x 1500 B never reaches it.
 	total := 0
 	for i := range pkts {
