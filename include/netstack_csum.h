@@ -22,6 +22,8 @@
  *   device-resident batch                                         -> ns_csum_batch_dev / _host
  *   ... and the header write that follows it, SetChecksum(^xsum)
  *   (connect.go:663, ipv4.go:236; tcp.go:252, ipv4.go:223)        -> ns_csum_batch_dev_store
+ *   sendTCPBatch's whole batch from its geometry: buildTCPHdr for every
+ *   segment (connect.go:668-702) and addIPHeader (ipv4.go:217-238)  -> ns_csum_tcp_tx
  *   any composition of Checksum(v, xsum) / view chaining (a whole
  *   TCP/UDP/ICMP/IPv4 checksum per chain)                         -> ns_csum_chains
  *   the checksum steps of a batch of tcpip.PacketBuffer
@@ -56,10 +58,11 @@
 extern "C" {
 #endif
 
-#define NS_CSUM_ABI_VERSION 5  /* 2: ns_csum_batch_dev_store, NS_DESC_STORE*;
+#define NS_CSUM_ABI_VERSION 6  /* 2: ns_csum_batch_dev_store, NS_DESC_STORE*;
                                   3: ns_csum_stage_*, ns_csum_packet_buffers;
                                   4: ns_csum_stream_release, _scratch_count;
-                                  5: ns_csum_get_stats */
+                                  5: ns_csum_get_stats;
+                                  6: ns_csum_tcp_tx */
 
 /* ---- status codes ------------------------------------------------------- */
 #define NS_OK 0
@@ -188,6 +191,56 @@ int ns_csum_batch_dev_store(ns_csum_ctx* ctx, uint8_t* d_arena,
                             uint64_t arena_bytes, const ns_pkt_desc* d_desc,
                             uint32_t n, uint16_t* d_out, uint32_t batch_flags,
                             void* stream);
+
+/* ---- sendTCPBatch from its geometry (no descriptor table) ----------------
+ * The transmit checksums of one sendTCPBatch call (transport/tcp/connect.go:
+ * 668-702) and of addIPHeader for its segments (network/ipv4/ipv4.go:217-238),
+ * over the layout sendTCPBatch builds, resident in d_arena:
+ * NewPacketDescriptors' one buffer of n header slots (stack/route.go:181-188)
+ * and the payload view.  n = ceil(size / mss) segments (connect.go:675);
+ * segment i's payload is [pay_off + i*mss, + min(mss, size - i*mss))
+ * (:679-691), its headers lie in slot i = [hdr_off + i*slot, + slot).
+ * Per segment, as buildTCPHdr and addIPHeader compute them:
+ *   TCP field (tcp_at + 16) := ^Checksum(tcp[:tcp_len], ChecksumVVWithOffset(
+ *       payload, PseudoHeaderChecksum(protocol, src, dst, tcp_len + size)))
+ *       (connect.go:652-663); with NS_TX_TCP_PARTIAL the pseudo-header sum
+ *       itself (gso.NeedsCsum, :655-660); NS_TX_TCP_NONE leaves it alone
+ *       (CapabilityTXChecksumOffload, :661);
+ *   IPv4 field (ip_at + 10) := ^Checksum(ip[:ip_len], 0) (ipv4.go:236);
+ *       ip_len = 0: no IPv4 header (an IPv6 route).
+ * Both fields are summed as zero, as freshly encoded headers hold them.  The
+ * pseudo-header's addresses enter as addr_sum = Checksum(dst, Checksum(src,
+ * 0)), the route's (route.go:93-95, checksum.go:113-114); tcp_len is the
+ * header's DataOffset (tcp.go:259-262) and the length word is
+ * uint16(tcp_len + size) (connect.go:652).
+ * The call owns the header slots until it completes: it writes them back whole
+ * (unchanged bytes included), unless NS_TX_FIELDS_ONLY (2-byte stores).
+ * Asynchronous on `stream`.  d_out (2n u16, or NULL): [2i] the IPv4 sum,
+ * [2i+1] the TCP sum, un-complemented (0 where not computed).
+ * NS_EINVAL: mss 0 or > 65535, slot 0 or > 4096, a header longer than 60 B
+ * or not inside the slot, a field not inside its header (ip_len < 12,
+ * tcp_len < 18), NS_TX_TCP_PARTIAL with NS_TX_TCP_NONE, n >= 2^32, payload
+ * and slots overlapping.  NS_ERANGE: slots or payload past the arena.
+ * Bytes per segment read: its payload and its slot; written: its slot.     */
+typedef struct ns_tcp_tx {
+  uint64_t hdr_off;   /* arena offset of header slot 0                        */
+  uint64_t pay_off;   /* arena offset of the payload's first byte              */
+  uint64_t size;      /* data.Size()                                           */
+  uint32_t mss;       /* gso.MSS                                               */
+  uint32_t slot;      /* hdrSize: TCPMinimumSize + MaxHeaderLength + optLen    */
+  uint16_t ip_at;     /* the IPv4 header's offset in a slot                    */
+  uint16_t ip_len;    /* its length, IHL * 4 (0: none)                         */
+  uint16_t tcp_at;    /* the TCP header's offset in a slot                     */
+  uint16_t tcp_len;   /* its length, DataOffset (20 + options)                 */
+  uint16_t addr_sum;  /* Checksum(dst, Checksum(src, 0))                       */
+  uint16_t protocol;  /* 6 (header.TCPProtocolNumber)                          */
+  uint32_t flags;     /* NS_TX_*                                               */
+} ns_tcp_tx;
+#define NS_TX_TCP_PARTIAL 0x1u
+#define NS_TX_TCP_NONE 0x2u
+#define NS_TX_FIELDS_ONLY 0x4u
+int ns_csum_tcp_tx(ns_csum_ctx* ctx, uint8_t* d_arena, uint64_t arena_bytes,
+                   const ns_tcp_tx* tx, uint16_t* d_out, void* stream);
 
 /* Frees the scratch the context keeps for `stream` (see ns_csum_batch_dev),
  * after the stream's last launch that used it; nothing waits.  Call it

@@ -17,7 +17,7 @@ CSRC = os.path.join(_HERE, "csrc")
 
 # The NS_CSUM_ABI_VERSION this binding is written against; lib() refuses a
 # library that reports another (a stale build).
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 NS_OK = 0
 NS_EINVAL = -1
@@ -42,7 +42,7 @@ EXPORTED = (
     "ns_csum_vv_batch", "ns_csum_views_restart", "ns_csum_pseudo_header",
     "ns_csum_combine", "ns_csum_shard_plan", "ns_csum_batch_multi", "ns_csum_chains",
     "ns_csum_stage_acquire", "ns_csum_stage_release", "ns_csum_packet_buffers",
-    "ns_csum_stream_release", "ns_csum_scratch_count", "ns_csum_get_stats",
+    "ns_csum_stream_release", "ns_csum_scratch_count", "ns_csum_get_stats", "ns_csum_tcp_tx",
 )
 NS_PIECE_RESTART = 0x1
 NS_PIECE_END = 0x2
@@ -103,13 +103,27 @@ class NsStats(ctypes.Structure):
         "stage_allocs", "stage_alloc_ns_max")]
 
 
+class NsTcpTx(ctypes.Structure):
+    """ns_tcp_tx: one sendTCPBatch batch's geometry (ns_csum_tcp_tx)."""
+    _fields_ = [("hdr_off", ctypes.c_uint64), ("pay_off", ctypes.c_uint64), ("size", ctypes.c_uint64),
+                ("mss", ctypes.c_uint32), ("slot", ctypes.c_uint32),
+                ("ip_at", ctypes.c_uint16), ("ip_len", ctypes.c_uint16),
+                ("tcp_at", ctypes.c_uint16), ("tcp_len", ctypes.c_uint16),
+                ("addr_sum", ctypes.c_uint16), ("protocol", ctypes.c_uint16), ("flags", ctypes.c_uint32)]
+
+
+NS_TX_TCP_PARTIAL = 0x1
+NS_TX_TCP_NONE = 0x2
+NS_TX_FIELDS_ONLY = 0x4
+
+
 class NsOpts(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int32), ("flags", ctypes.c_uint32),
                 ("staging_bytes", ctypes.c_uint64)]
 
 
 assert ctypes.sizeof(NsPktDesc) == 16 and ctypes.sizeof(NsSeg) == 24 and ctypes.sizeof(NsPiece) == 24
-assert ctypes.sizeof(NsPktBuf) == 40 and ctypes.sizeof(NsStats) == 13 * 8
+assert ctypes.sizeof(NsPktBuf) == 40 and ctypes.sizeof(NsStats) == 13 * 8 and ctypes.sizeof(NsTcpTx) == 48
 
 _lock = threading.Lock()
 _lib = None
@@ -150,6 +164,7 @@ def _declare(lib):
         "ns_csum_stream_release": (c.c_int, [vp, vp]),
         "ns_csum_scratch_count": (c.c_int, [vp, c.POINTER(c.c_uint32)]),
         "ns_csum_get_stats": (c.c_int, [vp, c.POINTER(NsStats), c.c_int]),
+        "ns_csum_tcp_tx": (c.c_int, [vp, u8p, c.c_uint64, c.POINTER(NsTcpTx), vp, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

@@ -1190,6 +1190,60 @@ int ns_csum_batch_dev_store(ns_csum_ctx* ctx, uint8_t* d_arena, uint64_t arena_b
   return batch_dev(ctx, d_arena, arena_bytes, d_desc, n, d_out, batch_flags, stream, true);
 }
 
+int ns_csum_tcp_tx(ns_csum_ctx* ctx, uint8_t* d_arena, uint64_t arena_bytes, const ns_tcp_tx* tx,
+                   uint16_t* d_out, void* stream) {
+  if (!ctx || !tx || (arena_bytes && !d_arena)) return NS_EINVAL;
+  const ns_tcp_tx& t = *tx;
+  if (t.mss == 0 || t.mss > 0xFFFFu || t.slot == 0 || t.slot > 4096) return NS_EINVAL;
+  const bool partial = (t.flags & NS_TX_TCP_PARTIAL) != 0, none = (t.flags & NS_TX_TCP_NONE) != 0;
+  if ((partial && none) || (t.flags & ~(NS_TX_TCP_PARTIAL | NS_TX_TCP_NONE | NS_TX_FIELDS_ONLY))) return NS_EINVAL;
+  if (t.ip_len && (t.ip_len < 12 || t.ip_len > 60 || (uint32_t)t.ip_at + t.ip_len > t.slot)) return NS_EINVAL;
+  if (!none && (t.tcp_len < 18 || t.tcp_len > 60 || (uint32_t)t.tcp_at + t.tcp_len > t.slot)) return NS_EINVAL;
+  const uint64_t n = t.size / t.mss + (t.size % t.mss != 0);
+  if (n >= (1ull << 32)) return NS_EINVAL;
+  const uint32_t mode = (t.ip_len ? nsk::kTxIp : 0u) | (none ? 0u : partial ? nsk::kTxTcpPartial : nsk::kTxTcpFull) |
+                        ((t.flags & NS_TX_FIELDS_ONLY) ? nsk::kTxFieldsOnly : 0u);
+  if (n == 0) return NS_OK;
+  if (!(mode & (nsk::kTxIp | nsk::kTxTcpFull | nsk::kTxTcpPartial))) {  // nothing to fill: the sums are 0
+    if (d_out) {
+      DeviceGuard g(ctx->device);
+      HIP_TRY(hipMemsetAsync(d_out, 0, 4 * n, (hipStream_t)stream));
+    }
+    return NS_OK;
+  }
+  const uint64_t hdr_bytes = n * t.slot;
+  if (t.hdr_off > arena_bytes || hdr_bytes > arena_bytes - t.hdr_off) return NS_ERANGE;
+  if (t.pay_off > arena_bytes || t.size > arena_bytes - t.pay_off) return NS_ERANGE;
+  // The payload is read while other waves write slots back: they must not meet.
+  if ((mode & nsk::kTxTcpFull) && t.pay_off < t.hdr_off + hdr_bytes && t.hdr_off < t.pay_off + t.size)
+    return NS_EINVAL;
+  DeviceGuard g(ctx->device);
+  nsk::TxGeo geo{};
+  const uint64_t base = (uint64_t)(uintptr_t)d_arena;
+  geo.hdr = base + t.hdr_off;
+  geo.pay = base + t.pay_off;
+  geo.size = t.size;
+  geo.n = n;
+  geo.mss = t.mss;
+  geo.slot = t.slot;
+  geo.ip_at = t.ip_at;
+  geo.ip_len = t.ip_len;
+  geo.tcp_at = t.tcp_at;
+  geo.tcp_len = t.tcp_len;
+  geo.addr_sum = t.addr_sum;
+  geo.proto = t.protocol;
+  geo.mode = mode;
+  geo.out = d_out;
+  // A/B diagnostics, read per call: NS_CSUM_TX_VARIANT=k, a variant of the
+  // kernel (csum_kernels.h launch_tcp_tx); NS_CSUM_TX_TILE=t, t segments per
+  // wave instead of the launcher's choice (tests and tuning).
+  const char* ev = std::getenv("NS_CSUM_TX_VARIANT");
+  const uint32_t variant = ev ? (uint32_t)std::atoi(ev) : 0u;
+  if (const char* v = std::getenv("NS_CSUM_TX_TILE")) geo.tile = (uint32_t)std::atoi(v);
+  HIP_TRY(nsk::launch_tcp_tx(geo, (hipStream_t)stream, variant));
+  return NS_OK;
+}
+
 int ns_csum_batch_host(ns_csum_ctx* ctx, const uint8_t* h_arena, uint64_t arena_bytes,
                        const ns_pkt_desc* h_desc, uint32_t n, uint16_t* h_out,
                        uint32_t batch_flags) {

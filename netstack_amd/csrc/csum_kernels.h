@@ -84,4 +84,28 @@ hipError_t launch_rebase(void* desc, uint32_t n, uint64_t bias, hipStream_t stre
 constexpr uint64_t split_min_avg() { return 1u << 20; }
 constexpr uint64_t split_words(uint64_t n) { return 2 * n; }
 
+// sendTCPBatch's transmit checksums from the batch geometry (tcp_tx.hip,
+// ns_csum_tcp_tx).  Absolute device addresses; validated by the caller:
+// n = ceil(size / mss) >= 1, mss <= 65535, every slot and the payload inside
+// the arena, the headers inside a slot (each <= 60 B), the fields inside the
+// headers, slots and payload disjoint.  tile = segments per wave (0: the
+// launcher picks; at most 64 and 12 KiB of slots); lds_rows and lds_wave
+// are set by the launcher.  out (or nullptr): [2i] the IPv4 sum, [2i+1] the TCP sum, both
+// un-complemented.
+constexpr uint32_t kTxIp = 1u;           // fill the IPv4 header checksum
+constexpr uint32_t kTxTcpFull = 2u;      // fill ^(pseudo + payload + TCP header)
+constexpr uint32_t kTxTcpPartial = 4u;   // fill the pseudo-header sum (CHECKSUM_PARTIAL)
+constexpr uint32_t kTxFieldsOnly = 8u;   // store the 2-byte fields, not whole slots
+struct TxGeo {
+  uint64_t hdr, pay, size, n;
+  uint32_t mss, slot, tile, lds_wave;
+  uint32_t ip_at, ip_len, tcp_at, tcp_len;
+  uint32_t addr_sum, proto, mode, lds_rows;
+  uint16_t* out;
+  uint32_t wpg, pad;  // waves (tiles) per workgroup, set by the launcher
+};
+// variant (A/B diagnostics; 0 = production): 1 = 8 windows in flight,
+// 2 = nontemporal write-back, 3 = segments reduced over the wave in the loop.
+hipError_t launch_tcp_tx(TxGeo g, hipStream_t stream, uint32_t variant = 0);
+
 }  // namespace nsk

@@ -1,0 +1,357 @@
+// tcp_tx.hip — the transmit checksums of sendTCPBatch (transport/tcp/
+// connect.go:668-702) taken from the batch's geometry instead of a
+// descriptor table (ns_csum_tcp_tx, include/netstack_csum.h).
+//
+// The layout is the one sendTCPBatch builds.  stack.NewPacketDescriptors(n,
+// hdrSize) allocates ONE buffer of n slots of hdrSize bytes (stack/route.go:
+// 181-188); buildTCPHdr prepends the TCP header in slot i and addIPHeader the
+// IPv4 header before it; the payload is one VectorisedView, segment i at
+// Off = i * MSS, Size = min(MSS, what is left) (connect.go:679-692).  Per
+// segment the reference computes
+//   tcp: xsum = PseudoHeaderChecksum(6, src, dst, tcp_len + size)    checksum.go:112-122
+//        xsum = ChecksumVVWithOffset(data, xsum, off, size)           connect.go:662
+//        field = ^Checksum(tcp[:DataOffset], xsum)                    connect.go:663, tcp.go:259-262
+//        (or field = xsum of the pseudo-header alone: CHECKSUM_PARTIAL, connect.go:655-660)
+//   ip:  field = ^Checksum(ip[:IHL], 0)                               ipv4.go:236, :251-253
+// with both fields zero while they are summed (freshly encoded headers).
+//
+// One wave owns a tile of `tile` consecutive segments: their payload bytes
+// are one contiguous span and their header slots one contiguous region.
+//   1. The wave starts an LDS-DMA copy of its header region (no registers).
+//   2. It streams the payload span in aligned 1-KiB windows (lane l reads
+//      16 B at window + 16 l, nontemporal: every 128-B line consumed by one
+//      instruction), U windows in flight.  Each lane keeps the little-endian
+//      word sum W of its bytes (one v_sad_u16 per dword).  Segment ends are
+//      wave-uniform: a window holding one splits the straddling lane's chunk
+//      with scalar byte masks, reduces the finished segment over the wave and
+//      parks the total in lane j (segment j of the tile).
+//   3. Lane j sums its slot's IPv4 and TCP headers from LDS (the fields read
+//      as zero), folds everything as the Go code does, and writes the two
+//      fields into the LDS copy.
+//   4. The wave writes its header region back whole (16-B stores of full
+//      chunks; byte stores where a chunk is shared with a neighbouring
+//      tile), while its lines are still in L2: whole-line writes instead of
+//      2M scattered 2-byte stores (tools/dense_store_probe.hip).
+//
+// Arithmetic.  A segment holds at most 65,535 bytes, so no sum here wraps a
+// uint32 and each folded value depends on W only through W mod 65535 and
+// whether it is zero (csum_kernels.hip, kWOnlyMaxChunks / s_class): the
+// result is bit-exact with the Go code for every byte pattern.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "csum_kernels.h"
+
+namespace nsk {
+namespace {
+
+// ChecksumCombine(uint16(v), uint16(v>>16)) — checksum.go:45, :104-107.
+__device__ __forceinline__ uint32_t tx_fold(uint32_t v) {
+  const uint32_t s = (v & 0xFFFFu) + (v >> 16);
+  return (s + (s >> 16)) & 0xFFFFu;
+}
+
+// A W total as a value with the fold behaviour of Go's S for a piece whose
+// first byte is at an address of parity `phase` (csum_kernels.hip s_class).
+__device__ __forceinline__ uint32_t tx_class(uint32_t W, uint32_t phase) {
+  const uint32_t w = tx_fold(W);
+  return phase ? w : tx_fold(w << 8);
+}
+
+__device__ __forceinline__ uint32_t wsum4(const uint4 v, uint32_t acc) {
+  acc = __builtin_amdgcn_sad_u16(v.x, 0u, acc);
+  acc = __builtin_amdgcn_sad_u16(v.y, 0u, acc);
+  acc = __builtin_amdgcn_sad_u16(v.z, 0u, acc);
+  return __builtin_amdgcn_sad_u16(v.w, 0u, acc);
+}
+
+__device__ __forceinline__ uint32_t below(int c) {  // bytes [0, c) of a dword, c clamped to [0, 4]
+  c = c < 0 ? 0 : (c > 4 ? 4 : c);
+  return c >= 4 ? 0xFFFFFFFFu : ((1u << (8 * c)) - 1u);
+}
+
+// Sum over the 64 lanes of the wave; every lane gets the (uniform) total.
+__device__ __forceinline__ uint32_t wave_total(uint32_t s) {
+  s += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)s, 0xB1, 0xF, 0xF, false);   // quad_perm 1,0,3,2
+  s += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)s, 0x4E, 0xF, 0xF, false);   // quad_perm 2,3,0,1
+  s += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)s, 0x141, 0xF, 0xF, false);  // row_half_mirror
+  s += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)s, 0x140, 0xF, 0xF, false);  // row_mirror
+  return (uint32_t)__builtin_amdgcn_readlane((int)s, 0) + (uint32_t)__builtin_amdgcn_readlane((int)s, 16) +
+         (uint32_t)__builtin_amdgcn_readlane((int)s, 32) + (uint32_t)__builtin_amdgcn_readlane((int)s, 48);
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t tx_srd(uint64_t base, uint32_t nrec) {
+  // readfirstlane returns int: widen through uint32_t
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)base);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(base >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | (uint64_t)lo), (short)0,
+                                           (int)__builtin_amdgcn_readfirstlane(nrec), 0x00020000);
+}
+
+template <int AUX>
+__device__ __forceinline__ uint4 tx_load(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  auto x = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, AUX);
+  return *reinterpret_cast<uint4*>(&x);
+}
+
+// The W sum of LDS bytes [a, a + len) (len <= 60), dword reads with masks;
+// `zero` (an offset inside the range, or ~0u) is a 2-byte field read as zero.
+template <int MAXD>
+__device__ __forceinline__ uint32_t lds_wsum(const uint8_t* L, uint32_t a, uint32_t len, uint32_t zero) {
+  const uint32_t* D = reinterpret_cast<const uint32_t*>(L);
+  const uint32_t d0 = a >> 2;
+  const uint32_t nd = ((a + len + 3) >> 2) - d0;
+  uint32_t w = 0;
+#pragma unroll
+  for (int k = 0; k < MAXD; ++k) {
+    if ((uint32_t)k < nd) {
+      const int b = (int)(4 * (d0 + k));
+      uint32_t m = below((int)(a + len) - b) & ~below((int)a - b);
+      if (zero != ~0u) m &= ~(below((int)(zero + 2) - b) & ~below((int)zero - b));
+      w = __builtin_amdgcn_sad_u16(D[d0 + k] & m, 0u, w);
+    }
+  }
+  return w;
+}
+
+__device__ __forceinline__ void lds_put_be16(uint8_t* L, uint32_t at, uint32_t v) {
+  L[at] = (uint8_t)(v >> 8);
+  L[at + 1] = (uint8_t)v;
+}
+
+// A relaxed agent-scope 2-byte store (written through), or two byte stores
+// at an odd address (csum_kernels.hip store_result).
+__device__ __forceinline__ void tx_store_be16(uint64_t addr, uint32_t v) {
+  uint8_t* p = reinterpret_cast<uint8_t*>((uintptr_t)addr);
+  if (!(addr & 1u)) {
+    __hip_atomic_store(reinterpret_cast<uint16_t*>(p), (uint16_t)(((v & 0xFFu) << 8) | ((v >> 8) & 0xFFu)),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+    p[0] = (uint8_t)(v >> 8);
+    p[1] = (uint8_t)v;
+  }
+}
+
+}  // namespace
+
+// U = payload windows (1 KiB per wave each) in flight; AUX = payload load
+// policy (2 = nontemporal); SP = header write-back policy (0 plain, 1 nt);
+// RED = how a finished segment's lane sums meet: 0 = reduced over the wave
+// at once (DPP + readlane), 1 = each lane's partial parked in an LDS row of
+// the segment, summed by the segment's lane at the end (no cross-lane
+// dependency inside the stream loop), 2 = not at all (timing probes only:
+// wrong sums).
+template <int U, int AUX, int SP, int RED>
+__global__ __launch_bounds__(256) void tcp_tx(TxGeo g) {
+  extern __shared__ uint4 tx_lds[];
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t s0 = ((uint64_t)blockIdx.x * g.wpg + wv) * g.tile;
+  if (s0 >= g.n) return;  // a whole wave leaves together
+  const uint32_t nseg = g.n - s0 < g.tile ? (uint32_t)(g.n - s0) : g.tile;
+  uint8_t* L = reinterpret_cast<uint8_t*>(tx_lds) + (size_t)wv * g.lds_wave;
+  uint32_t* rows = reinterpret_cast<uint32_t*>(L + g.lds_rows);  // RED 1: [tile][64] partials
+
+  // 1. the header region, into LDS by DMA
+  const uint64_t h_lo = g.hdr + s0 * g.slot, h_hi = h_lo + (uint64_t)nseg * g.slot;
+  const uint64_t h_base = h_lo & ~15ull;
+  const uint32_t h_chunks = (uint32_t)((h_hi - h_base + 15) >> 4);
+  const __amdgpu_buffer_rsrc_t hr = tx_srd(h_base, h_chunks * 16u);
+  for (uint32_t c = 0; c < h_chunks; c += 64) {
+    const uint32_t o = (c + lane) * 16u;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(hr, (__attribute__((address_space(3))) void*)(L + c * 16u), 16,
+                                             o < h_chunks * 16u ? o : h_chunks * 16u, 0, 0, 0);
+  }
+
+  // 2. the payload span: lane j ends up with segment j's W total
+  uint32_t wres = 0;
+  if (g.mode & kTxTcpFull) {
+    const uint64_t p_lo = g.pay + s0 * g.mss;
+    const uint64_t p_end = g.pay + g.size;
+    const uint64_t p_hi = p_lo + (uint64_t)nseg * g.mss < p_end ? p_lo + (uint64_t)nseg * g.mss : p_end;
+    const uint64_t p_base = p_lo & ~15ull;
+    const uint32_t span = (uint32_t)(p_hi - p_base);  // < 2^32: tile * mss <= 64 * 65535
+    const uint32_t nrec = (span + 15u) & ~15u;
+    const __amdgpu_buffer_rsrc_t pr = tx_srd(p_base, nrec);
+    const uint32_t nwin = (nrec / 16u + 63u) / 64u;
+    // Segment ends, relative to p_base (uniform).  "Segment -1" ends where
+    // the tile's first segment starts, and "segment nseg" holds what follows
+    // the last one in its chunk: those bytes belong to the neighbouring
+    // tiles and are dropped.
+    int seg = -1;
+    uint32_t nb = (uint32_t)(p_lo - p_base);  // where segment `seg` ends
+    uint32_t pc = 0;                           // where the previous one ended
+    uint32_t acc = 0;
+    for (uint32_t w0 = 0; w0 < nwin; w0 += U) {
+      uint4 v[U];
+#pragma unroll
+      for (int j = 0; j < U; ++j) {
+        const uint32_t o = ((w0 + j) * 64u + lane) * 16u;
+        v[j] = tx_load<AUX>(pr, o < nrec ? o : nrec);
+      }
+#pragma unroll
+      for (int j = 0; j < U; ++j) {
+        if (w0 + j >= nwin) break;
+        uint32_t w = wsum4(v[j], 0u);
+        const uint32_t wbase = (w0 + j) * 1024u;
+        while (RED != 2 && nb < wbase + 1024u) {
+          // lane lb holds the segment's last bytes [lo, cut) of its chunk
+          const uint32_t c = nb - wbase, lb = c >> 4, cut = c & 15u;
+          const uint32_t lo = ((pc >> 4) == (nb >> 4) && seg >= 0) ? (pc & 15u) : 0u;
+          const uint32_t m0 = below((int)cut) & ~below((int)lo), m1 = below((int)cut - 4) & ~below((int)lo - 4),
+                         m2 = below((int)cut - 8) & ~below((int)lo - 8), m3 = below((int)cut - 12) & ~below((int)lo - 12);
+          const uint32_t part = wsum4(make_uint4(v[j].x & m0, v[j].y & m1, v[j].z & m2, v[j].w & m3), 0u);
+          const uint32_t vc = lane < lb ? w : (lane == lb ? part : 0u);
+          if constexpr (RED == 0) {
+            const uint32_t tot = wave_total(acc + vc);
+            if ((int)lane == seg) wres = tot;
+          } else if constexpr (RED == 1) {
+            if (seg >= 0) rows[(uint32_t)seg * 64u + lane] = acc + vc;
+          }
+          acc = 0;
+          w -= vc;
+          pc = nb;
+          ++seg;
+          // the last segment ends at the span's end: the rest of its last
+          // chunk belongs to the next tile
+          nb = (uint32_t)seg < nseg ? min(nb + g.mss, span) : 0xFFFFFFFFu;
+        }
+        acc += w;
+      }
+    }
+    if constexpr (RED == 0) {
+      const uint32_t tot = wave_total(acc);
+      if ((int)lane == seg) wres = tot;
+    } else if constexpr (RED == 1) {
+      if ((uint32_t)seg < nseg) rows[(uint32_t)seg * 64u + lane] = acc;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      if (lane < nseg) {
+        const uint4* r = reinterpret_cast<const uint4*>(rows + lane * 64u);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+          const uint4 x = r[k];
+          wres += x.x + x.y + x.z + x.w;
+        }
+      }
+    } else {
+      wres = acc;
+    }
+  }
+
+  // 3. headers, then the fields (lane j = segment s0 + j)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the LDS-DMA copy is in
+  __builtin_amdgcn_wave_barrier();
+  const uint32_t o = (uint32_t)(h_lo - h_base) + lane * g.slot;  // slot j in LDS
+  uint32_t ipv = 0, tcpv = 0;
+  if (lane < nseg) {
+    const uint64_t si = s0 + lane;
+    const uint32_t size = si + 1 < g.n ? g.mss : (uint32_t)(g.size - (g.n - 1) * (uint64_t)g.mss);
+    if (g.mode & kTxIp) {
+      const uint32_t a = o + g.ip_at;
+      ipv = tx_fold(tx_class(lds_wsum<16>(L, a, g.ip_len, a + 10u), a & 1u));  // Checksum(ip[:IHL], 0)
+      lds_put_be16(L, a + 10u, ~ipv & 0xFFFFu);
+    }
+    if (g.mode & (kTxTcpFull | kTxTcpPartial)) {
+      uint32_t x = tx_fold(g.addr_sum + ((g.tcp_len + size) & 0xFFFFu));  // PseudoHeaderChecksum
+      x = tx_fold(x + g.proto);
+      const uint32_t a = o + g.tcp_at;
+      if (g.mode & kTxTcpFull) {
+        const uint32_t pa = (uint32_t)((g.pay + si * g.mss) & 1u);
+        x = tx_fold(x + tx_class(wres, pa));                                            // ChecksumVVWithOffset
+        x = tx_fold(x + tx_class(lds_wsum<16>(L, a, g.tcp_len, a + 16u), a & 1u));     // CalculateChecksum
+        lds_put_be16(L, a + 16u, ~x & 0xFFFFu);
+      } else {
+        lds_put_be16(L, a + 16u, x);
+      }
+      tcpv = x;
+    }
+    if (g.out) {
+      g.out[2 * si] = (uint16_t)ipv;
+      g.out[2 * si + 1] = (uint16_t)tcpv;
+    }
+  }
+  if (g.mode & kTxFieldsOnly) {  // only the 2-byte fields, as csum_hyb stores them
+    if (lane < nseg) {
+      const uint64_t slot = h_lo + (uint64_t)lane * g.slot;
+      if (g.mode & kTxIp) tx_store_be16(slot + g.ip_at + 10u, ~ipv & 0xFFFFu);
+      if (g.mode & kTxTcpFull) tx_store_be16(slot + g.tcp_at + 16u, ~tcpv & 0xFFFFu);
+      if (g.mode & kTxTcpPartial) tx_store_be16(slot + g.tcp_at + 16u, tcpv);
+    }
+    return;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+
+  // 4. the header region back, whole
+  const uint4* L4 = reinterpret_cast<const uint4*>(L);
+  for (uint32_t c = lane; c < h_chunks; c += 64) {
+    const uint64_t at = h_base + (uint64_t)c * 16u;
+    if (at >= h_lo && at + 16 <= h_hi) {
+      uint4* p = reinterpret_cast<uint4*>((uintptr_t)at);
+      if constexpr (SP == 1) {
+        const uint4 x = L4[c];
+        uint32_t* q = reinterpret_cast<uint32_t*>(p);
+        __builtin_nontemporal_store(x.x, q);
+        __builtin_nontemporal_store(x.y, q + 1);
+        __builtin_nontemporal_store(x.z, q + 2);
+        __builtin_nontemporal_store(x.w, q + 3);
+      } else {
+        *p = L4[c];
+      }
+    } else {  // a chunk shared with the neighbouring tile: only this tile's bytes
+      for (uint32_t k = 0; k < 16; ++k)
+        if (at + k >= h_lo && at + k < h_hi) reinterpret_cast<uint8_t*>((uintptr_t)at)[k] = L[c * 16u + k];
+    }
+  }
+}
+
+// Segments per wave for a batch: ~48 KiB of payload per wave, at most 32
+// segments, fewer when the batch would not give ~2,048 waves, and at most
+// ~8 KiB of header slots.
+static uint32_t tx_tile(const TxGeo& g) {
+  uint32_t t = (uint32_t)std::max<uint64_t>(1, (48u << 10) / std::max<uint32_t>(g.mss, 1));
+  t = std::min<uint32_t>(t, 32);
+  const uint64_t per = (g.n + 2047) / 2048;
+  if (per < t) t = (uint32_t)std::max<uint64_t>(1, per);
+  while (t > 1 && (uint64_t)t * g.slot > (8u << 10)) t /= 2;
+  return t;
+}
+
+// Tile, LDS and workgroup shape for a batch (tile = 0: tx_tile's choice).
+static hipError_t tx_shape(TxGeo& g, uint32_t* grid) {
+  if (g.tile == 0) g.tile = tx_tile(g);
+  if (g.tile > 64 || (uint64_t)g.tile * g.slot > (12u << 10)) return hipErrorInvalidValue;
+  // The LDS-DMA copy writes whole 64-chunk (1 KiB) rows, zeros past the
+  // region included: each wave's share is rounded up to whole rows; then the
+  // segments' rows of lane partials.
+  g.lds_rows = (uint32_t)(((uint64_t)g.tile * g.slot + 30) / 16 + 63) / 64 * 1024;
+  g.lds_wave = g.lds_rows + g.tile * 256u;
+  // 4 waves (tiles) per workgroup, fewer where their LDS would pass 64 KiB
+  g.wpg = g.lds_wave <= (16u << 10) ? 4u : g.lds_wave <= (32u << 10) ? 2u : 1u;
+  const uint64_t tiles = (g.n + g.tile - 1) / g.tile;
+  *grid = (uint32_t)((tiles + g.wpg - 1) / g.wpg);
+  return hipSuccess;
+}
+
+template <int U, int AUX, int SP, int RED>
+static hipError_t launch_tcp_tx_t(TxGeo g, hipStream_t stream) {
+  if (g.n == 0) return hipSuccess;
+  uint32_t grid = 0;
+  const hipError_t e = tx_shape(g, &grid);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL((tcp_tx<U, AUX, SP, RED>), dim3(grid), dim3(64 * g.wpg), (size_t)g.lds_wave * g.wpg, stream,
+                     g);
+  return hipGetLastError();
+}
+
+hipError_t launch_tcp_tx(TxGeo g, hipStream_t stream, uint32_t variant) {
+  switch (variant) {
+    case 1: return launch_tcp_tx_t<8, 2, 0, 1>(g, stream);
+    case 2: return launch_tcp_tx_t<16, 2, 1, 1>(g, stream);
+    case 3: return launch_tcp_tx_t<16, 2, 0, 0>(g, stream);
+    default: return launch_tcp_tx_t<16, 2, 0, 1>(g, stream);
+  }
+}
+
+}  // namespace nsk

@@ -115,6 +115,38 @@ class Engine:
                        out.data_ptr(), chained, stream.cuda_stream, store, paired)
         return out
 
+    def tcp_tx(self, arena, geo: dict, out=None, stream=None, mode: str = "full",
+               fields_only: bool = False):
+        """sendTCPBatch's transmit checksums from its geometry
+        (ns_csum_tcp_tx): `arena` a uint8 CUDA tensor holding the header slots
+        and the payload; `geo` the keys of ns_tcp_tx (hdr_off, pay_off, size,
+        mss, slot, ip_at, ip_len, tcp_at, tcp_len, protocol) plus the route's
+        `src` and `dst` addresses (or `addr_sum`).  mode: "full", "partial"
+        (CHECKSUM_PARTIAL) or "none" (TX checksum offload).  `out` (optional)
+        receives the 2n un-complemented sums.  Launches on `stream` (default:
+        torch's current stream) without synchronising; returns `out`."""
+        import torch
+
+        if not arena.is_cuda:
+            raise ValueError("arena must be a device tensor")
+        t = _lib.NsTcpTx()
+        for k in ("hdr_off", "pay_off", "size", "mss", "slot", "ip_at", "ip_len", "tcp_at", "tcp_len"):
+            setattr(t, k, int(geo[k]))
+        t.protocol = int(geo.get("protocol", 6))
+        t.addr_sum = int(geo["addr_sum"]) if "addr_sum" in geo else addr_sum(geo["src"], geo["dst"])
+        t.flags = {"full": 0, "partial": _lib.NS_TX_TCP_PARTIAL, "none": _lib.NS_TX_TCP_NONE}[mode] | \
+            (_lib.NS_TX_FIELDS_ONLY if fields_only else 0)
+        if out is not None:
+            n = -(-int(geo["size"]) // max(int(geo["mss"]), 1))
+            if not out.is_cuda or out.numel() < 2 * n or out.element_size() != 2:
+                raise ValueError("out must be a device tensor of 2n 16-bit sums")
+        if stream is None:
+            stream = torch.cuda.current_stream(arena.device)
+        check(lib().ns_csum_tcp_tx(self._h, arena.data_ptr(), arena.numel() * arena.element_size(),
+                                   ctypes.byref(t), out.data_ptr() if out is not None else None,
+                                   getattr(stream, "cuda_stream", stream)), "ns_csum_tcp_tx")
+        return out
+
     def stream_release(self, stream) -> None:
         """Free the scratch this context keeps for `stream` (a torch.cuda.Stream
         or a raw hipStream_t) after its last launch (ns_csum_stream_release);
@@ -229,6 +261,17 @@ class Engine:
                                           total_len & 0xFFFF, ctypes.byref(r)),
               "ns_csum_pseudo_header")
         return int(r.value)
+
+
+def addr_sum(src: bytes, dst: bytes) -> int:
+    """Checksum(dst, Checksum(src, 0)) (checksum.go:113-114): the address part
+    of a route's pseudo-header sum, as ns_tcp_tx.addr_sum takes it."""
+    x = 0
+    for a in (bytes(src), bytes(dst)):
+        v = x + sum((a[i] << 8) + (a[i + 1] if i + 1 < len(a) else 0) for i in range(0, len(a), 2))
+        v = (v & 0xFFFF) + (v >> 16)
+        x = (v + (v >> 16)) & 0xFFFF
+    return x
 
 
 def combine(a: int, b: int) -> int:

@@ -371,6 +371,8 @@ TX_HDR = 54     # TCPMinimumSize + MaxHeaderLength (IPv4 20 + Ethernet 14), no o
 TX_MSS = RX_TCP - 20  # 1460
 TX_IP_AT = 14   # the IPv4 header's offset in a slot
 TX_TCP_AT = 34  # the TCP header's offset in a slot
+TX_SRC = bytes([10, 0, 0, 1])  # the route's addresses (every segment of one
+TX_DST = bytes([10, 0, 0, 2])  # sendTCPBatch call shares them, route.go:93-95)
 
 
 def tx_split_layout(n: int) -> tuple[int, int]:
@@ -433,6 +435,8 @@ def _split_packets(n: int, seed: int, device):
     """The sendTCPBatch-layout arena (splitmix64 bytes with fixed header
     fields, both checksum fields zero) and views of its header slots and
     payloads."""
+    import torch
+
     pay, total = tx_split_layout(n)
     arena = random_bytes_torch(seed, total, device)
     h = arena[:n * TX_HDR].view(n, TX_HDR)
@@ -446,11 +450,22 @@ def _split_packets(n: int, seed: int, device):
     ip[:, 8] = 64
     ip[:, 9] = 6
     ip[:, 10:12] = 0
+    ip[:, 12:16] = torch.tensor(list(TX_SRC), dtype=torch.uint8, device=arena.device)
+    ip[:, 16:20] = torch.tensor(list(TX_DST), dtype=torch.uint8, device=arena.device)
     t = h[:, TX_TCP_AT:TX_TCP_AT + 20]
     t[:, 12] = 0x50
     t[:, 13] = 0x18
     t[:, 16:20] = 0
     return arena, h, arena[pay:pay + n * TX_MSS].view(n, TX_MSS)
+
+
+def tx_struct_geometry(n: int) -> dict:
+    """The geometry of the sendTCPBatch-layout arena (_split_packets) for
+    ns_csum_tcp_tx: the same fill as tx_split_desc's table, taken from the
+    layout itself (Engine.tcp_tx)."""
+    pay, _ = tx_split_layout(n)
+    return dict(hdr_off=0, pay_off=pay, size=n * TX_MSS, mss=TX_MSS, slot=TX_HDR, ip_at=TX_IP_AT, ip_len=RX_IHL,
+                tcp_at=TX_TCP_AT, tcp_len=20, src=TX_SRC, dst=TX_DST, protocol=6)
 
 
 def tx_split_batch(n: int, seed: int, device):

@@ -170,3 +170,67 @@ int oracle_batch_mt(const uint8_t* arena, const oracle_desc* d, uint32_t n,
   for (int t = 1; t < nthreads; t++) pthread_join(th[t], NULL);
   return 0;
 }
+
+/* transport/tcp/connect.go:668-702 (sendTCPBatch) with buildTCPHdr
+ * (:634-666) per segment, then network/ipv4/ipv4.go:217-238 (addIPHeader)
+ * per segment as WritePackets (:271-285) runs it.  The headers are already
+ * encoded in the slots (tcp.Encode / ip.Encode, checksum fields zero: a fresh
+ * Prependable is zeroed); what remains are the checksum steps:
+ *   length := uint16(hdr.UsedLength() + packetSize)        connect.go:652
+ *   xsum := r.PseudoHeaderChecksum(ProtocolNumber, length)  :653, route.go:93-95
+ *   CHECKSUM_PARTIAL: tcp.SetChecksum(xsum)                 :655-660
+ *   else: xsum = ChecksumVVWithOffset(data, xsum, off, packetSize)   :662
+ *         tcp.SetChecksum(^tcp.CalculateChecksum(xsum))     :663, tcp.go:259-262
+ *   ip.SetChecksum(^ip.CalculateChecksum())                 ipv4.go:236, :251-253
+ * The payload is one view (data flattened), so ChecksumVVWithOffset is called
+ * on it with the segment's offset, as the Go loop does (off += packetSize). */
+static void put_be16(uint8_t* p, uint16_t v) {
+  p[0] = (uint8_t)(v >> 8);
+  p[1] = (uint8_t)v;
+}
+
+uint64_t oracle_send_tcp_batch(uint8_t* arena, uint64_t hdr_off, uint64_t pay_off,
+                               uint64_t size, uint32_t mss, uint32_t slot,
+                               uint32_t ip_at, uint32_t ip_len, uint32_t tcp_at,
+                               uint32_t tcp_len, uint32_t protocol,
+                               const uint8_t* src, uint32_t src_len,
+                               const uint8_t* dst, uint32_t dst_len, int mode,
+                               uint16_t* out) {
+  const uint64_t n = (size + mss - 1) / mss; /* connect.go:675 */
+  const uint8_t* view = arena + pay_off;
+  const uint64_t vlen = size;
+  uint64_t left = size, off = 0;
+  for (uint64_t i = 0; i < n; i++) {
+    uint64_t packet_size = mss;
+    if (packet_size > left) packet_size = left;
+    left -= packet_size;
+    uint8_t* hdr = arena + hdr_off + i * slot;
+    uint16_t tsum = 0, isum = 0;
+    if (mode != 2) {
+      uint8_t* tcp = hdr + tcp_at;
+      put_be16(tcp + 16, 0);
+      const uint16_t length = (uint16_t)(tcp_len + packet_size);
+      uint16_t xsum = oracle_pseudo_header(protocol, src, src_len, dst, dst_len, length);
+      if (mode == 1) {
+        put_be16(tcp + 16, xsum);
+      } else {
+        oracle_vv_with_offset(&view, &vlen, 1, xsum, (int64_t)off, (int64_t)packet_size, &xsum);
+        xsum = oracle_checksum(tcp, tcp_len, xsum);
+        put_be16(tcp + 16, (uint16_t)~xsum);
+      }
+      tsum = xsum;
+    }
+    if (ip_len) {
+      uint8_t* ip = hdr + ip_at;
+      put_be16(ip + 10, 0);
+      isum = oracle_checksum(ip, ip_len, 0);
+      put_be16(ip + 10, (uint16_t)~isum);
+    }
+    if (out) {
+      out[2 * i] = isum;
+      out[2 * i + 1] = tsum;
+    }
+    off += packet_size;
+  }
+  return n;
+}

@@ -31,6 +31,17 @@ int oracle_batch(const uint8_t* arena, uint64_t arena_bytes,
                  const oracle_desc* d, uint32_t n, uint16_t* out, int chained);
 int oracle_batch_mt(const uint8_t* arena, const oracle_desc* d, uint32_t n,
                     uint16_t* out, int nthreads);
+/* sendTCPBatch's checksum steps over its header slots and payload view
+ * (mode: 0 full, 1 CHECKSUM_PARTIAL, 2 none for TCP); writes the fields into
+ * `arena` and the un-complemented sums into out[2n] (or NULL).  Returns the
+ * segment count. */
+uint64_t oracle_send_tcp_batch(uint8_t* arena, uint64_t hdr_off, uint64_t pay_off,
+                               uint64_t size, uint32_t mss, uint32_t slot,
+                               uint32_t ip_at, uint32_t ip_len, uint32_t tcp_at,
+                               uint32_t tcp_len, uint32_t protocol,
+                               const uint8_t* src, uint32_t src_len,
+                               const uint8_t* dst, uint32_t dst_len, int mode,
+                               uint16_t* out);
 
 #ifdef __cplusplus
 }

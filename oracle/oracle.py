@@ -199,6 +199,10 @@ class _C:
             lib.oracle_batch.argtypes = [u8p, ctypes.c_uint64, u8p, ctypes.c_uint32, u8p, ctypes.c_int]
             lib.oracle_batch_mt.restype = ctypes.c_int
             lib.oracle_batch_mt.argtypes = [u8p, u8p, ctypes.c_uint32, u8p, ctypes.c_int]
+            u64, u32 = ctypes.c_uint64, ctypes.c_uint32
+            lib.oracle_send_tcp_batch.restype = u64
+            lib.oracle_send_tcp_batch.argtypes = [u8p, u64, u64, u64, u32, u32, u32, u32, u32, u32, u32,
+                                                  u8p, u32, u8p, u32, ctypes.c_int, u8p]
             cls._lib = lib
         return cls._lib
 
@@ -275,6 +279,27 @@ def c_batch_paired(arena: np.ndarray, desc: np.ndarray) -> tuple[np.ndarray, int
     d = np.array(desc, dtype=DESC_DTYPE, copy=True)
     d["flags"][0::2] &= ~np.uint16(CONT)
     return c_batch(arena, d, chained=True)
+
+
+def c_send_tcp_batch(arena: np.ndarray, hdr_off: int, pay_off: int, size: int, mss: int, slot: int,
+                     ip_at: int, ip_len: int, tcp_at: int, tcp_len: int, src: bytes, dst: bytes,
+                     protocol: int = 6, mode: str = "full") -> tuple[np.ndarray, np.ndarray]:
+    """sendTCPBatch's checksum steps (transport/tcp/connect.go:668-702 with
+    buildTCPHdr :634-666, then addIPHeader network/ipv4/ipv4.go:217-238 per
+    segment) over its header slots and payload view in `arena`, restated in C
+    (oracle_send_tcp_batch).  mode: "full", "partial" (CHECKSUM_PARTIAL) or
+    "none" (TX checksum offload).  Returns (the arena with the fields
+    written, the 2n un-complemented sums [IPv4, TCP] per segment)."""
+    a = np.array(arena, dtype=np.uint8, copy=True)
+    n = (size + mss - 1) // mss
+    out = np.zeros(2 * max(n, 1), dtype=np.uint16)
+    s = np.frombuffer(bytes(src) or b"\0", dtype=np.uint8)
+    d = np.frombuffer(bytes(dst) or b"\0", dtype=np.uint8)
+    L = _C.lib()
+    L.oracle_send_tcp_batch(_ptr(a), hdr_off, pay_off, size, mss, slot, ip_at, ip_len, tcp_at, tcp_len,
+                            protocol, _ptr(s), len(src), _ptr(d), len(dst),
+                            {"full": 0, "partial": 1, "none": 2}[mode], _ptr(out))
+    return a, out[:2 * n]
 
 
 def c_batch_mt(arena: np.ndarray, desc: np.ndarray, nthreads: int, out: np.ndarray | None = None) -> np.ndarray:

@@ -1,0 +1,215 @@
+"""GPU: ns_csum_tcp_tx — sendTCPBatch's transmit checksums from the batch's
+geometry (transport/tcp/connect.go:668-702, buildTCPHdr :634-666, addIPHeader
+network/ipv4/ipv4.go:217-238) — against the oracle's C restatement of those
+functions (oracle.c_send_tcp_batch), bit-exact: the whole arena after the
+call (both fields of every segment written, every other byte unchanged) and
+the un-complemented sums.
+
+Geometries: netstack's own (54-B slots: Ethernet 14 + IPv4 20 + TCP 20,
+MSS 1460), slots at odd addresses, odd MSS and slot sizes, TCP options, an
+IPv6 route (no IPv4 header, 16-B addresses), MSS 1 and 16 (several segment
+ends per 16-B chunk and per window), jumbo and 64 KiB GSO segments, a last
+segment of 1 byte, CHECKSUM_PARTIAL, TX offload, 2-byte field stores, and
+forced tiles (segments per wave) from 1 to 64."""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+V4S, V4D = bytes([192, 168, 1, 7]), bytes([10, 200, 3, 99])
+V6S = bytes(range(0x20, 0x30))
+V6D = bytes(range(0xF0, 0x100))
+
+
+def _geo(size, mss, slot=54, ip_at=14, ip_len=20, tcp_at=34, tcp_len=20, hdr_off=0, gap=64, pay_first=False,
+         src=V4S, dst=V4D):
+    n = -(-size // mss)
+    if pay_first:
+        pay_off = hdr_off
+        hdr_off = pay_off + size + gap
+        total = hdr_off + n * slot + 37
+    else:
+        pay_off = hdr_off + n * slot + gap
+        total = pay_off + size + 37
+    return dict(hdr_off=hdr_off, pay_off=pay_off, size=size, mss=mss, slot=slot, ip_at=ip_at, ip_len=ip_len,
+                tcp_at=tcp_at, tcp_len=tcp_len, src=src, dst=dst, protocol=6), total
+
+
+CASES = {
+    "netstack_default": _geo(1460 * 40, 1460),
+    "short_last_odd": _geo(1460 * 39 + 7, 1460),
+    "last_is_one_byte": _geo(1460 * 5 + 1, 1460),
+    "odd_slots_odd_mss": _geo(1461 * 50 + 3, 1461, slot=55, hdr_off=3, gap=5),
+    "options_32b_tcp": _geo(1448 * 70 + 100, 1448, slot=66, tcp_len=32),
+    "ipv6_route": _geo(1440 * 33 + 11, 1440, slot=74, ip_len=0, tcp_at=54, src=V6S, dst=V6D),
+    "payload_before_slots": _geo(1460 * 20 + 9, 1460, pay_first=True, hdr_off=13),
+    "mss_16": _geo(16 * 700 + 5, 16),
+    "mss_7": _geo(7 * 900 + 3, 7, hdr_off=1),
+    "mss_1": _geo(3000, 1),
+    "size_below_mss": _geo(999, 1460),
+    "jumbo_9000": _geo(9000 * 9 + 17, 9000, hdr_off=8),
+    "gso_64k": _geo(65535 * 3 + 1, 65535, gap=1),
+    "ip_header_with_options": _geo(1460 * 12, 1460, slot=78, ip_len=44, tcp_at=58),
+}
+
+
+def _arena(total, geo, seed):
+    rng = np.random.default_rng(seed)
+    a = rng.integers(0, 256, total, dtype=np.uint8)
+    n = -(-geo["size"] // geo["mss"])
+    # the route's addresses in each IPv4 header (the fields stay random: the
+    # call must sum them as zero)
+    if geo["ip_len"]:
+        for i in range(n):
+            at = geo["hdr_off"] + i * geo["slot"] + geo["ip_at"]
+            a[at + 12:at + 16] = np.frombuffer(geo["src"], np.uint8)
+            a[at + 16:at + 20] = np.frombuffer(geo["dst"], np.uint8)
+    return a
+
+
+def _run(engine, a, geo, mode="full", fields_only=False, tile=None, offset=0):
+    import torch
+
+    buf = torch.empty(offset + a.size, dtype=torch.uint8, device="cuda")
+    buf[offset:].copy_(torch.from_numpy(a))
+    arena = buf[offset:]
+    n = -(-geo["size"] // geo["mss"])
+    out = torch.full((2 * n,), -1, dtype=torch.int16, device="cuda")
+    old = os.environ.get("NS_CSUM_TX_TILE")
+    if tile is not None:
+        os.environ["NS_CSUM_TX_TILE"] = str(tile)
+    try:
+        engine.tcp_tx(arena, geo, out=out, mode=mode, fields_only=fields_only)
+        torch.cuda.synchronize()
+    finally:
+        if tile is not None:
+            if old is None:
+                del os.environ["NS_CSUM_TX_TILE"]
+            else:
+                os.environ["NS_CSUM_TX_TILE"] = old
+    return arena.cpu().numpy(), out.cpu().numpy().view(np.uint16)
+
+
+def _want(oracle_mod, a, geo, mode="full"):
+    g = geo
+    return oracle_mod.c_send_tcp_batch(a, g["hdr_off"], g["pay_off"], g["size"], g["mss"], g["slot"], g["ip_at"],
+                                       g["ip_len"], g["tcp_at"], g["tcp_len"], g["src"], g["dst"], g["protocol"],
+                                       mode)
+
+
+def _check(got_arena, got_sums, want_arena, want_sums, what):
+    bad = np.flatnonzero(got_arena != want_arena)
+    assert bad.size == 0, f"{what}: {bad.size} arena bytes differ, first at {bad[:8]}"
+    diff = np.flatnonzero(got_sums != want_sums)
+    assert diff.size == 0, f"{what}: {diff.size} sums differ, first at {diff[:8]}"
+
+
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_geometry_bit_exact(engine, oracle_mod, name):
+    geo, total = CASES[name]
+    a = _arena(total, geo, seed=len(name))
+    wa, ws = _want(oracle_mod, a, geo)
+    for offset in (0, 5):
+        ga, gs = _run(engine, a, geo, offset=offset)
+        _check(ga, gs, wa, ws, f"{name} (arena at +{offset})")
+
+
+@pytest.mark.parametrize("tile", [1, 2, 7, 31, 32, 33, 64])
+def test_forced_tiles(engine, oracle_mod, tile):
+    for name in ("short_last_odd", "odd_slots_odd_mss", "mss_7", "options_32b_tcp"):
+        geo, total = CASES[name]
+        a = _arena(total, geo, seed=tile)
+        wa, ws = _want(oracle_mod, a, geo)
+        ga, gs = _run(engine, a, geo, tile=tile)
+        _check(ga, gs, wa, ws, f"{name} tile {tile}")
+
+
+@pytest.mark.parametrize("mode", ["partial", "none"])
+def test_partial_and_offload(engine, oracle_mod, mode):
+    for name in ("netstack_default", "odd_slots_odd_mss", "ipv6_route"):
+        geo, total = CASES[name]
+        a = _arena(total, geo, seed=3)
+        wa, ws = _want(oracle_mod, a, geo, mode)
+        ga, gs = _run(engine, a, geo, mode=mode)
+        _check(ga, gs, wa, ws, f"{name} {mode}")
+
+
+def test_fields_only_stores(engine, oracle_mod):
+    for name in ("netstack_default", "odd_slots_odd_mss", "mss_7", "ipv6_route"):
+        geo, total = CASES[name]
+        a = _arena(total, geo, seed=4)
+        for mode in ("full", "partial"):
+            wa, ws = _want(oracle_mod, a, geo, mode)
+            ga, gs = _run(engine, a, geo, mode=mode, fields_only=True, tile=32)
+            _check(ga, gs, wa, ws, f"{name} {mode} fields only")
+
+
+def test_many_segments_full_tiles(engine, oracle_mod):
+    """Batches large enough for the launcher's own 32-segment tiles, MSS 1460
+    and MSS 16 (up to two segment ends per window per lane row)."""
+    for size, mss in ((1460 * 70_000 - 3, 1460), (16 * 70_000 + 9, 16)):
+        geo, total = _geo(size, mss, hdr_off=7)
+        a = _arena(total, geo, seed=mss)
+        wa, ws = _want(oracle_mod, a, geo)
+        ga, gs = _run(engine, a, geo)
+        _check(ga, gs, wa, ws, f"{size} B at MSS {mss}")
+
+
+def test_bench_layout_matches_table_path(engine):
+    """workloads.tx_struct_geometry over the bench's sendTCPBatch-layout arena:
+    the same fill as the NS_BATCH_PAIRED table (tx_split_desc) and as
+    tx_split_expected, byte for byte."""
+    import torch
+
+    from netstack_amd import workloads as W
+
+    n = 20_000
+    arena, _ = W.tx_split_batch(n, 11, "cuda")
+    engine.tcp_tx(arena, W.tx_struct_geometry(n))
+    want = W.tx_split_expected(n, 11, "cuda")
+    torch.cuda.synchronize()
+    assert torch.equal(arena, want)
+    arena2, _ = W.tx_split_batch(n, 11, "cuda")
+    desc = torch.from_numpy(W.tx_split_desc(n, paired=True).view(np.uint8).copy()).cuda()
+    engine.batch_tensors(arena2, desc, store=True, paired=True)
+    torch.cuda.synchronize()
+    assert torch.equal(arena2, want)
+
+
+def test_errors(engine):
+    import ctypes
+
+    import torch
+
+    from netstack_amd import _lib
+
+    L = _lib.lib()
+    h = engine._h
+    geo, total = CASES["netstack_default"]
+    buf = torch.zeros(total, dtype=torch.uint8, device="cuda")
+
+    def call(**kw):
+        t = _lib.NsTcpTx()
+        g = dict(geo, **kw)
+        for k in ("hdr_off", "pay_off", "size", "mss", "slot", "ip_at", "ip_len", "tcp_at", "tcp_len"):
+            setattr(t, k, g[k])
+        t.protocol, t.flags = 6, g.get("flags", 0)
+        return L.ns_csum_tcp_tx(h, buf.data_ptr(), g.get("arena_bytes", total), ctypes.byref(t), None, None)
+
+    assert call() == _lib.NS_OK
+    assert L.ns_csum_tcp_tx(None, buf.data_ptr(), total, None, None, None) == _lib.NS_EINVAL
+    assert L.ns_csum_tcp_tx(h, buf.data_ptr(), total, None, None, None) == _lib.NS_EINVAL
+    for bad in (dict(mss=0), dict(mss=65536), dict(slot=0), dict(slot=5000), dict(ip_len=10),
+                dict(ip_len=64), dict(ip_at=40), dict(tcp_len=16), dict(tcp_len=64), dict(tcp_at=40),
+                dict(flags=_lib.NS_TX_TCP_PARTIAL | _lib.NS_TX_TCP_NONE), dict(flags=0x80),
+                dict(pay_off=geo["hdr_off"] + 100)):  # payload over the slots
+        assert call(**bad) == _lib.NS_EINVAL, bad
+    assert call(arena_bytes=geo["pay_off"] + 10) == _lib.NS_ERANGE
+    assert call(pay_off=total - 10) == _lib.NS_ERANGE
+    assert call(size=0) == _lib.NS_OK  # no segments (connect.go:675)
+    # TX offload and no IPv4 header: nothing to do, and the slots may be anything
+    assert call(flags=_lib.NS_TX_TCP_NONE, ip_len=0, tcp_len=0) == _lib.NS_OK
+    torch.cuda.synchronize()
+    assert engine.sync() == 0

@@ -337,3 +337,79 @@ def test_tx_split_layout_is_the_wire_segments_checksummed(oracle_mod):
         assert (res[ip] == 0xFFFF).all() and (res[tcp] == 0xFFFF).all()
     with pytest.raises(ValueError):
         W.tx_split_desc(3, True, paired=True)
+
+
+def test_send_tcp_batch_oracle_matches_the_table_fill(oracle_mod):
+    """oracle.c_send_tcp_batch (sendTCPBatch's checksum steps restated in C,
+    the checker of ns_csum_tcp_tx) over the bench's sendTCPBatch-layout arena
+    equals the independently computed fill (workloads.tx_split_expected) and
+    the descriptor-table fill; its sums are the un-complemented fields."""
+    import oracle as O
+    from netstack_amd import workloads as W
+
+    n = 700
+    arena, _ = W.tx_split_batch(n, 9, "cpu")
+    a = arena.numpy()
+    g = W.tx_struct_geometry(n)
+    got, sums = O.c_send_tcp_batch(a, g["hdr_off"], g["pay_off"], g["size"], g["mss"], g["slot"], g["ip_at"],
+                                   g["ip_len"], g["tcp_at"], g["tcp_len"], g["src"], g["dst"])
+    assert np.array_equal(got, W.tx_split_expected(n, 9, "cpu", chunk=256).numpy())
+    d = W.tx_split_desc(n, True, paired=True)
+    res, _ = O.c_batch_paired(a, d)
+    ip, tcp = W.tx_split_order(n, True)
+    assert np.array_equal(sums[0::2], res[ip]) and np.array_equal(sums[1::2], res[tcp])
+
+
+def test_send_tcp_batch_oracle_against_python_restatement(oracle_mod):
+    """The C restatement against the pure-Python functions of checksum.go,
+    segment by segment as connect.go:679-692 cuts them: odd MSS, odd slot
+    size and offsets, a short last segment, the three TCP modes."""
+    import oracle as O
+
+    rng = np.random.default_rng(77)
+    size, mss, slot, hdr_off, pay_off = 97 * 13 + 5, 97, 61, 3, 3 + 14 * 61 + 9
+    n = -(-size // mss)
+    a = rng.integers(0, 256, pay_off + size + 11, dtype=np.uint8)
+    src, dst = bytes(rng.integers(0, 256, 16, dtype=np.uint8)), bytes(rng.integers(0, 256, 16, dtype=np.uint8))
+    for mode in ("full", "partial", "none"):
+        got, sums = O.c_send_tcp_batch(a, hdr_off, pay_off, size, mss, slot, 7, 24, 31, 28, src, dst, 6, mode)
+        want = a.copy()
+        left, off = size, 0
+        for i in range(n):
+            ps = min(mss, left)
+            left -= ps
+            s = hdr_off + i * slot
+            tcp = bytearray(want[s + 31:s + 59])
+            tcp[16:18] = b"\0\0"
+            if mode != "none":
+                x = O.py_pseudo_header(6, src, dst, (28 + ps) & 0xFFFF)
+                if mode == "partial":
+                    tcp[16:18] = x.to_bytes(2, "big")
+                else:
+                    x = O.py_checksum_vv_with_offset([bytes(a[pay_off:pay_off + size])], x, off, ps)
+                    x = O.py_checksum(bytes(tcp), x)
+                    tcp[16:18] = (~x & 0xFFFF).to_bytes(2, "big")
+                want[s + 31:s + 59] = np.frombuffer(bytes(tcp), np.uint8)
+                assert sums[2 * i + 1] == x
+            ip = bytearray(want[s + 7:s + 31])
+            ip[10:12] = b"\0\0"
+            v = O.py_checksum(bytes(ip), 0)
+            ip[10:12] = (~v & 0xFFFF).to_bytes(2, "big")
+            want[s + 7:s + 31] = np.frombuffer(bytes(ip), np.uint8)
+            assert sums[2 * i] == v
+            off += ps
+        assert np.array_equal(got, want), mode
+
+
+def test_route_addr_sum_host_helper(oracle_mod):
+    """engine.addr_sum (what ns_tcp_tx.addr_sum takes) is Checksum(dst,
+    Checksum(src, 0)) for IPv4 and IPv6 addresses."""
+    import oracle as O
+    from netstack_amd.engine import addr_sum
+
+    rng = np.random.default_rng(3)
+    for ln in (4, 16):
+        for _ in range(50):
+            s, d = bytes(rng.integers(0, 256, ln, dtype=np.uint8)), bytes(rng.integers(0, 256, ln, dtype=np.uint8))
+            assert addr_sum(s, d) == O.c_checksum(d, O.c_checksum(s, 0))
+    assert addr_sum(b"\xff\xff\xff\xff", b"\xff\xff\xff\xff") == O.c_checksum(b"\xff" * 4, O.c_checksum(b"\xff" * 4))
