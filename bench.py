@@ -55,9 +55,10 @@ def parse():
     ap.add_argument("--rx-layout", default="fused", choices=("fused", "chained"),
                     help="--config 7 (and 8 with --tx-layout wire) descriptor table: 2 independent descriptors "
                          "per packet, or 3 chained")
-    ap.add_argument("--tx-layout", default="split", choices=("split", "wire"),
-                    help="--config 8 packets: as sendTCPBatch builds them (header slots + payload view, "
-                         "NS_BATCH_PAIRED), or wire-contiguous like config 7")
+    ap.add_argument("--tx-layout", default="struct", choices=("struct", "split", "wire"),
+                    help="--config 8 packets: as sendTCPBatch builds them (header slots + payload view) "
+                         "filled from the batch geometry by ns_csum_tcp_tx (struct) or through an "
+                         "NS_BATCH_PAIRED descriptor table (split), or wire-contiguous like config 7")
     ap.add_argument("--rotate", type=int, default=0,
                     help="distinct batches cycled per step (0 = auto: enough to exceed the 256 MiB MALL)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline time budget")
@@ -649,12 +650,15 @@ def packet_mode(args, dist, eng, dev, tx: bool):
     TX (config 8, rank 1: buildTCPHdr + addIPHeader for a whole batch): the
     same segments with zeroed checksum fields, ns_csum_batch_dev_store writes
     ^sum into both fields of every packet (connect.go:662-663, ipv4.go:236).
-    By default (`--tx-layout split`) the segments are laid out as
+    By default (`--tx-layout struct`) the segments are laid out as
     sendTCPBatch builds them: stack.NewPacketDescriptors' one buffer of 54-B
     header slots (route.go:181-188) and the payload in a view of its own
-    (workloads.tx_split_*), three descriptors per packet with the payload +
-    TCP header pair folded in the tile (NS_BATCH_PAIRED).  `--tx-layout wire`
-    keeps config 7's wire-contiguous packets.  The fields are re-zeroed after
+    (workloads.tx_split_*), and ns_csum_tcp_tx fills them from the batch's
+    geometry (no table: a payload pass, then a header pass that writes the
+    slots back whole).  `--tx-layout split` fills the same layout through a
+    table of three descriptors per packet, the payload + TCP header pair
+    folded in the tile (NS_BATCH_PAIRED).  `--tx-layout wire` keeps config
+    7's wire-contiguous packets.  The fields are re-zeroed after
     the timed region and filled by one more launch; the check requires the
     whole arena to equal one whose checksums torch integer ops computed
     independently, and every filled segment to verify.
@@ -665,10 +669,12 @@ def packet_mode(args, dist, eng, dev, tx: bool):
     from netstack_amd import workloads as W
 
     seed = 7000 + dist.rank
-    split = tx and args.tx_layout == "split"
+    struct = tx and args.tx_layout == "struct"
+    split = tx and args.tx_layout in ("split", "struct")
     fused = args.rx_layout == "fused"
     chained = not fused and not split
     k = W.per_packet(fused)
+    geo = W.tx_struct_geometry(RX_N)
     if split:
         arena, _ = W.tx_split_batch(RX_N, seed, dev)
         d = W.tx_split_desc(RX_N, True, paired=True)
@@ -681,16 +687,22 @@ def packet_mode(args, dist, eng, dev, tx: bool):
     else:
         arena, d, bad_idx = W.rx_batch(RX_N, seed, dev, corrupt_every=1000, fused=fused)
     desc = torch.from_numpy(d.view(np.uint8).copy()).to(dev)
-    out = torch.empty(len(d), dtype=torch.int16, device=dev)
+    out = torch.empty(2 * RX_N if struct else len(d), dtype=torch.int16, device=dev)
     stream = torch.cuda.current_stream(dev)
     ev = [torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)]
     state = {"i": 0}
+
+    def fill():
+        if struct:
+            eng.tcp_tx(arena, geo, out=out, stream=stream)
+        else:
+            eng.batch_tensors(arena, desc, out, chained=chained, stream=stream, store=tx, paired=split)
 
     def step():
         k = state["i"]
         if k == args.warmup:
             ev[0].record(stream)
-        eng.batch_tensors(arena, desc, out, chained=chained, stream=stream, store=tx, paired=split)
+        fill()
         state["i"] = k + 1
         if state["i"] == args.warmup + args.steps:
             ev[1].record(stream)
@@ -700,6 +712,8 @@ def packet_mode(args, dist, eng, dev, tx: bool):
     kern_avg_s = ev[0].elapsed_time(ev[1]) / 1e3 / args.steps
     k_cpu = k * 65536
     span = int((d["off"][:k_cpu] + d["len"][:k_cpu].astype(np.uint64)).max())
+    if struct:  # the oracle's sample: the first 65,536 segments' slots and payload
+        span = geo["pay_off"] + 65536 * geo["mss"]
     if tx:
         # untimed: re-zero both fields, fill them with one launch, check
         if split:
@@ -711,7 +725,7 @@ def packet_mode(args, dist, eng, dev, tx: bool):
             p[:, 10:12] = 0
             p[:, 36:38] = 0
         before = arena[:span].cpu().numpy() if dist.rank == 0 and not args.no_cpu else None
-        eng.batch_tensors(arena, desc, out, chained=chained, stream=stream, store=True, paired=split)
+        fill()
         torch.cuda.synchronize()
         bad += eng.sync()
         rx = W.tx_split_expected(RX_N, seed, dev) if split else W.rx_batch(RX_N, seed, dev)[0]
@@ -733,13 +747,19 @@ def packet_mode(args, dist, eng, dev, tx: bool):
     fails = dist.sum(0.0 if prop_ok else 1.0, dev)
     pkt_bytes = RX_N * W.RX_PKT
     total = dist.sum(float(pkt_bytes), dev)
-    n_desc = len(d)
+    n_desc = 0 if struct else len(d)
     # packet bytes + the 8-B address re-read + per descriptor: 16-B read and
     # a u16 result written (chained: also a u32 partial + u16 flag written,
-    # then read back); TX adds the two 2-B field stores per packet
-    algo = pkt_bytes + 8 * RX_N + n_desc * (16 + 2 + (12 if chained else 0)) + (4 * RX_N if tx else 0)
+    # then read back); TX adds the two 2-B field stores per packet.  The
+    # structured fill reads each segment's payload and its two headers (the
+    # pseudo-header's addresses are the route's) and writes the two fields.
+    if struct:
+        algo = pkt_bytes + 4 * RX_N
+    else:
+        algo = pkt_bytes + 8 * RX_N + n_desc * (16 + 2 + (12 if chained else 0)) + (4 * RX_N if tx else 0)
     achieved = algo / kern_avg_s / 1e9
-    traffic, traffic_src = (pmc_traffic(args.pmc_json, "8split") if split else
+    traffic, traffic_src = (pmc_traffic(args.pmc_json, "8struct") if struct else
+                            pmc_traffic(args.pmc_json, "8split") if split else
                             pmc_traffic(args.pmc_json, 8 if tx else 7) if fused else (None, None))
     check = {"ipv4_all_valid": bool(ip_ok.all()), "tcp_failures": int(tcp_fail.size),
              "expected_failures": int(bad_idx.size), "ok": prop_ok, "ranks_failed": int(fails)}
@@ -754,15 +774,20 @@ def packet_mode(args, dist, eng, dev, tx: bool):
         "data": ("synthetic packets to send (checksum fields zero), resident in HBM" if tx else
                  "synthetic received packets (valid IPv4/TCP checksums, 1 in 1000 corrupted), resident in HBM"),
         "config": {"workload": ("tx" if tx else "rx") + ": 1,048,576 x 1500-B IPv4/TCP packets per GPU, "
-                   + ("in sendTCPBatch's layout (54-B header slots + a payload view), 3 descriptors each "
+                   + ("in sendTCPBatch's layout (54-B header slots + a payload view), filled from the "
+                      "batch geometry (ns_csum_tcp_tx, no descriptor table)" if struct
+                      else "in sendTCPBatch's layout (54-B header slots + a payload view), 3 descriptors each "
                       "(IPv4 header; payload + pseudo-header addresses and TCP header, NS_BATCH_PAIRED)" if split
                       else "2 descriptors each (IPv4 header; pseudo-header addresses + TCP segment)" if fused
                       else "3 chained descriptors each") + (", 2 checksum stores" if tx else ""),
                    "packets_per_gpu": RX_N, "descriptors_per_gpu": n_desc},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
-                     "kernel": kernel_name(arena.numel(), n_desc, chained=chained) + (" + nsk::fold_scan" if chained else ""),
-                     "layout": "split (sendTCPBatch: header slots + payload view)" if split else "wire",
+                     "kernel": ("nsk::tcp_tx<16,2,0,1,0,1> (payload pass) + nsk::tcp_tx<16,2,0,1,0,2> (header pass)"
+                                if struct else kernel_name(arena.numel(), n_desc, chained=chained)
+                                + (" + nsk::fold_scan" if chained else "")),
+                     "layout": ("struct (sendTCPBatch: header slots + payload view, ns_csum_tcp_tx)" if struct
+                                else "split (sendTCPBatch: header slots + payload view)" if split else "wire"),
                      "algorithmic_bytes_per_launch": algo, "avg_launch_us": kern_avg_s * 1e6},
         "bad_descriptors": bad,
         "property_check": check,
@@ -773,9 +798,21 @@ def packet_mode(args, dist, eng, dev, tx: bool):
         # CPU leg: the oracle on the first 65,536 packets' descriptors, same
         # bytes (TX: the bytes before the checked launch, and its stores)
         src = before if tx else arena[:span].cpu().numpy()
-        want, _ = O.c_batch_paired(src, d[:k_cpu]) if split else O.c_batch(src, d[:k_cpu], chained=chained)
-        ps = {"packets": k_cpu // k, "bit_exact": bool(np.array_equal(res[:k_cpu], want))}
-        if tx:
+        if struct:  # sendTCPBatch's checksum steps over the first 65,536 segments
+            g = geo
+            stored, want = O.c_send_tcp_batch(src, g["hdr_off"], g["pay_off"], 65536 * g["mss"], g["mss"],
+                                              g["slot"], g["ip_at"], g["ip_len"], g["tcp_at"], g["tcp_len"],
+                                              g["src"], g["dst"], g["protocol"])
+            ps = {"packets": 65536, "bit_exact": bool(np.array_equal(res[:2 * 65536], want))}
+            # the sample's slots as filled, and its payload unchanged
+            hs, po = 65536 * g["slot"], g["pay_off"]
+            got = arena[:span].cpu().numpy()
+            ps["stores_bit_exact"] = bool(np.array_equal(got[:hs], stored[:hs]) and
+                                          np.array_equal(got[po:span], stored[po:span]))
+        else:
+            want, _ = O.c_batch_paired(src, d[:k_cpu]) if split else O.c_batch(src, d[:k_cpu], chained=chained)
+            ps = {"packets": k_cpu // k, "bit_exact": bool(np.array_equal(res[:k_cpu], want))}
+        if tx and not struct:
             stored, _ = O.apply_stores(src, d[:k_cpu], want)
             ps["stores_bit_exact"] = bool(np.array_equal(arena[:span].cpu().numpy(), stored))
         result["parity_sample"] = ps

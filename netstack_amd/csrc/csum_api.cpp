@@ -228,6 +228,7 @@ struct ChainBuf {
 struct StreamScratch : nsh::ScratchSlot {
   ChainBuf chain;
   DevBuf<uint32_t> split;  // csum_split accumulators (zero between launches)
+  DevBuf<uint16_t> txpay;  // ns_csum_tcp_tx: per-segment payload values between its passes
   hipEvent_t last = nullptr;
   std::mutex mu;  // held while growing it and launching with it
 };
@@ -349,11 +350,13 @@ void retire_scratch(ns_csum_ctx* ctx, StreamScratch* sc) {
   if (ctx->retire && hipStreamWaitEvent(ctx->retire, sc->last, 0) == hipSuccess) {
     sc->chain.release_async(ctx->retire);
     sc->split.release_async(ctx->retire);
+    sc->txpay.release_async(ctx->retire);
   } else {  // no retire stream: free once its last launch is done
     (void)hipGetLastError();
     (void)hipEventSynchronize(sc->last);
     sc->chain.release();
     sc->split.release();
+    sc->txpay.release();
   }
   (void)hipEventDestroy(sc->last);
   delete sc;
@@ -1236,12 +1239,43 @@ int ns_csum_tcp_tx(ns_csum_ctx* ctx, uint8_t* d_arena, uint64_t arena_bytes, con
   geo.out = d_out;
   // A/B diagnostics, read per call: NS_CSUM_TX_VARIANT=k, a variant of the
   // kernel (csum_kernels.h launch_tcp_tx); NS_CSUM_TX_TILE=t, t segments per
-  // wave instead of the launcher's choice (tests and tuning).
+  // wave instead of the launcher's choice (tests and tuning), for the payload
+  // (or the only) pass; NS_CSUM_TX_HTILE=t the same for the header pass.
   const char* ev = std::getenv("NS_CSUM_TX_VARIANT");
   const uint32_t variant = ev ? (uint32_t)std::atoi(ev) : 0u;
   if (const char* v = std::getenv("NS_CSUM_TX_TILE")) geo.tile = (uint32_t)std::atoi(v);
-  HIP_TRY(nsk::launch_tcp_tx(geo, (hipStream_t)stream, variant));
-  return NS_OK;
+  if (const char* v = std::getenv("NS_CSUM_TX_HTILE")) geo.htile = (uint32_t)std::atoi(v);
+  hipStream_t s = (hipStream_t)stream;
+  if (!(mode & nsk::kTxTcpFull)) {  // no payload to read: one header pass
+    HIP_TRY(nsk::launch_tcp_tx(geo, s, variant));
+    return NS_OK;
+  }
+  // The payload pass leaves each segment's payload value in per-stream
+  // scratch (2 B per segment) for the header pass.
+  StreamScratch* sc = ctx->scratch.pin(scratch_key(s), make_scratch,
+                                       [&](StreamScratch* old) { retire_scratch(ctx, old); });
+  if (!sc) return NS_ENOMEM;
+  int rc = NS_OK;
+  {
+    std::lock_guard<std::mutex> lk(sc->mu);
+    const size_t cap = sc->txpay.cap;
+    const uint64_t t0 = now_ns();
+    rc = sc->txpay.ensure_async((size_t)n, false, s);
+    if (sc->txpay.cap != cap) {
+      const uint64_t dt = now_ns() - t0;
+      ctx->st.growths.fetch_add(1, std::memory_order_relaxed);
+      ctx->st.growth_ns_total.fetch_add(dt, std::memory_order_relaxed);
+      bump_max(ctx->st.growth_ns_max, dt);
+    }
+    if (rc == NS_OK) {
+      geo.xs = sc->txpay.p;
+      hipError_t e = nsk::launch_tcp_tx(geo, s, variant);
+      if (e == hipSuccess) e = hipEventRecord(sc->last, s);
+      if (e != hipSuccess) rc = report_hip(e, "launch_tcp_tx", __FILE__, __LINE__);
+    }
+  }
+  ctx->scratch.unpin(sc);
+  return rc;
 }
 
 int ns_csum_batch_host(ns_csum_ctx* ctx, const uint8_t* h_arena, uint64_t arena_bytes,

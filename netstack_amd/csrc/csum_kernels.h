@@ -103,8 +103,10 @@ struct TxGeo {
   uint32_t addr_sum, proto, mode, lds_rows;
   uint16_t* out;
   uint32_t wpg, pad;  // waves (tiles) per workgroup, set by the launcher
+  uint16_t* xs;       // n u16 of scratch for the two-pass shape, or nullptr
+  uint32_t htile, pad2;  // the header pass's tile (0: the launcher's choice)
 };
-// variant (A/B diagnostics; 0 = production): 1 = 8 windows in flight,
+// variant (A/B diagnostics; 0 = production): 1 = one fused pass,
 // 2 = nontemporal write-back, 3 = segments reduced over the wave in the loop.
 hipError_t launch_tcp_tx(TxGeo g, hipStream_t stream, uint32_t variant = 0);
 

@@ -140,8 +140,11 @@ __device__ __forceinline__ void tx_store_be16(uint64_t addr, uint32_t v) {
 // at once (DPP + readlane), 1 = each lane's partial parked in an LDS row of
 // the segment, summed by the segment's lane at the end (no cross-lane
 // dependency inside the stream loop), 2 = not at all (timing probes only:
-// wrong sums).
-template <int U, int AUX, int SP, int RED>
+// wrong sums); XF & 1 (timing probes only): no write-back.
+// PH = the pass: 0 = everything in one kernel; 1 = the payload pass (each
+// segment's payload value to g.xs, no headers); 2 = the header pass (the
+// payload values from g.xs, no payload read).
+template <int U, int AUX, int SP, int RED, int XF = 0, int PH = 0>
 __global__ __launch_bounds__(256) void tcp_tx(TxGeo g) {
   extern __shared__ uint4 tx_lds[];
   const uint32_t lane = threadIdx.x & 63u;
@@ -157,7 +160,7 @@ __global__ __launch_bounds__(256) void tcp_tx(TxGeo g) {
   const uint64_t h_base = h_lo & ~15ull;
   const uint32_t h_chunks = (uint32_t)((h_hi - h_base + 15) >> 4);
   const __amdgpu_buffer_rsrc_t hr = tx_srd(h_base, h_chunks * 16u);
-  for (uint32_t c = 0; c < h_chunks; c += 64) {
+  for (uint32_t c = 0; PH != 1 && c < h_chunks; c += 64) {
     const uint32_t o = (c + lane) * 16u;
     __builtin_amdgcn_raw_ptr_buffer_load_lds(hr, (__attribute__((address_space(3))) void*)(L + c * 16u), 16,
                                              o < h_chunks * 16u ? o : h_chunks * 16u, 0, 0, 0);
@@ -165,7 +168,7 @@ __global__ __launch_bounds__(256) void tcp_tx(TxGeo g) {
 
   // 2. the payload span: lane j ends up with segment j's W total
   uint32_t wres = 0;
-  if (g.mode & kTxTcpFull) {
+  if (PH != 2 && (g.mode & kTxTcpFull)) {
     const uint64_t p_lo = g.pay + s0 * g.mss;
     const uint64_t p_end = g.pay + g.size;
     const uint64_t p_hi = p_lo + (uint64_t)nseg * g.mss < p_end ? p_lo + (uint64_t)nseg * g.mss : p_end;
@@ -191,7 +194,7 @@ __global__ __launch_bounds__(256) void tcp_tx(TxGeo g) {
       }
 #pragma unroll
       for (int j = 0; j < U; ++j) {
-        if (w0 + j >= nwin) break;
+        // (windows past the span read zeros and hold no segment end)
         uint32_t w = wsum4(v[j], 0u);
         const uint32_t wbase = (w0 + j) * 1024u;
         while (RED != 2 && nb < wbase + 1024u) {
@@ -239,6 +242,14 @@ __global__ __launch_bounds__(256) void tcp_tx(TxGeo g) {
     }
   }
 
+  if constexpr (PH == 1) {  // the payload pass ends here
+    if (lane < nseg) {
+      const uint64_t si = s0 + lane;
+      g.xs[si] = (uint16_t)tx_class(wres, (uint32_t)((g.pay + si * g.mss) & 1u));
+    }
+    return;
+  }
+
   // 3. headers, then the fields (lane j = segment s0 + j)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the LDS-DMA copy is in
   __builtin_amdgcn_wave_barrier();
@@ -257,8 +268,8 @@ __global__ __launch_bounds__(256) void tcp_tx(TxGeo g) {
       x = tx_fold(x + g.proto);
       const uint32_t a = o + g.tcp_at;
       if (g.mode & kTxTcpFull) {
-        const uint32_t pa = (uint32_t)((g.pay + si * g.mss) & 1u);
-        x = tx_fold(x + tx_class(wres, pa));                                            // ChecksumVVWithOffset
+        const uint32_t pv = PH == 2 ? (uint32_t)g.xs[si] : tx_class(wres, (uint32_t)((g.pay + si * g.mss) & 1u));
+        x = tx_fold(x + pv);                                                            // ChecksumVVWithOffset
         x = tx_fold(x + tx_class(lds_wsum<16>(L, a, g.tcp_len, a + 16u), a & 1u));     // CalculateChecksum
         lds_put_be16(L, a + 16u, ~x & 0xFFFFu);
       } else {
@@ -280,6 +291,7 @@ __global__ __launch_bounds__(256) void tcp_tx(TxGeo g) {
     }
     return;
   }
+  if constexpr ((XF & 1) != 0) return;
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
 
@@ -306,27 +318,30 @@ __global__ __launch_bounds__(256) void tcp_tx(TxGeo g) {
   }
 }
 
-// Segments per wave for a batch: ~48 KiB of payload per wave, at most 32
-// segments, fewer when the batch would not give ~2,048 waves, and at most
-// ~8 KiB of header slots.
-static uint32_t tx_tile(const TxGeo& g) {
-  uint32_t t = (uint32_t)std::max<uint64_t>(1, (48u << 10) / std::max<uint32_t>(g.mss, 1));
-  t = std::min<uint32_t>(t, 32);
+// Segments per wave for a pass.  A pass that reads payload: about 12 KiB of
+// it per wave, at most 32 segments (1M x 1460 B, payload pass: 218 us at 8
+// segments, 222-228 at 4 / 16 / 32; tools/tx_struct_probe.py).  A header
+// pass: 64 segments (28 us at 64, 36 at 32, 58 at 8).  Fewer when the batch
+// would not give ~2,048 waves, and at most ~8 KiB of header slots.
+static uint32_t tx_tile(const TxGeo& g, bool pay) {
+  uint32_t t = pay ? (uint32_t)std::min<uint64_t>(32, std::max<uint64_t>(1, (12u << 10) / std::max<uint32_t>(g.mss, 1)))
+                   : 64u;
   const uint64_t per = (g.n + 2047) / 2048;
   if (per < t) t = (uint32_t)std::max<uint64_t>(1, per);
   while (t > 1 && (uint64_t)t * g.slot > (8u << 10)) t /= 2;
   return t;
 }
 
-// Tile, LDS and workgroup shape for a batch (tile = 0: tx_tile's choice).
-static hipError_t tx_shape(TxGeo& g, uint32_t* grid) {
-  if (g.tile == 0) g.tile = tx_tile(g);
+// Tile, LDS and workgroup shape of a pass (g.tile = 0: tx_tile's choice).
+static hipError_t tx_shape(TxGeo& g, int ph, uint32_t* grid) {
+  const bool pay = ph != 2 && (g.mode & kTxTcpFull), hdr = ph != 1;
+  if (g.tile == 0) g.tile = tx_tile(g, pay);
   if (g.tile > 64 || (uint64_t)g.tile * g.slot > (12u << 10)) return hipErrorInvalidValue;
   // The LDS-DMA copy writes whole 64-chunk (1 KiB) rows, zeros past the
   // region included: each wave's share is rounded up to whole rows; then the
-  // segments' rows of lane partials.
-  g.lds_rows = (uint32_t)(((uint64_t)g.tile * g.slot + 30) / 16 + 63) / 64 * 1024;
-  g.lds_wave = g.lds_rows + g.tile * 256u;
+  // segments' rows of lane partials (passes that read payload).
+  g.lds_rows = hdr ? (uint32_t)(((uint64_t)g.tile * g.slot + 30) / 16 + 63) / 64 * 1024 : 0u;
+  g.lds_wave = g.lds_rows + (pay ? g.tile * 256u : 0u);
   // 4 waves (tiles) per workgroup, fewer where their LDS would pass 64 KiB
   g.wpg = g.lds_wave <= (16u << 10) ? 4u : g.lds_wave <= (32u << 10) ? 2u : 1u;
   const uint64_t tiles = (g.n + g.tile - 1) / g.tile;
@@ -334,23 +349,38 @@ static hipError_t tx_shape(TxGeo& g, uint32_t* grid) {
   return hipSuccess;
 }
 
-template <int U, int AUX, int SP, int RED>
+template <int U, int AUX, int SP, int RED, int XF = 0, int PH = 0>
 static hipError_t launch_tcp_tx_t(TxGeo g, hipStream_t stream) {
   if (g.n == 0) return hipSuccess;
   uint32_t grid = 0;
-  const hipError_t e = tx_shape(g, &grid);
+  const hipError_t e = tx_shape(g, PH, &grid);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((tcp_tx<U, AUX, SP, RED>), dim3(grid), dim3(64 * g.wpg), (size_t)g.lds_wave * g.wpg, stream,
-                     g);
+  hipLaunchKernelGGL((tcp_tx<U, AUX, SP, RED, XF, PH>), dim3(grid), dim3(64 * g.wpg), (size_t)g.lds_wave * g.wpg,
+                     stream, g);
   return hipGetLastError();
+}
+
+// The production shape: a batch that needs its payload read takes two passes
+// when it has scratch for the payload values (g.xs): the payload pass streams
+// only payload, the header pass then reads, fills and writes back the slots
+// (interleaving the slot write-back with the payload stream
+// cost ~45 us on 1M segments).  One fused pass otherwise.
+template <int U, int AUX, int SP, int RED>
+static hipError_t launch_passes(TxGeo g, hipStream_t stream) {
+  if (!(g.mode & kTxTcpFull) || g.xs == nullptr) return launch_tcp_tx_t<U, AUX, SP, RED>(g, stream);
+  TxGeo h = g;
+  h.tile = g.htile;
+  hipError_t e = launch_tcp_tx_t<U, AUX, SP, RED, 0, 1>(g, stream);
+  if (e == hipSuccess) e = launch_tcp_tx_t<U, AUX, SP, RED, 0, 2>(h, stream);
+  return e;
 }
 
 hipError_t launch_tcp_tx(TxGeo g, hipStream_t stream, uint32_t variant) {
   switch (variant) {
-    case 1: return launch_tcp_tx_t<8, 2, 0, 1>(g, stream);
-    case 2: return launch_tcp_tx_t<16, 2, 1, 1>(g, stream);
-    case 3: return launch_tcp_tx_t<16, 2, 0, 0>(g, stream);
-    default: return launch_tcp_tx_t<16, 2, 0, 1>(g, stream);
+    case 1: g.xs = nullptr; return launch_tcp_tx_t<16, 2, 0, 1>(g, stream);  // one fused pass
+    case 2: return launch_passes<16, 2, 1, 1>(g, stream);
+    case 3: return launch_passes<16, 2, 0, 0>(g, stream);
+    default: return launch_passes<16, 2, 0, 1>(g, stream);
   }
 }
 

@@ -47,13 +47,17 @@ def main():
         names[k] = r["Kernel_Name"]
     ours = [k for k in sorted(disp) if ("calib_" in names[k] or "nsk::" in names[k])]
     out = {}
-    for i, (lab, meta) in enumerate(labels):
-        ks = ours[i * REPS:(i + 1) * REPS]
-        if len(ks) < REPS:
+    pos = 0
+    for lab, meta in labels:
+        kpl = int(meta.get("kernels", 1))  # dispatches per launch
+        ks = ours[pos:pos + REPS * kpl]
+        pos += REPS * kpl
+        if len(ks) < REPS * kpl:
             break
         counters = sorted({c for k in ks for c in disp[k]})
-        avg = {c: sum(disp[k].get(c, 0.0) for k in ks) / len(ks) for c in counters}
-        out[lab] = {"kernel": names[ks[0]][:80], "meta": meta, "avg": avg}
+        avg = {c: sum(disp[k].get(c, 0.0) for k in ks) / REPS for c in counters}  # per launch
+        kern = " + ".join(dict.fromkeys(names[k][:80] for k in ks))
+        out[lab] = {"kernel": kern, "meta": meta, "avg": avg}
     # FETCH_SIZE calibration per access shape
     cal = {}
     for m in ("calib800", "calib400", "calib102", "calib2164"):
@@ -67,6 +71,8 @@ def main():
         # lines nontemporally: the 16-lane-group shape (calib2164)
         big = float(out[lab]["meta"].get("big_share", 1.0)) if lab != "cfg3" else 1.0
         shape = {"calib2164": big, "calib400": 1.0 - big}
+        if "shape" in out[lab]["meta"]:  # one named access shape
+            shape = {out[lab]["meta"]["shape"]: 1.0}
         f = None
         if all(cal.get(m) for m, w in shape.items() if w > 0):
             f = sum(w * cal[m] for m, w in shape.items() if w > 0)

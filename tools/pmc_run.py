@@ -12,8 +12,8 @@ batches in.
 --set cfg3probe: cfg3 rotated through the product's small-packet instance and
 the floor kernels of tools/tune.py (libns_tune.so), for the SQ counters.
 
-Each label covers REPS launches; tools/pmc_parse.py maps dispatches to labels
-in the order printed here."""
+Each label covers REPS launches (of `kernels` dispatches each, default 1);
+tools/pmc_parse.py maps dispatches to labels in the order printed here."""
 import argparse
 import ctypes
 import os
@@ -112,6 +112,20 @@ def main_set(dev, L):
     print(f"LABEL cfg8split algorithmic_bytes={algo} payload={n * W.RX_PKT} arena={arena.numel()} n={len(d)} "
           f"big_share={big_share(d):.4f}", flush=True)
     del arena, desc, out
+    torch.cuda.empty_cache()
+    # cfg 8 as bench.py runs it by default: the same layout filled from its
+    # geometry (ns_csum_tcp_tx: a payload pass and a header pass per call, so
+    # 2 dispatches per launch; the payload is read in whole 1-KiB windows per
+    # wave instruction, nontemporal: the coalesced calibration shape)
+    arena, _ = W.tx_split_batch(n, 7000, dev)
+    geo = W.tx_struct_geometry(n)
+    for _ in range(REPS):
+        eng.tcp_tx(arena, geo)
+    torch.cuda.synchronize()
+    algo = n * W.RX_PKT + 4 * n
+    print(f"LABEL cfg8struct algorithmic_bytes={algo} payload={n * W.RX_PKT} arena={arena.numel()} n={n} "
+          f"kernels=2 shape=calib102", flush=True)
+    del arena
     torch.cuda.empty_cache()
 
 

@@ -3,17 +3,19 @@
 (54-B header slots, one payload view):
   paired_rx / paired_tx   the NS_BATCH_PAIRED descriptor table (3M
                           descriptors, 48 MB), without / with the stores
-  struct                  ns_csum_tcp_tx: the geometry, no table; each wave's
-                          header slots written back whole
-  struct_v1..v3           its A/B variants (NS_CSUM_TX_VARIANT: 8 windows in
-                          flight, nontemporal write-back, default-policy loads)
-  struct_t8/t16/t64       8 / 16 / 64 segments per wave (NS_CSUM_TX_TILE)
+  struct                  ns_csum_tcp_tx: the geometry, no table; a payload
+                          pass, then a header pass writing the slots back whole
+  struct_v1..v3           its A/B variants (NS_CSUM_TX_VARIANT: one fused
+                          pass, nontemporal write-back, wave reductions)
+  struct_pP_hH            P segments per wave in the payload pass, H in the
+                          header pass (NS_CSUM_TX_TILE / _HTILE)
   struct_fields           2-byte field stores instead (NS_TX_FIELDS_ONLY)
   struct_hdr_only         the IPv4 fields and CHECKSUM_PARTIAL sums only (no
                           payload read: the header-side floor)
-  txv_noreduce            libns_txv.so (tools/tx_variants.hip): the stream
-                          without any segment reduction (timing only)
-  txv_u32 / txv_u4        32 / 4 windows in flight
+  txv_*                   libns_txv.so (tools/tx_variants.hip), timing
+                          only: noreduce (no segment reductions), u8 / u4 (8 /
+                          4 windows in flight), nowb (no header write-back),
+                          stream (neither: the bare stream + header reads)
 Each over 2 rotating batches, median of `--rounds` rounds of `--reps`
 back-to-back launches.  Every fill is checked byte for byte against
 workloads.tx_split_expected.
@@ -43,27 +45,31 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--n", type=int, default=1 << 20)
+    ap.add_argument("--only", default="", help="comma-separated variant names")
     args = ap.parse_args()
     n = args.n
     dev = torch.device("cuda", 0)
     stream = torch.cuda.current_stream(dev)
     eng = Engine(0)
     out = torch.empty(3 * n, dtype=torch.int16, device=dev)
+    out2 = torch.empty(2 * n, dtype=torch.int16, device=dev)
     geo = W.tx_struct_geometry(n)
     batches = [W.tx_split_batch(n, 7000 + r, dev)[0] for r in range(2)]
     pd = [torch.from_numpy(W.tx_split_desc(n, s, True).view(np.uint8).copy()).to(dev) for s in (True, False)]
 
-    def env(k, v):
+    def env(k, v, k2=None, v2=None):
         def f(r, **kw):
-            old = os.environ.get(k)
-            os.environ[k] = v
+            keys = {k: v} if k2 is None else {k: v, k2: v2}
+            old = {x: os.environ.get(x) for x in keys}
+            os.environ.update(keys)
             try:
                 eng.tcp_tx(batches[r], geo, stream=stream, **kw)
             finally:
-                if old is None:
-                    del os.environ[k]
-                else:
-                    os.environ[k] = old
+                for x, o in old.items():
+                    if o is None:
+                        del os.environ[x]
+                    else:
+                        os.environ[x] = o
         return f
 
     from netstack_amd.engine import addr_sum
@@ -72,16 +78,17 @@ def main():
         _fields_ = [(k, ctypes.c_uint64) for k in ("hdr", "pay", "size", "n")] + \
                    [(k, ctypes.c_uint32) for k in ("mss", "slot", "tile", "lds_wave", "ip_at", "ip_len", "tcp_at",
                                                    "tcp_len", "addr_sum", "proto", "mode", "lds_rows")] + \
-                   [("out", ctypes.c_void_p), ("wpg", ctypes.c_uint32), ("pad", ctypes.c_uint32)]
+                   [("out", ctypes.c_void_p), ("wpg", ctypes.c_uint32), ("pad", ctypes.c_uint32),
+                    ("xs", ctypes.c_void_p), ("htile", ctypes.c_uint32), ("pad2", ctypes.c_uint32)]
 
     TXV = ctypes.CDLL(os.path.join(ROOT, "netstack_amd", "lib", "libns_txv.so"))
     TXV.txv_launch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
 
-    def txv(k):
+    def txv(k, tile=0):
         def f(r):
             a = batches[r]
             t = TxGeo(hdr=a.data_ptr() + geo["hdr_off"], pay=a.data_ptr() + geo["pay_off"], size=geo["size"], n=n,
-                      mss=geo["mss"], slot=geo["slot"], tile=0, ip_at=geo["ip_at"], ip_len=geo["ip_len"],
+                      mss=geo["mss"], slot=geo["slot"], tile=tile, ip_at=geo["ip_at"], ip_len=geo["ip_len"],
                       tcp_at=geo["tcp_at"], tcp_len=geo["tcp_len"], addr_sum=addr_sum(geo["src"], geo["dst"]),
                       proto=6, mode=3)
             assert TXV.txv_launch(ctypes.byref(t), stream.cuda_stream, k) == 0
@@ -91,22 +98,24 @@ def main():
         "paired_rx": lambda r: eng.batch_tensors(batches[r], pd[1], out, paired=True, stream=stream),
         "paired_tx": lambda r: eng.batch_tensors(batches[r], pd[0], out, paired=True, stream=stream, store=True),
         "struct": lambda r: eng.tcp_tx(batches[r], geo, stream=stream),
-        "struct_v1": env("NS_CSUM_TX_VARIANT", "1"),
-        "struct_v2": env("NS_CSUM_TX_VARIANT", "2"),
-        "struct_v3": env("NS_CSUM_TX_VARIANT", "3"),
-        "struct_t8": env("NS_CSUM_TX_TILE", "8"),
-        "struct_t16": env("NS_CSUM_TX_TILE", "16"),
-        "struct_t64": env("NS_CSUM_TX_TILE", "64"),
+        "struct_fused": env("NS_CSUM_TX_VARIANT", "1"),
+        "struct_ntwb": env("NS_CSUM_TX_VARIANT", "2"),
         "struct_fields": lambda r: eng.tcp_tx(batches[r], geo, stream=stream, fields_only=True),
         "struct_hdr_only": lambda r: eng.tcp_tx(batches[r], geo, stream=stream, mode="partial"),
-        "txv_noreduce": txv(1),
-        "txv_u32": txv(2),
-        "txv_u4": txv(3),
+        "txv_stream_t8": txv(5, 8),
+        "struct_out": lambda r: eng.tcp_tx(batches[r], geo, out=out2, stream=stream),
+        "struct_norot": lambda r: eng.tcp_tx(batches[0], geo, stream=stream),
+        "struct_out_norot": lambda r: eng.tcp_tx(batches[0], geo, out=out2, stream=stream),
     }
+    for pt in (4, 8, 16, 32):
+        for ht in (16, 32, 64):
+            variants[f"struct_p{pt}_h{ht}"] = env("NS_CSUM_TX_TILE", str(pt), "NS_CSUM_TX_HTILE", str(ht))
+    if args.only:
+        variants = {k: v for k, v in variants.items() if k in args.only.split(",")}
     checks = {}
     want = W.tx_split_expected(n, 7000, dev)
     for name, f in variants.items():
-        if name.endswith("_rx") or name in ("struct_hdr_only", "txv_noreduce"):
+        if name.endswith("_rx") or name in ("struct_hdr_only", "txv_noreduce") or "nowb" in name or "stream" in name:
             continue
         h = batches[0][:n * W.TX_HDR].view(n, W.TX_HDR)
         h[:, W.TX_IP_AT + 10:W.TX_IP_AT + 12] = 0
@@ -117,19 +126,24 @@ def main():
     del want
     assert eng.sync() == 0
     times = {k: [] for k in variants}
+    host = {k: [] for k in variants}
+    import time
     for _ in range(args.rounds):
         for name, f in variants.items():
             for k in range(3):
                 f(k % 2)
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record(stream)
+            t0 = time.perf_counter()
             for k in range(args.reps):
                 f(k % 2)
+            host[name].append((time.perf_counter() - t0) * 1e6 / args.reps)
             b.record(stream)
             b.synchronize()
             times[name].append(a.elapsed_time(b) * 1e3 / args.reps)
     med = {k: round(float(np.median(v)), 2) for k, v in times.items()}
     print(json.dumps({"packets": n, "median_us": med, "fill_bit_exact": checks,
+                      "host_enqueue_us_per_call": {k: round(float(np.median(v)), 1) for k, v in host.items()},
                       "rounds_us": {k: [round(x, 2) for x in v] for k, v in times.items()}}, indent=1))
 
 
