@@ -1250,6 +1250,15 @@ int ns_csum_tcp_tx(ns_csum_ctx* ctx, uint8_t* d_arena, uint64_t arena_bytes, con
     HIP_TRY(nsk::launch_tcp_tx(geo, s, variant));
     return NS_OK;
   }
+  if (d_out) {
+    // The payload pass parks each segment's payload value in d_out[2i + 1],
+    // which the header pass then overwrites with the TCP sum: no scratch, and
+    // no event to record (an event per call put ~6 us between calls).
+    geo.xs = d_out + 1;
+    geo.xstride = 2;
+    HIP_TRY(nsk::launch_tcp_tx(geo, s, variant));
+    return NS_OK;
+  }
   // The payload pass leaves each segment's payload value in per-stream
   // scratch (2 B per segment) for the header pass.
   StreamScratch* sc = ctx->scratch.pin(scratch_key(s), make_scratch,
@@ -1269,6 +1278,7 @@ int ns_csum_tcp_tx(ns_csum_ctx* ctx, uint8_t* d_arena, uint64_t arena_bytes, con
     }
     if (rc == NS_OK) {
       geo.xs = sc->txpay.p;
+      geo.xstride = 1;
       hipError_t e = nsk::launch_tcp_tx(geo, s, variant);
       if (e == hipSuccess) e = hipEventRecord(sc->last, s);
       if (e != hipSuccess) rc = report_hip(e, "launch_tcp_tx", __FILE__, __LINE__);

@@ -103,8 +103,9 @@ struct TxGeo {
   uint32_t addr_sum, proto, mode, lds_rows;
   uint16_t* out;
   uint32_t wpg, pad;  // waves (tiles) per workgroup, set by the launcher
-  uint16_t* xs;       // n u16 of scratch for the two-pass shape, or nullptr
-  uint32_t htile, pad2;  // the header pass's tile (0: the launcher's choice)
+  uint16_t* xs;          // the two-pass shape's payload values (xs[i * xstride]), or nullptr
+  uint32_t htile;        // the header pass's tile (0: the launcher's choice)
+  uint32_t xstride;      // 1 (scratch) or 2 (parked in out[2i + 1])
 };
 // variant (A/B diagnostics; 0 = production): 1 = one fused pass,
 // 2 = nontemporal write-back, 3 = segments reduced over the wave in the loop.

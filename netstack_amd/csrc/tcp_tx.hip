@@ -245,7 +245,7 @@ __global__ __launch_bounds__(256) void tcp_tx(TxGeo g) {
   if constexpr (PH == 1) {  // the payload pass ends here
     if (lane < nseg) {
       const uint64_t si = s0 + lane;
-      g.xs[si] = (uint16_t)tx_class(wres, (uint32_t)((g.pay + si * g.mss) & 1u));
+      g.xs[si * g.xstride] = (uint16_t)tx_class(wres, (uint32_t)((g.pay + si * g.mss) & 1u));
     }
     return;
   }
@@ -268,7 +268,8 @@ __global__ __launch_bounds__(256) void tcp_tx(TxGeo g) {
       x = tx_fold(x + g.proto);
       const uint32_t a = o + g.tcp_at;
       if (g.mode & kTxTcpFull) {
-        const uint32_t pv = PH == 2 ? (uint32_t)g.xs[si] : tx_class(wres, (uint32_t)((g.pay + si * g.mss) & 1u));
+        const uint32_t pv = PH == 2 ? (uint32_t)g.xs[si * g.xstride]
+                                    : tx_class(wres, (uint32_t)((g.pay + si * g.mss) & 1u));
         x = tx_fold(x + pv);                                                            // ChecksumVVWithOffset
         x = tx_fold(x + tx_class(lds_wsum<16>(L, a, g.tcp_len, a + 16u), a & 1u));     // CalculateChecksum
         lds_put_be16(L, a + 16u, ~x & 0xFFFFu);

@@ -79,7 +79,7 @@ def main():
                    [(k, ctypes.c_uint32) for k in ("mss", "slot", "tile", "lds_wave", "ip_at", "ip_len", "tcp_at",
                                                    "tcp_len", "addr_sum", "proto", "mode", "lds_rows")] + \
                    [("out", ctypes.c_void_p), ("wpg", ctypes.c_uint32), ("pad", ctypes.c_uint32),
-                    ("xs", ctypes.c_void_p), ("htile", ctypes.c_uint32), ("pad2", ctypes.c_uint32)]
+                    ("xs", ctypes.c_void_p), ("htile", ctypes.c_uint32), ("xstride", ctypes.c_uint32)]
 
     TXV = ctypes.CDLL(os.path.join(ROOT, "netstack_amd", "lib", "libns_txv.so"))
     TXV.txv_launch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
