@@ -7,7 +7,8 @@ for c in 1 2 3 4 5 7 8; do
   echo "bench cfg$c"
   timeout -k 10 300 python bench.py --config $c > $OUT/bench_cfg$c.json 2> $OUT/bench_cfg$c.err
 done
-echo "bench cfg8 wire layout"
+echo "bench cfg8 paired table and wire layout"
+timeout -k 10 300 python bench.py --config 8 --tx-layout split > $OUT/bench_cfg8_split.json 2> $OUT/bench_cfg8_split.err
 timeout -k 10 300 python bench.py --config 8 --tx-layout wire > $OUT/bench_cfg8_wire.json 2> $OUT/bench_cfg8_wire.err
 echo "host modes"
 for c in 2 3 4; do
