@@ -250,14 +250,15 @@ __global__ __launch_bounds__(256) void tcp_tx(TxGeo g) {
     return;
   }
 
-  // 3. headers, then the fields (lane j = segment s0 + j)
+  // 3. headers, then the fields: lane l takes segments s0 + l, s0 + l + 64, ...
+  // (a pass that reads payload has at most 64, so lane j = segment j)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the LDS-DMA copy is in
   __builtin_amdgcn_wave_barrier();
-  const uint32_t o = (uint32_t)(h_lo - h_base) + lane * g.slot;  // slot j in LDS
-  uint32_t ipv = 0, tcpv = 0;
-  if (lane < nseg) {
-    const uint64_t si = s0 + lane;
+  for (uint32_t j = lane; j < nseg; j += 64) {
+    const uint32_t o = (uint32_t)(h_lo - h_base) + j * g.slot;  // slot j in LDS
+    const uint64_t si = s0 + j;
     const uint32_t size = si + 1 < g.n ? g.mss : (uint32_t)(g.size - (g.n - 1) * (uint64_t)g.mss);
+    uint32_t ipv = 0, tcpv = 0;
     if (g.mode & kTxIp) {
       const uint32_t a = o + g.ip_at;
       ipv = tx_fold(tx_class(lds_wsum<16>(L, a, g.ip_len, a + 10u), a & 1u));  // Checksum(ip[:IHL], 0)
@@ -282,16 +283,14 @@ __global__ __launch_bounds__(256) void tcp_tx(TxGeo g) {
       g.out[2 * si] = (uint16_t)ipv;
       g.out[2 * si + 1] = (uint16_t)tcpv;
     }
-  }
-  if (g.mode & kTxFieldsOnly) {  // only the 2-byte fields, as csum_hyb stores them
-    if (lane < nseg) {
-      const uint64_t slot = h_lo + (uint64_t)lane * g.slot;
+    if (g.mode & kTxFieldsOnly) {  // only the 2-byte fields, as csum_hyb stores them
+      const uint64_t slot = h_lo + (uint64_t)j * g.slot;
       if (g.mode & kTxIp) tx_store_be16(slot + g.ip_at + 10u, ~ipv & 0xFFFFu);
       if (g.mode & kTxTcpFull) tx_store_be16(slot + g.tcp_at + 16u, ~tcpv & 0xFFFFu);
       if (g.mode & kTxTcpPartial) tx_store_be16(slot + g.tcp_at + 16u, tcpv);
     }
-    return;
   }
+  if (g.mode & kTxFieldsOnly) return;
   if constexpr ((XF & 1) != 0) return;
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -337,7 +336,8 @@ static uint32_t tx_tile(const TxGeo& g, bool pay) {
 static hipError_t tx_shape(TxGeo& g, int ph, uint32_t* grid) {
   const bool pay = ph != 2 && (g.mode & kTxTcpFull), hdr = ph != 1;
   if (g.tile == 0) g.tile = tx_tile(g, pay);
-  if (g.tile > 64 || (uint64_t)g.tile * g.slot > (12u << 10)) return hipErrorInvalidValue;
+  // (a lane holds a payload-reading pass's segment; a header pass loops)
+  if (g.tile > (pay ? 64u : 256u) || (uint64_t)g.tile * g.slot > (12u << 10)) return hipErrorInvalidValue;
   // The LDS-DMA copy writes whole 64-chunk (1 KiB) rows, zeros past the
   // region included: each wave's share is rounded up to whole rows; then the
   // segments' rows of lane partials (passes that read payload).

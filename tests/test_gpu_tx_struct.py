@@ -69,7 +69,7 @@ def _arena(total, geo, seed):
     return a
 
 
-def _run(engine, a, geo, mode="full", fields_only=False, tile=None, offset=0):
+def _run(engine, a, geo, mode="full", fields_only=False, tile=None, offset=0, htile=None):
     import torch
 
     buf = torch.empty(offset + a.size, dtype=torch.uint8, device="cuda")
@@ -77,18 +77,18 @@ def _run(engine, a, geo, mode="full", fields_only=False, tile=None, offset=0):
     arena = buf[offset:]
     n = -(-geo["size"] // geo["mss"])
     out = torch.full((2 * n,), -1, dtype=torch.int16, device="cuda")
-    old = os.environ.get("NS_CSUM_TX_TILE")
-    if tile is not None:
-        os.environ["NS_CSUM_TX_TILE"] = str(tile)
+    knobs = {k: str(v) for k, v in (("NS_CSUM_TX_TILE", tile), ("NS_CSUM_TX_HTILE", htile)) if v is not None}
+    old = {k: os.environ.get(k) for k in knobs}
+    os.environ.update(knobs)
     try:
         engine.tcp_tx(arena, geo, out=out, mode=mode, fields_only=fields_only)
         torch.cuda.synchronize()
     finally:
-        if tile is not None:
-            if old is None:
-                del os.environ["NS_CSUM_TX_TILE"]
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
             else:
-                os.environ["NS_CSUM_TX_TILE"] = old
+                os.environ[k] = v
     return arena.cpu().numpy(), out.cpu().numpy().view(np.uint16)
 
 
@@ -124,6 +124,38 @@ def test_forced_tiles(engine, oracle_mod, tile):
         wa, ws = _want(oracle_mod, a, geo)
         ga, gs = _run(engine, a, geo, tile=tile)
         _check(ga, gs, wa, ws, f"{name} tile {tile}")
+
+
+@pytest.mark.parametrize("htile", [1, 3, 64, 100, 129, 222])
+def test_header_pass_tiles(engine, oracle_mod, htile):
+    """The header pass's tile (NS_CSUM_TX_HTILE): up to 256 segments per wave,
+    each lane looping over every 64th; with and without d_out (payload values
+    parked in d_out or in per-stream scratch)."""
+    for name in ("short_last_odd", "odd_slots_odd_mss", "ipv6_route"):
+        geo, total = CASES[name]
+        if htile * geo["slot"] > 12 << 10:
+            continue
+        a = _arena(total, geo, seed=htile)
+        wa, ws = _want(oracle_mod, a, geo)
+        ga, gs = _run(engine, a, geo, htile=htile)
+        _check(ga, gs, wa, ws, f"{name} header tile {htile}")
+        for mode in ("partial",):
+            wa2, ws2 = _want(oracle_mod, a, geo, mode)
+            ga2, gs2 = _run(engine, a, geo, mode=mode, tile=htile)  # one header-only pass
+            _check(ga2, gs2, wa2, ws2, f"{name} {mode} tile {htile}")
+
+
+def test_without_out_uses_scratch(engine, oracle_mod):
+    """d_out = NULL: the payload values go through the stream's scratch."""
+    import torch
+
+    geo, total = CASES["odd_slots_odd_mss"]
+    a = _arena(total, geo, seed=21)
+    wa, _ = _want(oracle_mod, a, geo)
+    buf = torch.from_numpy(a).cuda()
+    engine.tcp_tx(buf, geo)
+    torch.cuda.synchronize()
+    assert np.array_equal(buf.cpu().numpy(), wa)
 
 
 @pytest.mark.parametrize("mode", ["partial", "none"])

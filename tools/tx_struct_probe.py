@@ -108,7 +108,7 @@ def main():
         "struct_out_norot": lambda r: eng.tcp_tx(batches[0], geo, out=out2, stream=stream),
     }
     for pt in (4, 8, 16, 32):
-        for ht in (16, 32, 64):
+        for ht in (16, 32, 64, 96, 128, 192):
             variants[f"struct_p{pt}_h{ht}"] = env("NS_CSUM_TX_TILE", str(pt), "NS_CSUM_TX_HTILE", str(ht))
     if args.only:
         variants = {k: v for k, v in variants.items() if k in args.only.split(",")}
