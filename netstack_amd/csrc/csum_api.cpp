@@ -1197,15 +1197,13 @@ int ns_csum_tcp_tx(ns_csum_ctx* ctx, uint8_t* d_arena, uint64_t arena_bytes, con
                    uint16_t* d_out, void* stream) {
   if (!ctx || !tx || (arena_bytes && !d_arena)) return NS_EINVAL;
   const ns_tcp_tx& t = *tx;
-  if (t.mss == 0 || t.mss > 0xFFFFu || t.slot == 0 || t.slot > 4096) return NS_EINVAL;
-  const bool partial = (t.flags & NS_TX_TCP_PARTIAL) != 0, none = (t.flags & NS_TX_TCP_NONE) != 0;
-  if ((partial && none) || (t.flags & ~(NS_TX_TCP_PARTIAL | NS_TX_TCP_NONE | NS_TX_FIELDS_ONLY))) return NS_EINVAL;
-  if (t.ip_len && (t.ip_len < 12 || t.ip_len > 60 || (uint32_t)t.ip_at + t.ip_len > t.slot)) return NS_EINVAL;
-  if (!none && (t.tcp_len < 18 || t.tcp_len > 60 || (uint32_t)t.tcp_at + t.tcp_len > t.slot)) return NS_EINVAL;
-  const uint64_t n = t.size / t.mss + (t.size % t.mss != 0);
-  if (n >= (1ull << 32)) return NS_EINVAL;
-  const uint32_t mode = (t.ip_len ? nsk::kTxIp : 0u) | (none ? 0u : partial ? nsk::kTxTcpPartial : nsk::kTxTcpFull) |
-                        ((t.flags & NS_TX_FIELDS_ONLY) ? nsk::kTxFieldsOnly : 0u);
+  nsh::TxPlan plan;
+  const int vr = nsh::tx_plan(t, arena_bytes, &plan);
+  if (vr != NS_OK) return vr;
+  const uint64_t n = plan.n;
+  const uint32_t mode = plan.mode;
+  static_assert(nsk::kTxIp == 1u && nsk::kTxTcpFull == 2u && nsk::kTxTcpPartial == 4u && nsk::kTxFieldsOnly == 8u,
+                "nsh::tx_plan's mode bits");
   if (n == 0) return NS_OK;
   if (!(mode & (nsk::kTxIp | nsk::kTxTcpFull | nsk::kTxTcpPartial))) {  // nothing to fill: the sums are 0
     if (d_out) {
@@ -1214,12 +1212,6 @@ int ns_csum_tcp_tx(ns_csum_ctx* ctx, uint8_t* d_arena, uint64_t arena_bytes, con
     }
     return NS_OK;
   }
-  const uint64_t hdr_bytes = n * t.slot;
-  if (t.hdr_off > arena_bytes || hdr_bytes > arena_bytes - t.hdr_off) return NS_ERANGE;
-  if (t.pay_off > arena_bytes || t.size > arena_bytes - t.pay_off) return NS_ERANGE;
-  // The payload is read while other waves write slots back: they must not meet.
-  if ((mode & nsk::kTxTcpFull) && t.pay_off < t.hdr_off + hdr_bytes && t.hdr_off < t.pay_off + t.size)
-    return NS_EINVAL;
   DeviceGuard g(ctx->device);
   nsk::TxGeo geo{};
   const uint64_t base = (uint64_t)(uintptr_t)d_arena;

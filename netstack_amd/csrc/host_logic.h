@@ -769,4 +769,33 @@ class FlatCombiner {
   bool combining_ = false;
 };
 
+// ns_csum_tcp_tx's geometry, validated (include/netstack_csum.h): the
+// segment count n = ceil(size / mss) (connect.go:675) and what the passes
+// compute (tcp_tx.hip kTx* bits: 1 IPv4, 2 full TCP, 4 pseudo-header only,
+// 8 field-only stores).  NS_OK with n = 0 or mode & 7 = 0: nothing to fill.
+struct TxPlan {
+  uint64_t n = 0;
+  uint32_t mode = 0;
+};
+inline int tx_plan(const ns_tcp_tx& t, uint64_t arena_bytes, TxPlan* out) {
+  if (t.mss == 0 || t.mss > 0xFFFFu || t.slot == 0 || t.slot > 4096) return NS_EINVAL;
+  const bool partial = (t.flags & NS_TX_TCP_PARTIAL) != 0, none = (t.flags & NS_TX_TCP_NONE) != 0;
+  if ((partial && none) || (t.flags & ~(NS_TX_TCP_PARTIAL | NS_TX_TCP_NONE | NS_TX_FIELDS_ONLY))) return NS_EINVAL;
+  if (t.ip_len && (t.ip_len < 12 || t.ip_len > 60 || (uint32_t)t.ip_at + t.ip_len > t.slot)) return NS_EINVAL;
+  if (!none && (t.tcp_len < 18 || t.tcp_len > 60 || (uint32_t)t.tcp_at + t.tcp_len > t.slot)) return NS_EINVAL;
+  const uint64_t n = t.size / t.mss + (t.size % t.mss != 0);
+  if (n >= (1ull << 32)) return NS_EINVAL;
+  const uint32_t mode = (t.ip_len ? 1u : 0u) | (none ? 0u : partial ? 4u : 2u) |
+                        ((t.flags & NS_TX_FIELDS_ONLY) ? 8u : 0u);
+  out->n = n;
+  out->mode = mode;
+  if (n == 0 || !(mode & 7u)) return NS_OK;
+  const uint64_t hdr_bytes = n * t.slot;
+  if (t.hdr_off > arena_bytes || hdr_bytes > arena_bytes - t.hdr_off) return NS_ERANGE;
+  if (t.pay_off > arena_bytes || t.size > arena_bytes - t.pay_off) return NS_ERANGE;
+  // The payload is read while other waves write slots back: they must not meet.
+  if ((mode & 2u) && t.pay_off < t.hdr_off + hdr_bytes && t.hdr_off < t.pay_off + t.size) return NS_EINVAL;
+  return NS_OK;
+}
+
 }  // namespace nsh

@@ -512,6 +512,56 @@ static void TestScratchRegistry(int threads, int streams, int per_thread) {
               threads, streams, (unsigned long long)made.load(), (unsigned long long)busy_release.load());
 }
 
+// nsh::tx_plan (ns_csum_tcp_tx's geometry check): random geometries, fuzzed
+// near every bound.  Whatever it accepts with work to do, every slot, header,
+// field and payload byte the kernels touch lies in the arena, the fields in
+// their headers, and the payload (when read) apart from the slots; the
+// segment count is connect.go:675's.
+static void TestTxPlan(Rng& rng, int rounds) {
+  auto pick = [&](uint64_t lo, uint64_t hi) { return lo + rng() % (hi - lo + 1); };
+  int accepted = 0;
+  for (int round = 0; round < rounds * 50; ++round) {
+    ns_tcp_tx t{};
+    const uint64_t arena = pick(0, 1u << 22);
+    t.mss = (uint32_t)(rng() % 8 == 0 ? pick(0, 70000) : pick(1, 3000));
+    t.slot = (uint32_t)(rng() % 8 == 0 ? pick(0, 5000) : pick(40, 120));
+    t.ip_at = (uint16_t)pick(0, 70);
+    t.ip_len = (uint16_t)(rng() % 4 == 0 ? 0 : pick(8, 64));
+    t.tcp_at = (uint16_t)pick(0, 90);
+    t.tcp_len = (uint16_t)pick(14, 64);
+    t.size = rng() % 16 == 0 ? 0 : pick(1, 1u << 20);
+    t.hdr_off = pick(0, arena + 100);
+    t.pay_off = pick(0, arena + 100);
+    t.flags = (uint32_t)(rng() % 16 == 0 ? rng() : rng() % 8);
+    nsh::TxPlan p;
+    const int rc = nsh::tx_plan(t, arena, &p);
+    CHECK(rc == NS_OK || rc == NS_EINVAL || rc == NS_ERANGE, "rc %d", rc);
+    if (rc != NS_OK) continue;
+    CHECK(t.mss >= 1 && t.mss <= 65535 && t.slot >= 1 && t.slot <= 4096, "accepted mss %u slot %u", t.mss, t.slot);
+    CHECK(p.n == (t.size + t.mss - 1) / t.mss, "segment count");
+    if (p.n == 0 || !(p.mode & 7u)) continue;
+    ++accepted;
+    CHECK(t.hdr_off + p.n * t.slot <= arena, "slots inside the arena");
+    CHECK(t.pay_off + t.size <= arena, "payload inside the arena");
+    if (p.mode & 1u) CHECK(t.ip_len >= 12 && (uint32_t)t.ip_at + t.ip_len <= t.slot, "IPv4 header and field in a slot");
+    if (p.mode & 6u) CHECK(t.tcp_len >= 18 && (uint32_t)t.tcp_at + t.tcp_len <= t.slot, "TCP header and field in a slot");
+    if (p.mode & 2u)
+      CHECK(t.pay_off >= t.hdr_off + p.n * t.slot || t.hdr_off >= t.pay_off + t.size, "payload apart from the slots");
+  }
+  CHECK(accepted > 0, "no geometry accepted");
+  // the reference's own shape: 45 segments of a 64 KiB GSO write
+  ns_tcp_tx t{};
+  t.size = 65536, t.mss = 1460, t.slot = 54, t.ip_at = 14, t.ip_len = 20, t.tcp_at = 34, t.tcp_len = 20;
+  t.hdr_off = 0, t.pay_off = 45 * 54;
+  nsh::TxPlan p;
+  CHECK(nsh::tx_plan(t, t.pay_off + t.size, &p) == NS_OK && p.n == 45 && p.mode == 3u, "sendTCPBatch 64 KiB");
+  CHECK(nsh::tx_plan(t, t.pay_off + t.size - 1, &p) == NS_ERANGE, "payload one byte past the arena");
+  t.pay_off = 100;
+  CHECK(nsh::tx_plan(t, 1 << 20, &p) == NS_EINVAL, "payload over the slots");
+  t.flags = NS_TX_TCP_PARTIAL;
+  CHECK(nsh::tx_plan(t, 1 << 20, &p) == NS_OK && p.mode == 5u, "CHECKSUM_PARTIAL reads no payload");
+}
+
 int main(int argc, char** argv) {
   const bool quick = argc > 1 && std::strcmp(argv[1], "--quick") == 0;
   Rng rng(20261016);
@@ -521,6 +571,7 @@ int main(int argc, char** argv) {
   TestPackets(rng, 10 * r);
   TestCutChunk(rng, r);
   TestShardPlan(rng, r);
+  TestTxPlan(rng, r);
   TestCombiner(16, quick ? 200 : 2000);
   TestScratchRegistry(8, 1000, quick ? 2000 : 20000);
   std::printf("%d checks, %d failed\n", g_run.load(), g_fail.load());
