@@ -199,3 +199,29 @@ def test_per_rank_device_footprint(world):
     for s in shards:
         assert abs(s.arena_bytes - whole.arena_bytes / world) < 64
         assert s.arena_bytes + 18 * s.n < 13e9 / world
+
+
+def test_cfg8_defaults_to_the_structured_tx_fill():
+    """bench.py --config 8 measures ns_csum_tcp_tx over sendTCPBatch's layout
+    by default; the paired table and the wire layout stay
+    selectable, and the PMC entry each line reads is its own."""
+    import sys
+
+    import bench
+    from netstack_amd import workloads as W
+
+    old = sys.argv
+    try:
+        sys.argv = ["bench.py", "--config", "8"]
+        assert bench.parse().tx_layout == "struct"
+        for lay in ("split", "wire"):
+            sys.argv = ["bench.py", "--config", "8", "--tx-layout", lay]
+            assert bench.parse().tx_layout == lay
+    finally:
+        sys.argv = old
+    src = open(bench.__file__).read()
+    assert 'pmc_traffic(args.pmc_json, "8struct") if struct' in src
+    g = W.tx_struct_geometry(1 << 20)
+    pay, total = W.tx_split_layout(1 << 20)
+    assert g["pay_off"] == pay and g["hdr_off"] + (1 << 20) * g["slot"] <= pay
+    assert g["pay_off"] + g["size"] == total and g["tcp_at"] + g["tcp_len"] == g["slot"]
