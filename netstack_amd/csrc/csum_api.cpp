@@ -1237,8 +1237,12 @@ int ns_csum_tcp_tx(ns_csum_ctx* ctx, uint8_t* d_arena, uint64_t arena_bytes, con
   const uint32_t variant = ev ? (uint32_t)std::atoi(ev) : 0u;
   if (const char* v = std::getenv("NS_CSUM_TX_TILE")) geo.tile = (uint32_t)std::atoi(v);
   if (const char* v = std::getenv("NS_CSUM_TX_HTILE")) geo.htile = (uint32_t)std::atoi(v);
+  // NS_CSUM_TX_PASSES=1|2 (diagnostics, per call): force the fused or the
+  // two-pass shape whatever the payload size.
+  const char* ep = std::getenv("NS_CSUM_TX_PASSES");
+  const bool two = ep ? std::atoi(ep) == 2 : t.size >= nsk::kTxTwoPassMinBytes;
   hipStream_t s = (hipStream_t)stream;
-  if (!(mode & nsk::kTxTcpFull)) {  // no payload to read: one header pass
+  if (!(mode & nsk::kTxTcpFull) || !two) {  // one pass (no scratch)
     HIP_TRY(nsk::launch_tcp_tx(geo, s, variant));
     return NS_OK;
   }

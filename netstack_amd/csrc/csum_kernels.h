@@ -107,6 +107,12 @@ struct TxGeo {
   uint32_t htile;        // the header pass's tile (0: the launcher's choice)
   uint32_t xstride;      // 1 (scratch) or 2 (parked in out[2i + 1])
 };
+// A batch whose payload needs reading takes two passes (a payload pass, then
+// a header pass: g.xs set) from this many payload bytes, one fused pass below
+// (g.xs = nullptr).  tools/tx_struct_probe.py, 1460-B segments, two passes
+// against one: 16 MB 15.5 vs 13.1 us, 191 MB 41.2 vs 42.5, 383 MB 72.2 vs
+// 76.6, 1.5 GB 246 vs 271 (profiles/r04/tx_struct/sizes/).
+constexpr uint64_t kTxTwoPassMinBytes = 64ull << 20;
 // variant (A/B diagnostics; 0 = production): 1 = one fused pass,
 // 2 = nontemporal write-back, 3 = segments reduced over the wave in the loop.
 hipError_t launch_tcp_tx(TxGeo g, hipStream_t stream, uint32_t variant = 0);

@@ -69,7 +69,7 @@ def _arena(total, geo, seed):
     return a
 
 
-def _run(engine, a, geo, mode="full", fields_only=False, tile=None, offset=0, htile=None):
+def _run(engine, a, geo, mode="full", fields_only=False, tile=None, offset=0, htile=None, passes=None):
     import torch
 
     buf = torch.empty(offset + a.size, dtype=torch.uint8, device="cuda")
@@ -77,7 +77,8 @@ def _run(engine, a, geo, mode="full", fields_only=False, tile=None, offset=0, ht
     arena = buf[offset:]
     n = -(-geo["size"] // geo["mss"])
     out = torch.full((2 * n,), -1, dtype=torch.int16, device="cuda")
-    knobs = {k: str(v) for k, v in (("NS_CSUM_TX_TILE", tile), ("NS_CSUM_TX_HTILE", htile)) if v is not None}
+    knobs = {k: str(v) for k, v in (("NS_CSUM_TX_TILE", tile), ("NS_CSUM_TX_HTILE", htile),
+                                    ("NS_CSUM_TX_PASSES", passes)) if v is not None}
     old = {k: os.environ.get(k) for k in knobs}
     os.environ.update(knobs)
     try:
@@ -108,12 +109,15 @@ def _check(got_arena, got_sums, want_arena, want_sums, what):
 
 @pytest.mark.parametrize("name", sorted(CASES))
 def test_geometry_bit_exact(engine, oracle_mod, name):
+    """Each geometry in both shapes: one fused pass (what batches below
+    kTxTwoPassMinBytes take) and the payload + header passes."""
     geo, total = CASES[name]
     a = _arena(total, geo, seed=len(name))
     wa, ws = _want(oracle_mod, a, geo)
-    for offset in (0, 5):
-        ga, gs = _run(engine, a, geo, offset=offset)
-        _check(ga, gs, wa, ws, f"{name} (arena at +{offset})")
+    for passes in (1, 2):
+        for offset in (0, 5):
+            ga, gs = _run(engine, a, geo, offset=offset, passes=passes)
+            _check(ga, gs, wa, ws, f"{name} ({passes} passes, arena at +{offset})")
 
 
 @pytest.mark.parametrize("tile", [1, 2, 7, 31, 32, 33, 64])
@@ -122,8 +126,9 @@ def test_forced_tiles(engine, oracle_mod, tile):
         geo, total = CASES[name]
         a = _arena(total, geo, seed=tile)
         wa, ws = _want(oracle_mod, a, geo)
-        ga, gs = _run(engine, a, geo, tile=tile)
-        _check(ga, gs, wa, ws, f"{name} tile {tile}")
+        for passes in (1, 2):
+            ga, gs = _run(engine, a, geo, tile=tile, passes=passes)
+            _check(ga, gs, wa, ws, f"{name} tile {tile}, {passes} passes")
 
 
 @pytest.mark.parametrize("htile", [1, 3, 64, 100, 129, 222])
@@ -137,7 +142,7 @@ def test_header_pass_tiles(engine, oracle_mod, htile):
             continue
         a = _arena(total, geo, seed=htile)
         wa, ws = _want(oracle_mod, a, geo)
-        ga, gs = _run(engine, a, geo, htile=htile)
+        ga, gs = _run(engine, a, geo, htile=htile, passes=2)
         _check(ga, gs, wa, ws, f"{name} header tile {htile}")
         for mode in ("partial",):
             wa2, ws2 = _want(oracle_mod, a, geo, mode)
@@ -146,15 +151,20 @@ def test_header_pass_tiles(engine, oracle_mod, htile):
 
 
 def test_without_out_uses_scratch(engine, oracle_mod):
-    """d_out = NULL: the payload values go through the stream's scratch."""
+    """d_out = NULL: two passes keep the payload values in the stream's
+    scratch (forced here, and by size in the large batch below)."""
     import torch
 
     geo, total = CASES["odd_slots_odd_mss"]
     a = _arena(total, geo, seed=21)
     wa, _ = _want(oracle_mod, a, geo)
     buf = torch.from_numpy(a).cuda()
-    engine.tcp_tx(buf, geo)
-    torch.cuda.synchronize()
+    os.environ["NS_CSUM_TX_PASSES"] = "2"
+    try:
+        engine.tcp_tx(buf, geo)
+        torch.cuda.synchronize()
+    finally:
+        del os.environ["NS_CSUM_TX_PASSES"]
     assert np.array_equal(buf.cpu().numpy(), wa)
 
 
@@ -172,21 +182,28 @@ def test_fields_only_stores(engine, oracle_mod):
     for name in ("netstack_default", "odd_slots_odd_mss", "mss_7", "ipv6_route"):
         geo, total = CASES[name]
         a = _arena(total, geo, seed=4)
-        for mode in ("full", "partial"):
+        for mode, passes in (("full", 1), ("full", 2), ("partial", None)):
             wa, ws = _want(oracle_mod, a, geo, mode)
-            ga, gs = _run(engine, a, geo, mode=mode, fields_only=True, tile=32)
-            _check(ga, gs, wa, ws, f"{name} {mode} fields only")
+            ga, gs = _run(engine, a, geo, mode=mode, fields_only=True, tile=32, passes=passes)
+            _check(ga, gs, wa, ws, f"{name} {mode} fields only, {passes} passes")
 
 
 def test_many_segments_full_tiles(engine, oracle_mod):
-    """Batches large enough for the launcher's own 32-segment tiles, MSS 1460
-    and MSS 16 (up to two segment ends per window per lane row)."""
+    """Batches large enough for the launcher's own tiles, MSS 1460 (102 MB:
+    two passes by size) and MSS 16 (one pass; up to two segment ends per
+    window per lane row), with and without d_out."""
+    import torch
+
     for size, mss in ((1460 * 70_000 - 3, 1460), (16 * 70_000 + 9, 16)):
         geo, total = _geo(size, mss, hdr_off=7)
         a = _arena(total, geo, seed=mss)
         wa, ws = _want(oracle_mod, a, geo)
         ga, gs = _run(engine, a, geo)
         _check(ga, gs, wa, ws, f"{size} B at MSS {mss}")
+        buf = torch.from_numpy(a).cuda()
+        engine.tcp_tx(buf, geo)  # no d_out: per-stream scratch above kTxTwoPassMinBytes
+        torch.cuda.synchronize()
+        assert np.array_equal(buf.cpu().numpy(), wa)
 
 
 def test_bench_layout_matches_table_path(engine):
