@@ -6,6 +6,7 @@ arithmetic happens in the gfx950 kernels; this module only marshals pointers.
 from __future__ import annotations
 
 import ctypes
+import functools
 import threading
 
 import numpy as np
@@ -129,13 +130,11 @@ class Engine:
 
         if not arena.is_cuda:
             raise ValueError("arena must be a device tensor")
-        t = _lib.NsTcpTx()
-        for k in ("hdr_off", "pay_off", "size", "mss", "slot", "ip_at", "ip_len", "tcp_at", "tcp_len"):
-            setattr(t, k, int(geo[k]))
-        t.protocol = int(geo.get("protocol", 6))
-        t.addr_sum = int(geo["addr_sum"]) if "addr_sum" in geo else addr_sum(geo["src"], geo["dst"])
-        t.flags = {"full": 0, "partial": _lib.NS_TX_TCP_PARTIAL, "none": _lib.NS_TX_TCP_NONE}[mode] | \
-            (_lib.NS_TX_FIELDS_ONLY if fields_only else 0)
+        t = _lib.NsTcpTx(geo["hdr_off"], geo["pay_off"], geo["size"], geo["mss"], geo["slot"], geo["ip_at"],
+                         geo["ip_len"], geo["tcp_at"], geo["tcp_len"],
+                         geo["addr_sum"] if "addr_sum" in geo else addr_sum(bytes(geo["src"]), bytes(geo["dst"])),
+                         geo.get("protocol", 6),
+                         _TX_MODES[mode] | (_lib.NS_TX_FIELDS_ONLY if fields_only else 0))
         if out is not None:
             n = -(-int(geo["size"]) // max(int(geo["mss"]), 1))
             if not out.is_cuda or out.numel() < 2 * n or out.element_size() != 2:
@@ -263,6 +262,10 @@ class Engine:
         return int(r.value)
 
 
+_TX_MODES = {"full": 0, "partial": _lib.NS_TX_TCP_PARTIAL, "none": _lib.NS_TX_TCP_NONE}
+
+
+@functools.lru_cache(maxsize=1024)
 def addr_sum(src: bytes, dst: bytes) -> int:
     """Checksum(dst, Checksum(src, 0)) (checksum.go:113-114): the address part
     of a route's pseudo-header sum, as ns_tcp_tx.addr_sum takes it."""
