@@ -23,15 +23,20 @@
 //      instruction), U windows in flight.  Each lane keeps the little-endian
 //      word sum W of its bytes (one v_sad_u16 per dword).  Segment ends are
 //      wave-uniform: a window holding one splits the straddling lane's chunk
-//      with scalar byte masks, reduces the finished segment over the wave and
-//      parks the total in lane j (segment j of the tile).
+//      with scalar byte masks, and each lane parks its partial in the
+//      finished segment's LDS row; lane j sums row j at the end.
 //   3. Lane j sums its slot's IPv4 and TCP headers from LDS (the fields read
 //      as zero), folds everything as the Go code does, and writes the two
 //      fields into the LDS copy.
 //   4. The wave writes its header region back whole (16-B stores of full
 //      chunks; byte stores where a chunk is shared with a neighbouring
-//      tile), while its lines are still in L2: whole-line writes instead of
-//      2M scattered 2-byte stores (tools/dense_store_probe.hip).
+//      tile): whole-line writes instead of 2M scattered 2-byte stores
+//      (tools/dense_store_probe.hip).
+// Batches of 64 MiB of payload or more split that into two kernels (PH): a
+// payload pass (step 2, each segment's payload value to g.xs) and a header
+// pass (steps 1, 3, 4), because the slot writes cost ~45 us per 1M segments
+// when they are interleaved with the payload stream and ~12 us on their own.
+// A header pass's lanes loop over up to 256 segments per wave.
 //
 // Arithmetic.  A segment holds at most 65,535 bytes, so no sum here wraps a
 // uint32 and each folded value depends on W only through W mod 65535 and
