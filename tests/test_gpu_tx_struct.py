@@ -262,3 +262,31 @@ def test_errors(engine):
     assert call(flags=_lib.NS_TX_TCP_NONE, ip_len=0, tcp_len=0) == _lib.NS_OK
     torch.cuda.synchronize()
     assert engine.sync() == 0
+
+
+def test_two_streams_keep_their_own_scratch(engine, oracle_mod):
+    """Two-pass calls without d_out on two streams at once: each stream's
+    payload values live in that stream's scratch, so interleaved calls never
+    see each other's (ns_csum_stream_release frees them afterwards)."""
+    import torch
+
+    geos = [CASES["odd_slots_odd_mss"], CASES["options_32b_tcp"]]
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    bufs, wants = [], []
+    for k, (geo, total) in enumerate(geos):
+        a = _arena(total, geo, seed=100 + k)
+        wants.append(_want(oracle_mod, a, geo)[0])
+        bufs.append(torch.from_numpy(a).cuda())
+    torch.cuda.synchronize()
+    os.environ["NS_CSUM_TX_PASSES"] = "2"
+    try:
+        for _ in range(3):  # refills of the same fields: idempotent
+            for k in range(2):
+                engine.tcp_tx(bufs[k], geos[k][0], stream=streams[k])
+        torch.cuda.synchronize()
+    finally:
+        del os.environ["NS_CSUM_TX_PASSES"]
+    for k in range(2):
+        assert np.array_equal(bufs[k].cpu().numpy(), wants[k]), k
+        engine.stream_release(streams[k])
+    assert engine.sync() == 0
