@@ -84,13 +84,15 @@ def main():
     TXV = ctypes.CDLL(os.path.join(ROOT, "netstack_amd", "lib", "libns_txv.so"))
     TXV.txv_launch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
 
+    xs = torch.empty(n, dtype=torch.int16, device=dev)
+
     def txv(k, tile=0):
         def f(r):
             a = batches[r]
             t = TxGeo(hdr=a.data_ptr() + geo["hdr_off"], pay=a.data_ptr() + geo["pay_off"], size=geo["size"], n=n,
                       mss=geo["mss"], slot=geo["slot"], tile=tile, ip_at=geo["ip_at"], ip_len=geo["ip_len"],
                       tcp_at=geo["tcp_at"], tcp_len=geo["tcp_len"], addr_sum=addr_sum(geo["src"], geo["dst"]),
-                      proto=6, mode=3)
+                      proto=6, mode=3, xs=xs.data_ptr() if k >= 8 else None, xstride=1)
             assert TXV.txv_launch(ctypes.byref(t), stream.cuda_stream, k) == 0
         return f
 
@@ -103,6 +105,14 @@ def main():
         "struct_fields": lambda r: eng.tcp_tx(batches[r], geo, stream=stream, fields_only=True),
         "struct_hdr_only": lambda r: eng.tcp_tx(batches[r], geo, stream=stream, mode="partial"),
         "txv_stream_t8": txv(5, 8),
+        "txv_u16": txv(0),
+        "txv_u8": txv(2),
+        "txv_u4": txv(3),
+        "txv_noreduce": txv(1),
+        "txv_stream": txv(5),
+        "txv_2p_u12": txv(8),
+        "txv_2p_u16": txv(9),
+        "txv_2p_u8": txv(10),
         "struct_out": lambda r: eng.tcp_tx(batches[r], geo, out=out2, stream=stream),
         "struct_norot": lambda r: eng.tcp_tx(batches[0], geo, stream=stream),
         "struct_out_norot": lambda r: eng.tcp_tx(batches[0], geo, out=out2, stream=stream),

@@ -4,7 +4,8 @@
 //   reductions (wrong sums), 2 = 8 windows in flight, 3 = 4 windows in
 //   flight, 4 = production without the header write-back (fields unwritten),
 //   5 = neither reductions nor write-back (the bare stream + header reads),
-//   6 = 12 windows in flight, 7 = 6 without the write-back.
+//   6 = 12 windows in flight, 7 = 6 without the write-back; 8 / 9 / 10 = the
+//   two-pass shape (g->xs set) with 12 / 16 / 8 windows in flight.
 // Not part of the product ABI.
 #include "../netstack_amd/csrc/tcp_tx.hip"
 
@@ -19,6 +20,9 @@ extern "C" int txv_launch(const nsk::TxGeo* g, void* stream, int k) {
     case 5: e = nsk::launch_tcp_tx_t<16, 2, 0, 2, 1>(*g, s); break;
     case 6: e = nsk::launch_tcp_tx_t<12, 2, 0, 1>(*g, s); break;
     case 7: e = nsk::launch_tcp_tx_t<12, 2, 0, 1, 1>(*g, s); break;
+    case 8: e = nsk::launch_passes<12, 2, 0, 1>(*g, s); break;
+    case 9: e = nsk::launch_passes<16, 2, 0, 1>(*g, s); break;
+    case 10: e = nsk::launch_passes<8, 2, 0, 1>(*g, s); break;
     default: e = nsk::launch_tcp_tx_t<16, 2, 0, 1>(*g, s); break;
   }
   return (int)e;
