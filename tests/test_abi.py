@@ -141,6 +141,23 @@ def test_product_kernels_never_spill_and_keep_occupancy():
     for k, v in kernels.items():  # the huge-descriptor kernel runs the same scan
         if "csum_split" in k:
             assert v["Occupancy"] >= 6, (k, v)
+    # the structured TX kernels (tcp_tx.hip): no scratch; the payload-reading
+    # passes keep 6 waves per SIMD, the header pass 8
+    tx = {}
+    cur = None
+    for line in open(os.path.join(ROOT, "netstack_amd", "lib", "tcp_tx.resources.txt")).read().splitlines():
+        m = re.search(r"Function Name: (\S+)", line)
+        if m:
+            cur = m.group(1)
+            tx[cur] = {}
+            continue
+        m = re.search(r"(ScratchSize \[bytes/lane\]|Occupancy \[waves/SIMD\]|VGPRs): (\d+)", line)
+        if m and cur:
+            tx[cur][m.group(1).split()[0]] = int(m.group(2))
+    assert len(tx) >= 5 and all("tcp_tx" in k for k in tx), sorted(tx)
+    for k, v in tx.items():
+        assert v["ScratchSize"] == 0, (k, v)
+        assert v["Occupancy"] >= (8 if k.endswith("Li2EEEvNS_5TxGeoE") else 6), (k, v)
 
 
 GO_SHIM = os.path.join(ROOT, "go", "header", "checksum_batch_hip.go")
