@@ -816,6 +816,26 @@ def packet_mode(args, dist, eng, dev, tx: bool):
             stored, _ = O.apply_stores(src, d[:k_cpu], want)
             ps["stores_bit_exact"] = bool(np.array_equal(arena[:span].cpu().numpy(), stored))
         result["parity_sample"] = ps
+        if struct:
+            # CPU leg: the same 65,536 segments through the oracle's C
+            # restatement of sendTCPBatch's checksum steps, one core, timed
+            # (bounded by --cpu-seconds); value in packet bytes per second
+            g = geo
+            work = np.ascontiguousarray(src).copy()
+            reps, t0 = 0, time.perf_counter()
+            while True:
+                O.c_send_tcp_batch(work, g["hdr_off"], g["pay_off"], 65536 * g["mss"], g["mss"], g["slot"],
+                                   g["ip_at"], g["ip_len"], g["tcp_at"], g["tcp_len"], g["src"], g["dst"],
+                                   copy=False)
+                reps += 1
+                el = time.perf_counter() - t0
+                if el >= args.cpu_seconds:
+                    break
+            result["cpu_baseline"] = {
+                "value": 65536 * W.RX_PKT * reps / el / GIB, "unit": "GiB/s", "cores": 1, "kind": "port",
+                "sample": f"65,536 segments ({65536 * W.RX_PKT} packet bytes) of the rank-0 batch x {reps} passes, "
+                          f"{el:.1f} s; oracle_send_tcp_batch (sendTCPBatch + buildTCPHdr + addIPHeader's checksum "
+                          f"steps over oracle/csum_oracle.c's scalar loop), single thread"}
     if dist.rank == 0:
         print(json.dumps(result), flush=True)
     eng.close()

@@ -283,14 +283,19 @@ def c_batch_paired(arena: np.ndarray, desc: np.ndarray) -> tuple[np.ndarray, int
 
 def c_send_tcp_batch(arena: np.ndarray, hdr_off: int, pay_off: int, size: int, mss: int, slot: int,
                      ip_at: int, ip_len: int, tcp_at: int, tcp_len: int, src: bytes, dst: bytes,
-                     protocol: int = 6, mode: str = "full") -> tuple[np.ndarray, np.ndarray]:
+                     protocol: int = 6, mode: str = "full", copy: bool = True) -> tuple[np.ndarray, np.ndarray]:
     """sendTCPBatch's checksum steps (transport/tcp/connect.go:668-702 with
     buildTCPHdr :634-666, then addIPHeader network/ipv4/ipv4.go:217-238 per
     segment) over its header slots and payload view in `arena`, restated in C
     (oracle_send_tcp_batch).  mode: "full", "partial" (CHECKSUM_PARTIAL) or
     "none" (TX checksum offload).  Returns (the arena with the fields
-    written, the 2n un-complemented sums [IPv4, TCP] per segment)."""
-    a = np.array(arena, dtype=np.uint8, copy=True)
+    written, the 2n un-complemented sums [IPv4, TCP] per segment).  copy=False
+    writes into `arena` itself (a contiguous uint8 array)."""
+    if copy:
+        a = np.array(arena, dtype=np.uint8, copy=True)
+    else:
+        assert arena.dtype == np.uint8 and arena.flags["C_CONTIGUOUS"]
+        a = arena
     n = (size + mss - 1) // mss
     out = np.zeros(2 * max(n, 1), dtype=np.uint16)
     s = np.frombuffer(bytes(src) or b"\0", dtype=np.uint8)
