@@ -58,11 +58,12 @@
 extern "C" {
 #endif
 
-#define NS_CSUM_ABI_VERSION 6  /* 2: ns_csum_batch_dev_store, NS_DESC_STORE*;
+#define NS_CSUM_ABI_VERSION 7  /* 2: ns_csum_batch_dev_store, NS_DESC_STORE*;
                                   3: ns_csum_stage_*, ns_csum_packet_buffers;
                                   4: ns_csum_stream_release, _scratch_count;
                                   5: ns_csum_get_stats;
-                                  6: ns_csum_tcp_tx */
+                                  6: ns_csum_tcp_tx;
+                                  7: ns_csum_tcp_tx_multi */
 
 /* ---- status codes ------------------------------------------------------- */
 #define NS_OK 0
@@ -241,6 +242,16 @@ typedef struct ns_tcp_tx {
 #define NS_TX_FIELDS_ONLY 0x4u
 int ns_csum_tcp_tx(ns_csum_ctx* ctx, uint8_t* d_arena, uint64_t arena_bytes,
                    const ns_tcp_tx* tx, uint16_t* d_out, void* stream);
+/* Many sendTCPBatch calls (one per connection, say) over one arena in one
+ * launch: txs[0..count) (host memory) as for ns_csum_tcp_tx, each checked
+ * the same way; d_out (or NULL) holds call k's 2 n_k sums from
+ * 2 * (n_0 + ... + n_{k-1}).  One fused pass for all of them.  NS_EINVAL
+ * also when one call's slots overlap another's slots or a payload a
+ * full-mode call reads.  Asynchronous on `stream`; the geometry table is
+ * uploaded through the stream's scratch (released by ns_csum_stream_release).*/
+int ns_csum_tcp_tx_multi(ns_csum_ctx* ctx, uint8_t* d_arena, uint64_t arena_bytes,
+                         const ns_tcp_tx* txs, uint32_t count, uint16_t* d_out,
+                         void* stream);
 
 /* Frees the scratch the context keeps for `stream` (see ns_csum_batch_dev),
  * after the stream's last launch that used it; nothing waits.  Call it

@@ -17,7 +17,7 @@ CSRC = os.path.join(_HERE, "csrc")
 
 # The NS_CSUM_ABI_VERSION this binding is written against; lib() refuses a
 # library that reports another (a stale build).
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 NS_OK = 0
 NS_EINVAL = -1
@@ -43,6 +43,7 @@ EXPORTED = (
     "ns_csum_combine", "ns_csum_shard_plan", "ns_csum_batch_multi", "ns_csum_chains",
     "ns_csum_stage_acquire", "ns_csum_stage_release", "ns_csum_packet_buffers",
     "ns_csum_stream_release", "ns_csum_scratch_count", "ns_csum_get_stats", "ns_csum_tcp_tx",
+    "ns_csum_tcp_tx_multi",
 )
 NS_PIECE_RESTART = 0x1
 NS_PIECE_END = 0x2
@@ -165,6 +166,7 @@ def _declare(lib):
         "ns_csum_scratch_count": (c.c_int, [vp, c.POINTER(c.c_uint32)]),
         "ns_csum_get_stats": (c.c_int, [vp, c.POINTER(NsStats), c.c_int]),
         "ns_csum_tcp_tx": (c.c_int, [vp, u8p, c.c_uint64, c.POINTER(NsTcpTx), vp, vp]),
+        "ns_csum_tcp_tx_multi": (c.c_int, [vp, u8p, c.c_uint64, c.POINTER(NsTcpTx), c.c_uint32, vp, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

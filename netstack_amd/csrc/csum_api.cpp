@@ -229,6 +229,12 @@ struct StreamScratch : nsh::ScratchSlot {
   ChainBuf chain;
   DevBuf<uint32_t> split;  // csum_split accumulators (zero between launches)
   DevBuf<uint16_t> txpay;  // ns_csum_tcp_tx: per-segment payload values between its passes
+  // ns_csum_tcp_tx_multi: the calls' table on the device, its pinned host
+  // copy, and the event after which that copy may be rewritten
+  DevBuf<uint8_t> txtab;
+  uint8_t* htab = nullptr;
+  size_t htab_cap = 0;
+  hipEvent_t tab_ev = nullptr;
   hipEvent_t last = nullptr;
   std::mutex mu;  // held while growing it and launching with it
 };
@@ -351,13 +357,20 @@ void retire_scratch(ns_csum_ctx* ctx, StreamScratch* sc) {
     sc->chain.release_async(ctx->retire);
     sc->split.release_async(ctx->retire);
     sc->txpay.release_async(ctx->retire);
+    sc->txtab.release_async(ctx->retire);
   } else {  // no retire stream: free once its last launch is done
     (void)hipGetLastError();
     (void)hipEventSynchronize(sc->last);
     sc->chain.release();
     sc->split.release();
     sc->txpay.release();
+    sc->txtab.release();
   }
+  if (sc->htab) {  // host memory: free once its last copy has run
+    if (sc->tab_ev) (void)hipEventSynchronize(sc->tab_ev);
+    (void)hipHostFree(sc->htab);
+  }
+  if (sc->tab_ev) (void)hipEventDestroy(sc->tab_ev);
   (void)hipEventDestroy(sc->last);
   delete sc;
   ctx->st.retires.fetch_add(1, std::memory_order_relaxed);
@@ -1278,6 +1291,93 @@ int ns_csum_tcp_tx(ns_csum_ctx* ctx, uint8_t* d_arena, uint64_t arena_bytes, con
       hipError_t e = nsk::launch_tcp_tx(geo, s, variant);
       if (e == hipSuccess) e = hipEventRecord(sc->last, s);
       if (e != hipSuccess) rc = report_hip(e, "launch_tcp_tx", __FILE__, __LINE__);
+    }
+  }
+  ctx->scratch.unpin(sc);
+  return rc;
+}
+
+int ns_csum_tcp_tx_multi(ns_csum_ctx* ctx, uint8_t* d_arena, uint64_t arena_bytes, const ns_tcp_tx* txs,
+                         uint32_t count, uint16_t* d_out, void* stream) {
+  if (!ctx || (count && !txs) || (arena_bytes && !d_arena)) return NS_EINVAL;
+  std::vector<nsh::TxPlan> plans;
+  const int vr = nsh::tx_multi_plan(txs, count, arena_bytes, &plans);
+  if (vr != NS_OK) return vr;
+  DeviceGuard g(ctx->device);
+  hipStream_t s = (hipStream_t)stream;
+  const uint64_t base = (uint64_t)(uintptr_t)d_arena;
+  std::vector<nsk::TxGeo> calls;
+  calls.reserve(count);
+  uint64_t seg = 0;
+  for (uint32_t k = 0; k < count; ++k) {
+    const ns_tcp_tx& t = txs[k];
+    const nsh::TxPlan& p = plans[k];
+    if (p.n && !(p.mode & 7u) && d_out) HIP_TRY(hipMemsetAsync(d_out + 2 * seg, 0, 4 * p.n, s));  // nothing to fill
+    if (p.n && (p.mode & 7u)) {
+      nsk::TxGeo geo{};
+      geo.hdr = base + t.hdr_off;
+      geo.pay = base + t.pay_off;
+      geo.size = t.size;
+      geo.n = p.n;
+      geo.mss = t.mss;
+      geo.slot = t.slot;
+      geo.ip_at = t.ip_at;
+      geo.ip_len = t.ip_len;
+      geo.tcp_at = t.tcp_at;
+      geo.tcp_len = t.tcp_len;
+      geo.addr_sum = t.addr_sum;
+      geo.proto = t.protocol;
+      geo.mode = p.mode;
+      geo.out = d_out ? d_out + 2 * seg : nullptr;
+      calls.push_back(geo);
+    }
+    seg += p.n;
+  }
+  if (calls.empty()) return NS_OK;
+  const uint32_t nc = (uint32_t)calls.size();
+  std::vector<uint32_t> first(nc + 1);
+  nsk::TxGeo launch{};
+  const uint32_t grid = nsk::tx_multi_prepare(calls.data(), nc, &launch, first.data());
+  if (grid == 0) return NS_EINVAL;  // more than 2^31 tiles
+  const size_t tab = ((size_t)nc * sizeof(nsk::TxGeo) + 15) & ~(size_t)15;
+  const size_t bytes = tab + first.size() * sizeof(uint32_t);
+  StreamScratch* sc = ctx->scratch.pin(scratch_key(s), make_scratch,
+                                       [&](StreamScratch* old) { retire_scratch(ctx, old); });
+  if (!sc) return NS_ENOMEM;
+  int rc = NS_OK;
+  {
+    std::lock_guard<std::mutex> lk(sc->mu);
+    rc = sc->txtab.ensure_async(bytes, false, s);
+    if (rc == NS_OK && !sc->tab_ev && hipEventCreateWithFlags(&sc->tab_ev, hipEventDisableTiming) != hipSuccess) {
+      sc->tab_ev = nullptr;
+      rc = NS_EHIP;
+    }
+    if (rc == NS_OK) {
+      // the pinned copy may still be read by this stream's previous upload
+      (void)hipEventSynchronize(sc->tab_ev);
+      if (sc->htab_cap < bytes) {
+        if (sc->htab) (void)hipHostFree(sc->htab);
+        sc->htab = nullptr;
+        sc->htab_cap = 0;
+        const size_t cap = std::max<size_t>(bytes, 64u << 10);
+        if (hipHostMalloc(reinterpret_cast<void**>(&sc->htab), cap, hipHostMallocDefault) != hipSuccess) {
+          sc->htab = nullptr;
+          rc = NS_ENOMEM;
+        } else {
+          sc->htab_cap = cap;
+        }
+      }
+    }
+    if (rc == NS_OK) {
+      std::memcpy(sc->htab, calls.data(), (size_t)nc * sizeof(nsk::TxGeo));
+      std::memcpy(sc->htab + tab, first.data(), first.size() * sizeof(uint32_t));
+      hipError_t e = hipMemcpyAsync(sc->txtab.p, sc->htab, bytes, hipMemcpyHostToDevice, s);
+      if (e == hipSuccess) e = hipEventRecord(sc->tab_ev, s);
+      if (e == hipSuccess)
+        e = nsk::launch_tcp_tx_multi(launch, grid, reinterpret_cast<const nsk::TxGeo*>(sc->txtab.p),
+                                     reinterpret_cast<const uint32_t*>(sc->txtab.p + tab), nc, s);
+      if (e == hipSuccess) e = hipEventRecord(sc->last, s);
+      if (e != hipSuccess) rc = report_hip(e, "launch_tcp_tx_multi", __FILE__, __LINE__);
     }
   }
   ctx->scratch.unpin(sc);

@@ -116,5 +116,13 @@ constexpr uint64_t kTxTwoPassMinBytes = 64ull << 20;
 // variant (A/B diagnostics; 0 = production): 1 = one fused pass,
 // 2 = nontemporal write-back, 3 = segments reduced over the wave in the loop.
 hipError_t launch_tcp_tx(TxGeo g, hipStream_t stream, uint32_t variant = 0);
+// Many batches in one fused launch (ns_csum_tcp_tx_multi).  calls[] (host)
+// hold each batch's geometry with n, mode and out set; tx_multi_prepare sets
+// their tiles, fills first[ncalls + 1] and the launch-wide shape, and returns
+// the grid (0: more than 2^31 tiles).  The launch reads calls[] and first[]
+// from device memory (d_calls, d_first: copies of them).
+uint32_t tx_multi_prepare(TxGeo* calls, uint32_t ncalls, TxGeo* launch, uint32_t* first);
+hipError_t launch_tcp_tx_multi(const TxGeo& launch, uint32_t grid, const TxGeo* d_calls, const uint32_t* d_first,
+                               uint32_t ncalls, hipStream_t stream);
 
 }  // namespace nsk

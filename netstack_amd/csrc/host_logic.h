@@ -798,4 +798,37 @@ inline int tx_plan(const ns_tcp_tx& t, uint64_t arena_bytes, TxPlan* out) {
   return NS_OK;
 }
 
+// ns_csum_tcp_tx_multi: every call checked as above, then the ranges the
+// one launch touches: no call's slots may overlap another's slots, nor any
+// payload a full-mode call reads (waves of other calls write slots back while
+// it streams).  Payloads may overlap each other (they are only read).
+inline int tx_multi_plan(const ns_tcp_tx* t, uint32_t count, uint64_t arena_bytes, std::vector<TxPlan>* plans) {
+  plans->assign(count, TxPlan{});
+  struct Iv {
+    uint64_t lo, hi;
+    bool slots;
+  };
+  std::vector<Iv> iv;
+  for (uint32_t k = 0; k < count; ++k) {
+    const int rc = tx_plan(t[k], arena_bytes, &(*plans)[k]);
+    if (rc != NS_OK) return rc;
+    const TxPlan& p = (*plans)[k];
+    if (p.n == 0 || !(p.mode & 7u)) continue;
+    iv.push_back({t[k].hdr_off, t[k].hdr_off + p.n * t[k].slot, true});
+    if ((p.mode & 2u) && t[k].size) iv.push_back({t[k].pay_off, t[k].pay_off + t[k].size, false});
+  }
+  std::sort(iv.begin(), iv.end(), [](const Iv& a, const Iv& b) { return a.lo < b.lo; });
+  uint64_t slot_end = 0, pay_end = 0;
+  for (const Iv& v : iv) {
+    if (v.slots) {
+      if (v.lo < slot_end || v.lo < pay_end) return NS_EINVAL;
+      slot_end = std::max(slot_end, v.hi);
+    } else {
+      if (v.lo < slot_end) return NS_EINVAL;
+      pay_end = std::max(pay_end, v.hi);
+    }
+  }
+  return NS_OK;
+}
+
 }  // namespace nsh

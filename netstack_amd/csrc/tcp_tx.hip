@@ -149,16 +149,12 @@ __device__ __forceinline__ void tx_store_be16(uint64_t addr, uint32_t v) {
 // PH = the pass: 0 = everything in one kernel; 1 = the payload pass (each
 // segment's payload value to g.xs, no headers); 2 = the header pass (the
 // payload values from g.xs, no payload read).
-template <int U, int AUX, int SP, int RED, int XF = 0, int PH = 0>
-__global__ __launch_bounds__(256) void tcp_tx(TxGeo g) {
-  extern __shared__ uint4 tx_lds[];
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint64_t s0 = ((uint64_t)blockIdx.x * g.wpg + wv) * g.tile;
+// One wave's tile: segments [s0, s0 + tile) of batch g, its LDS share L
+// (header region, then `rows`).
+template <int U, int AUX, int SP, int RED, int XF, int PH>
+__device__ __forceinline__ void tx_tile(const TxGeo& g, uint64_t s0, uint8_t* L, uint32_t* rows, uint32_t lane) {
   if (s0 >= g.n) return;  // a whole wave leaves together
   const uint32_t nseg = g.n - s0 < g.tile ? (uint32_t)(g.n - s0) : g.tile;
-  uint8_t* L = reinterpret_cast<uint8_t*>(tx_lds) + (size_t)wv * g.lds_wave;
-  uint32_t* rows = reinterpret_cast<uint32_t*>(L + g.lds_rows);  // RED 1: [tile][64] partials
 
   // 1. the header region, into LDS by DMA
   const uint64_t h_lo = g.hdr + s0 * g.slot, h_hi = h_lo + (uint64_t)nseg * g.slot;
@@ -323,6 +319,40 @@ __global__ __launch_bounds__(256) void tcp_tx(TxGeo g) {
   }
 }
 
+template <int U, int AUX, int SP, int RED, int XF = 0, int PH = 0>
+__global__ __launch_bounds__(256) void tcp_tx(TxGeo g) {
+  extern __shared__ uint4 tx_lds[];
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  uint8_t* L = reinterpret_cast<uint8_t*>(tx_lds) + (size_t)wv * g.lds_wave;
+  uint32_t* rows = reinterpret_cast<uint32_t*>(L + g.lds_rows);  // RED 1: [tile][64] partials
+  tx_tile<U, AUX, SP, RED, XF, PH>(g, ((uint64_t)blockIdx.x * g.wpg + wv) * g.tile, L, rows, lane);
+}
+
+// Many batches (sendTCPBatch calls) in one launch, one fused pass each:
+// wave T takes tile T of the concatenation; first[c] is call c's first tile
+// (first[ncalls] the total), calls[c] its geometry.  g holds the launch-wide
+// LDS shape (the largest call's) and waves per workgroup.
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void tcp_tx_multi(TxGeo g, const TxGeo* __restrict__ calls,
+                                                    const uint32_t* __restrict__ first, uint32_t ncalls) {
+  extern __shared__ uint4 tx_lds[];
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  uint8_t* L = reinterpret_cast<uint8_t*>(tx_lds) + (size_t)wv * g.lds_wave;
+  uint32_t* rows = reinterpret_cast<uint32_t*>(L + g.lds_rows);
+  const uint32_t T = blockIdx.x * g.wpg + wv;
+  if (T >= first[ncalls]) return;
+  uint32_t lo = 0, hi = ncalls;  // first[lo] <= T < first[hi]
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (first[mid] <= T) lo = mid;
+    else hi = mid;
+  }
+  lo = (uint32_t)__builtin_amdgcn_readfirstlane(lo);
+  const TxGeo c = calls[lo];
+  tx_tile<16, 2, 0, 1, 0, 0>(c, (uint64_t)(T - first[lo]) * c.tile, L, rows, lane);
+}
+
 // Segments per wave for a pass.  A pass that reads payload: about 12 KiB of
 // it per wave, at most 32 segments (1M x 1460 B, payload pass: 218 us at 8
 // segments, 222-228 at 4 / 16 / 32; tools/tx_struct_probe.py).  A header
@@ -379,6 +409,41 @@ static hipError_t launch_passes(TxGeo g, hipStream_t stream) {
   hipError_t e = launch_tcp_tx_t<U, AUX, SP, RED, 0, 1>(g, stream);
   if (e == hipSuccess) e = launch_tcp_tx_t<U, AUX, SP, RED, 0, 2>(h, stream);
   return e;
+}
+
+// ns_csum_tcp_tx_multi's plan: each call's tile (tx_tile's rule without the
+// per-call wave floor: the launch has every call's waves), first[c] = call
+// c's first tile, first[ncalls] the total; the launch-wide LDS shape and
+// waves per workgroup in *launch.  Returns the grid (0: too many tiles).
+uint32_t tx_multi_prepare(TxGeo* calls, uint32_t ncalls, TxGeo* launch, uint32_t* first) {
+  uint64_t tiles = 0, max_hdr = 0;
+  uint32_t max_tile = 1;
+  for (uint32_t c = 0; c < ncalls; ++c) {
+    TxGeo& g = calls[c];
+    uint32_t t = (uint32_t)std::min<uint64_t>(32, std::max<uint64_t>(1, (12u << 10) / std::max<uint32_t>(g.mss, 1)));
+    while (t > 1 && (uint64_t)t * g.slot > (8u << 10)) t /= 2;
+    g.tile = t;
+    g.xs = nullptr;
+    first[c] = (uint32_t)tiles;
+    tiles += (g.n + t - 1) / t;
+    if (tiles >= (1ull << 31)) return 0;
+    max_tile = std::max(max_tile, t);
+    max_hdr = std::max<uint64_t>(max_hdr, (uint64_t)t * g.slot);
+  }
+  first[ncalls] = (uint32_t)tiles;
+  *launch = TxGeo{};
+  launch->lds_rows = (uint32_t)((max_hdr + 30) / 16 + 63) / 64 * 1024;
+  launch->lds_wave = launch->lds_rows + max_tile * 256u;
+  launch->wpg = launch->lds_wave <= (16u << 10) ? 4u : launch->lds_wave <= (32u << 10) ? 2u : 1u;
+  return (uint32_t)((tiles + launch->wpg - 1) / launch->wpg);
+}
+
+hipError_t launch_tcp_tx_multi(const TxGeo& launch, uint32_t grid, const TxGeo* d_calls, const uint32_t* d_first,
+                               uint32_t ncalls, hipStream_t stream) {
+  if (grid == 0) return hipSuccess;
+  hipLaunchKernelGGL(tcp_tx_multi, dim3(grid), dim3(64 * launch.wpg), (size_t)launch.lds_wave * launch.wpg, stream,
+                     launch, d_calls, d_first, ncalls);
+  return hipGetLastError();
 }
 
 hipError_t launch_tcp_tx(TxGeo g, hipStream_t stream, uint32_t variant) {

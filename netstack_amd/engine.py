@@ -146,6 +146,22 @@ class Engine:
                                    getattr(stream, "cuda_stream", stream)), "ns_csum_tcp_tx")
         return out
 
+    def tcp_tx_multi(self, arena, geos, out=None, stream=None, mode: str = "full"):
+        """Many sendTCPBatch calls over one arena in one launch
+        (ns_csum_tcp_tx_multi): `geos` a list of tcp_tx geometries; `out`
+        (optional) receives call k's 2n_k sums after those of calls < k."""
+        import torch
+
+        if not arena.is_cuda:
+            raise ValueError("arena must be a device tensor")
+        arr = geos if isinstance(geos, ctypes.Array) else tx_table(geos, mode)
+        if stream is None:
+            stream = torch.cuda.current_stream(arena.device)
+        check(lib().ns_csum_tcp_tx_multi(self._h, arena.data_ptr(), arena.numel() * arena.element_size(), arr,
+                                         len(arr) if len(geos) else 0, out.data_ptr() if out is not None else None,
+                                         getattr(stream, "cuda_stream", stream)), "ns_csum_tcp_tx_multi")
+        return out
+
     def stream_release(self, stream) -> None:
         """Free the scratch this context keeps for `stream` (a torch.cuda.Stream
         or a raw hipStream_t) after its last launch (ns_csum_stream_release);
@@ -263,6 +279,18 @@ class Engine:
 
 
 _TX_MODES = {"full": 0, "partial": _lib.NS_TX_TCP_PARTIAL, "none": _lib.NS_TX_TCP_NONE}
+
+
+def tx_table(geos, mode: str = "full"):
+    """The ns_tcp_tx array of a list of tcp_tx geometries (each may carry its
+    own "mode"), built once and reusable across Engine.tcp_tx_multi calls."""
+    arr = (_lib.NsTcpTx * max(len(geos), 1))()
+    for k, geo in enumerate(geos):
+        arr[k] = _lib.NsTcpTx(geo["hdr_off"], geo["pay_off"], geo["size"], geo["mss"], geo["slot"],
+                              geo["ip_at"], geo["ip_len"], geo["tcp_at"], geo["tcp_len"],
+                              geo["addr_sum"] if "addr_sum" in geo else addr_sum(bytes(geo["src"]), bytes(geo["dst"])),
+                              geo.get("protocol", 6), _TX_MODES[geo.get("mode", mode)])
+    return arr
 
 
 @functools.lru_cache(maxsize=1024)

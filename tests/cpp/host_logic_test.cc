@@ -562,6 +562,59 @@ static void TestTxPlan(Rng& rng, int rounds) {
   CHECK(nsh::tx_plan(t, 1 << 20, &p) == NS_OK && p.mode == 5u, "CHECKSUM_PARTIAL reads no payload");
 }
 
+// nsh::tx_multi_plan: random sets of calls; whatever it accepts, no call's
+// slots overlap another call's slots or a payload a full-mode call reads.
+static void TestTxMultiPlan(Rng& rng, int rounds) {
+  int accepted = 0;
+  for (int round = 0; round < rounds * 20; ++round) {
+    const uint32_t count = (uint32_t)(rng() % 6);
+    std::vector<ns_tcp_tx> t(count);
+    const uint64_t arena = 1u << 20;
+    for (auto& x : t) {
+      x = ns_tcp_tx{};
+      x.mss = 100 + (uint32_t)(rng() % 1400);
+      x.slot = 54;
+      x.ip_at = 14, x.ip_len = 20, x.tcp_at = 34, x.tcp_len = 20;
+      x.size = rng() % 20000;
+      x.hdr_off = rng() % (arena - 20000);
+      x.pay_off = rng() % (arena - 20000);
+      x.flags = (uint32_t)(rng() % 3);
+    }
+    std::vector<nsh::TxPlan> p;
+    const int rc = nsh::tx_multi_plan(t.data(), count, arena, &p);
+    if (rc != NS_OK) continue;
+    ++accepted;
+    for (uint32_t a = 0; a < count; ++a) {
+      if (!p[a].n || !(p[a].mode & 7u)) continue;
+      const uint64_t alo = t[a].hdr_off, ahi = alo + p[a].n * t[a].slot;
+      for (uint32_t b = 0; b < count; ++b) {
+        if (!p[b].n || !(p[b].mode & 7u)) continue;
+        if (b != a) {
+          const uint64_t blo = t[b].hdr_off, bhi = blo + p[b].n * t[b].slot;
+          CHECK(ahi <= blo || bhi <= alo, "slots of calls %u and %u overlap", a, b);
+        }
+        if ((p[b].mode & 2u) && t[b].size)
+          CHECK(ahi <= t[b].pay_off || t[b].pay_off + t[b].size <= alo, "slots of %u over payload of %u", a, b);
+      }
+    }
+  }
+  CHECK(accepted > 0, "no call set accepted");
+  ns_tcp_tx two[2]{};
+  for (auto& x : two) x.mss = 1460, x.slot = 54, x.ip_at = 14, x.ip_len = 20, x.tcp_at = 34, x.tcp_len = 20;
+  two[0].size = two[1].size = 14600;  // 10 segments each
+  two[0].hdr_off = 0, two[0].pay_off = 4096, two[1].hdr_off = 540, two[1].pay_off = 20000;
+  std::vector<nsh::TxPlan> p;
+  CHECK(nsh::tx_multi_plan(two, 2, 1 << 20, &p) == NS_OK, "adjacent slot regions");
+  two[1].hdr_off = 539;
+  CHECK(nsh::tx_multi_plan(two, 2, 1 << 20, &p) == NS_EINVAL, "slot regions overlap by one byte");
+  two[1].hdr_off = 4096 + 14599;
+  CHECK(nsh::tx_multi_plan(two, 2, 1 << 20, &p) == NS_EINVAL, "slots over another call's payload");
+  two[1].flags = NS_TX_TCP_NONE;  // that call's payload is not read; call 0's still is
+  CHECK(nsh::tx_multi_plan(two, 2, 1 << 20, &p) == NS_EINVAL, "slots over a read payload");
+  two[0].flags = NS_TX_TCP_PARTIAL;  // now no payload is read
+  CHECK(nsh::tx_multi_plan(two, 2, 1 << 20, &p) == NS_OK, "no payload read");
+}
+
 int main(int argc, char** argv) {
   const bool quick = argc > 1 && std::strcmp(argv[1], "--quick") == 0;
   Rng rng(20261016);
@@ -572,6 +625,7 @@ int main(int argc, char** argv) {
   TestCutChunk(rng, r);
   TestShardPlan(rng, r);
   TestTxPlan(rng, r);
+  TestTxMultiPlan(rng, r);
   TestCombiner(16, quick ? 200 : 2000);
   TestScratchRegistry(8, 1000, quick ? 2000 : 20000);
   std::printf("%d checks, %d failed\n", g_run.load(), g_fail.load());

@@ -290,3 +290,61 @@ def test_two_streams_keep_their_own_scratch(engine, oracle_mod):
         assert np.array_equal(bufs[k].cpu().numpy(), wants[k]), k
         engine.stream_release(streams[k])
     assert engine.sync() == 0
+
+
+def test_many_calls_in_one_launch(engine, oracle_mod):
+    """ns_csum_tcp_tx_multi: calls of different geometries (slot sizes, MSS,
+    IPv6, options, partial / offload modes, empty) laid out side by side in
+    one arena, in one launch; each call's fill and sums equal the oracle's
+    for that call alone, and every other byte is unchanged."""
+    import torch
+
+    rng = np.random.default_rng(77)
+    specs = [("netstack_default", "full"), ("odd_slots_odd_mss", "full"), ("ipv6_route", "full"),
+             ("options_32b_tcp", "partial"), ("mss_7", "full"), ("size_below_mss", "none"),
+             ("ip_header_with_options", "full"), ("last_is_one_byte", "full")]
+    geos, pos, parts = [], 3, []
+    for name, mode in specs * 3:
+        geo, total = CASES[name]
+        g = dict(geo)
+        g["hdr_off"] += pos
+        g["pay_off"] += pos
+        g["mode"] = mode
+        geos.append(g)
+        parts.append((pos, total, mode))
+        pos += total + int(rng.integers(0, 40))
+    geos.append(dict(CASES["netstack_default"][0], size=0, hdr_off=0, pay_off=0))  # no segments
+    a = rng.integers(0, 256, pos + 64, dtype=np.uint8)
+    want = a.copy()
+    sums = []
+    for g, (p, total, mode) in zip(geos, parts):
+        n = -(-g["size"] // g["mss"])
+        if g["ip_len"]:
+            for i in range(n):
+                at = g["hdr_off"] + i * g["slot"] + g["ip_at"]
+                a[at + 12:at + 16] = np.frombuffer(g["src"], np.uint8)
+                a[at + 16:at + 20] = np.frombuffer(g["dst"], np.uint8)
+    want = a.copy()
+    for g, (p, total, mode) in zip(geos, parts):
+        wa, ws = oracle_mod.c_send_tcp_batch(want, g["hdr_off"], g["pay_off"], g["size"], g["mss"], g["slot"],
+                                             g["ip_at"], g["ip_len"], g["tcp_at"], g["tcp_len"], g["src"], g["dst"],
+                                             g["protocol"], mode, copy=False)
+        sums.append(ws)
+    ntot = sum(len(x) // 2 for x in sums)
+    buf = torch.from_numpy(a).cuda()
+    out = torch.full((2 * ntot,), -1, dtype=torch.int16, device="cuda")
+    engine.tcp_tx_multi(buf, geos, out=out)
+    torch.cuda.synchronize()
+    got = buf.cpu().numpy()
+    bad = np.flatnonzero(got != want)
+    assert bad.size == 0, f"{bad.size} bytes differ, first at {bad[:8]}"
+    assert np.array_equal(out.cpu().numpy().view(np.uint16), np.concatenate(sums))
+    # again without d_out, and an overlap is refused
+    buf2 = torch.from_numpy(a).cuda()
+    engine.tcp_tx_multi(buf2, geos)
+    torch.cuda.synchronize()
+    assert np.array_equal(buf2.cpu().numpy(), want)
+    clash = [geos[0], dict(geos[1], hdr_off=geos[0]["hdr_off"] + 10)]
+    with pytest.raises(ValueError):  # NS_EINVAL
+        engine.tcp_tx_multi(buf2, clash)
+    assert engine.sync() == 0
