@@ -5,7 +5,8 @@
 //   flight, 4 = production without the header write-back (fields unwritten),
 //   5 = neither reductions nor write-back (the bare stream + header reads),
 //   6 = 12 windows in flight, 7 = 6 without the write-back; 8 / 9 / 10 = the
-//   two-pass shape (g->xs set) with 12 / 16 / 8 windows in flight.
+//   two-pass shape (g->xs set) with 12 / 16 / 8 windows in flight; 11 = the
+//   two passes with no header write-back (fields unwritten).
 // Not part of the product ABI.
 #include "../netstack_amd/csrc/tcp_tx.hip"
 
@@ -23,6 +24,13 @@ extern "C" int txv_launch(const nsk::TxGeo* g, void* stream, int k) {
     case 8: e = nsk::launch_passes<12, 2, 0, 1>(*g, s); break;
     case 9: e = nsk::launch_passes<16, 2, 0, 1>(*g, s); break;
     case 10: e = nsk::launch_passes<8, 2, 0, 1>(*g, s); break;
+    case 11: {  // the two passes, the header pass without its write-back (timing only)
+      nsk::TxGeo h = *g;
+      h.tile = g->htile;
+      e = nsk::launch_tcp_tx_t<16, 2, 0, 1, 0, 1>(*g, s);
+      if (e == hipSuccess) e = nsk::launch_tcp_tx_t<16, 2, 0, 1, 1, 2>(h, s);
+      break;
+    }
     default: e = nsk::launch_tcp_tx_t<16, 2, 0, 1>(*g, s); break;
   }
   return (int)e;
