@@ -34,6 +34,12 @@
  *   (udp/endpoint.go:808-815), the ICMP echo reply
  *   (network/ipv4/icmp.go:96-100), ICMPv6Checksum (icmpv6.go:202-221),
  *   addIPHeader (network/ipv4/ipv4.go:217-238)                  -> ns_csum_packet_buffers
+ *   the same receive checks for a recvmmsg ring resident in HBM, parsed on
+ *   the device: recvMMsgDispatcher.dispatch (link/fdbased/
+ *   packet_dispatchers.go:258-317), IPv4/IPv6 HandlePacket + IsValid
+ *   (network/ipv4/ipv4.go:341-394, header/ipv4.go:280-296; network/ipv6/
+ *   ipv6.go:168-188, header/ipv6.go:207-222), segment.parse
+ *   (tcp/segment.go:145-181), handleICMP                         -> ns_csum_rx_ring
  *
  * Semantics (bit-exact with checksum.go, including its un-folded uint32 wrap for
  * buffers > 128 KiB): every descriptor d is one calculateChecksum call over
@@ -58,12 +64,13 @@
 extern "C" {
 #endif
 
-#define NS_CSUM_ABI_VERSION 7  /* 2: ns_csum_batch_dev_store, NS_DESC_STORE*;
+#define NS_CSUM_ABI_VERSION 8  /* 2: ns_csum_batch_dev_store, NS_DESC_STORE*;
                                   3: ns_csum_stage_*, ns_csum_packet_buffers;
                                   4: ns_csum_stream_release, _scratch_count;
                                   5: ns_csum_get_stats;
                                   6: ns_csum_tcp_tx;
-                                  7: ns_csum_tcp_tx_multi */
+                                  7: ns_csum_tcp_tx_multi;
+                                  8: ns_csum_rx_ring, ns_csum_set_tx_tuning */
 
 /* ---- status codes ------------------------------------------------------- */
 #define NS_OK 0
@@ -381,6 +388,49 @@ typedef struct ns_pkt_buf {
 int ns_csum_packet_buffers(ns_csum_ctx* ctx, const ns_pkt_buf* pkts, uint32_t n,
                            uint32_t op, uint16_t* sums, uint8_t* verdict);
 
+/* ---- a receive ring in HBM, verified without host planning ---------------
+ * The receive mirror of ns_csum_tcp_tx: n slots of `stride` bytes from
+ * d_arena + ring_off, slot s holding one frame as recvmmsg wrote it (its
+ * length d_len[s], u32 device memory, counts from the slot's first byte).
+ * The kernel parses every frame itself and gives, per slot, exactly the
+ * verdict and sums ns_csum_packet_buffers(NS_PKB_VERIFY) gives for that
+ * packet delivered the way the link delivers it:
+ *   recvMMsgDispatcher.dispatch (link/fdbased/packet_dispatchers.go:258-317):
+ *     the frame is [frame_at, len) of the slot (frame_at: bytes before it,
+ *     e.g. a 10-B virtio-net header); a frame of no more than link_hdr bytes
+ *     is dropped (MALFORMED); link_hdr = 14 (Ethernet) picks IPv4/IPv6 by
+ *     EtherType (0x0800 / 0x86dd; any other: UNCHECKED, nothing the reference
+ *     checksums), link_hdr = 0 (TUN) by the version nibble (others dropped:
+ *     MALFORMED); Data = the frame less its link header, in views whose first
+ *     holds first_view - link_hdr bytes (BufConfig[0] = 128, :30; the later
+ *     views, all of even length, do not change any sum), first_view = 0: one
+ *     view;
+ *   then the rules of NS_PKB_VERIFY above (IsValid against the first view,
+ *   fragments UNCHECKED or MALFORMED, segment.parse, ICMPv4 echo, ICMPv6).
+ * d_verdict[s] (u8, or NULL) gets NS_PKB_*; d_sums (2n u16, or NULL) [2s] the
+ * IPv4 header sum, [2s+1] the transport sum, as ns_csum_packet_buffers.
+ * A slot whose length exceeds the stride is MALFORMED and counted
+ * (ns_csum_sync).  Asynchronous on `stream`; no scratch, no host work per
+ * packet.  Bytes read per slot: its frame (up to the IP packet's 65,575-B
+ * limit) and its length; written: 1 + 4.
+ * NS_EINVAL: d_arena + ring_off or stride not 16-B aligned, stride 0 or
+ * >= 2^24, frame_at + link_hdr odd or frame_at >= stride, link_hdr not 0 or 14,
+ * first_view neither 0 nor an even length with first_view - link_hdr >= 64,
+ * flags != 0, NULL d_len (n > 0), both outputs NULL.
+ * NS_ERANGE: the ring past the arena.                                       */
+typedef struct ns_rx_ring {
+  uint64_t ring_off;    /* arena offset of slot 0                            */
+  uint64_t stride;      /* bytes per slot                                    */
+  uint32_t n;           /* slots                                             */
+  uint16_t frame_at;    /* where the link frame starts in a slot              */
+  uint16_t link_hdr;    /* 0 (TUN) or 14 (Ethernet)                          */
+  uint32_t first_view;  /* the link's first buffer view (128), 0: one view   */
+  uint32_t flags;       /* reserved, 0                                       */
+} ns_rx_ring;
+int ns_csum_rx_ring(ns_csum_ctx* ctx, const uint8_t* d_arena, uint64_t arena_bytes,
+                    const ns_rx_ring* ring, const uint32_t* d_len, uint16_t* d_sums,
+                    uint8_t* d_verdict, void* stream);
+
 /* header.ChecksumCombine(a, b)                     checksum.go:104-107      */
 uint16_t ns_csum_combine(uint16_t a, uint16_t b);
 
@@ -427,6 +477,18 @@ typedef struct ns_csum_stats {
   uint64_t stage_alloc_ns_max;
 } ns_csum_stats;
 int ns_csum_get_stats(ns_csum_ctx* ctx, ns_csum_stats* out, int reset);
+
+/* A/B and test knobs of ns_csum_tcp_tx on this context (no reference
+ * counterpart; every result is the same whatever they are): variant (0 =
+ * production; 1 one fused pass, 2 nontemporal write-back, 3 segments reduced
+ * over the wave), tile / htile (segments per wave of the payload (or only)
+ * pass and of the header pass, 0 = the launcher's choice), passes (0 = by
+ * size, 1 = fused, 2 = two passes).  Read by each call without a lock; set
+ * them while no ns_csum_tcp_tx call runs on the context.  ns_csum_init takes
+ * their initial values from NS_CSUM_TX_VARIANT / _TILE / _HTILE / _PASSES,
+ * once.  NS_EINVAL for a variant above 3 or passes above 2.                 */
+int ns_csum_set_tx_tuning(ns_csum_ctx* ctx, uint32_t variant, uint32_t tile, uint32_t htile,
+                          uint32_t passes);
 
 #ifdef __cplusplus
 }

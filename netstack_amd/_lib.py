@@ -17,7 +17,7 @@ CSRC = os.path.join(_HERE, "csrc")
 
 # The NS_CSUM_ABI_VERSION this binding is written against; lib() refuses a
 # library that reports another (a stale build).
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 NS_OK = 0
 NS_EINVAL = -1
@@ -43,7 +43,7 @@ EXPORTED = (
     "ns_csum_combine", "ns_csum_shard_plan", "ns_csum_batch_multi", "ns_csum_chains",
     "ns_csum_stage_acquire", "ns_csum_stage_release", "ns_csum_packet_buffers",
     "ns_csum_stream_release", "ns_csum_scratch_count", "ns_csum_get_stats", "ns_csum_tcp_tx",
-    "ns_csum_tcp_tx_multi",
+    "ns_csum_tcp_tx_multi", "ns_csum_rx_ring", "ns_csum_set_tx_tuning",
 )
 NS_PIECE_RESTART = 0x1
 NS_PIECE_END = 0x2
@@ -113,6 +113,13 @@ class NsTcpTx(ctypes.Structure):
                 ("addr_sum", ctypes.c_uint16), ("protocol", ctypes.c_uint16), ("flags", ctypes.c_uint32)]
 
 
+class NsRxRing(ctypes.Structure):
+    """ns_rx_ring: a receive ring of fixed-stride slots (ns_csum_rx_ring)."""
+    _fields_ = [("ring_off", ctypes.c_uint64), ("stride", ctypes.c_uint64), ("n", ctypes.c_uint32),
+                ("frame_at", ctypes.c_uint16), ("link_hdr", ctypes.c_uint16),
+                ("first_view", ctypes.c_uint32), ("flags", ctypes.c_uint32)]
+
+
 NS_TX_TCP_PARTIAL = 0x1
 NS_TX_TCP_NONE = 0x2
 NS_TX_FIELDS_ONLY = 0x4
@@ -125,6 +132,7 @@ class NsOpts(ctypes.Structure):
 
 assert ctypes.sizeof(NsPktDesc) == 16 and ctypes.sizeof(NsSeg) == 24 and ctypes.sizeof(NsPiece) == 24
 assert ctypes.sizeof(NsPktBuf) == 40 and ctypes.sizeof(NsStats) == 13 * 8 and ctypes.sizeof(NsTcpTx) == 48
+assert ctypes.sizeof(NsRxRing) == 32
 
 _lock = threading.Lock()
 _lib = None
@@ -167,6 +175,8 @@ def _declare(lib):
         "ns_csum_get_stats": (c.c_int, [vp, c.POINTER(NsStats), c.c_int]),
         "ns_csum_tcp_tx": (c.c_int, [vp, u8p, c.c_uint64, c.POINTER(NsTcpTx), vp, vp]),
         "ns_csum_tcp_tx_multi": (c.c_int, [vp, u8p, c.c_uint64, c.POINTER(NsTcpTx), c.c_uint32, vp, vp]),
+        "ns_csum_rx_ring": (c.c_int, [vp, u8p, c.c_uint64, c.POINTER(NsRxRing), vp, vp, vp, vp]),
+        "ns_csum_set_tx_tuning": (c.c_int, [vp, c.c_uint32, c.c_uint32, c.c_uint32, c.c_uint32]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

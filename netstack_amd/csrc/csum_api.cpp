@@ -341,6 +341,8 @@ struct ns_csum_ctx {
   PinBuf<uint8_t> g_arena;
   std::vector<ns_pkt_desc> g_desc;
   StatCounters st;
+  // ns_csum_set_tx_tuning's knobs (A/B and tests), read by ns_csum_tcp_tx
+  std::atomic<uint32_t> tx_variant{0}, tx_tile{0}, tx_htile{0}, tx_passes{0};
 };
 
 namespace {
@@ -1054,6 +1056,16 @@ int ns_csum_init(const ns_csum_opts* opts, ns_csum_ctx** out) {
     (void)hipGetLastError();
   }
   ctx->bar_table = large_bar != 0 && std::getenv("NS_CSUM_NO_BAR_TABLE") == nullptr;
+  // ns_csum_tcp_tx's A/B knobs, read from the environment once, here (the
+  // tools set them per process; tests use ns_csum_set_tx_tuning).
+  auto knob = [](const char* name) -> uint32_t {
+    const char* v = std::getenv(name);
+    return v ? (uint32_t)std::strtoul(v, nullptr, 10) : 0u;
+  };
+  ctx->tx_variant = knob("NS_CSUM_TX_VARIANT");
+  ctx->tx_tile = knob("NS_CSUM_TX_TILE");
+  ctx->tx_htile = knob("NS_CSUM_TX_HTILE");
+  ctx->tx_passes = knob("NS_CSUM_TX_PASSES");
   *out = ctx;
   return NS_OK;
 }
@@ -1242,18 +1254,15 @@ int ns_csum_tcp_tx(ns_csum_ctx* ctx, uint8_t* d_arena, uint64_t arena_bytes, con
   geo.proto = t.protocol;
   geo.mode = mode;
   geo.out = d_out;
-  // A/B diagnostics, read per call: NS_CSUM_TX_VARIANT=k, a variant of the
-  // kernel (csum_kernels.h launch_tcp_tx); NS_CSUM_TX_TILE=t, t segments per
-  // wave instead of the launcher's choice (tests and tuning), for the payload
-  // (or the only) pass; NS_CSUM_TX_HTILE=t the same for the header pass.
-  const char* ev = std::getenv("NS_CSUM_TX_VARIANT");
-  const uint32_t variant = ev ? (uint32_t)std::atoi(ev) : 0u;
-  if (const char* v = std::getenv("NS_CSUM_TX_TILE")) geo.tile = (uint32_t)std::atoi(v);
-  if (const char* v = std::getenv("NS_CSUM_TX_HTILE")) geo.htile = (uint32_t)std::atoi(v);
-  // NS_CSUM_TX_PASSES=1|2 (diagnostics, per call): force the fused or the
-  // two-pass shape whatever the payload size.
-  const char* ep = std::getenv("NS_CSUM_TX_PASSES");
-  const bool two = ep ? std::atoi(ep) == 2 : t.size >= nsk::kTxTwoPassMinBytes;
+  // A/B and test knobs (ns_csum_set_tx_tuning): a variant of the kernel
+  // (csum_kernels.h launch_tcp_tx); segments per wave of the payload (or the
+  // only) pass and of the header pass instead of the launcher's choice; the
+  // fused or the two-pass shape whatever the payload size.
+  const uint32_t variant = ctx->tx_variant.load(std::memory_order_relaxed);
+  geo.tile = ctx->tx_tile.load(std::memory_order_relaxed);
+  geo.htile = ctx->tx_htile.load(std::memory_order_relaxed);
+  const uint32_t passes = ctx->tx_passes.load(std::memory_order_relaxed);
+  const bool two = passes ? passes == 2 : t.size >= nsk::kTxTwoPassMinBytes;
   hipStream_t s = (hipStream_t)stream;
   if (!(mode & nsk::kTxTcpFull) || !two) {  // one pass (no scratch)
     HIP_TRY(nsk::launch_tcp_tx(geo, s, variant));
@@ -1382,6 +1391,40 @@ int ns_csum_tcp_tx_multi(ns_csum_ctx* ctx, uint8_t* d_arena, uint64_t arena_byte
   }
   ctx->scratch.unpin(sc);
   return rc;
+}
+
+int ns_csum_set_tx_tuning(ns_csum_ctx* ctx, uint32_t variant, uint32_t tile, uint32_t htile, uint32_t passes) {
+  if (!ctx || variant > 3 || passes > 2) return NS_EINVAL;
+  ctx->tx_variant = variant;
+  ctx->tx_tile = tile;
+  ctx->tx_htile = htile;
+  ctx->tx_passes = passes;
+  return NS_OK;
+}
+
+int ns_csum_rx_ring(ns_csum_ctx* ctx, const uint8_t* d_arena, uint64_t arena_bytes, const ns_rx_ring* ring,
+                    const uint32_t* d_len, uint16_t* d_sums, uint8_t* d_verdict, void* stream) {
+  if (!ctx || !ring || (arena_bytes && !d_arena) || (!d_sums && !d_verdict)) return NS_EINVAL;
+  const ns_rx_ring& r = *ring;
+  if (r.n && !d_len) return NS_EINVAL;
+  const uint64_t base = (uint64_t)(uintptr_t)d_arena;
+  const int vr = nsh::rx_plan(r, base, arena_bytes);
+  if (vr != NS_OK) return vr;
+  if (r.n == 0) return NS_OK;
+  DeviceGuard g(ctx->device);
+  nsk::RxGeo geo{};
+  geo.ring = base + r.ring_off;
+  geo.stride = r.stride;
+  geo.len = d_len;
+  geo.sums = d_sums;
+  geo.verdict = d_verdict;
+  geo.err = ctx->d_err;
+  geo.n = r.n;
+  geo.frame_at = r.frame_at;
+  geo.link = r.link_hdr;
+  geo.view0 = r.first_view ? r.first_view - r.link_hdr : 0u;
+  HIP_TRY(nsk::launch_rx_ring(geo, (hipStream_t)stream));
+  return NS_OK;
 }
 
 int ns_csum_batch_host(ns_csum_ctx* ctx, const uint8_t* h_arena, uint64_t arena_bytes,

@@ -125,4 +125,22 @@ uint32_t tx_multi_prepare(TxGeo* calls, uint32_t ncalls, TxGeo* launch, uint32_t
 hipError_t launch_tcp_tx_multi(const TxGeo& launch, uint32_t grid, const TxGeo* d_calls, const uint32_t* d_first,
                                uint32_t ncalls, hipStream_t stream);
 
+// A receive ring verified on the device (rx_ring.hip, ns_csum_rx_ring).
+// Absolute device addresses; validated by the caller: ring and stride
+// 16-B aligned, stride < 2^24, frame_at + link even, view0 = 0 or >= 64 and
+// even.  Per slot s: the received length len[s] (bytes from the slot's first
+// byte); verdict[s] (NS_PKB_*) and sums[2s], sums[2s + 1] (or nullptr).
+struct RxGeo {
+  uint64_t ring, stride;
+  const uint32_t* len;
+  uint16_t* sums;
+  uint8_t* verdict;
+  unsigned long long* err;
+  uint32_t n;
+  uint32_t frame_at;  // bytes before the link frame in a slot (a virtio-net header)
+  uint32_t link;      // 0: the frame is the IP packet; 14: Ethernet
+  uint32_t view0;     // the IP packet's first view (BufConfig[0] - link), 0: one view
+};
+hipError_t launch_rx_ring(const RxGeo& g, hipStream_t stream);
+
 }  // namespace nsk

@@ -783,6 +783,15 @@ inline int tx_plan(const ns_tcp_tx& t, uint64_t arena_bytes, TxPlan* out) {
   if ((partial && none) || (t.flags & ~(NS_TX_TCP_PARTIAL | NS_TX_TCP_NONE | NS_TX_FIELDS_ONLY))) return NS_EINVAL;
   if (t.ip_len && (t.ip_len < 12 || t.ip_len > 60 || (uint32_t)t.ip_at + t.ip_len > t.slot)) return NS_EINVAL;
   if (!none && (t.tcp_len < 18 || t.tcp_len > 60 || (uint32_t)t.tcp_at + t.tcp_len > t.slot)) return NS_EINVAL;
+  // PseudoHeaderChecksum takes uint8(protocol) (checksum.go:121): a wider
+  // value has no reference meaning.
+  if (t.protocol > 0xFFu) return NS_EINVAL;
+  // The two headers are summed from one copy of the slot, each with the
+  // other's field already written: they must not share bytes (the reference
+  // prepends them one before the other, ipv4.go:217-238).
+  if (t.ip_len && !none && (uint32_t)t.ip_at < (uint32_t)t.tcp_at + t.tcp_len &&
+      (uint32_t)t.tcp_at < (uint32_t)t.ip_at + t.ip_len)
+    return NS_EINVAL;
   const uint64_t n = t.size / t.mss + (t.size % t.mss != 0);
   if (n >= (1ull << 32)) return NS_EINVAL;
   const uint32_t mode = (t.ip_len ? 1u : 0u) | (none ? 0u : partial ? 4u : 2u) |
@@ -828,6 +837,19 @@ inline int tx_multi_plan(const ns_tcp_tx* t, uint32_t count, uint64_t arena_byte
       pay_end = std::max(pay_end, v.hi);
     }
   }
+  return NS_OK;
+}
+
+// ns_csum_rx_ring's geometry, validated (include/netstack_csum.h).  `base`
+// is the device address of the arena (its alignment matters: 16-B loads).
+inline int rx_plan(const ns_rx_ring& r, uint64_t base, uint64_t arena_bytes) {
+  if (r.flags || r.stride == 0 || r.stride >= (1ull << 24) || (r.stride & 15u) || ((base + r.ring_off) & 15u))
+    return NS_EINVAL;
+  if ((r.link_hdr != 0 && r.link_hdr != 14) || ((r.frame_at + r.link_hdr) & 1u) || r.frame_at >= r.stride)
+    return NS_EINVAL;
+  if (r.first_view && ((r.first_view & 1u) || r.first_view < (uint32_t)r.link_hdr + 64u)) return NS_EINVAL;
+  const uint64_t bytes = (uint64_t)r.n * r.stride;
+  if (r.ring_off > arena_bytes || bytes > arena_bytes - r.ring_off) return NS_ERANGE;
   return NS_OK;
 }
 

@@ -155,12 +155,54 @@ class Engine:
         if not arena.is_cuda:
             raise ValueError("arena must be a device tensor")
         arr = geos if isinstance(geos, ctypes.Array) else tx_table(geos, mode)
+        if out is not None:
+            # every call's 2 n_k sums, n_k = ceil(size / mss) (connect.go:675)
+            total = sum(-(-int(t.size) // max(int(t.mss), 1)) for t in (arr[k] for k in range(len(geos))))
+            if not out.is_cuda or out.numel() < 2 * total or out.element_size() != 2:
+                raise ValueError("out must be a device tensor of 2 * sum(n_k) 16-bit sums")
         if stream is None:
             stream = torch.cuda.current_stream(arena.device)
         check(lib().ns_csum_tcp_tx_multi(self._h, arena.data_ptr(), arena.numel() * arena.element_size(), arr,
                                          len(arr) if len(geos) else 0, out.data_ptr() if out is not None else None,
                                          getattr(stream, "cuda_stream", stream)), "ns_csum_tcp_tx_multi")
         return out
+
+    def set_tx_tuning(self, variant: int = 0, tile: int = 0, htile: int = 0, passes: int = 0) -> None:
+        """ns_csum_tcp_tx's A/B and test knobs on this context
+        (ns_csum_set_tx_tuning; all zero = production)."""
+        check(lib().ns_csum_set_tx_tuning(self._h, variant, tile, htile, passes), "ns_csum_set_tx_tuning")
+
+    def rx_ring(self, arena, ring: dict, lens, sums=None, verdict=None, stream=None):
+        """Verify a receive ring resident in HBM (ns_csum_rx_ring): `arena` a
+        uint8 CUDA tensor holding n slots of `stride` bytes from `ring_off`;
+        `ring` the keys of ns_rx_ring (ring_off, stride, n, frame_at,
+        link_hdr, first_view); `lens` an int32/uint32 CUDA tensor of the n
+        received lengths.  `verdict` (uint8, n) and `sums` (16-bit, 2n) are
+        allocated when None.  Launches on `stream` (default: torch's current
+        stream) without synchronising; returns (verdict, sums)."""
+        import torch
+
+        n = int(ring["n"])
+        if not (arena.is_cuda and lens.is_cuda):
+            raise ValueError("arena and lens must be device tensors")
+        if lens.element_size() != 4 or lens.numel() < n or not lens.is_contiguous():
+            raise ValueError("lens must be a contiguous tensor of n 32-bit lengths")
+        if verdict is None:
+            verdict = torch.empty(max(n, 1), dtype=torch.uint8, device=arena.device)
+        if sums is None:
+            sums = torch.empty(max(2 * n, 1), dtype=torch.int16, device=arena.device)
+        if not verdict.is_cuda or verdict.element_size() != 1 or verdict.numel() < n:
+            raise ValueError("verdict must be a device tensor of n bytes")
+        if not sums.is_cuda or sums.element_size() != 2 or sums.numel() < 2 * n:
+            raise ValueError("sums must be a device tensor of 2n 16-bit sums")
+        r = _lib.NsRxRing(int(ring.get("ring_off", 0)), int(ring["stride"]), n, int(ring.get("frame_at", 0)),
+                          int(ring.get("link_hdr", 0)), int(ring.get("first_view", 0)), int(ring.get("flags", 0)))
+        if stream is None:
+            stream = torch.cuda.current_stream(arena.device)
+        check(lib().ns_csum_rx_ring(self._h, arena.data_ptr(), arena.numel() * arena.element_size(),
+                                    ctypes.byref(r), lens.data_ptr(), sums.data_ptr(), verdict.data_ptr(),
+                                    getattr(stream, "cuda_stream", stream)), "ns_csum_rx_ring")
+        return verdict, sums
 
     def stream_release(self, stream) -> None:
         """Free the scratch this context keeps for `stream` (a torch.cuda.Stream

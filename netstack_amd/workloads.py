@@ -319,6 +319,19 @@ def rx_batch(n: int, seed: int, device, corrupt_every: int = 0, fused: bool = Tr
     return arena, _tcp_desc(n, fused), bad
 
 
+def rx_ring_batch(n: int, seed: int, device, corrupt_every: int = 0):
+    """rx_batch's packets as a receive ring (ns_csum_rx_ring): the same n
+    valid 1500-B IPv4/TCP packets, one per RX_STRIDE slot, and the n received
+    lengths (int32 CUDA tensor) in place of a descriptor table; with
+    corrupt_every = k > 0 one payload byte of every k-th packet is flipped.
+    Returns (arena, lens, bad indices)."""
+    import torch
+
+    arena, _, bad = rx_batch(n, seed, device, corrupt_every)
+    lens = torch.full((n,), RX_PKT, dtype=torch.int32, device=device)
+    return arena, lens, bad
+
+
 TX_IP_CSUM = 10   # header.IPv4 checksum field (ipv4.go:35 checksum offset)
 TX_TCP_CSUM = 16  # header.TCP checksum field, from the TCP header start
 

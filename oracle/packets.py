@@ -66,15 +66,23 @@ def _icmpv6_checksum(h: bytearray, src: bytes, dst: bytes, payload_views) -> int
     return xsum
 
 
-def verify(hdr: bytes, views, size: int):
+def verify(hdr: bytes, views, size: int, net_proto: int | None = None):
     """The receive path for a packet as the link layer delivers it (Data =
     the IP packet): returns (verdict, ipv4 header sum, transport sum) — the
-    sums as ns_csum_packet_buffers reports them (0 where none is taken)."""
+    sums as ns_csum_packet_buffers reports them (0 where none is taken).
+    net_proto: the network protocol an Ethernet link picked by EtherType (4,
+    6, or 0 for anything else); None: a headerless link, which picks it by the
+    version nibble (packet_dispatchers.go:283-296)."""
     data = _cap(([bytes(hdr)] if len(hdr) else []) + [bytes(v) for v in views], size)
     first = data[0] if data else b""
     if not first:
         return MALFORMED, 0, 0
     ver = first[0] >> 4
+    if net_proto is not None:
+        if net_proto not in (4, 6):
+            return UNCHECKED, 0, 0  # not IP: nothing the reference checksums
+        if ver != net_proto:
+            return MALFORMED, 0, 0  # IsValid's version check (header/ipv4.go:292, ipv6.go:218)
     if ver == 4:
         # IPv4 HandlePacket (network/ipv4/ipv4.go:341-353) + IsValid (header/ipv4.go:280-296)
         if len(first) < 20:
@@ -203,3 +211,43 @@ def fill(hdr: bytes, views, size: int):
         net = c_checksum(bytes(hdr[:hlen]), 0)
         struct.pack_into(">H", h, 10, (~net) & 0xFFFF)
     return bytes(h), net, tr
+
+
+BUF_CONFIG = (128, 256, 256, 512, 1024, 2048, 4096, 8192, 16384, 32768)  # packet_dispatchers.go:30
+
+
+def frame_views(frame: bytes, first_view: int = 128):
+    """The views recvMMsgDispatcher hands up for a frame of len(frame) bytes
+    (allocateViews + capViews, packet_dispatchers.go:214-245): BufConfig's
+    buffers (the first one first_view bytes; 0: the frame as one view),
+    the last one capped."""
+    sizes = ((first_view,) + BUF_CONFIG[1:]) if first_view else (max(len(frame), 1),)
+    out, at = [], 0
+    for sz in sizes:
+        if at >= len(frame):
+            break
+        out.append(bytes(frame[at:at + sz]))
+        at += sz
+    return out
+
+
+def verify_frame(slot: bytes, rlen: int, frame_at: int = 0, link_hdr: int = 0, first_view: int = 0):
+    """One slot of a receive ring (ns_csum_rx_ring): recvmmsg wrote rlen bytes
+    into `slot`, the link frame starting at frame_at; recvMMsgDispatcher.
+    dispatch (packet_dispatchers.go:258-317) then drops a frame of no more
+    than link_hdr bytes, picks the network protocol (EtherType with an
+    Ethernet header, else the version nibble), trims the link header off
+    Data and delivers; verify() does the rest."""
+    if rlen > len(slot):
+        return MALFORMED, 0, 0  # longer than its slot: counted by the engine
+    frame = bytes(slot[frame_at:rlen]) if rlen > frame_at else b""
+    if len(frame) <= link_hdr:
+        return MALFORMED, 0, 0
+    views = frame_views(frame, first_view)
+    size = len(frame) - link_hdr
+    net_proto = None
+    if link_hdr:
+        et = (frame[12] << 8) | frame[13]
+        net_proto = 4 if et == 0x0800 else 6 if et == 0x86DD else 0
+        views = _trim_front(views, link_hdr)
+    return verify(b"", views, size, net_proto)

@@ -1,0 +1,158 @@
+"""Test infrastructure: packet builders shared by the receive-path GPU tests
+(tests/test_gpu_packet.py, tests/test_gpu_rx_ring.py).  Checksums of the
+packets they build are filled by the oracle's transmit restatement
+(oracle/packets.py fill), so a "valid" packet is what a peer running the
+reference would send.  Not part of the product."""
+import struct
+
+import numpy as np
+
+BUF_CONFIG = [128, 256, 256, 512, 1024, 2048, 4096, 8192, 16384, 32768]  # packet_dispatchers.go:30
+
+
+def views_bufconfig(pkt: bytes, link_hdr: int):
+    """recvMMsgDispatcher: the frame (link header + packet) read into
+    BufConfig views, the last used one capped (capViews), then
+    Data.TrimFront(hdrSize)."""
+    from netstack_amd.buffer import NewVectorisedView, View
+
+    frame = bytes(link_hdr) + pkt
+    views, c = [], 0
+    for s in BUF_CONFIG:
+        views.append(View(bytearray(frame[c:c + s])))
+        c += s
+        if c >= len(frame):
+            break
+    vv = NewVectorisedView(len(frame), views)
+    vv.TrimFront(link_hdr)
+    return vv
+
+
+def ip4(proto, src, dst, payload_len, ident=0, frag=0, ihl=20, tlen=None):
+    from netstack_amd.proto import IPv4Fields, encode_ipv4
+
+    h = encode_ipv4(IPv4Fields(IHL=ihl, TotalLength=tlen if tlen is not None else ihl + payload_len, ID=ident,
+                               TTL=64, Protocol=proto, SrcAddr=src, DstAddr=dst))
+    if frag:
+        struct.pack_into(">H", h, 6, frag)
+    return h
+
+
+def ip6(proto, src, dst, payload_len):
+    h = bytearray(40)
+    h[0] = 0x60
+    struct.pack_into(">HBB", h, 4, payload_len & 0xFFFF, proto, 64)
+    h[8:24] = src
+    h[24:40] = dst
+    return h
+
+
+def tcp_header(rng, opts_words=0):
+    from netstack_amd.tcp import TCPFields, encode_tcp
+
+    off = 20 + 4 * opts_words
+    return encode_tcp(TCPFields(int(rng.integers(1, 65536)), int(rng.integers(1, 65536)),
+                                int(rng.integers(0, 2**32)), int(rng.integers(0, 2**32)), off, 0x18,
+                                int(rng.integers(0, 65536))), bytes(rng.integers(0, 256, 4 * opts_words,
+                                                                                 dtype=np.uint8)))
+
+
+def valid_packet(rng, kind, plen):
+    """A well-formed packet of `kind` with correct checksums (filled by the
+    oracle's transmit restatement) — the bytes a peer would send."""
+    import packets as P
+
+    from netstack_amd.proto import encode_udp
+
+    payload = bytes(rng.integers(0, 256, plen, dtype=np.uint8))
+    v6 = kind.endswith("6")
+    src, dst = (bytes(rng.integers(0, 256, 16, dtype=np.uint8)), bytes(rng.integers(0, 256, 16, dtype=np.uint8))) \
+        if v6 else (bytes(rng.integers(0, 256, 4, dtype=np.uint8)), bytes(rng.integers(0, 256, 4, dtype=np.uint8)))
+    if kind.startswith("tcp"):
+        t = tcp_header(rng, int(rng.integers(0, 4)))
+        proto = 6
+    elif kind.startswith("udp"):
+        t = encode_udp(int(rng.integers(1, 65536)), int(rng.integers(1, 65536)), 8 + plen)
+        proto = 17
+    elif kind == "icmp4":
+        t = bytearray(8)
+        t[0] = 8  # echo request
+        struct.pack_into(">HH", t, 4, int(rng.integers(0, 65536)), int(rng.integers(0, 65536)))
+        proto = 1
+    else:  # icmp6: echo request
+        t = bytearray(8)
+        t[0] = 128
+        proto = 58
+    ip = ip6(proto, src, dst, len(t) + plen) if v6 else ip4(proto, src, dst, len(t) + plen,
+                                                               int(rng.integers(0, 65536)))
+    hdr, _, _ = P.fill(bytes(ip + t), [payload], plen)
+    if kind == "icmp4":  # fill() wrote an echo-reply style sum: valid for the request too
+        pass
+    return bytearray(hdr + payload)
+
+
+def frag_packet(rng, how, plen):
+    """IPv4 fragments of every kind HandlePacket tells apart
+    (network/ipv4/ipv4.go:355-385; FragmentOffset() = field << 3 in a uint16):
+    0 MF with a TCP header and payload (reassembled: UNCHECKED); 1 the last
+    fragment (no MF, an offset; UNCHECKED); 2 MF and no payload (MALFORMED,
+    :357-363); 3 an offset with no payload (MALFORMED); 4 the highest offset
+    with `last = offset + size - 1` wrapping past 0xffff (MALFORMED,
+    :365-373); 5 the same offset with exactly 8 bytes, last = 0xffff (no wrap:
+    UNCHECKED)."""
+    if how in (0, 1):
+        p = valid_packet(rng, "tcp4", plen)
+        struct.pack_into(">H", p, 6, 0x2000 if how == 0 else int(rng.integers(1, 0x2000)))
+        return p
+    src, dst = bytes(rng.integers(0, 256, 4, dtype=np.uint8)), bytes(rng.integers(0, 256, 4, dtype=np.uint8))
+    size = 0 if how in (2, 3) else int(rng.integers(9, 3000)) if how == 4 else 8
+    frag = {2: 0x2000 | int(rng.integers(0, 0x2000)), 3: int(rng.integers(1, 0x2000)),
+            4: 0x1FFF | (0x2000 if rng.random() < 0.5 else 0), 5: 0x1FFF}[how]
+    p = ip4(6, src, dst, size, int(rng.integers(0, 65536)), frag=frag)
+    p += bytes(rng.integers(0, 256, size, dtype=np.uint8))
+    # the IPv4 header checksum as addIPHeader writes it (the reference does not check it on receive)
+    import oracle as O
+
+    struct.pack_into(">H", p, 10, 0)
+    struct.pack_into(">H", p, 10, (~O.c_checksum(bytes(p[:20]), 0)) & 0xFFFF)
+    return p
+
+
+def random_packet(rng, max_payload: int = 9000) -> bytearray:
+    """One received IP packet of a recvmmsg-like mix: mostly TCP (v4/v6),
+    plus ICMPv4/v6, UDP, fragments of every kind and malformed packets; ~1/7
+    of the valid ones carry one corrupted byte, ~1/10 trailing bytes past
+    their TotalLength (Data.CapLength)."""
+    r = rng.random()
+    kind = "tcp4" if r < 0.45 else "tcp6" if r < 0.65 else "icmp4" if r < 0.72 else \
+        "icmp6" if r < 0.79 else "udp4" if r < 0.85 else "frag" if r < 0.88 else "bad"
+    plen = int(rng.choice([0, 1, 7, int(rng.integers(0, 1460)), int(rng.integers(0, max_payload))]))
+    if kind == "frag":
+        p = frag_packet(rng, int(rng.integers(0, 6)), plen)
+    elif kind == "bad":
+        p = valid_packet(rng, "tcp4", plen)
+        how = int(rng.integers(0, 4))
+        if how == 0:
+            p = p[:int(rng.integers(1, 20))]                 # shorter than an IPv4 header
+        elif how == 1:
+            p[0] = 0x43                                      # IHL 12 < 20
+        elif how == 2:
+            struct.pack_into(">H", p, 2, len(p) + 1)         # TotalLength past the packet
+        else:
+            p[20 + 12] = 0x40                                # TCP data offset 16 < 20
+    else:
+        p = valid_packet(rng, kind, plen)
+        if rng.random() < 1 / 7 and len(p) > 0:
+            k = int(rng.integers(0, len(p)))
+            p[k] ^= int(rng.integers(1, 256))
+    if rng.random() < 0.1:
+        p += bytes(rng.integers(0, 256, int(rng.integers(1, 30)), dtype=np.uint8))
+    return bytearray(p)
+
+
+def ethernet(pkt: bytes, etype: int | None = None) -> bytes:
+    """An Ethernet frame around an IP packet (header.Ethernet: dst, src,
+    EtherType); the type follows the version nibble unless given."""
+    if etype is None:
+        etype = 0x86DD if pkt and (pkt[0] >> 4) == 6 else 0x0800
+    return bytes(range(1, 13)) + struct.pack(">H", etype) + bytes(pkt)

@@ -18,115 +18,13 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 
-BUF_CONFIG = [128, 256, 256, 512, 1024, 2048, 4096, 8192, 16384, 32768]  # packet_dispatchers.go:30
-
-
-def _views_bufconfig(pkt: bytes, link_hdr: int):
-    """recvMMsgDispatcher: the frame (link header + packet) read into
-    BufConfig views, the last used one capped (capViews), then
-    Data.TrimFront(hdrSize)."""
-    from netstack_amd.buffer import NewVectorisedView, View
-
-    frame = bytes(link_hdr) + pkt
-    views, c = [], 0
-    for s in BUF_CONFIG:
-        views.append(View(bytearray(frame[c:c + s])))
-        c += s
-        if c >= len(frame):
-            break
-    vv = NewVectorisedView(len(frame), views)
-    vv.TrimFront(link_hdr)
-    return vv
-
-
-def _ip4(proto, src, dst, payload_len, ident=0, frag=0, ihl=20, tlen=None):
-    from netstack_amd.proto import IPv4Fields, encode_ipv4
-
-    h = encode_ipv4(IPv4Fields(IHL=ihl, TotalLength=tlen if tlen is not None else ihl + payload_len, ID=ident,
-                               TTL=64, Protocol=proto, SrcAddr=src, DstAddr=dst))
-    if frag:
-        struct.pack_into(">H", h, 6, frag)
-    return h
-
-
-def _ip6(proto, src, dst, payload_len):
-    h = bytearray(40)
-    h[0] = 0x60
-    struct.pack_into(">HBB", h, 4, payload_len & 0xFFFF, proto, 64)
-    h[8:24] = src
-    h[24:40] = dst
-    return h
-
-
-def _tcp(rng, opts_words=0):
-    from netstack_amd.tcp import TCPFields, encode_tcp
-
-    off = 20 + 4 * opts_words
-    return encode_tcp(TCPFields(int(rng.integers(1, 65536)), int(rng.integers(1, 65536)),
-                                int(rng.integers(0, 2**32)), int(rng.integers(0, 2**32)), off, 0x18,
-                                int(rng.integers(0, 65536))), bytes(rng.integers(0, 256, 4 * opts_words,
-                                                                                 dtype=np.uint8)))
-
-
-def _valid_packet(rng, kind, plen):
-    """A well-formed packet of `kind` with correct checksums (filled by the
-    oracle's transmit restatement) — the bytes a peer would send."""
-    import packets as P
-
-    from netstack_amd.proto import encode_udp
-
-    payload = bytes(rng.integers(0, 256, plen, dtype=np.uint8))
-    v6 = kind.endswith("6")
-    src, dst = (bytes(rng.integers(0, 256, 16, dtype=np.uint8)), bytes(rng.integers(0, 256, 16, dtype=np.uint8))) \
-        if v6 else (bytes(rng.integers(0, 256, 4, dtype=np.uint8)), bytes(rng.integers(0, 256, 4, dtype=np.uint8)))
-    if kind.startswith("tcp"):
-        t = _tcp(rng, int(rng.integers(0, 4)))
-        proto = 6
-    elif kind.startswith("udp"):
-        t = encode_udp(int(rng.integers(1, 65536)), int(rng.integers(1, 65536)), 8 + plen)
-        proto = 17
-    elif kind == "icmp4":
-        t = bytearray(8)
-        t[0] = 8  # echo request
-        struct.pack_into(">HH", t, 4, int(rng.integers(0, 65536)), int(rng.integers(0, 65536)))
-        proto = 1
-    else:  # icmp6: echo request
-        t = bytearray(8)
-        t[0] = 128
-        proto = 58
-    ip = _ip6(proto, src, dst, len(t) + plen) if v6 else _ip4(proto, src, dst, len(t) + plen,
-                                                               int(rng.integers(0, 65536)))
-    hdr, _, _ = P.fill(bytes(ip + t), [payload], plen)
-    if kind == "icmp4":  # fill() wrote an echo-reply style sum: valid for the request too
-        pass
-    return bytearray(hdr + payload)
-
-
-def _frag_packet(rng, how, plen):
-    """IPv4 fragments of every kind HandlePacket tells apart
-    (network/ipv4/ipv4.go:355-385; FragmentOffset() = field << 3 in a uint16):
-    0 MF with a TCP header and payload (reassembled: UNCHECKED); 1 the last
-    fragment (no MF, an offset; UNCHECKED); 2 MF and no payload (MALFORMED,
-    :357-363); 3 an offset with no payload (MALFORMED); 4 the highest offset
-    with `last = offset + size - 1` wrapping past 0xffff (MALFORMED,
-    :365-373); 5 the same offset with exactly 8 bytes, last = 0xffff (no wrap:
-    UNCHECKED)."""
-    if how in (0, 1):
-        p = _valid_packet(rng, "tcp4", plen)
-        struct.pack_into(">H", p, 6, 0x2000 if how == 0 else int(rng.integers(1, 0x2000)))
-        return p
-    src, dst = bytes(rng.integers(0, 256, 4, dtype=np.uint8)), bytes(rng.integers(0, 256, 4, dtype=np.uint8))
-    size = 0 if how in (2, 3) else int(rng.integers(9, 3000)) if how == 4 else 8
-    frag = {2: 0x2000 | int(rng.integers(0, 0x2000)), 3: int(rng.integers(1, 0x2000)),
-            4: 0x1FFF | (0x2000 if rng.random() < 0.5 else 0), 5: 0x1FFF}[how]
-    p = _ip4(6, src, dst, size, int(rng.integers(0, 65536)), frag=frag)
-    p += bytes(rng.integers(0, 256, size, dtype=np.uint8))
-    # the IPv4 header checksum as addIPHeader writes it (the reference does not check it on receive)
-    import oracle as O
-
-    struct.pack_into(">H", p, 10, 0)
-    struct.pack_into(">H", p, 10, (~O.c_checksum(bytes(p[:20]), 0)) & 0xFFFF)
-    return p
+from pktgen import BUF_CONFIG  # noqa: F401
+from pktgen import frag_packet as _frag_packet
+from pktgen import ip4 as _ip4
+from pktgen import ip6 as _ip6
+from pktgen import tcp_header as _tcp
+from pktgen import valid_packet as _valid_packet
+from pktgen import views_bufconfig as _views_bufconfig
 
 
 def _rx_batch(rng, n):

@@ -11,7 +11,6 @@ IPv6 route (no IPv4 header, 16-B addresses), MSS 1 and 16 (several segment
 ends per 16-B chunk and per window), jumbo and 64 KiB GSO segments, a last
 segment of 1 byte, CHECKSUM_PARTIAL, TX offload, 2-byte field stores, and
 forced tiles (segments per wave) from 1 to 64."""
-import os
 
 import numpy as np
 import pytest
@@ -77,19 +76,13 @@ def _run(engine, a, geo, mode="full", fields_only=False, tile=None, offset=0, ht
     arena = buf[offset:]
     n = -(-geo["size"] // geo["mss"])
     out = torch.full((2 * n,), -1, dtype=torch.int16, device="cuda")
-    knobs = {k: str(v) for k, v in (("NS_CSUM_TX_TILE", tile), ("NS_CSUM_TX_HTILE", htile),
-                                    ("NS_CSUM_TX_PASSES", passes)) if v is not None}
-    old = {k: os.environ.get(k) for k in knobs}
-    os.environ.update(knobs)
+    # the A/B knobs go through ns_csum_set_tx_tuning (never the environment)
+    engine.set_tx_tuning(tile=tile or 0, htile=htile or 0, passes=passes or 0)
     try:
         engine.tcp_tx(arena, geo, out=out, mode=mode, fields_only=fields_only)
         torch.cuda.synchronize()
     finally:
-        for k, v in old.items():
-            if v is None:
-                del os.environ[k]
-            else:
-                os.environ[k] = v
+        engine.set_tx_tuning()
     return arena.cpu().numpy(), out.cpu().numpy().view(np.uint16)
 
 
@@ -133,7 +126,7 @@ def test_forced_tiles(engine, oracle_mod, tile):
 
 @pytest.mark.parametrize("htile", [1, 3, 64, 100, 129, 222])
 def test_header_pass_tiles(engine, oracle_mod, htile):
-    """The header pass's tile (NS_CSUM_TX_HTILE): up to 256 segments per wave,
+    """The header pass's tile (ns_csum_set_tx_tuning htile): up to 256 segments per wave,
     each lane looping over every 64th; with and without d_out (payload values
     parked in d_out or in per-stream scratch)."""
     for name in ("short_last_odd", "odd_slots_odd_mss", "ipv6_route"):
@@ -159,12 +152,12 @@ def test_without_out_uses_scratch(engine, oracle_mod):
     a = _arena(total, geo, seed=21)
     wa, _ = _want(oracle_mod, a, geo)
     buf = torch.from_numpy(a).cuda()
-    os.environ["NS_CSUM_TX_PASSES"] = "2"
+    engine.set_tx_tuning(passes=2)
     try:
         engine.tcp_tx(buf, geo)
         torch.cuda.synchronize()
     finally:
-        del os.environ["NS_CSUM_TX_PASSES"]
+        engine.set_tx_tuning()
     assert np.array_equal(buf.cpu().numpy(), wa)
 
 
@@ -278,14 +271,14 @@ def test_two_streams_keep_their_own_scratch(engine, oracle_mod):
         wants.append(_want(oracle_mod, a, geo)[0])
         bufs.append(torch.from_numpy(a).cuda())
     torch.cuda.synchronize()
-    os.environ["NS_CSUM_TX_PASSES"] = "2"
+    engine.set_tx_tuning(passes=2)
     try:
         for _ in range(3):  # refills of the same fields: idempotent
             for k in range(2):
                 engine.tcp_tx(bufs[k], geos[k][0], stream=streams[k])
         torch.cuda.synchronize()
     finally:
-        del os.environ["NS_CSUM_TX_PASSES"]
+        engine.set_tx_tuning()
     for k in range(2):
         assert np.array_equal(bufs[k].cpu().numpy(), wants[k]), k
         engine.stream_release(streams[k])
