@@ -52,9 +52,10 @@ def parse():
                     help="BASELINE.json configs[k-1]; 7 = device-resident RX verification, "
                          "8 = device-resident TX checksum fill (SURVEY §8(f) ranks 2 and 1)")
     ap.add_argument("--mode", default="dev", choices=("dev", "host"))
-    ap.add_argument("--rx-layout", default="fused", choices=("fused", "chained"),
+    ap.add_argument("--rx-layout", default="fused", choices=("fused", "chained", "ring"),
                     help="--config 7 (and 8 with --tx-layout wire) descriptor table: 2 independent descriptors "
-                         "per packet, or 3 chained")
+                         "per packet, or 3 chained; --config 7 ring: no table, a receive ring parsed and verified "
+                         "on the device (ns_csum_rx_ring)")
     ap.add_argument("--tx-layout", default="struct", choices=("struct", "split", "wire"),
                     help="--config 8 packets: as sendTCPBatch builds them (header slots + payload view) "
                          "filled from the batch geometry by ns_csum_tcp_tx (struct) or through an "
@@ -669,6 +670,8 @@ def packet_mode(args, dist, eng, dev, tx: bool):
     from netstack_amd import workloads as W
 
     seed = 7000 + dist.rank
+    if not tx and args.rx_layout == "ring":
+        return ring_mode(args, dist, eng, dev, seed)
     struct = tx and args.tx_layout == "struct"
     split = tx and args.tx_layout in ("split", "struct")
     fused = args.rx_layout == "fused"
@@ -836,6 +839,102 @@ def packet_mode(args, dist, eng, dev, tx: bool):
                 "sample": f"65,536 segments ({65536 * W.RX_PKT} packet bytes) of the rank-0 batch x {reps} passes, "
                           f"{el:.1f} s; oracle_send_tcp_batch (sendTCPBatch + buildTCPHdr + addIPHeader's checksum "
                           f"steps over oracle/csum_oracle.c's scalar loop), single thread"}
+    if dist.rank == 0:
+        print(json.dumps(result), flush=True)
+    eng.close()
+    dist.close()
+
+
+def ring_mode(args, dist, eng, dev, seed):
+    """`--config 7 --rx-layout ring`: the receive path of 1M received 1500-B
+    IPv4/TCP packets per GPU, one per 1504-B slot of a ring in HBM, with no
+    descriptor table: one ns_csum_rx_ring per step parses every packet's
+    headers on the device (IsValid, the fragment checks, segment.parse's
+    length checks), takes the pseudo-header from the packet's own addresses
+    and writes each slot's verdict (NS_PKB_*) and its two sums.  Every 1000th
+    packet has a corrupted payload byte: the check after the timed region
+    requires exactly those to be INVALID, every other VALID and every IPv4
+    header to sum to 0xffff, over all 1M slots; the first 65,536 slots are
+    compared bit for bit with the oracle's C restatement (oracle_rx_ring),
+    which is also the timed CPU leg.  value = packet bytes / s (GiB/s)."""
+    import torch
+
+    from netstack_amd import workloads as W
+
+    arena, lens, bad_idx = W.rx_ring_batch(RX_N, seed, dev, corrupt_every=1000)
+    ring = dict(stride=W.RX_STRIDE, n=RX_N)
+    verdict = torch.empty(RX_N, dtype=torch.uint8, device=dev)
+    sums = torch.empty(2 * RX_N, dtype=torch.int16, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    ev = [torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)]
+    state = {"i": 0}
+
+    def step():
+        k = state["i"]
+        if k == args.warmup:
+            ev[0].record(stream)
+        eng.rx_ring(arena, ring, lens, sums=sums, verdict=verdict, stream=stream)
+        state["i"] = k + 1
+        if state["i"] == args.warmup + args.steps:
+            ev[1].record(stream)
+
+    wall, _ = timed_region(step, torch.cuda.synchronize, dist, args.steps, args.warmup, dev)
+    bad = eng.sync()
+    kern_avg_s = ev[0].elapsed_time(ev[1]) / 1e3 / args.steps
+    v = verdict.cpu().numpy()
+    sm = sums.cpu().numpy().view(np.uint16)
+    want = np.ones(RX_N, dtype=np.uint8)
+    want[bad_idx] = 0
+    ip_ok = bool((sm[0::2] == 0xFFFF).all())
+    tcp_fail = np.flatnonzero(sm[1::2] != 0xFFFF)
+    prop_ok = ip_ok and bool((v == want).all()) and np.array_equal(tcp_fail, bad_idx) and bad == 0
+    fails = dist.sum(0.0 if prop_ok else 1.0, dev)
+    pkt_bytes = RX_N * W.RX_PKT
+    total = dist.sum(float(pkt_bytes), dev)
+    # per slot: the packet's bytes and its u32 length read; its verdict (1 B)
+    # and its two u16 sums written
+    algo = pkt_bytes + RX_N * (4 + 1 + 4)
+    achieved = algo / kern_avg_s / 1e9
+    traffic, traffic_src = pmc_traffic(args.pmc_json, "7ring")
+    result = {
+        "metric": "RX checksum verification GiB/s device-resident (IPv4 + TCP, 1500-B packets)",
+        "value": total * args.steps / wall / GIB, "unit": "GiB/s", "n_gpus": dist.world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": wall / args.steps * 1e3,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic received packets (valid IPv4/TCP checksums, 1 in 1000 corrupted), resident in HBM",
+        "config": {"workload": "rx ring: 1,048,576 x 1500-B IPv4/TCP packets per GPU in 1504-B slots, parsed and "
+                               "verified on the device from the slots' lengths (ns_csum_rx_ring, no table)",
+                   "packets_per_gpu": RX_N, "descriptors_per_gpu": 0},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
+                     "kernel": "nsk::rx_ring<13>", "layout": "ring (1504-B slots, u32 lengths)",
+                     "algorithmic_bytes_per_launch": algo, "avg_launch_us": kern_avg_s * 1e6},
+        "bad_descriptors": bad,
+        "property_check": {"ipv4_all_valid": ip_ok, "tcp_failures": int(tcp_fail.size),
+                           "expected_failures": int(bad_idx.size), "verdicts_as_expected": bool((v == want).all()),
+                           "ok": prop_ok, "ranks_failed": int(fails)},
+    }
+    if dist.rank == 0 and not args.no_cpu:
+        import oracle as O
+
+        k = 65536
+        src = arena[:k * W.RX_STRIDE].cpu().numpy()
+        ln = lens[:k].cpu().numpy().view(np.uint32)
+        ov, osm = O.c_rx_ring(src, ln, W.RX_STRIDE, k)
+        result["parity_sample"] = {"packets": k, "bit_exact": bool(np.array_equal(ov, v[:k]) and
+                                                                      np.array_equal(osm, sm[:2 * k]))}
+        reps, t0 = 0, time.perf_counter()
+        while True:
+            O.c_rx_ring(src, ln, W.RX_STRIDE, k)
+            reps += 1
+            el = time.perf_counter() - t0
+            if el >= args.cpu_seconds:
+                break
+        result["cpu_baseline"] = {
+            "value": k * W.RX_PKT * reps / el / GIB, "unit": "GiB/s", "cores": 1, "kind": "port",
+            "sample": f"{k:,} slots ({k * W.RX_PKT} packet bytes) of the rank-0 ring x {reps} passes, {el:.1f} s; "
+                      "oracle_rx_ring (dispatch + HandlePacket + IsValid + segment.parse's checksum over "
+                      "oracle/csum_oracle.c's scalar loop), single thread"}
     if dist.rank == 0:
         print(json.dumps(result), flush=True)
     eng.close()

@@ -80,44 +80,27 @@ __device__ __forceinline__ uint32_t rx_below(int c) {  // bytes [0, c) of a dwor
   return c >= 4 ? 0xFFFFFFFFu : ((1u << (8 * c)) - 1u);
 }
 
-// Bytes [lo, hi) of a 16-B chunk, without [zl, zl + 2).
-__device__ __forceinline__ uint32_t rx_dmask(int lo, int hi, int zl, int d) {
-  const int b = 4 * d;
-  return rx_below(hi - b) & ~rx_below(lo - b) & ~(rx_below(zl + 2 - b) & ~rx_below(zl - b));
-}
-
-__device__ __forceinline__ uint32_t rx_masked(uint4 v, int lo, int hi, int zl) {
-  v.x &= rx_dmask(lo, hi, zl, 0);
-  v.y &= rx_dmask(lo, hi, zl, 1);
-  v.z &= rx_dmask(lo, hi, zl, 2);
-  v.w &= rx_dmask(lo, hi, zl, 3);
-  return rx_wsum4(v);
-}
-
-// One chunk's contribution: its bytes inside [a, b) minus the field at z,
-// where r is the chunk's offset from the IP packet's first byte.
-__device__ __forceinline__ uint32_t rx_chunk(const uint4 v, int r, int a, int b, int z) {
-  const int lo = a - r, hi = b - r, zl = z - r;
-  const bool full = (lo <= 0) & (hi >= 16) & ((zl >= 16) | (zl <= -2));
-  if (full) return rx_wsum4(v);
-  if ((hi <= 0) | (lo >= 16)) return 0u;
-  return rx_masked(v, lo, hi, zl);
-}
-
-// The W sum of LDS bytes [a, a + len) (4-B-aligned row, len <= 4 * MAXD - 3).
+// The W sum of row bytes [x, y) of a packet's LDS row (x even; y may be
+// odd): dwords with halfword masks, the odd last byte on its own.  Every
+// range the receive path sums from the row starts at an even offset, so a
+// boundary never splits a halfword except at an odd end.
 template <int MAXD>
-__device__ __forceinline__ uint32_t rx_lds_wsum(const uint8_t* row, uint32_t a, uint32_t len) {
+__device__ __forceinline__ uint32_t rx_row_wsum(const uint8_t* row, uint32_t x, uint32_t y) {
   const uint32_t* D = reinterpret_cast<const uint32_t*>(row);
-  const uint32_t d0 = a >> 2;
-  const uint32_t nd = ((a + len + 3) >> 2) - d0;
+  const uint32_t ye = y & ~1u;
+  const uint32_t len = ye > x ? ye - x : 0u;
+  const uint32_t d0 = x >> 2;
+  const uint32_t nd = len ? ((ye + 3) >> 2) - d0 : 0u;
   uint32_t w = 0;
 #pragma unroll
   for (int k = 0; k < MAXD; ++k) {
     if ((uint32_t)k < nd) {
-      const int b = (int)(4 * (d0 + k));
-      w = __builtin_amdgcn_sad_u16(D[d0 + k] & rx_below((int)(a + len) - b) & ~rx_below((int)a - b), 0u, w);
+      const uint32_t o = 4u * (d0 + (uint32_t)k);
+      const uint32_t m = ((o - x) < len ? 0x0000FFFFu : 0u) | ((o + 2u - x) < len ? 0xFFFF0000u : 0u);
+      w = __builtin_amdgcn_sad_u16(D[d0 + k] & m, 0u, w);
     }
   }
+  if ((y & 1u) && y > x) w += row[y - 1];  // a lone byte at an even offset: the low byte of its word
   return w;
 }
 
@@ -155,53 +138,52 @@ __global__ __launch_bounds__(256) void rx_ring(RxGeo g) {
   const uint32_t rlen = live ? g.len[s] : 0u;
   const bool over = (uint64_t)rlen > g.stride;
   const uint32_t pre = g.frame_at + g.link;
-  const uint32_t P = (!over && rlen > pre) ? rlen - pre : 0u;       // Data.Size()
-  const uint32_t Pl = P < kMaxIp ? P : kMaxIp;                       // bytes any header can cover
-  const uint64_t pa = g.ring + s * g.stride + pre;                   // the IP packet's first byte
-  const uint64_t l0 = pa >> 7;
-  const uint32_t nl = Pl ? (uint32_t)(((pa + Pl - 1) >> 7) - l0 + 1) : 0u;  // its HBM lines
+  const uint32_t P = (!over && rlen > pre) ? rlen - pre : 0u;  // Data.Size()
+  const uint32_t Pl = P < kMaxIp ? P : kMaxIp;                  // bytes any header can cover
+  const uint64_t slot = g.ring + s * g.stride;
+  uint32_t etype = 0;  // issued before the payload loads: waiting for it waits for nothing else
+  if (g.link && P) {
+    const uint32_t e = *reinterpret_cast<const uint16_t*>((uintptr_t)(slot + g.frame_at + 12));
+    etype = ((e & 0xFFu) << 8) | (e >> 8);
+  }
 
-  // One buffer resource over the wave's slots (< 8 strides + a line).
+  // Wave-relative 32-bit coordinates: one buffer resource from the 128-B
+  // line of the wave's first packet over its slots (< 8 strides + a line).
   const uint64_t wbase = (g.ring + s0 * g.stride + pre) & ~127ull;
   const uint64_t s_end = s0 + kPerWave < g.n ? s0 + kPerWave : g.n;
   const uint32_t nrec = (uint32_t)(g.ring + s_end * g.stride - wbase);
   const __amdgpu_buffer_rsrc_t rsrc = rx_srd(wbase, nrec);
-  const uint64_t pe = pa + Pl;
-  // chunk li of line k: loaded only where it holds packet bytes, else the
-  // range check returns zeros without touching memory
-  auto off_of = [&](uint32_t k) -> uint32_t {
-    const uint64_t c = ((l0 + k) << 7) + 16u * li;
-    return (k < nl && c + 16 > pa && c < pe) ? (uint32_t)(c - wbase) : nrec;
-  };
+  const uint32_t pa = (uint32_t)(slot + pre - wbase);  // the IP packet's first byte
+  const uint32_t po = pa & 15u;                         // its offset in its 16-B chunk (even)
+  const uint32_t cl = (pa & ~127u) + 16u * li;          // lane li's chunk of line 0
+  // chunk at o: loaded only where it holds packet bytes, else the range
+  // check returns zeros without touching memory
+  const uint32_t lim = Pl ? Pl + 15u : 0u;
+  auto off_of = [&](uint32_t o) -> uint32_t { return (o + 15u - pa) < lim ? o : nrec; };
 
   uint4 v[NB];
-  v[0] = rx_load<0>(rsrc, off_of(0));
+  v[0] = rx_load<0>(rsrc, off_of(cl));
 #pragma unroll
-  for (int k = 1; k < NB; ++k) v[k] = rx_load<2>(rsrc, off_of((uint32_t)k));
-  uint32_t etype = 0;
-  if (g.link && P) {
-    const uint8_t* e = reinterpret_cast<const uint8_t*>((uintptr_t)(g.ring + s * g.stride + g.frame_at + 12));
-    etype = ((uint32_t)e[0] << 8) | e[1];
-  }
+  for (int k = 1; k < NB; ++k) v[k] = rx_load<2>(rsrc, off_of(cl + 128u * k));
 
-  // The first 96 B from floor16(pa) into the group's LDS row.
+  // The first 96 B from the packet's 16-B chunk into the group's LDS row.
   uint8_t* row = reinterpret_cast<uint8_t*>(rx_lds) + (wv * kPerWave + grp) * kRowBytes;
-  const uint64_t f16 = pa & ~15ull;
+  const uint32_t f16 = pa & ~15u;
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
-    const uint64_t c = ((l0 + k) << 7) + 16u * li;
-    if (c >= f16 && c < f16 + kRowBytes) *reinterpret_cast<uint4*>(row + (c - f16)) = v[k];
+    const uint32_t o = cl + 128u * k - f16;
+    if (o < kRowBytes) *reinterpret_cast<uint4*>(row + o) = v[k];
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 
   // Parse (every lane of the group, same LDS bytes).  h(i) = IP byte i.
-  const uint32_t po = (uint32_t)(pa & 15u);
   auto h = [&](uint32_t i) -> uint32_t { return row[po + i]; };
   const uint32_t first = g.view0 && g.view0 < P ? g.view0 : P;  // the first view's length
-  uint32_t verdict = kMalformed, net = 0, init = 0, want = 0, kind = 0;
-  int a = 0, b = 0, z = -64;  // sum [a, b) but [z, z + 2) as zeros
+  uint32_t verdict = kMalformed, want = 0, kind = 0, hlen = 0, asz = 0, tsize = 0, proto = 0;
+  uint32_t a = 0, b = 0;  // the transport range [a, b); ICMP: its field [a + 2, a + 4) read as zero
+  bool v4 = false;
   do {
     if (P == 0) break;
     const uint32_t ver = h(0) >> 4;
@@ -210,13 +192,14 @@ __global__ __launch_bounds__(256) void rx_ring(RxGeo g) {
       verdict = kUnchecked;
       break;
     }
-    uint32_t proto, asum, tend, tb;
+    uint32_t tend;
     if (np == 4) {
       if (first < 20) break;
-      const uint32_t hlen = (h(0) & 15u) * 4u, tlen = (h(2) << 8) | h(3);
+      hlen = (h(0) & 15u) * 4u;
+      const uint32_t tlen = (h(2) << 8) | h(3);
       // hlen > first is not in IsValid (tests/golden/rx_choices.json)
       if (hlen < 20 || hlen > tlen || tlen > P || hlen > first || ver != 4) break;
-      net = rx_class(rx_lds_wsum<16>(row, po, hlen));  // IPv4.CalculateChecksum (ipv4.go:251-253)
+      v4 = true;  // IPv4.CalculateChecksum (ipv4.go:251-253) is reported from here on
       const uint32_t more = h(6) & 0x20u;
       const uint32_t foff = ((((h(6) & 0x1Fu) << 8) | h(7)) << 3) & 0xFFFFu;
       if (more || foff) {  // ipv4.go:355-385
@@ -225,86 +208,117 @@ __global__ __launch_bounds__(256) void rx_ring(RxGeo g) {
         break;
       }
       proto = h(9);
-      asum = rx_class(rx_lds_wsum<3>(row, po + 12, 8));
-      tb = hlen;
+      a = hlen;
       tend = tlen;
+      asz = 8;
     } else if (np == 6) {
       if (first < 40) break;
       const uint32_t plen = (h(4) << 8) | h(5);
       if (plen > P - 40 || ver != 6) break;
       proto = h(6);
-      asum = rx_class(rx_lds_wsum<9>(row, po + 8, 32));
-      tb = 40;
+      a = 40;
       tend = 40 + plen;
+      asz = 32;
     } else {
       break;  // a headerless link drops other versions
     }
-    const uint32_t tsize = tend - tb;
-    const uint32_t tfl = (first < tend ? first : tend) - tb;  // the transport's first view
+    tsize = tend - a;
+    const uint32_t tfl = (first < tend ? first : tend) - a;  // the transport's first view
     verdict = kUnchecked;
     if (proto == 6) {  // segment.parse (segment.go:160-180)
-      const uint32_t off = (h(tb + 12) >> 4) * 4u;
+      const uint32_t off = (h(a + 12) >> 4) * 4u;
       if (tfl < 20 || off < 20 || off > tfl) {
         verdict = kMalformed;
         break;
       }
       kind = 1;
-      init = rx_fold(asum + (tsize & 0xFFFFu) + 6u);  // PseudoHeaderChecksum (checksum.go:112-122)
     } else if (proto == 1 && np == 4) {  // handleICMP: echo requests only
       if (tfl < 8) {
         verdict = kMalformed;
         break;
       }
-      if (h(tb) != 8) break;
+      if (h(a) != 8) break;
       kind = 2;
-      want = (h(tb + 2) << 8) | h(tb + 3);
-      z = (int)tb + 2;
+      want = (h(a + 2) << 8) | h(a + 3);
     } else if (proto == 58 && np == 6) {  // ICMPv6Checksum
       if (tfl < 4) {
         verdict = kMalformed;
         break;
       }
       kind = 3;
-      want = (h(tb + 2) << 8) | h(tb + 3);
-      z = (int)tb + 2;
-      init = rx_fold(asum + tsize + 58u);
+      want = (h(a + 2) << 8) | h(a + 3);
     } else {
       break;
     }
-    a = (int)tb;
-    b = (int)tend;
+    b = tend;
   } while (false);
 
-  // The transport range, masked chunk by chunk.
-  uint32_t w = 0;
-  const int r0 = (int)((int64_t)((l0 << 7) + 16u * li) - (int64_t)pa);  // chunk offset of line 0
+  // The transport range splits at 16-B chunk boundaries (offsets r with
+  // (r + po) % 16 == 0) into a head [hx, min(b, A)) summed from the LDS row
+  // (after the ICMP field), whole chunks [A, B) summed from the registers, and
+  // a tail [B, b) re-read by one lane.
+  const uint32_t hs = kind == 0 ? 0u : kind == 1 ? a : a + 4u;
+  const uint32_t A = ((hs + po + 15u) & ~15u) - po, B = ((b + po) & ~15u) - po;
+  const uint32_t span = kind && B > A ? B - A : 0u;
+  // lanes 0, 1, 2: the IPv4 header, the pseudo-header's addresses, the head
+  uint32_t x = 0, y = 0;
+  if (li == 0 && v4) {
+    x = po;
+    y = po + hlen;
+  } else if (li == 1 && kind) {
+    x = po + (asz == 8 ? 12u : 8u);
+    y = x + asz;
+  } else if (li == 2 && kind) {
+    x = po + hs;
+    y = po + (b < A ? b : A);
+  }
+  uint32_t tail = 0;
+  if (li == 3 && kind && b > B && B >= A) {  // bytes [B, b): one 16-B chunk, an L2 hit
+    const uint4 t = *reinterpret_cast<const uint4*>((uintptr_t)(wbase + pa + B));
+    const int c = (int)(b - B);
+    tail = rx_wsum4(make_uint4(t.x & rx_below(c), t.y & rx_below(c - 4), t.z & rx_below(c - 8),
+                               t.w & rx_below(c - 12)));
+  }
+  uint32_t rs = rx_row_wsum<16>(row, x, y);
+  if (li == 2 && kind >= 2) rs += *reinterpret_cast<const uint16_t*>(row + po + a);  // ICMP bytes [a, a + 2)
+
+  // The whole chunks: chunk at o (lane li, line k) counts iff A <= o - pa < B.
+  uint32_t w = (li == 2 ? rs : 0u) + tail;
+  const uint32_t d = cl - pa - A;
 #pragma unroll
-  for (int k = 0; k < NB; ++k) w += rx_chunk(v[k], r0 + 128 * k, a, b, z);
-  for (uint32_t k0 = NB; __builtin_amdgcn_ballot_w64(k0 < nl && (int)(r0 + 128 * k0) < b) != 0; k0 += NB) {
+  for (int k = 0; k < NB; ++k) {
+    const uint32_t t = rx_wsum4(v[k]);
+    w += (d + 128u * k) < span ? t : 0u;
+  }
+  for (uint32_t k0 = NB; __builtin_amdgcn_ballot_w64((d + 128u * k0) < span) != 0; k0 += NB) {
 #pragma unroll
-    for (int k = 0; k < NB; ++k) v[k] = rx_load<2>(rsrc, off_of(k0 + k));
+    for (int k = 0; k < NB; ++k) v[k] = rx_load<2>(rsrc, off_of(cl + 128u * (k0 + k)));
 #pragma unroll
-    for (int k = 0; k < NB; ++k) w += rx_chunk(v[k], r0 + 128 * (int)(k0 + k), a, b, z);
+    for (int k = 0; k < NB; ++k) {
+      const uint32_t t = rx_wsum4(v[k]);
+      w += (d + 128u * (k0 + k)) < span ? t : 0u;
+    }
   }
   w += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)w, 0xB1, 0xF, 0xF, false);   // quad_perm 1,0,3,2
   w += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)w, 0x4E, 0xF, 0xF, false);   // quad_perm 2,3,0,1
   w += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)w, 0x141, 0xF, 0xF, false);  // row_half_mirror
+  const uint32_t addr = (uint32_t)__builtin_amdgcn_mov_dpp((int)rs, 0x55, 0xF, 0xF, false);  // lane 1's
 
   if (li == 0 && live) {
     uint32_t tr = 0;
-    if (kind == 1) {  // xsum == 0xffff (segment.go:180)
-      tr = rx_fold(init + rx_class(w));
+    if (kind == 1) {  // PseudoHeaderChecksum (checksum.go:112-122), then xsum == 0xffff (segment.go:180)
+      tr = rx_fold(rx_fold(rx_class(addr) + (tsize & 0xFFFFu) + 6u) + rx_class(w));
       verdict = tr == 0xFFFFu ? kValid : kInvalid;
     } else if (kind == 2) {  // ^ChecksumVV(data with the field zeroed) == the field (icmp.go:72-80)
       tr = rx_class(w);
       verdict = (~tr & 0xFFFFu) == want ? kValid : kInvalid;
     } else if (kind == 3) {  // ICMPv6Checksum == the field (ipv6/icmp.go:76-84)
-      tr = rx_fold(init + rx_class(w));
+      tr = rx_fold(rx_fold(rx_class(addr) + tsize + 58u) + rx_class(w));
       verdict = (~tr & 0xFFFFu) == want ? kValid : kInvalid;
     }
     if (g.verdict) g.verdict[s] = (uint8_t)verdict;
     if (g.sums) {
-      g.sums[2 * s] = (uint16_t)net;
+      g.sums[2 * s] = (uint16_t)(v4 ? rx_class(rs) : 0u);
       g.sums[2 * s + 1] = (uint16_t)tr;
     }
     if (over) atomicAdd(g.err, 1ull);

@@ -234,3 +234,231 @@ uint64_t oracle_send_tcp_batch(uint8_t* arena, uint64_t hdr_off, uint64_t pay_of
   }
   return n;
 }
+
+/* ---- the receive path over a ring of recvmmsg slots ----------------------
+ * One slot as the reference handles it, call for call:
+ *   recvMMsgDispatcher.dispatch (link/fdbased/packet_dispatchers.go:258-317):
+ *     views = BufConfig buffers (:30; the first of first_view bytes, 0: one
+ *     view) capped to the frame (capViews :214-224); n <= hdrSize: dropped;
+ *     protocol by EtherType, or by the version nibble without a link header
+ *     (:283-296); Data.TrimFront(hdrSize) (:304).
+ *   IPv4 HandlePacket (network/ipv4/ipv4.go:341-394), IsValid (header/
+ *     ipv4.go:280-296); IPv6 HandlePacket (network/ipv6/ipv6.go:168-188),
+ *     IsValid (header/ipv6.go:207-222).
+ *   segment.parse (transport/tcp/segment.go:145-181); handleICMP (network/
+ *     ipv4/icmp.go:60-80, network/ipv6/icmp.go:62-84, header/icmpv6.go:
+ *     202-221).
+ * Verdicts and sums as oracle/packets.py verify (0 invalid, 1 valid,
+ * 2 unchecked, 3 malformed). */
+typedef struct {
+  const uint8_t* p;
+  uint64_t n;
+} o_view;
+typedef struct {
+  o_view v[16];
+  uint32_t k;
+} o_vv;
+
+static uint64_t ovv_size(const o_vv* vv) {
+  uint64_t s = 0;
+  for (uint32_t i = 0; i < vv->k; i++) s += vv->v[i].n;
+  return s;
+}
+
+/* VectorisedView.TrimFront (tcpip/buffer/view.go:69-79) */
+static void ovv_trim_front(o_vv* vv, uint64_t count) {
+  while (count > 0 && vv->k > 0) {
+    if (count < vv->v[0].n) {
+      vv->v[0].p += count;
+      vv->v[0].n -= count;
+      return;
+    }
+    count -= vv->v[0].n;
+    memmove(&vv->v[0], &vv->v[1], (vv->k - 1) * sizeof(o_view));
+    vv->k--;
+  }
+}
+
+/* VectorisedView.CapLength (view.go:82-103) */
+static void ovv_cap(o_vv* vv, uint64_t length) {
+  uint64_t left = length;
+  for (uint32_t i = 0; i < vv->k; i++) {
+    if (left == 0) {
+      vv->k = i;
+      return;
+    }
+    if (vv->v[i].n > left) vv->v[i].n = left;
+    left -= vv->v[i].n;
+  }
+}
+
+/* ChecksumVV (checksum.go:61-63) */
+static uint16_t ovv_checksum(const o_vv* vv, uint16_t initial) {
+  const uint8_t* ptrs[16];
+  uint64_t lens[16];
+  for (uint32_t i = 0; i < vv->k; i++) {
+    ptrs[i] = vv->v[i].p;
+    lens[i] = vv->v[i].n;
+  }
+  uint16_t out = initial;
+  oracle_vv_with_offset(ptrs, lens, vv->k, initial, 0, (int64_t)ovv_size(vv), &out);
+  return out;
+}
+
+static const uint32_t kBufConfig[10] = {128, 256, 256, 512, 1024, 2048, 4096, 8192, 16384, 32768};
+
+int oracle_rx_verify(const uint8_t* slot, uint64_t slot_bytes, uint64_t rlen, uint32_t frame_at,
+                     uint32_t link_hdr, uint32_t first_view, uint16_t* net_out, uint16_t* tr_out) {
+  *net_out = *tr_out = 0;
+  if (rlen > slot_bytes || rlen <= frame_at) return 3;
+  const uint8_t* f = slot + frame_at;
+  const uint64_t n = rlen - frame_at;
+  if (n <= link_hdr) return 3; /* packet_dispatchers.go:268-270 */
+  o_vv vv = {0};
+  if (first_view == 0) {
+    vv.v[0].p = f;
+    vv.v[0].n = n;
+    vv.k = 1;
+  } else {
+    uint64_t at = 0;
+    for (int i = 0; i < 10 && at < n; i++) {
+      const uint64_t sz = i ? kBufConfig[i] : first_view;
+      vv.v[vv.k].p = f + at;
+      vv.v[vv.k].n = n - at < sz ? n - at : sz;
+      vv.k++;
+      at += sz;
+    }
+  }
+  int np = -1;
+  if (link_hdr) {
+    const uint32_t et = ((uint32_t)f[12] << 8) | f[13];
+    np = et == 0x0800 ? 4 : et == 0x86DD ? 6 : 0;
+    ovv_trim_front(&vv, link_hdr);
+  }
+  const uint64_t size = n - link_hdr; /* pkt.Data.Size() */
+  if (vv.k == 0 || vv.v[0].n == 0) return 3;
+  const o_view first = vv.v[0];
+  const int ver = first.p[0] >> 4;
+  if (np == 0) return 2; /* not IP: nothing the reference checksums */
+  if (np > 0 && ver != np) return 3; /* IsValid's version check */
+  const uint8_t *src, *dst;
+  uint32_t alen, proto;
+  uint16_t net = 0;
+  if (ver == 4) {
+    if (first.n < 20) return 3;
+    const uint32_t hlen = (first.p[0] & 0xFu) * 4u, tlen = ((uint32_t)first.p[2] << 8) | first.p[3];
+    /* hlen > len(first): not in IsValid; MALFORMED here */
+    if (hlen < 20 || hlen > tlen || tlen > size || hlen > first.n) return 3;
+    net = oracle_checksum(first.p, hlen, 0); /* IPv4.CalculateChecksum, reported only */
+    *net_out = net;
+    src = first.p + 12;
+    dst = first.p + 16;
+    alen = 4;
+    proto = first.p[9];
+    const int more = (first.p[6] & 0x20) != 0;
+    const uint16_t foff = (uint16_t)(((((uint32_t)first.p[6] & 0x1Fu) << 8) | first.p[7]) << 3);
+    ovv_trim_front(&vv, hlen);
+    ovv_cap(&vv, tlen - hlen);
+    if (more || foff) { /* ipv4.go:355-385 */
+      const uint64_t ts = ovv_size(&vv);
+      if (ts == 0) return 3;
+      const uint16_t last = (uint16_t)(foff + (uint16_t)ts - 1);
+      return last < foff ? 3 : 2;
+    }
+  } else if (ver == 6) {
+    if (first.n < 40) return 3;
+    const uint32_t plen = ((uint32_t)first.p[4] << 8) | first.p[5];
+    if ((uint64_t)plen > size - 40) return 3;
+    src = first.p + 8;
+    dst = first.p + 24;
+    alen = 16;
+    proto = first.p[6];
+    ovv_trim_front(&vv, 40);
+    ovv_cap(&vv, plen);
+  } else {
+    return 3;
+  }
+  const o_view tfirst = vv.k ? vv.v[0] : (o_view){NULL, 0};
+  if (proto == 6) { /* segment.parse */
+    if (tfirst.n < 20) return 3;
+    const uint32_t off = (uint32_t)(tfirst.p[12] >> 4) * 4u;
+    if (off < 20 || off > tfirst.n) return 3;
+    uint16_t xsum = oracle_pseudo_header(6, src, alen, dst, alen, (uint16_t)ovv_size(&vv));
+    xsum = oracle_checksum(tfirst.p, off, xsum);
+    ovv_trim_front(&vv, off);
+    xsum = ovv_checksum(&vv, xsum);
+    *tr_out = xsum;
+    return xsum == 0xFFFF ? 1 : 0;
+  }
+  if (proto == 1 && ver == 4) { /* handleICMP, echo requests */
+    if (tfirst.n < 8) return 3;
+    if (tfirst.p[0] != 8) return 2;
+    const uint16_t want = (uint16_t)(((uint32_t)tfirst.p[2] << 8) | tfirst.p[3]);
+    uint8_t* h = (uint8_t*)malloc(tfirst.n);
+    memcpy(h, tfirst.p, tfirst.n);
+    h[2] = h[3] = 0; /* h.SetChecksum(0) */
+    vv.v[0].p = h;
+    const uint16_t s = ovv_checksum(&vv, 0);
+    free(h);
+    *tr_out = s;
+    return (uint16_t)~s == want ? 1 : 0;
+  }
+  if (proto == 58 && ver == 6) { /* ICMPv6Checksum(h, src, dst, the other views) */
+    if (tfirst.n < 4) return 3;
+    const uint16_t want = (uint16_t)(((uint32_t)tfirst.p[2] << 8) | tfirst.p[3]);
+    const uint64_t total = ovv_size(&vv);
+    uint16_t xsum = oracle_checksum(src, 16, 0);
+    xsum = oracle_checksum(dst, 16, xsum);
+    const uint8_t l4[4] = {(uint8_t)(total >> 24), (uint8_t)(total >> 16), (uint8_t)(total >> 8), (uint8_t)total};
+    xsum = oracle_checksum(l4, 4, xsum);
+    const uint8_t nh[4] = {0, 0, 0, 58};
+    xsum = oracle_checksum(nh, 4, xsum);
+    for (uint32_t i = 1; i < vv.k; i++) xsum = oracle_checksum(vv.v[i].p, vv.v[i].n, xsum);
+    uint8_t* h = (uint8_t*)malloc(tfirst.n);
+    memcpy(h, tfirst.p, tfirst.n);
+    h[2] = h[3] = 0;
+    const uint16_t got = (uint16_t)~oracle_checksum(h, tfirst.n, xsum);
+    free(h);
+    *tr_out = (uint16_t)~got;
+    return got == want ? 1 : 0;
+  }
+  return 2;
+}
+
+typedef struct {
+  const uint8_t* ring;
+  uint64_t stride;
+  const uint32_t* lens;
+  uint32_t frame_at, link_hdr, first_view;
+  uint8_t* verdict;
+  uint16_t* sums;
+  uint32_t lo, hi;
+} rx_job;
+
+static void* rx_worker(void* p) {
+  rx_job* j = (rx_job*)p;
+  for (uint32_t s = j->lo; s < j->hi; s++) {
+    uint16_t net, tr;
+    j->verdict[s] = (uint8_t)oracle_rx_verify(j->ring + (uint64_t)s * j->stride, j->stride, j->lens[s], j->frame_at,
+                                              j->link_hdr, j->first_view, &net, &tr);
+    j->sums[2 * (uint64_t)s] = net;
+    j->sums[2 * (uint64_t)s + 1] = tr;
+  }
+  return NULL;
+}
+
+int oracle_rx_ring(const uint8_t* ring, uint64_t stride, uint32_t n, const uint32_t* lens, uint32_t frame_at,
+                   uint32_t link_hdr, uint32_t first_view, uint8_t* verdict, uint16_t* sums, int nthreads) {
+  if (nthreads < 1) nthreads = 1;
+  if (nthreads > 256) nthreads = 256;
+  pthread_t th[256];
+  rx_job jobs[256];
+  for (int t = 0; t < nthreads; t++) {
+    jobs[t] = (rx_job){ring, stride, lens, frame_at, link_hdr, first_view, verdict, sums,
+                       (uint32_t)(((uint64_t)n * t) / nthreads), (uint32_t)(((uint64_t)n * (t + 1)) / nthreads)};
+  }
+  for (int t = 1; t < nthreads; t++) pthread_create(&th[t], NULL, rx_worker, &jobs[t]);
+  rx_worker(&jobs[0]);
+  for (int t = 1; t < nthreads; t++) pthread_join(th[t], NULL);
+  return 0;
+}

@@ -43,6 +43,15 @@ uint64_t oracle_send_tcp_batch(uint8_t* arena, uint64_t hdr_off, uint64_t pay_of
                                const uint8_t* dst, uint32_t dst_len, int mode,
                                uint16_t* out);
 
+/* The receive path of one recvmmsg slot (link dispatch, IPv4/IPv6
+ * HandlePacket, segment.parse, handleICMP): returns the verdict (0 invalid,
+ * 1 valid, 2 unchecked, 3 malformed) and the IPv4 / transport sums. */
+int oracle_rx_verify(const uint8_t* slot, uint64_t slot_bytes, uint64_t rlen, uint32_t frame_at,
+                     uint32_t link_hdr, uint32_t first_view, uint16_t* net_out, uint16_t* tr_out);
+/* ... over n slots of `stride` bytes from `ring`, slot-parallel over nthreads. */
+int oracle_rx_ring(const uint8_t* ring, uint64_t stride, uint32_t n, const uint32_t* lens, uint32_t frame_at,
+                   uint32_t link_hdr, uint32_t first_view, uint8_t* verdict, uint16_t* sums, int nthreads);
+
 #ifdef __cplusplus
 }
 #endif

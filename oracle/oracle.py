@@ -203,6 +203,8 @@ class _C:
             lib.oracle_send_tcp_batch.restype = u64
             lib.oracle_send_tcp_batch.argtypes = [u8p, u64, u64, u64, u32, u32, u32, u32, u32, u32, u32,
                                                   u8p, u32, u8p, u32, ctypes.c_int, u8p]
+            lib.oracle_rx_ring.restype = ctypes.c_int
+            lib.oracle_rx_ring.argtypes = [u8p, u64, u32, u8p, u32, u32, u32, u8p, u8p, ctypes.c_int]
             cls._lib = lib
         return cls._lib
 
@@ -305,6 +307,20 @@ def c_send_tcp_batch(arena: np.ndarray, hdr_off: int, pay_off: int, size: int, m
                             protocol, _ptr(s), len(src), _ptr(d), len(dst),
                             {"full": 0, "partial": 1, "none": 2}[mode], _ptr(out))
     return a, out[:2 * n]
+
+
+def c_rx_ring(arena: np.ndarray, lens: np.ndarray, stride: int, n: int, ring_off: int = 0, frame_at: int = 0,
+              link_hdr: int = 0, first_view: int = 0, nthreads: int = 1) -> tuple[np.ndarray, np.ndarray]:
+    """The receive path of n recvmmsg slots (oracle_rx_ring, the C
+    restatement of oracle/packets.py verify_frame): (verdicts, 2n sums)."""
+    assert arena.dtype == np.uint8 and arena.flags["C_CONTIGUOUS"]
+    assert ring_off + n * stride <= arena.size
+    ln = np.ascontiguousarray(lens[:n], dtype=np.uint32)
+    verdict = np.zeros(max(n, 1), dtype=np.uint8)
+    sums = np.zeros(2 * max(n, 1), dtype=np.uint16)
+    _C.lib().oracle_rx_ring(_ptr(arena) + ring_off, stride, n, _ptr(ln), frame_at, link_hdr, first_view,
+                            _ptr(verdict), _ptr(sums), int(nthreads))
+    return verdict[:n], sums[:2 * n]
 
 
 def c_batch_mt(arena: np.ndarray, desc: np.ndarray, nthreads: int, out: np.ndarray | None = None) -> np.ndarray:
