@@ -229,12 +229,18 @@ struct StreamScratch : nsh::ScratchSlot {
   ChainBuf chain;
   DevBuf<uint32_t> split;  // csum_split accumulators (zero between launches)
   DevBuf<uint16_t> txpay;  // ns_csum_tcp_tx: per-segment payload values between its passes
-  // ns_csum_tcp_tx_multi: the calls' table on the device, its pinned host
-  // copy, and the event after which that copy may be rewritten
+  // ns_csum_tcp_tx_multi: the calls' table on the device (stream-ordered:
+  // one suffices) and a ring of pinned host copies, each with the event
+  // after which its upload has run and it may be rewritten
   DevBuf<uint8_t> txtab;
-  uint8_t* htab = nullptr;
-  size_t htab_cap = 0;
-  hipEvent_t tab_ev = nullptr;
+  struct TabSlot {
+    uint8_t* h = nullptr;
+    size_t cap = 0;
+    hipEvent_t ev = nullptr;
+  };
+  static constexpr uint32_t kTabSlots = 8;
+  TabSlot tab[kTabSlots];
+  uint32_t tab_next = 0;
   hipEvent_t last = nullptr;
   std::mutex mu;  // held while growing it and launching with it
 };
@@ -297,10 +303,19 @@ void bump_max(std::atomic<uint64_t>& m, uint64_t v) {
 struct ns_csum_ctx {
   int device = 0;
   uint64_t staging = kDefaultStaging;
+  // The host-batch DMA pipeline (ns_csum_batch_host, gathers above
+  // kZeroCopyMax): its two streams, slots and g_arena, under pmu.  It never
+  // takes mu, so a 1.5 GB host batch does not hold up the zero-copy passes
+  // of small synchronous calls (a 29 ms head-of-line block).
   hipStream_t stream[2] = {nullptr, nullptr};
   hipEvent_t done[2] = {nullptr, nullptr};
+  std::mutex pmu;
+  // Zero-copy passes and ns_csum_sync run on zstream, a stream of their own
+  // (at the greatest priority like the pipeline's: a hardware queue apart
+  // from callers' streams and from the pipeline), under mu.
+  hipStream_t zstream = nullptr;
   unsigned long long* d_err = nullptr;
-  std::mutex mu;  // guards everything below
+  std::mutex mu;  // guards everything below but the pipeline's state
 
   // device-resident API scratch, one per caller stream (allocated on first
   // use), under its own lock: growing one never holds up synchronous calls
@@ -310,6 +325,8 @@ struct ns_csum_ctx {
   // ns_csum_sync's exchanged error count (mapped: written by take_err)
   MappedPin err_taken;
   // host-path slots (double-buffered)
+  ChainBuf z_chain;  // a chained zero-copy pass's scratch
+  // host-path slots (double-buffered; pmu)
   DevBuf<uint8_t> d_arena[2];
   DevBuf<ns_pkt_desc> d_desc[2];
   DevBuf<uint16_t> d_out[2];
@@ -337,7 +354,7 @@ struct ns_csum_ctx {
   std::vector<MappedPin*> stage_all;
   std::vector<MappedPin*> big_free;  // pooled caller stages above kStageBytes
   std::vector<MappedPin*> leased;    // stages a caller holds (ns_csum_stage_acquire)
-  // gather staging for the VectorisedView entry points
+  // gather staging for the VectorisedView entry points above kZeroCopyMax (pmu)
   PinBuf<uint8_t> g_arena;
   std::vector<ns_pkt_desc> g_desc;
   StatCounters st;
@@ -368,11 +385,11 @@ void retire_scratch(ns_csum_ctx* ctx, StreamScratch* sc) {
     sc->txpay.release();
     sc->txtab.release();
   }
-  if (sc->htab) {  // host memory: free once its last copy has run
-    if (sc->tab_ev) (void)hipEventSynchronize(sc->tab_ev);
-    (void)hipHostFree(sc->htab);
+  for (StreamScratch::TabSlot& t : sc->tab) {  // host memory: free once its last copy has run
+    if (t.ev) (void)hipEventSynchronize(t.ev);
+    if (t.h) (void)hipHostFree(t.h);
+    if (t.ev) (void)hipEventDestroy(t.ev);
   }
-  if (sc->tab_ev) (void)hipEventDestroy(sc->tab_ev);
   (void)hipEventDestroy(sc->last);
   delete sc;
   ctx->st.retires.fetch_add(1, std::memory_order_relaxed);
@@ -480,7 +497,7 @@ int run_zero_copy(ns_csum_ctx* ctx, SmallReq* const* reqs, size_t nreq) {
     if ((rc = ctx->z_done.ensure(64)) != NS_OK) return rc;
     __atomic_store_n(reinterpret_cast<uint32_t*>(ctx->z_done.p), 0u, __ATOMIC_RELEASE);
   }
-  if (chained && (rc = ctx->d_chain[0].ensure(nd)) != NS_OK) return rc;
+  if (chained && (rc = ctx->z_chain.ensure(nd)) != NS_OK) return rc;
   if ((rc = ctx->z_ctr.ensure(1, true)) != NS_OK) return rc;
   uint8_t* z = ctx->z_buf.p;
   ns_pkt_desc* zd = reinterpret_cast<ns_pkt_desc*>(z);
@@ -506,7 +523,7 @@ int run_zero_copy(ns_csum_ctx* ctx, SmallReq* const* reqs, size_t nreq) {
   }
   // BAR writes are write-combined: drain them before the launch's doorbell.
   __builtin_ia32_sfence();
-  hipStream_t s = ctx->stream[0];
+  hipStream_t s = ctx->zstream;
   // Completion: the pass's sequence number lands in coherent host memory once
   // every result is there — stored by the checksum launch's last workgroup
   // (unchained passes: the results are written through, nsk::ZcSignal) or by
@@ -524,7 +541,7 @@ int run_zero_copy(ns_csum_ctx* ctx, SmallReq* const* reqs, size_t nreq) {
   if (self) zc = nsk::ZcSignal{ctx->z_ctr.p, done_dev, seq};
   HIP_TRY(nsk::launch_batch(nullptr, kWholeSpace, ctx->z_buf.dev, (uint32_t)nd,
                             reinterpret_cast<uint16_t*>(ctx->z_res.dev),
-                            chained ? ctx->d_chain[0].get() : nsk::ChainScratch{}, ctx->d_err, s,
+                            chained ? ctx->z_chain.get() : nsk::ChainScratch{}, ctx->d_err, s,
                             std::max<uint64_t>(nb, 1), 0, nullptr, zc));
   if (!self) HIP_TRY(nsk::launch_signal(done_dev, seq, s));
   ctx->st.zc_passes.fetch_add(1, std::memory_order_relaxed);
@@ -655,7 +672,7 @@ int submit_small(ns_csum_ctx* ctx, SmallReq* req) {
   });
 }
 
-// Host batch core, caller holds ctx->mu and the device guard.  Pipelines
+// Host batch core, caller holds ctx->pmu and the device guard.  Pipelines
 // chunks of the descriptor table over the two slots/streams: H2D of chunk k+1
 // overlaps the kernel of chunk k.  Chunks never split a NS_DESC_CONT run.
 // Descriptors per host-pipeline chunk (cfg3, 1M x 64 B: 64K 3.11 ms, 128K
@@ -836,7 +853,7 @@ struct SpanProbe {
 // Where a gather assembles its bytes.  Small gathers go to a mapped staging
 // buffer leased from the context's pool (the kernel reads it in place).  A
 // gather that outgrows it moves, under the context lock it then keeps until
-// the call ends, into the context's pinned arena `g_arena` (grown by doubling
+// the call ends, into the pipeline's pinned arena `g_arena` (grown by doubling
 // and kept between calls) and takes the DMA pipeline: one CPU copy per byte
 // either way (a 64 MiB VectorisedView batch went from 31 ms through a
 // growing std::vector to a few ms; tools/latency.cc).  A gather whose bytes
@@ -846,7 +863,7 @@ struct ByteSink {
   ns_csum_ctx* ctx;
   BarBuf* stage = nullptr;       // leased from the pool (copy mode)
   MappedPin* adopted = nullptr;  // the caller's acquired stage (adopt mode)
-  std::unique_lock<std::mutex> big;  // held once the bytes live in ctx->g_arena
+  std::unique_lock<std::mutex> big;  // ctx->pmu, held once the bytes live in ctx->g_arena
   uint64_t n = 0;  // copy: bytes appended; adopt: end of the highest byte used
   int rc = NS_OK;
   // the pieces copied into the stage so far: a move to g_arena copies them
@@ -893,9 +910,9 @@ struct ByteSink {
     stage = nb;
     return NS_OK;
   }
-  // Move to g_arena (taking the context lock) with room for `need` bytes.
+  // Move to g_arena (taking the pipeline lock) with room for `need` bytes.
   int to_big(uint64_t need) {
-    big = std::unique_lock<std::mutex>(ctx->mu);
+    big = std::unique_lock<std::mutex>(ctx->pmu);
     const int r = reserve_big(std::max<uint64_t>(need, 1ull << 20), 0);
     if (r != NS_OK) return r;
     uint64_t at = 0;
@@ -943,7 +960,7 @@ struct Gather : SinkHolder, nsh::ChainBuilder<ByteSink> {  // the sink is constr
     const bool chained = any_cont(desc.data(), (uint32_t)desc.size());
     if (sink.adopted && !(zero_copy_enabled() && sink.size() <= kStageBytes)) {
       // A large caller stage: pinned already, so the DMA pipeline reads it.
-      std::lock_guard<std::mutex> lk(ctx->mu);
+      std::lock_guard<std::mutex> lk(ctx->pmu);
       DeviceGuard g(ctx->device);
       rc = run_host_batch(ctx, sink.base(), sink.size(), desc.data(), (uint32_t)desc.size(), res.data(), chained);
     } else if (!sink.in_big()) {
@@ -958,7 +975,7 @@ struct Gather : SinkHolder, nsh::ChainBuilder<ByteSink> {  // the sink is constr
       rq.chained = chained;
       rc = submit_small(ctx, &rq);
     } else {
-      // Large: the bytes are in the pinned g_arena and ctx->mu is held.
+      // Large: the bytes are in the pinned g_arena and ctx->pmu is held.
       DeviceGuard g(ctx->device);
       rc = run_host_batch(ctx, ctx->g_arena.p, sink.size(), desc.data(), (uint32_t)desc.size(), res.data(),
                           chained);
@@ -1037,6 +1054,7 @@ int ns_csum_init(const ns_csum_opts* opts, ns_csum_ctx** out) {
     e = hipStreamCreateWithPriority(&ctx->stream[s], hipStreamNonBlocking, greatest);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->done[s], hipEventDisableTiming);
   }
+  if (e == hipSuccess) e = hipStreamCreateWithPriority(&ctx->zstream, hipStreamNonBlocking, greatest);
   if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&ctx->d_err), sizeof(unsigned long long));
   if (e == hipSuccess) e = hipMemset(ctx->d_err, 0, sizeof(unsigned long long));
   if (e != hipSuccess) {
@@ -1076,6 +1094,7 @@ void ns_csum_destroy(ns_csum_ctx* ctx) {
     DeviceGuard g(ctx->device);
     for (int s = 0; s < 2; ++s)
       if (ctx->stream[s]) (void)hipStreamSynchronize(ctx->stream[s]);
+    if (ctx->zstream) (void)hipStreamSynchronize(ctx->zstream);
     ctx->scratch.clear([&](StreamScratch* sc) { retire_scratch(ctx, sc); });
     if (ctx->retire) {
       (void)hipStreamSynchronize(ctx->retire);
@@ -1109,6 +1128,8 @@ void ns_csum_destroy(ns_csum_ctx* ctx) {
       if (ctx->stream[s]) (void)hipStreamDestroy(ctx->stream[s]);
     }
     ctx->g_arena.release();
+    ctx->z_chain.release();
+    if (ctx->zstream) (void)hipStreamDestroy(ctx->zstream);
     if (ctx->d_err) (void)hipFree(ctx->d_err);
   }
   delete ctx;
@@ -1129,8 +1150,8 @@ int ns_csum_sync(ns_csum_ctx* ctx, void* stream, uint64_t* bad) {
     std::lock_guard<std::mutex> lk(ctx->mu);
     unsigned long long* taken = reinterpret_cast<unsigned long long*>(ctx->err_taken.p);
     HIP_TRY(nsk::launch_take_err(ctx->d_err, reinterpret_cast<unsigned long long*>(ctx->err_taken.dev),
-                                 ctx->stream[0]));
-    HIP_TRY(hipStreamSynchronize(ctx->stream[0]));
+                                 ctx->zstream));
+    HIP_TRY(hipStreamSynchronize(ctx->zstream));
     v = *reinterpret_cast<volatile unsigned long long*>(taken);
   }
   if (bad) *bad = v;
@@ -1357,31 +1378,37 @@ int ns_csum_tcp_tx_multi(ns_csum_ctx* ctx, uint8_t* d_arena, uint64_t arena_byte
   {
     std::lock_guard<std::mutex> lk(sc->mu);
     rc = sc->txtab.ensure_async(bytes, false, s);
-    if (rc == NS_OK && !sc->tab_ev && hipEventCreateWithFlags(&sc->tab_ev, hipEventDisableTiming) != hipSuccess) {
-      sc->tab_ev = nullptr;
+    // The next pinned copy of the ring.  Its previous upload was enqueued
+    // kTabSlots calls ago on this stream: waiting for it here (only when the
+    // device is that far behind) is back-pressure, not a per-call stall.
+    StreamScratch::TabSlot& ts = sc->tab[sc->tab_next++ % StreamScratch::kTabSlots];
+    if (rc == NS_OK && !ts.ev && hipEventCreateWithFlags(&ts.ev, hipEventDisableTiming) != hipSuccess) {
+      ts.ev = nullptr;
       rc = NS_EHIP;
     }
     if (rc == NS_OK) {
-      // the pinned copy may still be read by this stream's previous upload
-      (void)hipEventSynchronize(sc->tab_ev);
-      if (sc->htab_cap < bytes) {
-        if (sc->htab) (void)hipHostFree(sc->htab);
-        sc->htab = nullptr;
-        sc->htab_cap = 0;
+      if (hipEventQuery(ts.ev) != hipSuccess) {
+        (void)hipGetLastError();
+        (void)hipEventSynchronize(ts.ev);
+      }
+      if (ts.cap < bytes) {
+        if (ts.h) (void)hipHostFree(ts.h);
+        ts.h = nullptr;
+        ts.cap = 0;
         const size_t cap = std::max<size_t>(bytes, 64u << 10);
-        if (hipHostMalloc(reinterpret_cast<void**>(&sc->htab), cap, hipHostMallocDefault) != hipSuccess) {
-          sc->htab = nullptr;
+        if (hipHostMalloc(reinterpret_cast<void**>(&ts.h), cap, hipHostMallocDefault) != hipSuccess) {
+          ts.h = nullptr;
           rc = NS_ENOMEM;
         } else {
-          sc->htab_cap = cap;
+          ts.cap = cap;
         }
       }
     }
     if (rc == NS_OK) {
-      std::memcpy(sc->htab, calls.data(), (size_t)nc * sizeof(nsk::TxGeo));
-      std::memcpy(sc->htab + tab, first.data(), first.size() * sizeof(uint32_t));
-      hipError_t e = hipMemcpyAsync(sc->txtab.p, sc->htab, bytes, hipMemcpyHostToDevice, s);
-      if (e == hipSuccess) e = hipEventRecord(sc->tab_ev, s);
+      std::memcpy(ts.h, calls.data(), (size_t)nc * sizeof(nsk::TxGeo));
+      std::memcpy(ts.h + tab, first.data(), first.size() * sizeof(uint32_t));
+      hipError_t e = hipMemcpyAsync(sc->txtab.p, ts.h, bytes, hipMemcpyHostToDevice, s);
+      if (e == hipSuccess) e = hipEventRecord(ts.ev, s);
       if (e == hipSuccess)
         e = nsk::launch_tcp_tx_multi(launch, grid, reinterpret_cast<const nsk::TxGeo*>(sc->txtab.p),
                                      reinterpret_cast<const uint32_t*>(sc->txtab.p + tab), nc, s);
@@ -1461,7 +1488,7 @@ int ns_csum_batch_host(ns_csum_ctx* ctx, const uint8_t* h_arena, uint64_t arena_
     return_gather_stage(ctx, st);
     return rc;
   }
-  std::lock_guard<std::mutex> lk(ctx->mu);
+  std::lock_guard<std::mutex> lk(ctx->pmu);
   DeviceGuard g(ctx->device);
   return run_host_batch(ctx, h_arena, arena_bytes, h_desc, n, h_out,
                         (batch_flags & NS_BATCH_CHAINED) != 0);

@@ -120,13 +120,16 @@ __device__ __forceinline__ uint4 rx_load(__amdgpu_buffer_rsrc_t r, uint32_t off)
 }  // namespace
 
 // NB = lines per load batch (line 0 included); a packet longer than NB lines
-// takes further batches of NB nontemporal lines.
-template <int NB>
-__global__ __launch_bounds__(256) void rx_ring(RxGeo g) {
-  __shared__ uint4 rx_lds[kWaves * kPerWave * kRowBytes / 16];
+// takes further batches of NB lines.  A0 / AN = the cache policy of line 0 /
+// of the others (0 default, 2 nontemporal), WV = waves per workgroup, OCC =
+// a waves-per-SIMD floor for the register allocator (1: none).  The product
+// runs <NB, 0, 2, 4, 1>; tools/rx_ring_variants.hip times the others.
+template <int NB, int A0 = 0, int AN = 2, int WV = kWaves, int OCC = 1>
+__global__ __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(OCC))) void rx_ring(RxGeo g) {
+  __shared__ uint4 rx_lds[WV * kPerWave * kRowBytes / 16];
   const uint32_t lane = threadIdx.x & 63u, grp = lane >> 3, li = lane & 7u;
   const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint64_t s0 = ((uint64_t)blockIdx.x * kWaves + wv) * kPerWave;  // the wave's first slot
+  const uint64_t s0 = ((uint64_t)blockIdx.x * WV + wv) * kPerWave;  // the wave's first slot
   if (s0 >= g.n) return;  // a whole wave leaves together
   const uint64_t s = s0 + grp;
   const bool live = s < g.n;
@@ -162,9 +165,9 @@ __global__ __launch_bounds__(256) void rx_ring(RxGeo g) {
   auto off_of = [&](uint32_t o) -> uint32_t { return (o + 15u - pa) < lim ? o : nrec; };
 
   uint4 v[NB];
-  v[0] = rx_load<0>(rsrc, off_of(cl));
+  v[0] = rx_load<A0>(rsrc, off_of(cl));
 #pragma unroll
-  for (int k = 1; k < NB; ++k) v[k] = rx_load<2>(rsrc, off_of(cl + 128u * k));
+  for (int k = 1; k < NB; ++k) v[k] = rx_load<AN>(rsrc, off_of(cl + 128u * k));
 
   // The first 96 B from the packet's 16-B chunk into the group's LDS row.
   uint8_t* row = reinterpret_cast<uint8_t*>(rx_lds) + (wv * kPerWave + grp) * kRowBytes;
@@ -292,7 +295,7 @@ __global__ __launch_bounds__(256) void rx_ring(RxGeo g) {
   }
   for (uint32_t k0 = NB; __builtin_amdgcn_ballot_w64((d + 128u * k0) < span) != 0; k0 += NB) {
 #pragma unroll
-    for (int k = 0; k < NB; ++k) v[k] = rx_load<2>(rsrc, off_of(cl + 128u * (k0 + k)));
+    for (int k = 0; k < NB; ++k) v[k] = rx_load<AN>(rsrc, off_of(cl + 128u * (k0 + k)));
 #pragma unroll
     for (int k = 0; k < NB; ++k) {
       const uint32_t t = rx_wsum4(v[k]);
@@ -333,18 +336,23 @@ static int rx_batch_lines(const RxGeo& g) {
   return lines <= 2 ? 2 : lines <= 4 ? 4 : lines <= 8 ? 8 : lines <= 13 ? 13 : 16;
 }
 
-hipError_t launch_rx_ring(const RxGeo& g, hipStream_t stream) {
+template <int NB, int A0 = 0, int AN = 2, int WV = kWaves, int OCC = 1>
+static hipError_t launch_rx_ring_t(const RxGeo& g, hipStream_t stream) {
   if (g.n == 0) return hipSuccess;
-  const uint64_t per_wg = (uint64_t)kWaves * kPerWave;
-  const dim3 grid((uint32_t)((g.n + per_wg - 1) / per_wg)), block(64 * kWaves);
-  switch (rx_batch_lines(g)) {
-    case 2: hipLaunchKernelGGL(rx_ring<2>, grid, block, 0, stream, g); break;
-    case 4: hipLaunchKernelGGL(rx_ring<4>, grid, block, 0, stream, g); break;
-    case 8: hipLaunchKernelGGL(rx_ring<8>, grid, block, 0, stream, g); break;
-    case 13: hipLaunchKernelGGL(rx_ring<13>, grid, block, 0, stream, g); break;
-    default: hipLaunchKernelGGL(rx_ring<16>, grid, block, 0, stream, g); break;
-  }
+  const uint64_t per_wg = (uint64_t)WV * kPerWave;
+  hipLaunchKernelGGL((rx_ring<NB, A0, AN, WV, OCC>), dim3((uint32_t)((g.n + per_wg - 1) / per_wg)), dim3(64 * WV), 0,
+                     stream, g);
   return hipGetLastError();
+}
+
+hipError_t launch_rx_ring(const RxGeo& g, hipStream_t stream) {
+  switch (rx_batch_lines(g)) {
+    case 2: return launch_rx_ring_t<2>(g, stream);
+    case 4: return launch_rx_ring_t<4>(g, stream);
+    case 8: return launch_rx_ring_t<8>(g, stream);
+    case 13: return launch_rx_ring_t<13>(g, stream);
+    default: return launch_rx_ring_t<16>(g, stream);
+  }
 }
 
 }  // namespace nsk

@@ -547,6 +547,9 @@ static void TestTxPlan(Rng& rng, int rounds) {
     if (p.mode & 6u) CHECK(t.tcp_len >= 18 && (uint32_t)t.tcp_at + t.tcp_len <= t.slot, "TCP header and field in a slot");
     if (p.mode & 2u)
       CHECK(t.pay_off >= t.hdr_off + p.n * t.slot || t.hdr_off >= t.pay_off + t.size, "payload apart from the slots");
+    if ((p.mode & 1u) && (p.mode & 6u))
+      CHECK((uint32_t)t.ip_at + t.ip_len <= t.tcp_at || (uint32_t)t.tcp_at + t.tcp_len <= t.ip_at,
+            "IPv4 and TCP headers apart");
   }
   CHECK(accepted > 0, "no geometry accepted");
   // the reference's own shape: 45 segments of a 64 KiB GSO write
@@ -560,6 +563,51 @@ static void TestTxPlan(Rng& rng, int rounds) {
   CHECK(nsh::tx_plan(t, 1 << 20, &p) == NS_EINVAL, "payload over the slots");
   t.flags = NS_TX_TCP_PARTIAL;
   CHECK(nsh::tx_plan(t, 1 << 20, &p) == NS_OK && p.mode == 5u, "CHECKSUM_PARTIAL reads no payload");
+  t.protocol = 256;  // PseudoHeaderChecksum takes uint8(protocol)
+  CHECK(nsh::tx_plan(t, 1 << 20, &p) == NS_EINVAL, "protocol above 255");
+  t.protocol = 6;
+  t.tcp_at = 30;  // TCP header over the IPv4 header's last 4 bytes
+  CHECK(nsh::tx_plan(t, 1 << 20, &p) == NS_EINVAL, "overlapping headers");
+  t.flags = NS_TX_TCP_NONE;  // no TCP field written: only the IPv4 header matters
+  CHECK(nsh::tx_plan(t, 1 << 20, &p) == NS_OK && p.mode == 1u, "overlap irrelevant under TX offload");
+}
+
+// nsh::rx_plan (ns_csum_rx_ring's geometry check): random rings.  Whatever it
+// accepts: 16-B-aligned slots of a stride below 2^24, an even IP packet start,
+// a first view the parse can rely on, and every slot inside the arena.
+static void TestRxPlan(Rng& rng, int rounds) {
+  auto pick = [&](uint64_t lo, uint64_t hi) { return lo + rng() % (hi - lo + 1); };
+  int accepted = 0;
+  for (int round = 0; round < rounds * 50; ++round) {
+    ns_rx_ring r{};
+    const uint64_t base = rng() % 4 == 0 ? pick(0, 64) : 256 * pick(0, 1000);
+    const uint64_t arena = pick(0, 1u << 24);
+    r.ring_off = rng() % 2 ? 16 * pick(0, 4096) : pick(0, 1u << 16);
+    r.stride = rng() % 8 == 0 ? pick(0, 1u << 25) : 16 * pick(0, 200);
+    r.n = (uint32_t)pick(0, 5000);
+    r.frame_at = (uint16_t)pick(0, 40);
+    r.link_hdr = (uint16_t)(rng() % 4 == 0 ? pick(0, 20) : 14 * (rng() % 2));
+    r.first_view = (uint32_t)(rng() % 2 ? 0 : pick(0, 300));
+    r.flags = rng() % 16 == 0 ? 1u : 0u;
+    const int rc = nsh::rx_plan(r, base, arena);
+    CHECK(rc == NS_OK || rc == NS_EINVAL || rc == NS_ERANGE, "rc %d", rc);
+    if (rc != NS_OK) continue;
+    ++accepted;
+    CHECK(r.stride && r.stride < (1u << 24) && r.stride % 16 == 0 && (base + r.ring_off) % 16 == 0, "slot shape");
+    CHECK((r.link_hdr == 0 || r.link_hdr == 14) && (r.frame_at + r.link_hdr) % 2 == 0 && r.frame_at < r.stride,
+          "frame placement");
+    CHECK(r.first_view == 0 || (r.first_view % 2 == 0 && r.first_view >= r.link_hdr + 64u), "first view");
+    CHECK(r.ring_off + (uint64_t)r.n * r.stride <= arena, "ring inside the arena");
+    CHECK(r.flags == 0, "flags");
+  }
+  CHECK(accepted > 0, "no ring accepted");
+  ns_rx_ring r{};
+  r.stride = 1504, r.n = 1000, r.first_view = 128, r.link_hdr = 14;
+  CHECK(nsh::rx_plan(r, 4096, 1504000) == NS_OK, "an MTU ring");
+  CHECK(nsh::rx_plan(r, 4096, 1503999) == NS_ERANGE, "one byte short");
+  CHECK(nsh::rx_plan(r, 4104, 1504000) == NS_EINVAL, "8-B-aligned arena");
+  r.first_view = 76;
+  CHECK(nsh::rx_plan(r, 4096, 1504000) == NS_EINVAL, "first view below 64 B of IP");
 }
 
 // nsh::tx_multi_plan: random sets of calls; whatever it accepts, no call's
@@ -626,6 +674,7 @@ int main(int argc, char** argv) {
   TestShardPlan(rng, r);
   TestTxPlan(rng, r);
   TestTxMultiPlan(rng, r);
+  TestRxPlan(rng, r);
   TestCombiner(16, quick ? 200 : 2000);
   TestScratchRegistry(8, 1000, quick ? 2000 : 20000);
   std::printf("%d checks, %d failed\n", g_run.load(), g_fail.load());

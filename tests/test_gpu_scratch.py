@@ -187,3 +187,71 @@ def test_growing_scratch_does_not_hold_up_synchronous_calls(engine):
     # interpreter's own GC pause (shorter ones can be GIL hand-offs between
     # the two threads: sys.getswitchinterval() is 5 ms).
     assert not [d for d in unexplained if d > 1e-2], sorted(unexplained)[-5:]
+
+
+@pytest.mark.latency
+def test_host_batch_pipeline_does_not_block_small_calls(engine):
+    """Thread A runs ns_csum_batch_host over a 1 GB host arena (the DMA
+    pipeline: ~20 ms per call) again and again; thread B meanwhile makes 1 KiB
+    Checksum calls on the same context.  Round 4 ran the pipeline under the
+    context lock that every zero-copy pass takes, so B's calls waited for
+    whole host batches (~29 ms at 1.5 GB).  The pipeline now has a lock and
+    streams of its own: B's passes never wait for it (the library's own
+    longest lock wait and longest call stay small), and every result of both
+    threads is checked against the oracle."""
+    import oracle as O
+    from netstack_amd import workloads as W
+
+    rng = np.random.default_rng(67)
+    n_big = 700_000
+    lengths = np.full(n_big, 1500, np.uint32)
+    bd, bend = W.make_desc(lengths, rng.integers(0, 65536, n_big).astype(np.uint16), align=16)
+    big = rng.integers(0, 256, bend, dtype=np.uint8)
+    want_big = O.c_batch_mt(big, bd, 8)
+    errors, lat = [], []
+    stop = threading.Event()
+    done_calls = []
+
+    def a_thread():
+        try:
+            for _ in range(6):
+                t0 = time.perf_counter()
+                out = engine.batch_host(big, bd)
+                done_calls.append(time.perf_counter() - t0)
+                if not np.array_equal(out, want_big):
+                    errors.append("batch_host")
+        except Exception as e:  # surfaced below
+            errors.append(repr(e))
+        finally:
+            stop.set()
+
+    def b_thread():
+        r = np.random.default_rng(68)
+        while not stop.is_set():
+            buf = r.integers(0, 256, 1024, dtype=np.uint8)
+            t0 = time.perf_counter()
+            got = engine.checksum(buf, 0)
+            lat.append(time.perf_counter() - t0)
+            if got != O.c_checksum(bytes(buf), 0):
+                errors.append("checksum")
+
+    engine.batch_host(big[:1 << 20], bd[:600])  # the pipeline's buffers exist before the clock starts
+    engine.stats(reset=True)
+    ta, tb = threading.Thread(target=a_thread), threading.Thread(target=b_thread)
+    tb.start()
+    ta.start()
+    ta.join()
+    tb.join()
+    st = engine.stats()
+    assert not errors, errors[:5]
+    lat_s = sorted(lat)
+    print(f"host batches: {len(done_calls)}, {np.median(done_calls) * 1e3:.1f} ms each; small calls during them: "
+          f"{len(lat_s)}, median {lat_s[len(lat_s) // 2] * 1e6:.1f} us, p99 {lat_s[int(len(lat_s) * 0.99)] * 1e6:.1f} "
+          f"us, max {lat_s[-1] * 1e6:.1f} us")
+    print(f"library: calls {st['calls']}, longest call {st['call_ns_max'] / 1e3:.1f} us, "
+          f"longest lock wait {st['lock_ns_max'] / 1e3:.1f} us, passes {st['zc_passes']} (late {st['zc_late']}, "
+          f"longest {st['zc_pass_ns_max'] / 1e3:.1f} us)")
+    assert len(lat_s) > 100
+    assert min(done_calls) > 5e-3  # each host batch is long enough to have blocked B before
+    assert st["lock_ns_max"] < 2e6, st  # a pass never waits for a host batch's pipeline
+    assert st["zc_late"] == 0, st

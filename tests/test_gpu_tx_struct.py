@@ -237,7 +237,7 @@ def test_errors(engine):
         g = dict(geo, **kw)
         for k in ("hdr_off", "pay_off", "size", "mss", "slot", "ip_at", "ip_len", "tcp_at", "tcp_len"):
             setattr(t, k, g[k])
-        t.protocol, t.flags = 6, g.get("flags", 0)
+        t.protocol, t.flags = g.get("protocol", 6), g.get("flags", 0)
         return L.ns_csum_tcp_tx(h, buf.data_ptr(), g.get("arena_bytes", total), ctypes.byref(t), None, None)
 
     assert call() == _lib.NS_OK
@@ -246,7 +246,9 @@ def test_errors(engine):
     for bad in (dict(mss=0), dict(mss=65536), dict(slot=0), dict(slot=5000), dict(ip_len=10),
                 dict(ip_len=64), dict(ip_at=40), dict(tcp_len=16), dict(tcp_len=64), dict(tcp_at=40),
                 dict(flags=_lib.NS_TX_TCP_PARTIAL | _lib.NS_TX_TCP_NONE), dict(flags=0x80),
-                dict(pay_off=geo["hdr_off"] + 100)):  # payload over the slots
+                dict(pay_off=geo["hdr_off"] + 100),  # payload over the slots
+                dict(protocol=256),  # PseudoHeaderChecksum takes uint8(protocol) (checksum.go:121)
+                dict(tcp_at=30)):  # TCP header over the IPv4 header's last bytes
         assert call(**bad) == _lib.NS_EINVAL, bad
     assert call(arena_bytes=geo["pay_off"] + 10) == _lib.NS_ERANGE
     assert call(pay_off=total - 10) == _lib.NS_ERANGE
@@ -341,3 +343,34 @@ def test_many_calls_in_one_launch(engine, oracle_mod):
     with pytest.raises(ValueError):  # NS_EINVAL
         engine.tcp_tx_multi(buf2, clash)
     assert engine.sync() == 0
+
+
+@pytest.mark.latency
+def test_multi_calls_do_not_wait_for_a_busy_stream(engine, oracle_mod):
+    """ns_csum_tcp_tx_multi is asynchronous: back-to-back calls behind ~100 ms
+    of queued work on their stream return without waiting for it (each call's
+    pinned table copy comes from a ring of 8; a wait happens only when the
+    device is 8 uploads behind).  Round 4's single copy made call k wait for
+    call k-1's upload, i.e. for everything queued before it.  The fills are
+    then checked against the oracle."""
+    import time
+
+    import torch
+
+    geo, total = CASES["netstack_default"]
+    a = _arena(total, geo, seed=31)
+    wa, _ = _want(oracle_mod, a, geo)
+    bufs = [torch.from_numpy(a).cuda() for _ in range(6)]
+    stream = torch.cuda.Stream()
+    torch.cuda.synchronize()
+    with torch.cuda.stream(stream):
+        torch.cuda._sleep(200_000_000)  # ~100 ms of GPU time queued first
+        t0 = time.perf_counter()
+        for b in bufs:
+            engine.tcp_tx_multi(b, [geo], stream=stream)
+        host = time.perf_counter() - t0
+    torch.cuda.synchronize()
+    assert host < 0.03, f"{len(bufs)} calls took {host * 1e3:.1f} ms on the host"
+    for b in bufs:
+        assert np.array_equal(b.cpu().numpy(), wa)
+    engine.stream_release(stream)

@@ -99,6 +99,21 @@ def main_set(dev, L):
               f"big_share={big_share(d):.4f}", flush=True)
         del arena, desc, out
         torch.cuda.empty_cache()
+    # cfg 7 as a receive ring (bench.py --rx-layout ring): ns_csum_rx_ring,
+    # 8-lane groups reading whole 128-B lines (line 0 default policy, the
+    # rest nontemporal): the 16-lane-group calibration shape
+    n = 1 << 20
+    arena, lens, _ = W.rx_ring_batch(n, 7000, dev, corrupt_every=1000)
+    verdict = torch.empty(n, dtype=torch.uint8, device=dev)
+    sums = torch.empty(2 * n, dtype=torch.int16, device=dev)
+    for _ in range(REPS):
+        eng.rx_ring(arena, dict(stride=W.RX_STRIDE, n=n), lens, sums=sums, verdict=verdict)
+    torch.cuda.synchronize()
+    algo = n * (W.RX_PKT + 9)  # bench.py ring_mode
+    print(f"LABEL cfg7ring algorithmic_bytes={algo} payload={n * W.RX_PKT} arena={arena.numel()} n={n} "
+          f"shape=calib2164", flush=True)
+    del arena, lens, verdict, sums
+    torch.cuda.empty_cache()
     # cfg 8 as bench.py runs it by default: sendTCPBatch's layout, NS_BATCH_PAIRED
     n = 1 << 20
     arena, _ = W.tx_split_batch(n, 7000, dev)

@@ -1,0 +1,108 @@
+#!/usr/bin/env python3
+"""The receive-ring kernel's timing variants (tools/rx_ring_variants.hip,
+libns_rxv.so) against the product (ns_csum_rx_ring) on bench.py's
+`--config 7 --rx-layout ring` workload: 1M x 1500-B IPv4/TCP packets in
+1504-B slots.  Rounds of back-to-back launches per variant, interleaved;
+median microseconds per launch and the fraction of 8 TB/s over the
+algorithmic bytes (packet bytes + 4-B length + 1-B verdict + 4-B sums per
+slot).  Every variant's verdicts and sums must equal the product's.
+  python tools/rx_ring_probe.py [--rounds 5] [--reps 20] [--only 0,1,2]
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+from netstack_amd import Engine  # noqa: E402
+from netstack_amd import workloads as W  # noqa: E402
+
+NAMES = {0: "product", 1: "all_default", 2: "all_nt", 3: "wg2", 4: "wg8", 5: "wg1", 6: "nb16", 7: "nb8",
+         8: "occ6", 9: "nb12"}
+
+
+class RxGeo(ctypes.Structure):
+    _fields_ = [("ring", ctypes.c_uint64), ("stride", ctypes.c_uint64), ("len", ctypes.c_void_p),
+                ("sums", ctypes.c_void_p), ("verdict", ctypes.c_void_p), ("err", ctypes.c_void_p),
+                ("n", ctypes.c_uint32), ("frame_at", ctypes.c_uint32), ("link", ctypes.c_uint32),
+                ("view0", ctypes.c_uint32)]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--n", type=int, default=1 << 20)
+    ap.add_argument("--only", default="")
+    ap.add_argument("--trend", type=int, default=0,
+                    help="then time this many back-to-back launches of the product one by one (run-long drift)")
+    args = ap.parse_args()
+    n = args.n
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.current_stream(dev)
+    eng = Engine(0)
+    lib = ctypes.CDLL(os.path.join(ROOT, "netstack_amd", "lib", "libns_rxv.so"))
+    lib.rxv_launch.argtypes = [ctypes.POINTER(RxGeo), ctypes.c_void_p, ctypes.c_int]
+    lib.rxv_launch.restype = ctypes.c_int
+    arena, lens, bad = W.rx_ring_batch(n, 9, dev, corrupt_every=1000)
+    ring = dict(stride=W.RX_STRIDE, n=n)
+    v0, s0 = eng.rx_ring(arena, ring, lens)
+    torch.cuda.synchronize()
+    err = torch.zeros(1, dtype=torch.int64, device=dev)
+    verdict = torch.empty(n, dtype=torch.uint8, device=dev)
+    sums = torch.empty(2 * n, dtype=torch.int16, device=dev)
+    g = RxGeo(arena.data_ptr(), W.RX_STRIDE, lens.data_ptr(), sums.data_ptr(), verdict.data_ptr(), err.data_ptr(),
+              n, 0, 0, 0)
+    algo = n * (W.RX_PKT + 9)
+    ks = [int(k) for k in args.only.split(",")] if args.only else sorted(NAMES)
+    res = {k: [] for k in ks}
+    ok = {}
+    for k in ks:  # parity first
+        verdict.fill_(0xEE)
+        sums.fill_(0x1234)
+        assert lib.rxv_launch(ctypes.byref(g), stream.cuda_stream, k) == 0
+        torch.cuda.synchronize()
+        ok[k] = bool(torch.equal(verdict, v0) and torch.equal(sums, s0))
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    for _ in range(args.rounds):
+        for k in ks:
+            for _ in range(3):
+                lib.rxv_launch(ctypes.byref(g), stream.cuda_stream, k)
+            ev[0].record(stream)
+            for _ in range(args.reps):
+                lib.rxv_launch(ctypes.byref(g), stream.cuda_stream, k)
+            ev[1].record(stream)
+            torch.cuda.synchronize()
+            res[k].append(ev[0].elapsed_time(ev[1]) * 1e3 / args.reps)
+    out = {}
+    for k in ks:
+        us = float(np.median(res[k]))
+        out[NAMES[k]] = {"us": round(us, 2), "min_us": round(min(res[k]), 2), "frac": round(algo / us / 1e3 / 8000, 4),
+                         "parity": ok[k]}
+    trend = None
+    if args.trend:
+        evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.trend + 1)]
+        evs[0].record(stream)
+        for i in range(args.trend):
+            lib.rxv_launch(ctypes.byref(g), stream.cuda_stream, 0)
+            evs[i + 1].record(stream)
+        torch.cuda.synchronize()
+        t = [evs[i].elapsed_time(evs[i + 1]) * 1e3 for i in range(args.trend)]
+        q = max(1, args.trend // 10)
+        trend = {"per_launch_us": [round(x, 1) for x in t],
+                 "first_decile_us": round(float(np.median(t[:q])), 2), "last_decile_us": round(float(np.median(t[-q:])), 2)}
+    print(json.dumps({"workload": "1M x 1500-B IPv4/TCP in 1504-B slots", "algo_bytes": algo, "variants": out,
+                      "trend": trend}, indent=1))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,27 @@
+// rx_ring_variants.hip — timing variants of the receive-ring kernel
+// (rx_ring.hip) that the product library does not carry, for
+// tools/rx_ring_probe.py.  rxv_launch(geo, stream, k):
+//   0 the product shape <13, default line 0, nt rest, 4 waves/WG>
+//   1 every line default policy      2 every line nontemporal
+//   3 2 waves/WG   4 8 waves/WG   5 1 wave/WG
+//   6 16 lines per batch   7 8 lines per batch (two batches for 1500 B)
+//   8 the product shape with a 6-waves/SIMD register floor
+//   9 12 lines per batch
+// Every variant computes the same verdicts and sums.  Not part of the ABI.
+#include "../netstack_amd/csrc/rx_ring.hip"
+
+extern "C" int rxv_launch(const nsk::RxGeo* g, void* stream, int k) {
+  hipStream_t s = (hipStream_t)stream;
+  switch (k) {
+    case 1: return (int)nsk::launch_rx_ring_t<13, 0, 0>(*g, s);
+    case 2: return (int)nsk::launch_rx_ring_t<13, 2, 2>(*g, s);
+    case 3: return (int)nsk::launch_rx_ring_t<13, 0, 2, 2>(*g, s);
+    case 4: return (int)nsk::launch_rx_ring_t<13, 0, 2, 8>(*g, s);
+    case 5: return (int)nsk::launch_rx_ring_t<13, 0, 2, 1>(*g, s);
+    case 6: return (int)nsk::launch_rx_ring_t<16>(*g, s);
+    case 7: return (int)nsk::launch_rx_ring_t<8>(*g, s);
+    case 8: return (int)nsk::launch_rx_ring_t<13, 0, 2, 4, 6>(*g, s);
+    case 9: return (int)nsk::launch_rx_ring_t<12>(*g, s);
+    default: return (int)nsk::launch_rx_ring_t<13>(*g, s);
+  }
+}
