@@ -23,6 +23,18 @@
 // handed to C hold only C pointers.  Contiguous Go buffers (ChecksumBatch)
 // are passed directly, as cgo allows.
 //
+// Errors (SURVEY.md §8(b)): the exported batch functions keep no-error
+// signatures.  When the engine cannot run a call (no device, an allocation
+// or HIP failure, a stale library), the call is computed by the reference's
+// own Go code in this package instead — calculateChecksum, Checksum,
+// ChecksumVVWithOffset and the header types' CalculateChecksum /
+// SetChecksum, in the callers' order — and EngineFallbacks() counts it.  The
+// result is the same either way.  The ...Err variants the build-tagged
+// callers use report the failure instead, so those callers run their
+// default-build path (csum_batch_go.go, csum_rx_go.go).  Only argument misuse
+// the reference would also trip over (an out slice too short, a negative
+// slice bound) panics.
+//
 // Compiled only with -tags hipcsum; include and library paths come from
 // CGO_CFLAGS / CGO_LDFLAGS (INTEGRATION.md §2).
 
@@ -38,9 +50,9 @@ package header
 import "C"
 
 import (
-	"fmt"
 	"reflect"
 	"sync"
+	"sync/atomic"
 	"unsafe"
 
 	"github.com/google/netstack/tcpip"
@@ -52,61 +64,83 @@ var (
 	csumCtx  *C.ns_csum_ctx
 	csumErr  C.int
 	csumABI  C.int
+
+	engineFallbacks uint64 // calls computed by the Go code instead (atomic)
+	engineLastRC    int32  // the last failing status (atomic)
 )
 
+// EngineFallbacks returns how many batch calls the engine could not run and
+// the reference's Go code computed instead (see the file comment).
+func EngineFallbacks() uint64 {
+	return atomic.LoadUint64(&engineFallbacks)
+}
+
+// EngineError is an engine call's failure: the operation and its NS_E*
+// status (include/netstack_csum.h).
+type EngineError struct {
+	Op     string
+	Status int
+}
+
+func (e *EngineError) Error() string {
+	return "netstack_csum: " + e.Op + ": " + C.GoString(C.ns_csum_strerror(C.int(e.Status)))
+}
+
+// engineFailed counts one call that falls back and returns its error.
+func engineFailed(op string, rc C.int) error {
+	atomic.AddUint64(&engineFallbacks, 1)
+	atomic.StoreInt32(&engineLastRC, int32(rc))
+	return &EngineError{Op: op, Status: int(rc)}
+}
+
 // csumEngine returns the process-wide engine context for device 0, created
-// once.  It refuses a library whose C ABI differs from the header this file
-// was compiled against (a stale libnetstack_csum.so).
-func csumEngine() *C.ns_csum_ctx {
+// once.  A library whose C ABI differs from the header this file was
+// compiled against (a stale libnetstack_csum.so), or a failed init, is an
+// engine failure like any other: every call falls back.
+func csumEngine() (*C.ns_csum_ctx, C.int) {
 	csumOnce.Do(func() {
 		csumABI = C.ns_csum_abi_version()
 		if csumABI != C.NS_CSUM_ABI_VERSION {
+			csumErr = C.NS_EINVAL
 			return
 		}
 		var opts C.ns_csum_opts
 		csumErr = C.ns_csum_init(&opts, &csumCtx)
 	})
-	if csumABI != C.NS_CSUM_ABI_VERSION {
-		panic(fmt.Sprintf("netstack_csum: libnetstack_csum.so has C ABI %d, netstack_csum.h has %d: rebuild the library",
-			int(csumABI), int(C.NS_CSUM_ABI_VERSION)))
-	}
 	if csumErr != C.NS_OK {
-		// No host fallback: these batch functions exist only in the hipcsum
-		// build, and a missing GPU is fatal like a slice-bound panic.
-		panic(fmt.Sprintf("netstack_csum: ns_csum_init: %s", C.GoString(C.ns_csum_strerror(csumErr))))
+		return nil, csumErr
 	}
-	return csumCtx
-}
-
-func csumMust(rc C.int, what string) {
-	if rc != C.NS_OK {
-		panic(fmt.Sprintf("netstack_csum: %s: %s", what, C.GoString(C.ns_csum_strerror(rc))))
-	}
+	return csumCtx, C.NS_OK
 }
 
 // csumStage is a leased engine staging buffer: pinned host memory the GPU
 // reads in place.  mem is the same C memory as a Go slice.
 type csumStage struct {
+	ctx  *C.ns_csum_ctx
 	base *C.uint8_t
 	mem  []byte
 	used int
 }
 
-func acquireStage(n int) *csumStage {
+func acquireStage(ctx *C.ns_csum_ctx, n int) (*csumStage, C.int) {
 	if n < 1 {
 		n = 1
 	}
-	s := &csumStage{}
-	csumMust(C.ns_csum_stage_acquire(csumEngine(), C.uint64_t(n), &s.base), "ns_csum_stage_acquire")
+	s := &csumStage{ctx: ctx}
+	if rc := C.ns_csum_stage_acquire(ctx, C.uint64_t(n), &s.base); rc != C.NS_OK {
+		return nil, rc
+	}
 	h := (*reflect.SliceHeader)(unsafe.Pointer(&s.mem))
 	h.Data = uintptr(unsafe.Pointer(s.base))
 	h.Len = n
 	h.Cap = n
-	return s
+	return s, C.NS_OK
 }
 
 func (s *csumStage) release() {
-	csumMust(C.ns_csum_stage_release(csumEngine(), s.base), "ns_csum_stage_release")
+	// a stage the engine does not know is a library bug, not a call's
+	// failure: the call's results stand
+	_ = C.ns_csum_stage_release(s.ctx, s.base)
 }
 
 // put copies b into the stage; it returns b's C address there (nil if empty)
@@ -161,16 +195,29 @@ func ChecksumVVBatch(vv buffer.VectorisedView, segs []SegDesc, out []uint16) {
 	if len(out) < len(segs) {
 		panic("ChecksumVVBatch: out too short")
 	}
-	if len(segs) == 0 {
-		return
-	}
 	for _, s := range segs {
 		if s.Off < 0 || s.Size < 0 {
 			panic("slice bounds out of range") // as v[off:] / v[:l] would in checksum.go
 		}
 	}
+	if len(segs) == 0 || checksumVVBatch(vv, segs, out) == nil {
+		return
+	}
+	for i, s := range segs { // the reference's own function, segment by segment
+		out[i] = ChecksumVVWithOffset(vv, s.Initial, s.Off, s.Size)
+	}
+}
+
+func checksumVVBatch(vv buffer.VectorisedView, segs []SegDesc, out []uint16) error {
+	ctx, rc := csumEngine()
+	if rc != C.NS_OK {
+		return engineFailed("ns_csum_init", rc)
+	}
 	vs := vv.Views()
-	st := acquireStage(viewBytes(vs))
+	st, rc := acquireStage(ctx, viewBytes(vs))
+	if rc != C.NS_OK {
+		return engineFailed("ns_csum_stage_acquire", rc)
+	}
 	defer st.release()
 	tab := make([]C.ns_view, len(vs)) // Go memory holding only C pointers
 	for i, v := range vs {
@@ -188,8 +235,11 @@ func ChecksumVVBatch(vv buffer.VectorisedView, segs []SegDesc, out []uint16) {
 	if len(tab) > 0 {
 		tp = &tab[0]
 	}
-	csumMust(C.ns_csum_vv_batch(csumEngine(), tp, C.uint32_t(len(tab)), &cs[0], C.uint32_t(len(cs)),
-		(*C.uint16_t)(unsafe.Pointer(&out[0]))), "ChecksumVVBatch")
+	if rc := C.ns_csum_vv_batch(ctx, tp, C.uint32_t(len(tab)), &cs[0], C.uint32_t(len(cs)),
+		(*C.uint16_t)(unsafe.Pointer(&out[0]))); rc != C.NS_OK {
+		return engineFailed("ns_csum_vv_batch", rc)
+	}
+	return nil
 }
 
 // ChecksumPiece is one buffer of a checksum chain.  Restart = a fresh
@@ -213,11 +263,24 @@ type ChecksumChain struct {
 // so sendTCPBatch (connect.go:668-702) and a recvmmsg batch of segment.parse
 // checks (segment.go:174-180) each take one call.
 func ChecksumChains(chains []ChecksumChain, out []uint16) {
+	if err := ChecksumChainsErr(chains, out); err != nil {
+		checksumChainsGo(chains, out)
+	}
+}
+
+// ChecksumChainsErr is ChecksumChains without the fallback: on an engine
+// failure it returns the error (counted in EngineFallbacks) and out is
+// undefined; the caller computes the sums its own way.
+func ChecksumChainsErr(chains []ChecksumChain, out []uint16) error {
 	if len(out) < len(chains) {
 		panic("ChecksumChains: out too short")
 	}
 	if len(chains) == 0 {
-		return
+		return nil
+	}
+	ctx, rc := csumEngine()
+	if rc != C.NS_OK {
+		return engineFailed("ns_csum_init", rc)
 	}
 	n, bytes := 0, 0
 	for _, ch := range chains {
@@ -229,7 +292,10 @@ func ChecksumChains(chains []ChecksumChain, out []uint16) {
 			bytes += len(pc.Buf)
 		}
 	}
-	st := acquireStage(bytes)
+	st, rc := acquireStage(ctx, bytes)
+	if rc != C.NS_OK {
+		return engineFailed("ns_csum_stage_acquire", rc)
+	}
 	defer st.release()
 	tab := make([]C.ns_piece, n) // Go memory holding only C pointers
 	k := 0
@@ -254,8 +320,30 @@ func ChecksumChains(chains []ChecksumChain, out []uint16) {
 			k++
 		}
 	}
-	csumMust(C.ns_csum_chains(csumEngine(), &tab[0], C.uint32_t(n), (*C.uint16_t)(unsafe.Pointer(&out[0])),
-		C.uint32_t(len(chains))), "ChecksumChains")
+	if rc := C.ns_csum_chains(ctx, &tab[0], C.uint32_t(n), (*C.uint16_t)(unsafe.Pointer(&out[0])),
+		C.uint32_t(len(chains))); rc != C.NS_OK {
+		return engineFailed("ns_csum_chains", rc)
+	}
+	return nil
+}
+
+// checksumChainsGo is a chain evaluated by the reference's own functions: a
+// restart piece is Checksum(buf, xsum) (checksum.go:52-55), a continuing one
+// carries the odd byte on, as ChecksumVVWithOffset chains views
+// (checksum.go:89); empty continuing pieces are skipped like empty views
+// (:73-75).
+func checksumChainsGo(chains []ChecksumChain, out []uint16) {
+	for i, ch := range chains {
+		xsum, odd := ch.Initial, false
+		for _, pc := range ch.Pieces {
+			if pc.Restart {
+				xsum, odd = calculateChecksum(pc.Buf, false, uint32(xsum))
+			} else if len(pc.Buf) > 0 {
+				xsum, odd = calculateChecksum(pc.Buf, odd, uint32(xsum))
+			}
+		}
+		out[i] = xsum
+	}
 }
 
 // BatchDesc is one packet of a contiguous batch: ns_pkt_desc (16 bytes) —
@@ -278,8 +366,25 @@ func ChecksumBatch(arena []byte, descs []BatchDesc, out []uint16, chained bool) 
 	if len(out) < len(descs) {
 		panic("ChecksumBatch: out too short")
 	}
-	if len(descs) == 0 {
+	if len(descs) == 0 || checksumBatch(arena, descs, out, chained) == nil {
 		return
+	}
+	var prev uint16
+	for i, d := range descs { // calculateChecksum (checksum.go:26-46) per descriptor
+		init := d.Initial
+		if chained && d.Flags&2 != 0 {
+			init = prev
+		}
+		b := arena[d.Off : d.Off+uint64(d.Len)] // past the arena: a slice-bound panic, as in Go
+		prev, _ = calculateChecksum(b, d.Flags&1 != 0 && len(b) > 0, uint32(init))
+		out[i] = prev
+	}
+}
+
+func checksumBatch(arena []byte, descs []BatchDesc, out []uint16, chained bool) error {
+	ctx, rc := csumEngine()
+	if rc != C.NS_OK {
+		return engineFailed("ns_csum_init", rc)
 	}
 	var flags C.uint32_t
 	if chained {
@@ -289,9 +394,12 @@ func ChecksumBatch(arena []byte, descs []BatchDesc, out []uint16, chained bool) 
 	if len(arena) > 0 {
 		ap = (*C.uint8_t)(unsafe.Pointer(&arena[0]))
 	}
-	csumMust(C.ns_csum_batch_host(csumEngine(), ap, C.uint64_t(len(arena)),
+	if rc := C.ns_csum_batch_host(ctx, ap, C.uint64_t(len(arena)),
 		(*C.ns_pkt_desc)(unsafe.Pointer(&descs[0])), C.uint32_t(len(descs)),
-		(*C.uint16_t)(unsafe.Pointer(&out[0])), flags), "ChecksumBatch")
+		(*C.uint16_t)(unsafe.Pointer(&out[0])), flags); rc != C.NS_OK {
+		return engineFailed("ns_csum_batch_host", rc)
+	}
+	return nil
 }
 
 // Verdicts of VerifyPacketBuffers (NS_PKB_*).
@@ -327,10 +435,23 @@ const (
 // 72-80), ICMPv6 (network/ipv6/icmp.go:76-84).  verdict[i] is one of the
 // constants above.
 func VerifyPacketBuffers(pkts []tcpip.PacketBuffer, verdict []uint8) {
+	if err := VerifyPacketBuffersErr(pkts, verdict); err != nil {
+		// Nothing verified: the stack's own checks (segment.parse, handleICMP)
+		// run on every packet, as the reference's receive path does.
+		for i := range pkts {
+			verdict[i] = PacketChecksumUnchecked
+		}
+	}
+}
+
+// VerifyPacketBuffersErr is VerifyPacketBuffers without the fallback: on an
+// engine failure it returns the error (counted in EngineFallbacks) and
+// verdict is undefined.
+func VerifyPacketBuffersErr(pkts []tcpip.PacketBuffer, verdict []uint8) error {
 	if len(verdict) < len(pkts) {
 		panic("VerifyPacketBuffers: verdict too short")
 	}
-	packetBuffers(pkts, C.NS_PKB_VERIFY, verdict)
+	return packetBuffers(pkts, C.NS_PKB_VERIFY, verdict)
 }
 
 // FillPacketBuffers writes the checksums of a batch of outbound packets whose
@@ -341,13 +462,72 @@ func VerifyPacketBuffers(pkts []tcpip.PacketBuffer, verdict []uint8) {
 // ICMPv6Checksum (icmpv6.go:202-221) compute it, and the IPv4 header
 // checksum of addIPHeader (network/ipv4/ipv4.go:236).
 func FillPacketBuffers(pkts []tcpip.PacketBuffer) {
-	packetBuffers(pkts, C.NS_PKB_FILL, nil)
+	if packetBuffers(pkts, C.NS_PKB_FILL, nil) != nil {
+		for i := range pkts {
+			fillPacketGo(&pkts[i])
+		}
+	}
 }
 
-func packetBuffers(pkts []tcpip.PacketBuffer, op C.uint32_t, verdict []uint8) {
+// fillPacketGo writes one packet's fields with the reference's own functions,
+// in its callers' order (the engine's NS_PKB_FILL rules): the transport
+// checksum unless the packet is an IPv4 fragment (writePacketFragments,
+// ipv4.go:159-160), then the IPv4 header checksum over the header as encoded.
+func fillPacketGo(pkt *tcpip.PacketBuffer) {
+	h := pkt.Header.View()
+	if len(h) == 0 {
+		return
+	}
+	var src, dst tcpip.Address
+	var proto uint8
+	var t []byte
+	v4 := IPVersion(h) == IPv4Version
+	frag := false
+	if v4 {
+		ip := IPv4(h)
+		src, dst, proto, t = ip.SourceAddress(), ip.DestinationAddress(), ip.Protocol(), h[ip.HeaderLength():]
+		frag = ip.Flags()&IPv4FlagMoreFragments != 0 || ip.FragmentOffset() != 0
+	} else {
+		ip := IPv6(h)
+		src, dst, proto, t = ip.SourceAddress(), ip.DestinationAddress(), ip.NextHeader(), h[IPv6MinimumSize:]
+	}
+	length := uint16(len(t) + pkt.Data.Size())
+	switch {
+	case frag:
+	case proto == uint8(TCPProtocolNumber): // buildTCPHdr (connect.go:653-663)
+		tcp := TCP(t)
+		xsum := PseudoHeaderChecksum(TCPProtocolNumber, src, dst, length)
+		xsum = ChecksumVV(pkt.Data, xsum)
+		tcp.SetChecksum(^tcp.CalculateChecksum(xsum))
+	case proto == uint8(UDPProtocolNumber): // sendUDP (udp/endpoint.go:808-815)
+		udp := UDP(t)
+		xsum := PseudoHeaderChecksum(UDPProtocolNumber, src, dst, length)
+		for _, v := range pkt.Data.Views() {
+			xsum = Checksum(v, xsum)
+		}
+		udp.SetChecksum(^udp.CalculateChecksum(xsum))
+	case proto == uint8(ICMPv4ProtocolNumber) && v4: // the echo reply (ipv4/icmp.go:96-100)
+		icmp := ICMPv4(t)
+		icmp.SetChecksum(0)
+		icmp.SetChecksum(^Checksum(icmp, ChecksumVV(pkt.Data, 0)))
+	case proto == uint8(ICMPv6ProtocolNumber) && !v4:
+		icmp := ICMPv6(t)
+		icmp.SetChecksum(ICMPv6Checksum(icmp, src, dst, pkt.Data))
+	}
+	if v4 { // addIPHeader (ipv4.go:236)
+		ip := IPv4(h)
+		ip.SetChecksum(^ip.CalculateChecksum())
+	}
+}
+
+func packetBuffers(pkts []tcpip.PacketBuffer, op C.uint32_t, verdict []uint8) error {
 	n := len(pkts)
 	if n == 0 {
-		return
+		return nil
+	}
+	ctx, rc := csumEngine()
+	if rc != C.NS_OK {
+		return engineFailed("ns_csum_init", rc)
 	}
 	need := 8
 	for i := range pkts {
@@ -355,7 +535,10 @@ func packetBuffers(pkts []tcpip.PacketBuffer, op C.uint32_t, verdict []uint8) {
 		need += (len(pkts[i].Data.Views()) + 1) * viewEntry
 		need += 8
 	}
-	st := acquireStage(need)
+	st, rc := acquireStage(ctx, need)
+	if rc != C.NS_OK {
+		return engineFailed("ns_csum_stage_acquire", rc)
+	}
 	defer st.release()
 	tab := make([]C.ns_pkt_buf, n) // Go memory holding only C pointers
 	hdrAt := make([]int, n)
@@ -398,7 +581,9 @@ func packetBuffers(pkts []tcpip.PacketBuffer, op C.uint32_t, verdict []uint8) {
 	if verdict != nil {
 		vp = (*C.uint8_t)(unsafe.Pointer(&verdict[0]))
 	}
-	csumMust(C.ns_csum_packet_buffers(csumEngine(), &tab[0], C.uint32_t(n), op, nil, vp), "ns_csum_packet_buffers")
+	if rc := C.ns_csum_packet_buffers(ctx, &tab[0], C.uint32_t(n), op, nil, vp); rc != C.NS_OK {
+		return engineFailed("ns_csum_packet_buffers", rc)
+	}
 	if op == C.NS_PKB_FILL {
 		// the checksum fields were written into the staged Header bytes
 		for i := range pkts {
@@ -406,4 +591,39 @@ func packetBuffers(pkts []tcpip.PacketBuffer, op C.uint32_t, verdict []uint8) {
 			copy(hv, st.mem[hdrAt[i]:hdrAt[i]+len(hv)])
 		}
 	}
+	return nil
+}
+
+// RxRing is a receive ring resident in device memory (ns_rx_ring): n slots
+// of Stride bytes from the arena's RingOff, the frame at FrameAt of a slot,
+// LinkHdr 0 (TUN) or 14 (Ethernet), FirstView the link's first buffer view
+// (BufConfig[0], packet_dispatchers.go:30; 0: one view).
+type RxRing struct {
+	RingOff, Stride  uint64
+	N                uint32
+	FrameAt, LinkHdr uint16
+	FirstView        uint32
+}
+
+// VerifyRingDevice verifies a ring of received frames that a GPU-attached
+// receive path left in device memory (ns_csum_rx_ring): every slot's verdict
+// (the constants above) and its two sums go to device memory, asynchronously
+// on stream (a hipStream_t, 0 = the null stream).  arena, lens, sums (or 0)
+// and verdict (or 0) are device addresses.  There is nothing to fall back to
+// on the host for bytes that live on the device: the error is returned
+// (and counted in EngineFallbacks), and the caller delivers the frames
+// unverified (RXChecksumUnknown), as the default build does.
+func VerifyRingDevice(arena uintptr, arenaBytes uint64, r RxRing, lens, sums, verdict, stream uintptr) error {
+	ctx, rc := csumEngine()
+	if rc != C.NS_OK {
+		return engineFailed("ns_csum_init", rc)
+	}
+	cr := C.ns_rx_ring{ring_off: C.uint64_t(r.RingOff), stride: C.uint64_t(r.Stride), n: C.uint32_t(r.N),
+		frame_at: C.uint16_t(r.FrameAt), link_hdr: C.uint16_t(r.LinkHdr), first_view: C.uint32_t(r.FirstView)}
+	if rc := C.ns_csum_rx_ring(ctx, (*C.uint8_t)(unsafe.Pointer(arena)), C.uint64_t(arenaBytes), &cr,
+		(*C.uint32_t)(unsafe.Pointer(lens)), (*C.uint16_t)(unsafe.Pointer(sums)),
+		(*C.uint8_t)(unsafe.Pointer(verdict)), unsafe.Pointer(stream)); rc != C.NS_OK {
+		return engineFailed("ns_csum_rx_ring", rc)
+	}
+	return nil
 }

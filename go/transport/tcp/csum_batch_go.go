@@ -4,7 +4,7 @@
 // deferTCPBatchChecksums false, sendTCPBatch never defers, and buildTCPHdr
 // computes every segment's checksum itself exactly as the reference does
 // (connect.go:661-663).  finishTCPBatchChecksums is that same per-segment
-// computation, for completeness.
+// computation (tcpBatchChecksumsRef, csum_batch_ref.go), for completeness.
 
 // +build !hipcsum
 
@@ -12,7 +12,6 @@ package tcp
 
 import (
 	"github.com/google/netstack/tcpip/buffer"
-	"github.com/google/netstack/tcpip/header"
 	"github.com/google/netstack/tcpip/stack"
 )
 
@@ -21,9 +20,5 @@ func deferTCPBatchChecksums(payload int) bool {
 }
 
 func finishTCPBatchChecksums(hdrs []stack.PacketDescriptor, data buffer.VectorisedView, pseudo []uint16) {
-	for i := range hdrs {
-		xsum := header.ChecksumVVWithOffset(data, pseudo[i], hdrs[i].Off, hdrs[i].Size)
-		tcp := header.TCP(hdrs[i].Hdr.View())
-		tcp.SetChecksum(^tcp.CalculateChecksum(xsum))
-	}
+	tcpBatchChecksumsRef(hdrs, data, pseudo)
 }

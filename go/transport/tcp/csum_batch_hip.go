@@ -33,7 +33,8 @@ func deferTCPBatchChecksums(payload int) bool {
 //   tcp.SetChecksum(^tcp.CalculateChecksum(xsum))             (connect.go:663)
 // as one chain per segment — the payload views (the first a restart, the
 // rest continuing its odd-byte carry, checksum.go:69-98), then the header
-// (a restart, tcp.go:259-262) — and all n chains in one device pass.
+// (a restart, tcp.go:259-262) — and all n chains in one device pass.  If the
+// engine fails, the default build's loop computes them instead.
 func finishTCPBatchChecksums(hdrs []stack.PacketDescriptor, data buffer.VectorisedView, pseudo []uint16) {
 	chains := make([]header.ChecksumChain, len(hdrs))
 	views := data.Views()
@@ -44,7 +45,13 @@ func finishTCPBatchChecksums(hdrs []stack.PacketDescriptor, data buffer.Vectoris
 		chains[i] = header.ChecksumChain{Initial: pseudo[i], Pieces: pieces}
 	}
 	sums := make([]uint16, len(hdrs))
-	header.ChecksumChains(chains, sums)
+	if err := header.ChecksumChainsErr(chains, sums); err != nil {
+		// The engine could not run the call (counted in
+		// header.EngineFallbacks): the reference's own per-segment loop, as
+		// the default build runs it (csum_batch_ref.go).
+		tcpBatchChecksumsRef(hdrs, data, pseudo)
+		return
+	}
 	for i := range hdrs {
 		header.TCP(hdrs[i].Hdr.View()).SetChecksum(^sums[i])
 	}

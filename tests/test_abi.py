@@ -239,6 +239,9 @@ GO_CALLERS = {  # file -> (package, build tag)
     "go/link/fdbased/csum_rx_hip.go": ("fdbased", "linux,hipcsum"),
     "go/link/fdbased/csum_rx_go.go": ("fdbased", "linux,!hipcsum"),
 }
+GO_SHARED = {  # untagged files both builds compile -> package
+    "go/transport/tcp/csum_batch_ref.go": "tcp",
+}
 GO_PATCH = os.path.join(ROOT, "go", "netstack-hipcsum.patch")
 
 
@@ -275,6 +278,14 @@ def test_go_caller_files_pair_up_and_use_only_what_exists():
             assert name in shim or name in REF_HEADER_NAMES or not os.path.isdir("/root/reference"), (rel, name)
         for name in set(re.findall(r"\btcpip\.(RXChecksum\w*)", code)):
             assert re.search(rf"\b{name}\b", added), (rel, name)
+    for rel, pkg in GO_SHARED.items():
+        raw = open(os.path.join(ROOT, rel)).read()
+        code = _go_code(raw)
+        for pat in POST_GO114:
+            assert not re.search(pat, code), (rel, pat)
+        assert "+build" not in raw and f"\npackage {pkg}\n" in raw, rel
+        for name in set(re.findall(r"\bheader\.(\w+)", code)):
+            assert name in REF_HEADER_NAMES or not os.path.isdir("/root/reference"), (rel, name)  # reference only
     for pkg, files in by_pkg.items():
         (t1, s1, c1), (t2, s2, c2) = files
         assert t1.replace("!", "") == t2.replace("!", "") and t1 != t2
@@ -343,6 +354,41 @@ def test_latency_bounds_are_collected_after_every_parity_test():
     assert par and max(par) < lat[0]
 
 
+def test_go_engine_errors_fall_back_to_the_reference_go():
+    """SURVEY §8(b)'s error policy: no engine status ever panics.  Every
+    C.ns_csum_* call's status goes to engineFailed (counted, exported as
+    EngineFallbacks); the no-error batch functions then compute with the
+    reference's own package-header functions, and the build-tagged callers
+    use the ...Err variants and run their default-build path: TX the
+    reference's per-segment loop (csum_batch_ref.go, shared with the default
+    build), RX nothing (RXChecksumUnknown: segment.parse verifies).  The only
+    panics left are argument misuse the reference's Go panics on too."""
+    shim = _go_code(open(GO_SHIM).read())
+    raw = open(GO_SHIM).read()
+    assert "csumMust" not in shim and "strerror" not in "".join(re.findall(r"panic\((.*?)\)\n", raw))
+    for m in re.finditer(r"panic\(\"([^\"]*)\"\)", raw):
+        assert re.search(r"too short|slice bounds|views in one packet", m.group(1)), m.group(1)
+    # every engine call's status is checked and routed to engineFailed
+    calls = re.findall(r"C\.(ns_csum_\w+)\(", shim)
+    checked = re.findall(r"(?:rc :=|rc =|csumErr =) C\.(ns_csum_\w+)\(", shim)
+    passive = {"ns_csum_abi_version", "ns_csum_strerror", "ns_csum_stage_release"}
+    assert set(calls) - passive <= set(checked), set(calls) - passive - set(checked)
+    assert shim.count("engineFailed(") >= len(set(checked)) and "func EngineFallbacks() uint64" in shim
+    for fn, ref in (("ChecksumVVBatch", "ChecksumVVWithOffset(vv"), ("ChecksumChains", "checksumChainsGo(chains"),
+                    ("ChecksumBatch", "calculateChecksum(b"), ("VerifyPacketBuffers", "PacketChecksumUnchecked"),
+                    ("FillPacketBuffers", "fillPacketGo(")):
+        body = re.search(rf"^func {fn}\(.*?^}}", shim, flags=re.M | re.S).group(0)
+        assert ref in body, fn
+    tx = _go_code(open(os.path.join(ROOT, "go/transport/tcp/csum_batch_hip.go")).read())
+    rx = _go_code(open(os.path.join(ROOT, "go/link/fdbased/csum_rx_hip.go")).read())
+    assert "header.ChecksumChainsErr(" in tx and "tcpBatchChecksumsRef(hdrs, data, pseudo)" in tx
+    assert "header.VerifyPacketBuffersErr(" in rx
+    dflt = _go_code(open(os.path.join(ROOT, "go/transport/tcp/csum_batch_go.go")).read())
+    assert "tcpBatchChecksumsRef(hdrs, data, pseudo)" in dflt
+    for rel in list(GO_CALLERS) + list(GO_SHARED):
+        assert "panic(" not in _go_code(open(os.path.join(ROOT, rel)).read()), rel
+
+
 def test_go_offload_gates_sit_at_the_measured_crossover():
     """The build-tagged callers offload only calls at or above the sizes
     where one engine call beat one core (tools/crossover.cc on MI355X,
@@ -370,6 +416,6 @@ def test_go_offload_gates_sit_at_the_measured_crossover():
     assert re.search(r"return payload >= header\.ChainsOffloadMinBytes", tx)
     rx = _go_code(open(os.path.join(ROOT, "go/link/fdbased/csum_rx_hip.go")).read())
     assert re.search(r"if total < header\.VerifyOffloadMinBytes \{\s*return\s*\}", rx)
-    assert rx.index("VerifyOffloadMinBytes") < rx.index("header.VerifyPacketBuffers(")
+    assert rx.index("VerifyOffloadMinBytes") < rx.index("header.VerifyPacketBuffersErr(")
     patch = open(GO_PATCH).read()
     assert "+\tdeferCsum := deferTCPBatchChecksums(data.Size()) &&" in patch
