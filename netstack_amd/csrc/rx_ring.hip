@@ -122,9 +122,14 @@ __device__ __forceinline__ uint4 rx_load(__amdgpu_buffer_rsrc_t r, uint32_t off)
 // NB = lines per load batch (line 0 included); a packet longer than NB lines
 // takes further batches of NB lines.  A0 / AN = the cache policy of line 0 /
 // of the others (0 default, 2 nontemporal), WV = waves per workgroup, OCC =
-// a waves-per-SIMD floor for the register allocator (1: none).  The product
-// runs <NB, 0, 2, 4, 1>; tools/rx_ring_variants.hip times the others.
-template <int NB, int A0 = 0, int AN = 2, int WV = kWaves, int OCC = 1>
+// a waves-per-SIMD floor for the register allocator (1: none).  F = 1: the
+// lines past line 1 are summed whole, as they arrive, with no per-chunk range
+// check (the chunk holding the transport's end is corrected by the lane that
+// re-reads it); a wave with a frame padded past its transport's end beyond
+// line 1 re-reads those lines with the range check.  F = 0: every chunk
+// range-checked.  The product runs <NB, 0, 2, 4, 1, 1>;
+// tools/rx_ring_variants.hip times the others.
+template <int NB, int A0 = 0, int AN = 2, int WV = kWaves, int OCC = 1, int F = 1>
 __global__ __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(OCC))) void rx_ring(RxGeo g) {
   __shared__ uint4 rx_lds[WV * kPerWave * kRowBytes / 16];
   const uint32_t lane = threadIdx.x & 63u, grp = lane >> 3, li = lane & 7u;
@@ -163,11 +168,31 @@ __global__ __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(OCC))) 
   // check returns zeros without touching memory
   const uint32_t lim = Pl ? Pl + 15u : 0u;
   auto off_of = [&](uint32_t o) -> uint32_t { return (o + 15u - pa) < lim ? o : nrec; };
+  // F: lines k >= 1 start past pa, so a chunk there holds packet bytes iff
+  // it starts before pe: k <= klast.  The voffset is cl (or nrec) and the
+  // line's 128 k goes in the instruction's offset field.
+  const uint32_t pe = pa + Pl;
+  const uint32_t klast = Pl && pe > cl ? (pe - 1u - cl) >> 7 : 0u;
+  const bool any1 = Pl && pe > cl + 128u;  // some line k >= 1 holds packet bytes for this lane
+  const uint32_t cl1 = any1 ? cl : nrec;
 
   uint4 v[NB];
   v[0] = rx_load<A0>(rsrc, off_of(cl));
 #pragma unroll
-  for (int k = 1; k < NB; ++k) v[k] = rx_load<AN>(rsrc, off_of(cl + 128u * k));
+  for (int k = 1; k < NB; ++k) {
+    if constexpr (F) v[k] = rx_load<AN>(rsrc, ((uint32_t)k <= klast ? cl1 : nrec) + 128u * k);
+    else v[k] = rx_load<AN>(rsrc, off_of(cl + 128u * k));
+  }
+  uint32_t w2 = 0;  // F: every loaded chunk of lines >= 2
+  if constexpr (F) {
+#pragma unroll
+    for (int k = 2; k < NB; ++k) {
+      w2 = __builtin_amdgcn_sad_u16(v[k].x, 0u, w2);
+      w2 = __builtin_amdgcn_sad_u16(v[k].y, 0u, w2);
+      w2 = __builtin_amdgcn_sad_u16(v[k].z, 0u, w2);
+      w2 = __builtin_amdgcn_sad_u16(v[k].w, 0u, w2);
+    }
+  }
 
   // The first 96 B from the packet's 16-B chunk into the group's LDS row.
   uint8_t* row = reinterpret_cast<uint8_t*>(rx_lds) + (wv * kPerWave + grp) * kRowBytes;
@@ -275,12 +300,23 @@ __global__ __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(OCC))) 
     x = po + hs;
     y = po + (b < A ? b : A);
   }
+  // The last loaded chunk (its offset from pa) and the first of line 2.
+  const uint32_t rl = Pl ? ((pa + Pl - 1u) & ~15u) - pa : 0u;
+  const uint32_t r2 = (pa & ~127u) + 256u - pa;
+  // F: a frame padded past its transport's end with loaded chunks beyond the
+  // transport's last chunk in lines >= 2 (their bytes are in w2; the chunk at
+  // B is corrected below only if it holds transport bytes): the whole wave
+  // sums lines >= 2 again with the range check.
+  const bool slow = F && kind && rl >= r2 && (rl > B || (rl == B && b == B));
+  const bool wslow = F && __builtin_amdgcn_ballot_w64(slow) != 0;
   uint32_t tail = 0;
   if (li == 3 && kind && b > B && B >= A) {  // bytes [B, b): one 16-B chunk, an L2 hit
     const uint4 t = *reinterpret_cast<const uint4*>((uintptr_t)(wbase + pa + B));
     const int c = (int)(b - B);
     tail = rx_wsum4(make_uint4(t.x & rx_below(c), t.y & rx_below(c - 4), t.z & rx_below(c - 8),
                                t.w & rx_below(c - 12)));
+    // F: in line >= 2 this chunk is in w2 whole; take its bytes past b back out
+    if (F && B >= r2 && !wslow) tail -= rx_wsum4(t);
   }
   uint32_t rs = rx_row_wsum<16>(row, x, y);
   if (li == 2 && kind >= 2) rs += *reinterpret_cast<const uint16_t*>(row + po + a);  // ICMP bytes [a, a + 2)
@@ -289,17 +325,44 @@ __global__ __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(OCC))) 
   uint32_t w = (li == 2 ? rs : 0u) + tail;
   const uint32_t d = cl - pa - A;
 #pragma unroll
-  for (int k = 0; k < NB; ++k) {
+  for (int k = 0; k < (F ? 2 : NB); ++k) {
     const uint32_t t = rx_wsum4(v[k]);
     w += (d + 128u * k) < span ? t : 0u;
   }
-  for (uint32_t k0 = NB; __builtin_amdgcn_ballot_w64((d + 128u * k0) < span) != 0; k0 += NB) {
+  if constexpr (F) {
+    // (both loops below take 4 lines at a time: their registers are not the
+    // kernel's peak, and they run only for long or padded frames)
+    if (wslow) {  // a padded frame in this wave: lines >= 2 re-read, range-checked
+      w2 = 0;
+      for (uint32_t k0 = 2; __builtin_amdgcn_ballot_w64((d + 128u * k0) < span) != 0; k0 += 4) {
 #pragma unroll
-    for (int k = 0; k < NB; ++k) v[k] = rx_load<AN>(rsrc, off_of(cl + 128u * (k0 + k)));
+        for (int k = 0; k < 4; ++k) {
+          const uint32_t t = rx_wsum4(rx_load<AN>(rsrc, off_of(cl + 128u * (k0 + k))));
+          w2 += (d + 128u * (k0 + k)) < span ? t : 0u;
+        }
+      }
+    } else {
+      for (uint32_t k0 = NB; __builtin_amdgcn_ballot_w64(k0 <= klast && kind) != 0; k0 += 4) {
 #pragma unroll
-    for (int k = 0; k < NB; ++k) {
-      const uint32_t t = rx_wsum4(v[k]);
-      w += (d + 128u * (k0 + k)) < span ? t : 0u;
+        for (int k = 0; k < 4; ++k) {
+          const uint4 x4 = rx_load<AN>(rsrc, ((k0 + k) <= klast ? cl1 : nrec) + 128u * (k0 + k));
+          w2 = __builtin_amdgcn_sad_u16(x4.x, 0u, w2);
+          w2 = __builtin_amdgcn_sad_u16(x4.y, 0u, w2);
+          w2 = __builtin_amdgcn_sad_u16(x4.z, 0u, w2);
+          w2 = __builtin_amdgcn_sad_u16(x4.w, 0u, w2);
+        }
+      }
+    }
+    w += w2;
+  } else {
+    for (uint32_t k0 = NB; __builtin_amdgcn_ballot_w64((d + 128u * k0) < span) != 0; k0 += NB) {
+#pragma unroll
+      for (int k = 0; k < NB; ++k) v[k] = rx_load<AN>(rsrc, off_of(cl + 128u * (k0 + k)));
+#pragma unroll
+      for (int k = 0; k < NB; ++k) {
+        const uint32_t t = rx_wsum4(v[k]);
+        w += (d + 128u * (k0 + k)) < span ? t : 0u;
+      }
     }
   }
   w += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)w, 0xB1, 0xF, 0xF, false);   // quad_perm 1,0,3,2
@@ -336,11 +399,11 @@ static int rx_batch_lines(const RxGeo& g) {
   return lines <= 2 ? 2 : lines <= 4 ? 4 : lines <= 8 ? 8 : lines <= 13 ? 13 : 16;
 }
 
-template <int NB, int A0 = 0, int AN = 2, int WV = kWaves, int OCC = 1>
+template <int NB, int A0 = 0, int AN = 2, int WV = kWaves, int OCC = 1, int F = 1>
 static hipError_t launch_rx_ring_t(const RxGeo& g, hipStream_t stream) {
   if (g.n == 0) return hipSuccess;
   const uint64_t per_wg = (uint64_t)WV * kPerWave;
-  hipLaunchKernelGGL((rx_ring<NB, A0, AN, WV, OCC>), dim3((uint32_t)((g.n + per_wg - 1) / per_wg)), dim3(64 * WV), 0,
+  hipLaunchKernelGGL((rx_ring<NB, A0, AN, WV, OCC, F>), dim3((uint32_t)((g.n + per_wg - 1) / per_wg)), dim3(64 * WV), 0,
                      stream, g);
   return hipGetLastError();
 }

@@ -333,3 +333,28 @@ def test_full_size_ring(engine):
     for i, k in enumerate(pick):
         got = (int(v[k]), int(s[2 * k]), int(s[2 * k + 1]))
         assert got == P.verify_frame(bytes(a[i]), W.RX_PKT), k
+
+
+@pytest.mark.parametrize("frame_at", [0, 2, 4, 10])
+def test_padded_frames_and_chunk_edges(engine, frame_at):
+    """Frames carrying bytes past their transport's end (Ethernet padding,
+    CapLength) of every size, next to unpadded ones in the same waves, with
+    the transport's end at every offset inside its 16-B chunk: the kernel
+    sums lines past line 1 whole, corrects the chunk holding the end, and
+    re-reads a wave with a padded frame beyond line 1 with the range check
+    (rx_ring.hip F = 1).  Every slot against the oracle."""
+    rng = np.random.default_rng(41 + frame_at)
+    frames = []
+    for i in range(400):
+        kind = ("tcp4", "tcp6", "icmp4", "icmp6")[i % 4]
+        plen = int(rng.integers(100, 2600)) if i % 3 else int(rng.integers(0, 120))
+        p = bytearray(valid_packet(rng, kind, plen))
+        if rng.random() < 0.15:  # a corrupted byte
+            k = int(rng.integers(0, len(p)))
+            p[k] ^= 0x21
+        pad = int(rng.choice([0, 0, 0, 1, 2, 15, 16, 17, 31, 100, 300, 1000]))
+        p += bytes(rng.integers(0, 256, pad, dtype=np.uint8))
+        frames.append(bytes(p))
+    stride = (max(len(f) for f in frames) + frame_at + 15) // 16 * 16
+    got = _check(engine, frames, stride, frame_at=frame_at, first_view=128 if frame_at % 4 == 0 else 0)
+    assert {0, 1} <= set(got)

@@ -144,6 +144,40 @@ def main_set(dev, L):
     torch.cuda.empty_cache()
 
 
+def rx_set(dev, L):
+    """The receive paths only: the 16-lane-group calibration read, cfg7 as a
+    fused descriptor table and cfg7 as a ring (ns_csum_rx_ring)."""
+    sp = torch.cuda.current_stream(dev).cuda_stream
+    buf = torch.ones(CAL_BYTES, dtype=torch.uint8, device=dev)
+    outb = torch.zeros(65536, dtype=torch.int32, device=dev)
+    for _ in range(REPS):
+        assert L.nsk_calib_launch(2164, buf.data_ptr(), CAL_BYTES, outb.data_ptr(), 8192, sp) == 0
+    torch.cuda.synchronize()
+    print(f"LABEL calib2164 bytes={CAL_BYTES}", flush=True)
+    del buf
+    eng = Engine(0)
+    n = 1 << 20
+    arena, d, _ = W.rx_batch(n, 7000, dev, corrupt_every=1000, fused=True)
+    desc = torch.from_numpy(d.view(np.uint8).copy()).to(dev)
+    out = torch.empty(len(d), dtype=torch.int16, device=dev)
+    for _ in range(REPS):
+        eng.batch_tensors(arena, desc, out)
+    torch.cuda.synchronize()
+    algo = n * W.RX_PKT + 8 * n + len(d) * 18
+    print(f"LABEL cfg7 algorithmic_bytes={algo} payload={n * W.RX_PKT} arena={arena.numel()} n={len(d)} "
+          f"big_share={big_share(d):.4f}", flush=True)
+    del arena, desc, out
+    torch.cuda.empty_cache()
+    arena, lens, _ = W.rx_ring_batch(n, 7000, dev, corrupt_every=1000)
+    verdict = torch.empty(n, dtype=torch.uint8, device=dev)
+    sums = torch.empty(2 * n, dtype=torch.int16, device=dev)
+    for _ in range(REPS):
+        eng.rx_ring(arena, dict(stride=W.RX_STRIDE, n=n), lens, sums=sums, verdict=verdict)
+    torch.cuda.synchronize()
+    print(f"LABEL cfg7ring algorithmic_bytes={n * (W.RX_PKT + 9)} payload={n * W.RX_PKT} arena={arena.numel()} "
+          f"n={n} shape=calib2164", flush=True)
+
+
 def cfg3probe_set(dev, L):
     names = [L.nsk_tune_name(v).decode() for v in range(L.nsk_tune_count())]
     sp = torch.cuda.current_stream(dev).cuda_stream
@@ -164,7 +198,7 @@ def cfg3probe_set(dev, L):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--set", default="main", choices=("main", "cfg3probe"))
+    ap.add_argument("--set", default="main", choices=("main", "cfg3probe", "rx"))
     args = ap.parse_args()
     L = ctypes.CDLL(os.path.join(ROOT, "netstack_amd", "lib", "libns_tune.so"))
     L.nsk_calib_launch.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
@@ -178,6 +212,8 @@ def main():
     dev = torch.device("cuda", 0)
     if args.set == "main":
         main_set(dev, L)
+    elif args.set == "rx":
+        rx_set(dev, L)
     else:
         cfg3probe_set(dev, L)
 

@@ -7,6 +7,8 @@
 //   6 16 lines per batch   7 8 lines per batch (two batches for 1500 B)
 //   8 the product shape with a 6-waves/SIMD register floor
 //   9 12 lines per batch
+//  10 every chunk range-checked (F = 0: round 5's first product shape)
+//  11 F with 8 lines per batch
 // Every variant computes the same verdicts and sums.  Not part of the ABI.
 #include "../netstack_amd/csrc/rx_ring.hip"
 
@@ -22,6 +24,8 @@ extern "C" int rxv_launch(const nsk::RxGeo* g, void* stream, int k) {
     case 7: return (int)nsk::launch_rx_ring_t<8>(*g, s);
     case 8: return (int)nsk::launch_rx_ring_t<13, 0, 2, 4, 6>(*g, s);
     case 9: return (int)nsk::launch_rx_ring_t<12>(*g, s);
+    case 10: return (int)nsk::launch_rx_ring_t<13, 0, 2, 4, 1, 0>(*g, s);
+    case 11: return (int)nsk::launch_rx_ring_t<8, 0, 2, 4, 1, 1>(*g, s);
     default: return (int)nsk::launch_rx_ring_t<13>(*g, s);
   }
 }
