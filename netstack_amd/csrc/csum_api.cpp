@@ -1421,7 +1421,7 @@ int ns_csum_tcp_tx_multi(ns_csum_ctx* ctx, uint8_t* d_arena, uint64_t arena_byte
 }
 
 int ns_csum_set_tx_tuning(ns_csum_ctx* ctx, uint32_t variant, uint32_t tile, uint32_t htile, uint32_t passes) {
-  if (!ctx || variant > 3 || passes > 2) return NS_EINVAL;
+  if (!ctx || variant > 4 || passes > 2) return NS_EINVAL;
   ctx->tx_variant = variant;
   ctx->tx_tile = tile;
   ctx->tx_htile = htile;

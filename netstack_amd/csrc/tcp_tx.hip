@@ -45,6 +45,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "csum_kernels.h"
 
 namespace nsk {
@@ -119,6 +121,23 @@ __device__ __forceinline__ uint32_t lds_wsum(const uint8_t* L, uint32_t a, uint3
   return w;
 }
 
+// lds_wsum as a loop (no unrolling): fewer registers where two tiles are in
+// flight (tcp_tx_hdr).
+__device__ __forceinline__ uint32_t lds_wsum_loop(const uint8_t* L, uint32_t a, uint32_t len, uint32_t zero) {
+  const uint32_t* D = reinterpret_cast<const uint32_t*>(L);
+  const uint32_t d0 = a >> 2;
+  const uint32_t nd = ((a + len + 3) >> 2) - d0;
+  uint32_t w = 0;
+#pragma nounroll
+  for (uint32_t k = 0; k < nd; ++k) {
+    const int b = (int)(4 * (d0 + k));
+    uint32_t m = below((int)(a + len) - b) & ~below((int)a - b);
+    m &= ~(below((int)(zero + 2) - b) & ~below((int)zero - b));
+    w = __builtin_amdgcn_sad_u16(D[d0 + k] & m, 0u, w);
+  }
+  return w;
+}
+
 __device__ __forceinline__ void lds_put_be16(uint8_t* L, uint32_t at, uint32_t v) {
   L[at] = (uint8_t)(v >> 8);
   L[at + 1] = (uint8_t)v;
@@ -138,6 +157,106 @@ __device__ __forceinline__ void tx_store_be16(uint64_t addr, uint32_t v) {
 }
 
 }  // namespace
+
+// Step 3 of a tile (below): lane l finishes segments s0 + l, s0 + l + 64, ...
+// of the tile whose slots sit in LDS from byte `ho` (h_lo - h_base): sums
+// the IPv4 and TCP headers (the fields read as zero), folds them with the
+// pseudo-header and the payload value (wres, or g.xs in the header pass), as
+// the Go code does, and writes both fields into the LDS copy (and d_out; or
+// straight to the slots with kTxFieldsOnly).
+template <int PH>
+__device__ __forceinline__ void tx_fields(const TxGeo& g, uint64_t s0, uint32_t nseg, uint8_t* L, uint32_t ho,
+                                          uint32_t lane, uint32_t wres) {
+  const uint64_t h_lo = g.hdr + s0 * g.slot;
+  for (uint32_t j = lane; j < nseg; j += 64) {
+    const uint32_t o = ho + j * g.slot;  // slot j in LDS
+    const uint64_t si = s0 + j;
+    const uint32_t size = si + 1 < g.n ? g.mss : (uint32_t)(g.size - (g.n - 1) * (uint64_t)g.mss);
+    uint32_t ipv = 0, tcpv = 0;
+    if (g.mode & kTxIp) {
+      const uint32_t a = o + g.ip_at;
+      ipv = tx_fold(tx_class(lds_wsum<16>(L, a, g.ip_len, a + 10u), a & 1u));  // Checksum(ip[:IHL], 0)
+      lds_put_be16(L, a + 10u, ~ipv & 0xFFFFu);
+    }
+    if (g.mode & (kTxTcpFull | kTxTcpPartial)) {
+      uint32_t x = tx_fold(g.addr_sum + ((g.tcp_len + size) & 0xFFFFu));  // PseudoHeaderChecksum
+      x = tx_fold(x + g.proto);
+      const uint32_t a = o + g.tcp_at;
+      if (g.mode & kTxTcpFull) {
+        // PH 3: the payload value itself was handed in as wres (one segment per lane)
+        const uint32_t pv = PH == 2 ? (uint32_t)g.xs[si * g.xstride]
+                            : PH == 3 ? wres
+                                      : tx_class(wres, (uint32_t)((g.pay + si * g.mss) & 1u));
+        x = tx_fold(x + pv);                                                            // ChecksumVVWithOffset
+        x = tx_fold(x + tx_class(lds_wsum<16>(L, a, g.tcp_len, a + 16u), a & 1u));     // CalculateChecksum
+        lds_put_be16(L, a + 16u, ~x & 0xFFFFu);
+      } else {
+        lds_put_be16(L, a + 16u, x);
+      }
+      tcpv = x;
+    }
+    if (g.out) {
+      g.out[2 * si] = (uint16_t)ipv;
+      g.out[2 * si + 1] = (uint16_t)tcpv;
+    }
+    if (g.mode & kTxFieldsOnly) {  // only the 2-byte fields, as csum_hyb stores them
+      const uint64_t slot = h_lo + (uint64_t)j * g.slot;
+      if (g.mode & kTxIp) tx_store_be16(slot + g.ip_at + 10u, ~ipv & 0xFFFFu);
+      if (g.mode & kTxTcpFull) tx_store_be16(slot + g.tcp_at + 16u, ~tcpv & 0xFFFFu);
+      if (g.mode & kTxTcpPartial) tx_store_be16(slot + g.tcp_at + 16u, tcpv);
+    }
+  }
+}
+
+// Step 4: the tile's region [h_lo, h_hi) back from LDS, whole (16-B stores of
+// full chunks; byte stores where a chunk is shared with a neighbouring tile).
+template <int SP>
+__device__ __forceinline__ void tx_writeback(const uint8_t* L, uint64_t h_lo, uint64_t h_hi, uint64_t h_base,
+                                             uint32_t h_chunks, uint32_t lane) {
+  const uint4* L4 = reinterpret_cast<const uint4*>(L);
+  for (uint32_t c = lane; c < h_chunks; c += 64) {
+    const uint64_t at = h_base + (uint64_t)c * 16u;
+    if (at >= h_lo && at + 16 <= h_hi) {
+      uint4* p = reinterpret_cast<uint4*>((uintptr_t)at);
+      if constexpr (SP == 1) {
+        const uint4 x = L4[c];
+        uint32_t* q = reinterpret_cast<uint32_t*>(p);
+        __builtin_nontemporal_store(x.x, q);
+        __builtin_nontemporal_store(x.y, q + 1);
+        __builtin_nontemporal_store(x.z, q + 2);
+        __builtin_nontemporal_store(x.w, q + 3);
+      } else {
+        *p = L4[c];
+      }
+    } else {  // a chunk shared with the neighbouring tile: only this tile's bytes
+      for (uint32_t k = 0; k < 16; ++k)
+        if (at + k >= h_lo && at + k < h_hi) reinterpret_cast<uint8_t*>((uintptr_t)at)[k] = L[c * 16u + k];
+    }
+  }
+}
+
+// Step 4 through the tile's buffer resource (hr: [h_base, h_base + 16
+// h_chunks)): buffer stores, which count in vmcnt only.  A flat store would
+// make every later LDS access wait for all of the wave's memory operations
+// (flat_* complete out of order: vmcnt(0) and lgkmcnt(0)), which in a loop
+// over tiles drains the next tile's prefetch too.
+template <int SP>
+__device__ __forceinline__ void tx_writeback_buf(const uint8_t* L, __amdgpu_buffer_rsrc_t hr, uint64_t h_lo,
+                                                 uint64_t h_hi, uint64_t h_base, uint32_t h_chunks, uint32_t lane) {
+  const uint4* L4 = reinterpret_cast<const uint4*>(L);
+  const uint32_t lo = (uint32_t)(h_lo - h_base), hi = (uint32_t)(h_hi - h_base);
+  for (uint32_t c = lane; c < h_chunks; c += 64) {
+    const uint32_t at = c * 16u;
+    if (at >= lo && at + 16 <= hi) {
+      const uint4 x = L4[c];
+      __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const __attribute__((ext_vector_type(4))) uint32_t*>(&x),
+                                             hr, (int)at, 0, SP == 1 ? 2 : 0);
+    } else {  // a chunk shared with the neighbouring tile: only this tile's bytes
+      for (uint32_t k = 0; k < 16; ++k)
+        if (at + k >= lo && at + k < hi) __builtin_amdgcn_raw_buffer_store_b8(L[at + k], hr, (int)(at + k), 0, 0);
+    }
+  }
+}
 
 // U = payload windows (1 KiB per wave each) in flight; AUX = payload load
 // policy (2 = nontemporal); SP = header write-back policy (0 plain, 1 nt);
@@ -255,68 +374,13 @@ __device__ __forceinline__ void tx_tile(const TxGeo& g, uint64_t s0, uint8_t* L,
   // (a pass that reads payload has at most 64, so lane j = segment j)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the LDS-DMA copy is in
   __builtin_amdgcn_wave_barrier();
-  for (uint32_t j = lane; j < nseg; j += 64) {
-    const uint32_t o = (uint32_t)(h_lo - h_base) + j * g.slot;  // slot j in LDS
-    const uint64_t si = s0 + j;
-    const uint32_t size = si + 1 < g.n ? g.mss : (uint32_t)(g.size - (g.n - 1) * (uint64_t)g.mss);
-    uint32_t ipv = 0, tcpv = 0;
-    if (g.mode & kTxIp) {
-      const uint32_t a = o + g.ip_at;
-      ipv = tx_fold(tx_class(lds_wsum<16>(L, a, g.ip_len, a + 10u), a & 1u));  // Checksum(ip[:IHL], 0)
-      lds_put_be16(L, a + 10u, ~ipv & 0xFFFFu);
-    }
-    if (g.mode & (kTxTcpFull | kTxTcpPartial)) {
-      uint32_t x = tx_fold(g.addr_sum + ((g.tcp_len + size) & 0xFFFFu));  // PseudoHeaderChecksum
-      x = tx_fold(x + g.proto);
-      const uint32_t a = o + g.tcp_at;
-      if (g.mode & kTxTcpFull) {
-        const uint32_t pv = PH == 2 ? (uint32_t)g.xs[si * g.xstride]
-                                    : tx_class(wres, (uint32_t)((g.pay + si * g.mss) & 1u));
-        x = tx_fold(x + pv);                                                            // ChecksumVVWithOffset
-        x = tx_fold(x + tx_class(lds_wsum<16>(L, a, g.tcp_len, a + 16u), a & 1u));     // CalculateChecksum
-        lds_put_be16(L, a + 16u, ~x & 0xFFFFu);
-      } else {
-        lds_put_be16(L, a + 16u, x);
-      }
-      tcpv = x;
-    }
-    if (g.out) {
-      g.out[2 * si] = (uint16_t)ipv;
-      g.out[2 * si + 1] = (uint16_t)tcpv;
-    }
-    if (g.mode & kTxFieldsOnly) {  // only the 2-byte fields, as csum_hyb stores them
-      const uint64_t slot = h_lo + (uint64_t)j * g.slot;
-      if (g.mode & kTxIp) tx_store_be16(slot + g.ip_at + 10u, ~ipv & 0xFFFFu);
-      if (g.mode & kTxTcpFull) tx_store_be16(slot + g.tcp_at + 16u, ~tcpv & 0xFFFFu);
-      if (g.mode & kTxTcpPartial) tx_store_be16(slot + g.tcp_at + 16u, tcpv);
-    }
-  }
+  tx_fields<PH>(g, s0, nseg, L, (uint32_t)(h_lo - h_base), lane, wres);
   if (g.mode & kTxFieldsOnly) return;
   if constexpr ((XF & 1) != 0) return;
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
-
   // 4. the header region back, whole
-  const uint4* L4 = reinterpret_cast<const uint4*>(L);
-  for (uint32_t c = lane; c < h_chunks; c += 64) {
-    const uint64_t at = h_base + (uint64_t)c * 16u;
-    if (at >= h_lo && at + 16 <= h_hi) {
-      uint4* p = reinterpret_cast<uint4*>((uintptr_t)at);
-      if constexpr (SP == 1) {
-        const uint4 x = L4[c];
-        uint32_t* q = reinterpret_cast<uint32_t*>(p);
-        __builtin_nontemporal_store(x.x, q);
-        __builtin_nontemporal_store(x.y, q + 1);
-        __builtin_nontemporal_store(x.z, q + 2);
-        __builtin_nontemporal_store(x.w, q + 3);
-      } else {
-        *p = L4[c];
-      }
-    } else {  // a chunk shared with the neighbouring tile: only this tile's bytes
-      for (uint32_t k = 0; k < 16; ++k)
-        if (at + k >= h_lo && at + k < h_hi) reinterpret_cast<uint8_t*>((uintptr_t)at)[k] = L[c * 16u + k];
-    }
-  }
+  tx_writeback<SP>(L, h_lo, h_hi, h_base, h_chunks, lane);
 }
 
 template <int U, int AUX, int SP, int RED, int XF = 0, int PH = 0>
@@ -327,6 +391,123 @@ __global__ __launch_bounds__(256) void tcp_tx(TxGeo g) {
   uint8_t* L = reinterpret_cast<uint8_t*>(tx_lds) + (size_t)wv * g.lds_wave;
   uint32_t* rows = reinterpret_cast<uint32_t*>(L + g.lds_rows);  // RED 1: [tile][64] partials
   tx_tile<U, AUX, SP, RED, XF, PH>(g, ((uint64_t)blockIdx.x * g.wpg + wv) * g.tile, L, rows, lane);
+}
+
+// The header pass as a persistent grid: wave W takes tiles W, W + NW, ...
+// with two tiles' slot regions in flight in registers (plain buffer loads,
+// CPL 16-B chunks per lane, plus the tile's payload values, one segment per
+// lane) while it finishes a third from LDS: the one-shot header pass (tcp_tx
+// PH = 2) does one memory round per wave, its DMA, the wait, then the stores
+// (22-28 us where the writes alone take ~12).
+// Every memory operation of an iteration is a buffer operation issued
+// unconditionally (out-of-range offsets where there is nothing to do; a
+// resource of 0 bytes where a fetch runs past the last tile), so the
+// compiler knows how many are younger than the registers it waits for: the
+// wait for tile t's region leaves tile t+1's fetch and tile t-1's stores in
+// flight.  A flat store, or a store count it cannot know, would make it wait
+// for all of them.  For tiles that start 16-B aligned (hdr, tile * slot) and
+// hold at most 64 segments and 64 CPL chunks; the last tile's unaligned end
+// is written with byte stores as the wave's last act.
+template <int CPL, int SP>
+__global__ __launch_bounds__(256) void tcp_tx_hdr(TxGeo g, uint32_t ntiles) {
+  extern __shared__ uint4 tx_lds[];
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  uint8_t* L = reinterpret_cast<uint8_t*>(tx_lds) + (size_t)wv * g.lds_wave;
+  uint4* L4 = reinterpret_cast<uint4*>(L);
+  const uint32_t NW = gridDim.x * g.wpg;
+  const uint32_t t0 = blockIdx.x * g.wpg + wv;
+  if (t0 >= ntiles) return;  // a whole wave leaves together
+  const uint32_t region = g.tile * g.slot;  // bytes of a full tile (a multiple of 16)
+  const uint64_t end = g.hdr + g.n * (uint64_t)g.slot;
+  // the payload values and the sums, through resources of their own
+  const __amdgpu_buffer_rsrc_t xr = tx_srd((uint64_t)(uintptr_t)g.xs, (uint32_t)(g.n * g.xstride * 2u));
+  const __amdgpu_buffer_rsrc_t orr = tx_srd((uint64_t)(uintptr_t)g.out, g.out ? (uint32_t)(g.n * 4u) : 0u);
+  auto fetch = [&](uint32_t tt, uint4* v, uint32_t& pv) {
+    const bool live = tt < ntiles;
+    const uint64_t lo = g.hdr + (uint64_t)(live ? tt : 0u) * region;
+    const uint32_t bytes = live ? (uint32_t)(end - lo < region ? ((end - lo + 15) & ~15ull) : region) : 0u;
+    const __amdgpu_buffer_rsrc_t hr = tx_srd(lo, bytes);
+#pragma unroll
+    for (int i = 0; i < CPL; ++i) v[i] = tx_load<0>(hr, (lane + 64u * i) * 16u);
+    const uint64_t si = (uint64_t)tt * g.tile + lane;
+    pv = __builtin_amdgcn_raw_buffer_load_b16(xr, (int)(live && si < g.n ? si * g.xstride * 2u : 0xFFFFFFF0u), 0, 0);
+  };
+  auto finish = [&](uint32_t t, const uint4* v, uint32_t pv) {
+    const uint64_t s0 = (uint64_t)t * g.tile;
+    const uint32_t nseg = g.n - s0 < g.tile ? (uint32_t)(g.n - s0) : g.tile;
+    const uint64_t lo = g.hdr + s0 * g.slot, hi = lo + (uint64_t)nseg * g.slot;
+    const uint32_t chunks = (uint32_t)((hi - lo + 15) >> 4);
+#pragma unroll
+    for (int i = 0; i < CPL; ++i)
+      if (lane + 64u * i < chunks) L4[lane + 64u * i] = v[i];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // the fields (tx_fields' arithmetic for the lane's one segment)
+    uint32_t ipv = 0, tcpv = 0;
+    if (lane < nseg) {
+      const uint32_t o = lane * g.slot;
+      const uint64_t si = s0 + lane;
+      const uint32_t size = si + 1 < g.n ? g.mss : (uint32_t)(g.size - (g.n - 1) * (uint64_t)g.mss);
+      if (g.mode & kTxIp) {
+        const uint32_t a = o + g.ip_at;
+        ipv = tx_fold(tx_class(lds_wsum_loop(L, a, g.ip_len, a + 10u), a & 1u));  // Checksum(ip[:IHL], 0)
+        lds_put_be16(L, a + 10u, ~ipv & 0xFFFFu);
+      }
+      uint32_t x = tx_fold(g.addr_sum + ((g.tcp_len + size) & 0xFFFFu));  // PseudoHeaderChecksum
+      x = tx_fold(x + g.proto);
+      const uint32_t a = o + g.tcp_at;
+      x = tx_fold(x + (pv & 0xFFFFu));                                               // ChecksumVVWithOffset
+      x = tx_fold(x + tx_class(lds_wsum_loop(L, a, g.tcp_len, a + 16u), a & 1u));    // CalculateChecksum
+      lds_put_be16(L, a + 16u, ~x & 0xFFFFu);
+      tcpv = x;
+    }
+    __builtin_amdgcn_raw_buffer_store_b32(ipv | (tcpv << 16), orr, (int)(lane < nseg ? (s0 + lane) * 4u : 0xFFFFFFF0u), 0,
+                                          0);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // the region back, whole chunks (the tile's own: it starts 16-B aligned)
+    const uint32_t full = (uint32_t)((hi - lo) >> 4);
+    const __amdgpu_buffer_rsrc_t hr = tx_srd(lo, full * 16u);
+#pragma unroll
+    for (int i = 0; i < CPL; ++i) {
+      const uint32_t c = lane + 64u * i;
+      const uint4 x = L4[c < chunks ? c : 0u];
+      __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const __attribute__((ext_vector_type(4))) uint32_t*>(&x),
+                                             hr, (int)(c * 16u), 0, SP == 1 ? 2 : 0);
+    }
+    return full < chunks;  // an unaligned end: the last tile
+  };
+  auto tail = [&](uint32_t t) {  // the last tile's partial chunk, byte by byte
+    const uint64_t s0 = (uint64_t)t * g.tile;
+    const uint32_t nseg = (uint32_t)(g.n - s0);
+    const uint64_t lo = g.hdr + s0 * g.slot, hi = lo + (uint64_t)nseg * g.slot;
+    const uint32_t full = (uint32_t)((hi - lo) >> 4);
+    if (lane < (uint32_t)((hi - lo) & 15u)) reinterpret_cast<uint8_t*>((uintptr_t)(lo + full * 16u))[lane] = L[full * 16u + lane];
+  };
+  uint4 x[CPL], y[CPL];
+  uint32_t px = 0, py = 0;
+  fetch(t0, x, px);
+  fetch(t0 + NW, y, py);
+  for (uint32_t t = t0;; t += 2 * NW) {
+    // tile t from x, then tile t + 2 NW's fetch into x (x is in LDS by then)
+    bool ragged = finish(t, x, px);
+    if (ragged) {
+      tail(t);
+      break;
+    }
+    fetch(t + 2 * NW, x, px);
+    if (t + NW >= ntiles) break;
+    ragged = finish(t + NW, y, py);
+    if (ragged) {
+      tail(t + NW);
+      break;
+    }
+    fetch(t + 3 * NW, y, py);
+    if (t + 2 * NW >= ntiles) break;
+  }
 }
 
 // Many batches (sendTCPBatch calls) in one launch, one fused pass each:
@@ -396,18 +577,57 @@ static hipError_t launch_tcp_tx_t(TxGeo g, hipStream_t stream) {
   return hipGetLastError();
 }
 
+// Compute units of the current device (cached per device ordinal).
+static uint32_t tx_cu_count() {
+  static uint32_t cus[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (!cus[dev]) {
+    int c = 0;
+    if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0) c = 256;
+    cus[dev] = (uint32_t)c;
+  }
+  return cus[dev];
+}
+
+// The header pass on a persistent grid (tcp_tx_hdr), `per_cu` waves per CU
+// (0: 24; tools/tx_struct_probe.py, 1M x 1460-B segments, both passes: 244.1
+// us at 24, 245.2 at 32, 245.6 at 16, 250.7 at 8, 254.6 at 4, against 248.3
+// for the one-shot header pass; profiles/r05/tx_hdr/), or the one-shot
+// kernel where tcp_tx_hdr's conditions do not hold.
+template <int SP>
+static hipError_t launch_header_pass(TxGeo h, hipStream_t stream, uint32_t per_cu) {
+  if (h.n == 0) return hipSuccess;
+  uint32_t grid = 0;
+  hipError_t e = tx_shape(h, 2, &grid);
+  if (e != hipSuccess) return e;
+  // the persistent kernel's conditions (tcp_tx_hdr): full TCP mode with whole
+  // write-back, tiles of <= 64 segments starting 16-B aligned, <= 4 KiB of
+  // slots each, d_out 4-B aligned
+  if (h.tile > 64 || (uint64_t)h.tile * h.slot > 4096 || ((uint64_t)h.tile * h.slot) % 16 || (h.hdr & 15) ||
+      !(h.mode & kTxTcpFull) || (h.mode & kTxFieldsOnly) || ((uintptr_t)h.out & 3) || h.xs == nullptr)
+    return launch_tcp_tx_t<16, 2, SP, 1, 0, 2>(h, stream);
+  const uint64_t tiles = (h.n + h.tile - 1) / h.tile;
+  const uint64_t waves = std::min<uint64_t>(tiles, (uint64_t)tx_cu_count() * (per_cu ? per_cu : 24u));
+  const uint32_t wgs = (uint32_t)((waves + h.wpg - 1) / h.wpg);
+  hipLaunchKernelGGL((tcp_tx_hdr<4, SP>), dim3(wgs), dim3(64 * h.wpg), (size_t)h.lds_wave * h.wpg, stream, h,
+                     (uint32_t)tiles);
+  return hipGetLastError();
+}
+
 // The production shape: a batch that needs its payload read takes two passes
 // when it has scratch for the payload values (g.xs): the payload pass streams
 // only payload, the header pass then reads, fills and writes back the slots
 // (interleaving the slot write-back with the payload stream
-// cost ~45 us on 1M segments).  One fused pass otherwise.
-template <int U, int AUX, int SP, int RED>
-static hipError_t launch_passes(TxGeo g, hipStream_t stream) {
+// cost ~45 us on 1M segments).  One fused pass otherwise.  HP: the header
+// pass persistent (tcp_tx_hdr) or one-shot (tcp_tx PH = 2).
+template <int U, int AUX, int SP, int RED, int HP = 1>
+static hipError_t launch_passes(TxGeo g, hipStream_t stream, uint32_t per_cu = 0) {
   if (!(g.mode & kTxTcpFull) || g.xs == nullptr) return launch_tcp_tx_t<U, AUX, SP, RED>(g, stream);
   TxGeo h = g;
   h.tile = g.htile;
   hipError_t e = launch_tcp_tx_t<U, AUX, SP, RED, 0, 1>(g, stream);
-  if (e == hipSuccess) e = launch_tcp_tx_t<U, AUX, SP, RED, 0, 2>(h, stream);
+  if (e == hipSuccess) e = HP ? launch_header_pass<SP>(h, stream, per_cu) : launch_tcp_tx_t<U, AUX, SP, RED, 0, 2>(h, stream);
   return e;
 }
 
@@ -451,6 +671,7 @@ hipError_t launch_tcp_tx(TxGeo g, hipStream_t stream, uint32_t variant) {
     case 1: g.xs = nullptr; return launch_tcp_tx_t<16, 2, 0, 1>(g, stream);  // one fused pass
     case 2: return launch_passes<16, 2, 1, 1>(g, stream);
     case 3: return launch_passes<16, 2, 0, 0>(g, stream);
+    case 4: return launch_passes<16, 2, 0, 1, 0>(g, stream);  // the one-shot header pass (round 4)
     default: return launch_passes<16, 2, 0, 1>(g, stream);
   }
 }

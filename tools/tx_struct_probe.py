@@ -5,8 +5,9 @@
                           descriptors, 48 MB), without / with the stores
   struct                  ns_csum_tcp_tx: the geometry, no table; a payload
                           pass, then a header pass writing the slots back whole
-  struct_v1..v3           its A/B variants (NS_CSUM_TX_VARIANT: one fused
-                          pass, nontemporal write-back, wave reductions)
+  struct_v1..v3           its A/B variants (ns_csum_set_tx_tuning variant: one
+                          fused pass, nontemporal write-back, wave reductions)
+  struct_hdr1shot         the header pass one-shot (round 4's), not persistent
   struct_pP_hH            P segments per wave in the payload pass, H in the
                           header pass (NS_CSUM_TX_TILE / _HTILE)
   struct_fields           2-byte field stores instead (NS_TX_FIELDS_ONLY)
@@ -57,19 +58,22 @@ def main():
     batches = [W.tx_split_batch(n, 7000 + r, dev)[0] for r in range(2)]
     pd = [torch.from_numpy(W.tx_split_desc(n, s, True).view(np.uint8).copy()).to(dev) for s in (True, False)]
 
+    _knob = {"NS_CSUM_TX_VARIANT": "variant", "NS_CSUM_TX_TILE": "tile", "NS_CSUM_TX_HTILE": "htile",
+             "NS_CSUM_TX_PASSES": "passes"}
+
     def env(k, v, k2=None, v2=None):
+        """A call with ns_csum_tcp_tx's A/B knobs set through
+        ns_csum_set_tx_tuning (the library reads the environment only at
+        ns_csum_init), reset to production after it."""
         def f(r, **kw):
-            keys = {k: v} if k2 is None else {k: v, k2: v2}
-            old = {x: os.environ.get(x) for x in keys}
-            os.environ.update(keys)
+            kn = {_knob[k]: int(v)}
+            if k2 is not None:
+                kn[_knob[k2]] = int(v2)
+            eng.set_tx_tuning(**kn)
             try:
                 eng.tcp_tx(batches[r], geo, stream=stream, **kw)
             finally:
-                for x, o in old.items():
-                    if o is None:
-                        del os.environ[x]
-                    else:
-                        os.environ[x] = o
+                eng.set_tx_tuning()
         return f
 
     from netstack_amd.engine import addr_sum
@@ -102,6 +106,7 @@ def main():
         "struct": lambda r: eng.tcp_tx(batches[r], geo, stream=stream),
         "struct_fused": env("NS_CSUM_TX_VARIANT", "1"),
         "struct_ntwb": env("NS_CSUM_TX_VARIANT", "2"),
+        "struct_hdr1shot": env("NS_CSUM_TX_VARIANT", "4"),
         "struct_fields": lambda r: eng.tcp_tx(batches[r], geo, stream=stream, fields_only=True),
         "struct_hdr_only": lambda r: eng.tcp_tx(batches[r], geo, stream=stream, mode="partial"),
         "txv_stream_t8": txv(5, 8),
@@ -113,6 +118,12 @@ def main():
         "txv_2p_u12": txv(8),
         "txv_2p_u16": txv(9),
         "txv_2p_u8": txv(10),
+        "txv_2p_hdr4": txv(12),
+        "txv_2p_hdr16": txv(13),
+        "txv_2p_hdr2": txv(14),
+        "txv_2p_1shot": txv(15),
+        "txv_2p_hdr24": txv(16),
+        "txv_2p_hdr32": txv(17),
         "struct_out": lambda r: eng.tcp_tx(batches[r], geo, out=out2, stream=stream),
         "struct_norot": lambda r: eng.tcp_tx(batches[0], geo, stream=stream),
         "struct_out_norot": lambda r: eng.tcp_tx(batches[0], geo, out=out2, stream=stream),
