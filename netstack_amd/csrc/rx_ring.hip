@@ -92,13 +92,12 @@ __device__ __forceinline__ uint32_t rx_row_wsum(const uint8_t* row, uint32_t x, 
   const uint32_t d0 = x >> 2;
   const uint32_t nd = len ? ((ye + 3) >> 2) - d0 : 0u;
   uint32_t w = 0;
-#pragma unroll
-  for (int k = 0; k < MAXD; ++k) {
-    if ((uint32_t)k < nd) {
-      const uint32_t o = 4u * (d0 + (uint32_t)k);
-      const uint32_t m = ((o - x) < len ? 0x0000FFFFu : 0u) | ((o + 2u - x) < len ? 0xFFFF0000u : 0u);
-      w = __builtin_amdgcn_sad_u16(D[d0 + k] & m, 0u, w);
-    }
+  // a wave-uniform trip count (the longest lane's), the lanes past their own
+  // end masked: no divergent branch per dword
+  for (uint32_t k = 0; k < MAXD && __builtin_amdgcn_ballot_w64(k < nd) != 0; ++k) {
+    const uint32_t o = 4u * (d0 + k);
+    const uint32_t m = ((o - x) < len ? 0x0000FFFFu : 0u) | ((o + 2u - x) < len ? 0xFFFF0000u : 0u);
+    w = __builtin_amdgcn_sad_u16(D[k < nd ? d0 + k : 0u] & m, 0u, w);
   }
   if ((y & 1u) && y > x) w += row[y - 1];  // a lone byte at an even offset: the low byte of its word
   return w;
@@ -149,11 +148,6 @@ __global__ __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(OCC))) 
   const uint32_t P = (!over && rlen > pre) ? rlen - pre : 0u;  // Data.Size()
   const uint32_t Pl = P < kMaxIp ? P : kMaxIp;                  // bytes any header can cover
   const uint64_t slot = g.ring + s * g.stride;
-  uint32_t etype = 0;  // issued before the payload loads: waiting for it waits for nothing else
-  if (g.link && P) {
-    const uint32_t e = *reinterpret_cast<const uint16_t*>((uintptr_t)(slot + g.frame_at + 12));
-    etype = ((e & 0xFFu) << 8) | (e >> 8);
-  }
 
   // Wave-relative 32-bit coordinates: one buffer resource from the 128-B
   // line of the wave's first packet over its slots (< 8 strides + a line).
@@ -178,11 +172,22 @@ __global__ __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(OCC))) 
 
   uint4 v[NB];
   v[0] = rx_load<A0>(rsrc, off_of(cl));
-#pragma unroll
-  for (int k = 1; k < NB; ++k) {
+  auto line = [&](int k) {
     if constexpr (F) v[k] = rx_load<AN>(rsrc, ((uint32_t)k <= klast ? cl1 : nrec) + 128u * k);
     else v[k] = rx_load<AN>(rsrc, off_of(cl + 128u * k));
+  };
+  line(1);
+  // The EtherType (the link header's bytes 12-13, pa - 2): a buffer load on
+  // a resource one line lower (pa - 2 may precede wbase), issued after the
+  // lines the parse reads, so waiting for it waits for nothing more.
+  uint32_t etype = 0;
+  if (g.link) {
+    const __amdgpu_buffer_rsrc_t re = rx_srd(wbase - 128u, nrec + 128u);
+    const uint32_t e = (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(re, (int)(P ? pa + 126u : nrec + 128u), 0, 0);
+    etype = ((e & 0xFFu) << 8) | ((e >> 8) & 0xFFu);
   }
+#pragma unroll
+  for (int k = 2; k < NB; ++k) line(k);
   uint32_t w2 = 0;  // F: every loaded chunk of lines >= 2
   if constexpr (F) {
 #pragma unroll
@@ -206,80 +211,44 @@ __global__ __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(OCC))) 
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 
-  // Parse (every lane of the group, same LDS bytes).  h(i) = IP byte i.
+  // Parse (every lane of the group, same LDS bytes).  h(i) = IP byte i.  The
+  // rules are evaluated side by side and combined with selects (one path for
+  // every packet kind: no divergent branches, few scalar instructions); every
+  // byte read lies in the row, and a field only decides anything where the
+  // rule that reads it has passed its length checks.
   auto h = [&](uint32_t i) -> uint32_t { return row[po + i]; };
   const uint32_t first = g.view0 && g.view0 < P ? g.view0 : P;  // the first view's length
-  uint32_t verdict = kMalformed, want = 0, kind = 0, hlen = 0, asz = 0, tsize = 0, proto = 0;
-  uint32_t a = 0, b = 0;  // the transport range [a, b); ICMP: its field [a + 2, a + 4) read as zero
-  bool v4 = false;
-  do {
-    if (P == 0) break;
-    const uint32_t ver = h(0) >> 4;
-    const uint32_t np = g.link ? (etype == 0x0800u ? 4u : etype == 0x86DDu ? 6u : 0u) : ver;
-    if (g.link && np == 0) {  // not IP: nothing the reference checksums
-      verdict = kUnchecked;
-      break;
-    }
-    uint32_t tend;
-    if (np == 4) {
-      if (first < 20) break;
-      hlen = (h(0) & 15u) * 4u;
-      const uint32_t tlen = (h(2) << 8) | h(3);
-      // hlen > first is not in IsValid (tests/golden/rx_choices.json)
-      if (hlen < 20 || hlen > tlen || tlen > P || hlen > first || ver != 4) break;
-      v4 = true;  // IPv4.CalculateChecksum (ipv4.go:251-253) is reported from here on
-      const uint32_t more = h(6) & 0x20u;
-      const uint32_t foff = ((((h(6) & 0x1Fu) << 8) | h(7)) << 3) & 0xFFFFu;
-      if (more || foff) {  // ipv4.go:355-385
-        const uint32_t size = tlen - hlen;
-        verdict = (size == 0 || ((foff + (size & 0xFFFFu) - 1u) & 0xFFFFu) < foff) ? kMalformed : kUnchecked;
-        break;
-      }
-      proto = h(9);
-      a = hlen;
-      tend = tlen;
-      asz = 8;
-    } else if (np == 6) {
-      if (first < 40) break;
-      const uint32_t plen = (h(4) << 8) | h(5);
-      if (plen > P - 40 || ver != 6) break;
-      proto = h(6);
-      a = 40;
-      tend = 40 + plen;
-      asz = 32;
-    } else {
-      break;  // a headerless link drops other versions
-    }
-    tsize = tend - a;
-    const uint32_t tfl = (first < tend ? first : tend) - a;  // the transport's first view
-    verdict = kUnchecked;
-    if (proto == 6) {  // segment.parse (segment.go:160-180)
-      const uint32_t off = (h(a + 12) >> 4) * 4u;
-      if (tfl < 20 || off < 20 || off > tfl) {
-        verdict = kMalformed;
-        break;
-      }
-      kind = 1;
-    } else if (proto == 1 && np == 4) {  // handleICMP: echo requests only
-      if (tfl < 8) {
-        verdict = kMalformed;
-        break;
-      }
-      if (h(a) != 8) break;
-      kind = 2;
-      want = (h(a + 2) << 8) | h(a + 3);
-    } else if (proto == 58 && np == 6) {  // ICMPv6Checksum
-      if (tfl < 4) {
-        verdict = kMalformed;
-        break;
-      }
-      kind = 3;
-      want = (h(a + 2) << 8) | h(a + 3);
-    } else {
-      break;
-    }
-    b = tend;
-  } while (false);
+  const uint32_t h0 = h(0), h2 = h(2), h3 = h(3), h4 = h(4), h5 = h(5), h6 = h(6), h7 = h(7), h9 = h(9);
+  const uint32_t ver = h0 >> 4;
+  const uint32_t np = g.link ? (etype == 0x0800u ? 4u : etype == 0x86DDu ? 6u : 0u) : ver;
+  // IPv4 HandlePacket + IsValid (ipv4.go:341-353, header/ipv4.go:280-296);
+  // hlen > first is not in IsValid (tests/golden/rx_choices.json)
+  const uint32_t hlen = (h0 & 15u) * 4u, tlen = (h2 << 8) | h3;
+  const bool v4 = P && np == 4 && first >= 20 && hlen >= 20 && hlen <= tlen && tlen <= P && hlen <= first && ver == 4;
+  const uint32_t foff = ((((h6 & 0x1Fu) << 8) | h7) << 3) & 0xFFFFu;
+  const bool frag = v4 && ((h6 & 0x20u) || foff);  // ipv4.go:355-385
+  const uint32_t fsize = (tlen - hlen) & 0xFFFFu;
+  const bool fragbad = tlen == hlen || ((foff + fsize - 1u) & 0xFFFFu) < foff;
+  // IPv6 HandlePacket + IsValid (ipv6.go:168-177, header/ipv6.go:207-222)
+  const uint32_t plen = (h4 << 8) | h5;
+  const bool v6 = P && np == 6 && first >= 40 && plen <= P - 40 && ver == 6;
+  const bool ip = (v4 && !frag) || v6;
+  const uint32_t proto = v4 ? h9 : h6;
+  const uint32_t a = v4 ? hlen : 40u;                  // the transport range [a, tend)
+  const uint32_t tend = v4 ? tlen : 40u + plen;
+  const uint32_t tsize = tend - a;
+  const uint32_t tfl = (first < tend ? first : tend) - a;  // the transport's first view
+  const uint32_t ta = h(a), toff = (h(a + 12) >> 4) * 4u;
+  const uint32_t want = (h(a + 2) << 8) | h(a + 3);
+  const bool tcp = ip && proto == 6, icmp4 = ip && v4 && proto == 1, icmp6 = ip && !v4 && proto == 58;
+  const bool tcp_bad = tfl < 20 || toff < 20 || toff > tfl;  // segment.parse (segment.go:160-180)
+  // kind: 1 TCP, 2 ICMPv4 echo request (handleICMP, icmp.go:60-80), 3 ICMPv6
+  const uint32_t kind = tcp && !tcp_bad ? 1u : icmp4 && tfl >= 8 && ta == 8 ? 2u : icmp6 && tfl >= 4 ? 3u : 0u;
+  const bool malformed = !P || (g.link ? np != 0 && !v4 && !v6 : !v4 && !v6) || (frag && fragbad) ||
+                         (tcp && tcp_bad) || (icmp4 && tfl < 8) || (icmp6 && tfl < 4);
+  uint32_t verdict = malformed ? kMalformed : kUnchecked;  // the checked kinds are decided below
+  const uint32_t b = kind ? tend : 0u;
+  const uint32_t asz = v4 ? 8u : 32u;
 
   // The transport range splits at 16-B chunk boundaries (offsets r with
   // (r + po) % 16 == 0) into a head [hx, min(b, A)) summed from the LDS row
@@ -311,7 +280,7 @@ __global__ __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(OCC))) 
   const bool wslow = F && __builtin_amdgcn_ballot_w64(slow) != 0;
   uint32_t tail = 0;
   if (li == 3 && kind && b > B && B >= A) {  // bytes [B, b): one 16-B chunk, an L2 hit
-    const uint4 t = *reinterpret_cast<const uint4*>((uintptr_t)(wbase + pa + B));
+    const uint4 t = rx_load<0>(rsrc, pa + B);  // a buffer load: no wait on the LDS traffic
     const int c = (int)(b - B);
     tail = rx_wsum4(make_uint4(t.x & rx_below(c), t.y & rx_below(c - 4), t.z & rx_below(c - 8),
                                t.w & rx_below(c - 12)));

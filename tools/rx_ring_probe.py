@@ -43,6 +43,9 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--n", type=int, default=1 << 20)
     ap.add_argument("--only", default="")
+    ap.add_argument("--prev", default="",
+                    help="a variants library built from an earlier rx_ring.hip: its product shape is timed "
+                         "beside the others as 'prev' (an A/B on one box)")
     ap.add_argument("--trend", type=int, default=0,
                     help="then time this many back-to-back launches of the product one by one (run-long drift)")
     args = ap.parse_args()
@@ -64,29 +67,38 @@ def main():
               n, 0, 0, 0)
     algo = n * (W.RX_PKT + 9)
     ks = [int(k) for k in args.only.split(",")] if args.only else sorted(NAMES)
+    libs = {k: lib for k in ks}
+    names = dict(NAMES)
+    if args.prev:
+        plib = ctypes.CDLL(os.path.abspath(args.prev))
+        plib.rxv_launch.argtypes = lib.rxv_launch.argtypes
+        plib.rxv_launch.restype = ctypes.c_int
+        ks.append(-1)
+        libs[-1] = plib
+        names[-1] = "prev"
     res = {k: [] for k in ks}
     ok = {}
     for k in ks:  # parity first
         verdict.fill_(0xEE)
         sums.fill_(0x1234)
-        assert lib.rxv_launch(ctypes.byref(g), stream.cuda_stream, k) == 0
+        assert libs[k].rxv_launch(ctypes.byref(g), stream.cuda_stream, max(k, 0)) == 0
         torch.cuda.synchronize()
         ok[k] = bool(torch.equal(verdict, v0) and torch.equal(sums, s0))
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     for _ in range(args.rounds):
         for k in ks:
             for _ in range(3):
-                lib.rxv_launch(ctypes.byref(g), stream.cuda_stream, k)
+                libs[k].rxv_launch(ctypes.byref(g), stream.cuda_stream, max(k, 0))
             ev[0].record(stream)
             for _ in range(args.reps):
-                lib.rxv_launch(ctypes.byref(g), stream.cuda_stream, k)
+                libs[k].rxv_launch(ctypes.byref(g), stream.cuda_stream, max(k, 0))
             ev[1].record(stream)
             torch.cuda.synchronize()
             res[k].append(ev[0].elapsed_time(ev[1]) * 1e3 / args.reps)
     out = {}
     for k in ks:
         us = float(np.median(res[k]))
-        out[NAMES[k]] = {"us": round(us, 2), "min_us": round(min(res[k]), 2), "frac": round(algo / us / 1e3 / 8000, 4),
+        out[names[k]] = {"us": round(us, 2), "min_us": round(min(res[k]), 2), "frac": round(algo / us / 1e3 / 8000, 4),
                          "parity": ok[k]}
     trend = None
     if args.trend:
