@@ -88,7 +88,8 @@ def main():
     TXV = ctypes.CDLL(os.path.join(ROOT, "netstack_amd", "lib", "libns_txv.so"))
     TXV.txv_launch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
 
-    xs = torch.empty(n, dtype=torch.int16, device=dev)
+    xs = torch.zeros(n, dtype=torch.int16, device=dev)
+    sink = torch.zeros(4, dtype=torch.int32, device=dev)
 
     def txv(k, tile=0):
         def f(r):
@@ -96,7 +97,8 @@ def main():
             t = TxGeo(hdr=a.data_ptr() + geo["hdr_off"], pay=a.data_ptr() + geo["pay_off"], size=geo["size"], n=n,
                       mss=geo["mss"], slot=geo["slot"], tile=tile, ip_at=geo["ip_at"], ip_len=geo["ip_len"],
                       tcp_at=geo["tcp_at"], tcp_len=geo["tcp_len"], addr_sum=addr_sum(geo["src"], geo["dst"]),
-                      proto=6, mode=3, xs=xs.data_ptr() if k >= 8 else None, xstride=1)
+                      proto=6, mode=3, xs=xs.data_ptr() if k >= 8 else None, xstride=1,
+                      out=sink.data_ptr() if k >= 19 else None)
             assert TXV.txv_launch(ctypes.byref(t), stream.cuda_stream, k) == 0
         return f
 
@@ -124,6 +126,16 @@ def main():
         "txv_2p_1shot": txv(15),
         "txv_2p_hdr24": txv(16),
         "txv_2p_hdr32": txv(17),
+        "txv_hdr_pass": txv(18),
+        "floor_slots_rw": txv(19),
+        "floor_slots_rd": txv(20),
+        "floor_slots_wr": txv(21),
+        "floor_slots_wr_a1": txv(22),
+        "floor_slots_wr_a2": txv(23),
+        "floor_slots_wr_a3": txv(24),
+        "floor_slots_rw_a1": txv(25),
+        "floor_slots_rw_a2": txv(26),
+        "floor_slots_rw_a3": txv(27),
         "struct_out": lambda r: eng.tcp_tx(batches[r], geo, out=out2, stream=stream),
         "struct_norot": lambda r: eng.tcp_tx(batches[0], geo, stream=stream),
         "struct_out_norot": lambda r: eng.tcp_tx(batches[0], geo, out=out2, stream=stream),
@@ -136,7 +148,8 @@ def main():
     checks = {}
     want = W.tx_split_expected(n, 7000, dev)
     for name, f in variants.items():
-        if name.endswith("_rx") or name in ("struct_hdr_only", "txv_noreduce") or "nowb" in name or "stream" in name:
+        if name.endswith("_rx") or name in ("struct_hdr_only", "txv_noreduce") or "nowb" in name or "stream" in name \
+                or name.startswith(("floor_", "txv_hdr_pass")):
             continue
         h = batches[0][:n * W.TX_HDR].view(n, W.TX_HDR)
         h[:, W.TX_IP_AT + 10:W.TX_IP_AT + 12] = 0
