@@ -300,15 +300,26 @@ void bump_max(std::atomic<uint64_t>& m, uint64_t v) {
 
 }  // namespace
 
+// The host-batch pipeline's shape: chunks in flight and descriptors per chunk
+// (cfg3, 1M x 64 B, two slots: 64K 3.11 ms, 128K 2.18, 256K 2.16, 512K 2.52
+// ms per call).
+constexpr uint32_t kMaxHostSlots = 4;
+constexpr uint32_t kHostSlots = 2;
+constexpr uint32_t kHostChunkDesc = 1u << 17;
+
 struct ns_csum_ctx {
   int device = 0;
   uint64_t staging = kDefaultStaging;
   // The host-batch DMA pipeline (ns_csum_batch_host, gathers above
-  // kZeroCopyMax): its two streams, slots and g_arena, under pmu.  It never
+  // kZeroCopyMax): its streams, slots and g_arena, under pmu.  It never
   // takes mu, so a 1.5 GB host batch does not hold up the zero-copy passes
   // of small synchronous calls (a 29 ms head-of-line block).
-  hipStream_t stream[2] = {nullptr, nullptr};
-  hipEvent_t done[2] = {nullptr, nullptr};
+  // nslots chunks in flight (one stream each), chunk_desc descriptors per
+  // chunk at most: set once at init (NS_CSUM_HOST_SLOTS / _CHUNK, A/B only).
+  uint32_t nslots = kHostSlots;
+  uint32_t chunk_desc = kHostChunkDesc;
+  hipStream_t stream[kMaxHostSlots] = {};
+  hipEvent_t done[kMaxHostSlots] = {};
   std::mutex pmu;
   // Zero-copy passes and ns_csum_sync run on zstream, a stream of their own
   // (at the greatest priority like the pipeline's: a hardware queue apart
@@ -326,13 +337,13 @@ struct ns_csum_ctx {
   MappedPin err_taken;
   // host-path slots (double-buffered)
   ChainBuf z_chain;  // a chained zero-copy pass's scratch
-  // host-path slots (double-buffered; pmu)
-  DevBuf<uint8_t> d_arena[2];
-  DevBuf<ns_pkt_desc> d_desc[2];
-  DevBuf<uint16_t> d_out[2];
-  ChainBuf d_chain[2];
-  PinBuf<ns_pkt_desc> h_desc[2];
-  PinBuf<uint16_t> h_out[2];
+  // host-path slots (nslots in flight; pmu)
+  DevBuf<uint8_t> d_arena[kMaxHostSlots];
+  DevBuf<ns_pkt_desc> d_desc[kMaxHostSlots];
+  DevBuf<uint16_t> d_out[kMaxHostSlots];
+  ChainBuf d_chain[kMaxHostSlots];
+  PinBuf<ns_pkt_desc> h_desc[kMaxHostSlots];
+  PinBuf<uint16_t> h_out[kMaxHostSlots];
   // zero-copy pass buffers for small calls: the table (read by the kernel),
   // the results and the completion word (written by it)
   BarBuf z_buf;
@@ -673,11 +684,9 @@ int submit_small(ns_csum_ctx* ctx, SmallReq* req) {
 }
 
 // Host batch core, caller holds ctx->pmu and the device guard.  Pipelines
-// chunks of the descriptor table over the two slots/streams: H2D of chunk k+1
-// overlaps the kernel of chunk k.  Chunks never split a NS_DESC_CONT run.
-// Descriptors per host-pipeline chunk (cfg3, 1M x 64 B: 64K 3.11 ms, 128K
-// 2.18, 256K 2.16, 512K 2.52 ms per call).
-constexpr uint32_t kHostChunkDesc = 1u << 17;
+// chunks of the descriptor table over the context's slots/streams: H2D of
+// chunk k+1 overlaps the kernel of chunk k.  Chunks never split a
+// NS_DESC_CONT run.
 
 // Whether [p, p + bytes) is page-locked host memory the DMA engines read
 // directly (hipHostMalloc, hipHostRegister, torch pin_memory).  A pageable
@@ -709,12 +718,13 @@ int run_host_batch(ns_csum_ctx* ctx, const uint8_t* h_arena, uint64_t arena_byte
   struct Pending {
     bool live = false;
     uint32_t first = 0, count = 0;
-  } pend[2];
+  } pend[kMaxHostSlots];
+  const uint32_t nslots = ctx->nslots;
   // Drain whatever is in flight (on an error return too: the staging
   // buffers must be idle before the next call reuses them).
   auto drain = [&](int slot) -> int {
-    for (int s = 0; s < 2; ++s) {
-      const int sl = slot ^ s ^ 1;  // older chunk first
+    for (uint32_t s = 0; s < nslots; ++s) {
+      const int sl = (int)((slot + s) % nslots);
       if (pend[sl].live) {
         HIP_TRY(hipEventSynchronize(ctx->done[sl]));
         std::memcpy(h_out + pend[sl].first, ctx->h_out[sl].p, pend[sl].count * sizeof(uint16_t));
@@ -733,7 +743,7 @@ int run_host_batch(ns_csum_ctx* ctx, const uint8_t* h_arena, uint64_t arena_byte
     // (profiles/r01/bench_host3.json).
     uint32_t cut = k;
     uint64_t cut_lo = 0, cut_hi = 0;
-    const int crc = nsh::cut_chunk(h_desc, n, k, arena_bytes, budget, kHostChunkDesc, chained, &cut, &cut_lo,
+    const int crc = nsh::cut_chunk(h_desc, n, k, arena_bytes, budget, ctx->chunk_desc, chained, &cut, &cut_lo,
                                    &cut_hi);
     if (crc != NS_OK) {
       const int rc = drain(slot);
@@ -788,7 +798,7 @@ int run_host_batch(ns_csum_ctx* ctx, const uint8_t* h_arena, uint64_t arena_byte
     pend[slot].first = k;
     pend[slot].count = cnt;
     k = cut;
-    slot ^= 1;
+    slot = (int)((slot + 1) % nslots);
   }
   return drain(slot);
 }
@@ -1049,8 +1059,17 @@ int ns_csum_init(const ns_csum_opts* opts, ns_csum_ctx** out) {
   }
   (void)least;
   if (std::getenv("NS_CSUM_NORMAL_PRIORITY")) greatest = 0;
+  // the pipeline's shape (A/B diagnostics; read here once, never per call)
+  if (const char* v = std::getenv("NS_CSUM_HOST_SLOTS")) {
+    const long x = std::strtol(v, nullptr, 10);
+    if (x >= 1 && x <= (long)kMaxHostSlots) ctx->nslots = (uint32_t)x;
+  }
+  if (const char* v = std::getenv("NS_CSUM_HOST_CHUNK")) {
+    const long x = std::strtol(v, nullptr, 10);
+    if (x >= 1024 && x <= (1l << 22)) ctx->chunk_desc = (uint32_t)x;
+  }
   hipError_t e = hipSuccess;
-  for (int s = 0; s < 2 && e == hipSuccess; ++s) {
+  for (uint32_t s = 0; s < ctx->nslots && e == hipSuccess; ++s) {
     e = hipStreamCreateWithPriority(&ctx->stream[s], hipStreamNonBlocking, greatest);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->done[s], hipEventDisableTiming);
   }
@@ -1092,7 +1111,7 @@ void ns_csum_destroy(ns_csum_ctx* ctx) {
   if (!ctx) return;
   {
     DeviceGuard g(ctx->device);
-    for (int s = 0; s < 2; ++s)
+    for (uint32_t s = 0; s < kMaxHostSlots; ++s)
       if (ctx->stream[s]) (void)hipStreamSynchronize(ctx->stream[s]);
     if (ctx->zstream) (void)hipStreamSynchronize(ctx->zstream);
     ctx->scratch.clear([&](StreamScratch* sc) { retire_scratch(ctx, sc); });
@@ -1117,7 +1136,7 @@ void ns_csum_destroy(ns_csum_ctx* ctx) {
     }
     ctx->gstage_all.clear();
     ctx->gstage_free.clear();
-    for (int s = 0; s < 2; ++s) {
+    for (uint32_t s = 0; s < kMaxHostSlots; ++s) {
       ctx->d_arena[s].release();
       ctx->d_desc[s].release();
       ctx->d_out[s].release();
@@ -1421,7 +1440,7 @@ int ns_csum_tcp_tx_multi(ns_csum_ctx* ctx, uint8_t* d_arena, uint64_t arena_byte
 }
 
 int ns_csum_set_tx_tuning(ns_csum_ctx* ctx, uint32_t variant, uint32_t tile, uint32_t htile, uint32_t passes) {
-  if (!ctx || variant > 4 || passes > 2) return NS_EINVAL;
+  if (!ctx || variant > 5 || passes > 2) return NS_EINVAL;
   ctx->tx_variant = variant;
   ctx->tx_tile = tile;
   ctx->tx_htile = htile;

@@ -577,6 +577,101 @@ static hipError_t launch_tcp_tx_t(TxGeo g, hipStream_t stream) {
   return hipGetLastError();
 }
 
+// The payload pass in the receive ring's shape (rx_ring.hip; round 5): a wave
+// takes 8 consecutive segments, one 8-lane group per segment, and the group's
+// load instruction k reads its segment's k-th 128-B line whole (lane i: 16 B
+// at line + 16 i), line 0 with the default policy (its first bytes belong to
+// the segment before), the others nontemporal.  The segment's byte range
+// alone decides which chunks exist, so all NB loads are issued at once; a
+// chunk past the segment reads the buffer resource's out-of-range zeros.
+// Every loaded chunk is summed whole (4 v_sad_u16) except two: the chunk
+// holding the segment's first byte is masked below it, and the chunk holding
+// its last byte is re-read (an L2 hit, issued with the others) by the lane
+// that loaded it, which takes the bytes past the end back out.  One 3-step
+// DPP reduction gives the group its W; lane 0 writes the payload value.  No
+// LDS, no cross-group step, no per-window segment bookkeeping.
+__device__ __forceinline__ uint32_t tx_bytes_from(const uint4 v, int c) {  // W of bytes [c, 16)
+  return wsum4(make_uint4(v.x & ~below(c), v.y & ~below(c - 4), v.z & ~below(c - 8), v.w & ~below(c - 12)), 0u);
+}
+
+template <int NB>
+__global__ __launch_bounds__(256) void tcp_tx_pay(TxGeo g) {
+  const uint32_t lane = threadIdx.x & 63u, grp = lane >> 3, li = lane & 7u;
+  const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t s0 = ((uint64_t)blockIdx.x * 4u + wv) * 8u;  // the wave's first segment
+  if (s0 >= g.n) return;  // a whole wave leaves together
+  const uint64_t s = s0 + grp;
+  const uint64_t tail0 = (g.n - 1) * (uint64_t)g.mss;  // where the last segment starts
+  const uint32_t sz = s < g.n ? (s + 1 < g.n ? g.mss : (uint32_t)(g.size - tail0)) : 0u;
+  // wave-relative 32-bit coordinates: one resource over the wave's bytes
+  // (< 8 * 65,535 + 128)
+  const uint64_t wbase = (g.pay + s0 * g.mss) & ~127ull;
+  const uint64_t s_end = s0 + 8u < g.n ? s0 + 8u : g.n;
+  const uint64_t w_end = g.pay + (s_end < g.n ? s_end * (uint64_t)g.mss : g.size);
+  const uint32_t nrec = (uint32_t)(w_end - wbase);
+  const __amdgpu_buffer_rsrc_t r = tx_srd(wbase, nrec);
+  const uint32_t pa = sz ? (uint32_t)(g.pay + s * g.mss - wbase) : 0u;  // the segment's first byte
+  const uint32_t pe = pa + sz;
+  const uint32_t cl = (pa & ~127u) + 16u * li;  // lane li's chunk of line 0
+  // lines k >= 1 start past pa: the lane's chunk there holds segment bytes
+  // iff it starts before pe (k <= klast)
+  const uint32_t klast = sz && pe > cl ? (pe - 1u - cl) >> 7 : 0u;
+  const uint32_t cl1 = sz && pe > cl + 128u ? cl : nrec;
+  const bool in0 = sz && cl + 16u > pa && cl < pe;
+  // the chunk holding the last byte, re-read by the lane that loads it
+  const uint32_t tc = (pe - 1u) & ~15u;
+  const bool owner = sz && ((tc >> 4) & 7u) == li;
+  uint4 v[NB];
+  v[0] = tx_load<0>(r, in0 ? cl : nrec);
+  const uint4 t = tx_load<0>(r, owner ? tc : nrec);
+#pragma unroll
+  for (int k = 1; k < NB; ++k) v[k] = tx_load<2>(r, ((uint32_t)k <= klast ? cl1 : nrec) + 128u * k);
+  uint32_t w = tx_bytes_from(v[0], pa > cl ? (int)(pa - cl) : 0);
+#pragma unroll
+  for (int k = 1; k < NB; ++k) w = wsum4(v[k], w);
+  // segments longer than NB lines: the rest in batches of 4 lines
+  for (uint32_t k0 = NB; __builtin_amdgcn_ballot_w64(k0 <= klast) != 0; k0 += 4) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) w = wsum4(tx_load<2>(r, ((k0 + k) <= klast ? cl1 : nrec) + 128u * (k0 + k)), w);
+  }
+  // the bytes [pe, tc + 16) were summed whole with the last chunk (none when
+  // pe ends a chunk); the first chunk's bytes below pa were masked, so if it
+  // is also the last, what is taken out lies above pa
+  if (owner) w -= tx_bytes_from(t, (int)(pe - tc));
+  w += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)w, 0xB1, 0xF, 0xF, false);   // quad_perm 1,0,3,2
+  w += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)w, 0x4E, 0xF, 0xF, false);   // quad_perm 2,3,0,1
+  w += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)w, 0x141, 0xF, 0xF, false);  // row_half_mirror
+  if (li == 0 && s < g.n) g.xs[s * g.xstride] = (uint16_t)tx_class(w, (uint32_t)((g.pay + s * g.mss) & 1u));
+}
+
+// Lines per load batch for a segment of `mss` bytes from any offset.
+static int tx_pay_lines(uint32_t mss) {
+  const uint64_t lines = ((uint64_t)mss + 127 + 127) / 128;
+  return lines <= 2 ? 2 : lines <= 4 ? 4 : lines <= 8 ? 8 : lines <= 13 ? 13 : 16;
+}
+
+template <int NB>
+static hipError_t launch_tx_pay_t(const TxGeo& g, hipStream_t stream) {
+  const uint64_t wgs = (g.n + 31) / 32;  // 4 waves x 8 segments
+  hipLaunchKernelGGL((tcp_tx_pay<NB>), dim3((uint32_t)wgs), dim3(256), 0, stream, g);
+  return hipGetLastError();
+}
+
+// The payload pass: the group shape above, or tcp_tx PH = 1 (GP = 0, the
+// round-4 shape, kept for A/B).
+template <int U, int AUX, int SP, int RED, int GP = 1>
+static hipError_t launch_payload_pass(const TxGeo& g, hipStream_t stream) {
+  if (g.n == 0) return hipSuccess;
+  if (!GP || (g.n + 31) / 32 >= (1ull << 31)) return launch_tcp_tx_t<U, AUX, SP, RED, 0, 1>(g, stream);
+  switch (tx_pay_lines(g.mss)) {
+    case 2: return launch_tx_pay_t<2>(g, stream);
+    case 4: return launch_tx_pay_t<4>(g, stream);
+    case 8: return launch_tx_pay_t<8>(g, stream);
+    case 13: return launch_tx_pay_t<13>(g, stream);
+    default: return launch_tx_pay_t<16>(g, stream);
+  }
+}
+
 // Compute units of the current device (cached per device ordinal).
 static uint32_t tx_cu_count() {
   static uint32_t cus[64] = {};
@@ -621,12 +716,12 @@ static hipError_t launch_header_pass(TxGeo h, hipStream_t stream, uint32_t per_c
 // (interleaving the slot write-back with the payload stream
 // cost ~45 us on 1M segments).  One fused pass otherwise.  HP: the header
 // pass persistent (tcp_tx_hdr) or one-shot (tcp_tx PH = 2).
-template <int U, int AUX, int SP, int RED, int HP = 1>
+template <int U, int AUX, int SP, int RED, int HP = 1, int GP = 1>
 static hipError_t launch_passes(TxGeo g, hipStream_t stream, uint32_t per_cu = 0) {
   if (!(g.mode & kTxTcpFull) || g.xs == nullptr) return launch_tcp_tx_t<U, AUX, SP, RED>(g, stream);
   TxGeo h = g;
   h.tile = g.htile;
-  hipError_t e = launch_tcp_tx_t<U, AUX, SP, RED, 0, 1>(g, stream);
+  hipError_t e = launch_payload_pass<U, AUX, SP, RED, GP>(g, stream);
   if (e == hipSuccess) e = HP ? launch_header_pass<SP>(h, stream, per_cu) : launch_tcp_tx_t<U, AUX, SP, RED, 0, 2>(h, stream);
   return e;
 }
@@ -672,6 +767,7 @@ hipError_t launch_tcp_tx(TxGeo g, hipStream_t stream, uint32_t variant) {
     case 2: return launch_passes<16, 2, 1, 1>(g, stream);
     case 3: return launch_passes<16, 2, 0, 0>(g, stream);
     case 4: return launch_passes<16, 2, 0, 1, 0>(g, stream);  // the one-shot header pass (round 4)
+    case 5: return launch_passes<16, 2, 0, 1, 1, 0>(g, stream);  // the windowed payload pass (round 4)
     default: return launch_passes<16, 2, 0, 1>(g, stream);
   }
 }

@@ -68,7 +68,7 @@ def _arena(total, geo, seed):
     return a
 
 
-def _run(engine, a, geo, mode="full", fields_only=False, tile=None, offset=0, htile=None, passes=None):
+def _run(engine, a, geo, mode="full", fields_only=False, tile=None, offset=0, htile=None, passes=None, variant=0):
     import torch
 
     buf = torch.empty(offset + a.size, dtype=torch.uint8, device="cuda")
@@ -77,7 +77,7 @@ def _run(engine, a, geo, mode="full", fields_only=False, tile=None, offset=0, ht
     n = -(-geo["size"] // geo["mss"])
     out = torch.full((2 * n,), -1, dtype=torch.int16, device="cuda")
     # the A/B knobs go through ns_csum_set_tx_tuning (never the environment)
-    engine.set_tx_tuning(tile=tile or 0, htile=htile or 0, passes=passes or 0)
+    engine.set_tx_tuning(variant=variant, tile=tile or 0, htile=htile or 0, passes=passes or 0)
     try:
         engine.tcp_tx(arena, geo, out=out, mode=mode, fields_only=fields_only)
         torch.cuda.synchronize()
@@ -102,15 +102,17 @@ def _check(got_arena, got_sums, want_arena, want_sums, what):
 
 @pytest.mark.parametrize("name", sorted(CASES))
 def test_geometry_bit_exact(engine, oracle_mod, name):
-    """Each geometry in both shapes: one fused pass (what batches below
-    kTxTwoPassMinBytes take) and the payload + header passes."""
+    """Each geometry in every shape: one fused pass (what batches below
+    kTxTwoPassMinBytes take), the payload + header passes (the payload pass
+    in 8-lane groups, one segment each), and the same with round 4's
+    windowed payload pass (variant 5)."""
     geo, total = CASES[name]
     a = _arena(total, geo, seed=len(name))
     wa, ws = _want(oracle_mod, a, geo)
-    for passes in (1, 2):
+    for passes, variant in ((1, 0), (2, 0), (2, 5)):
         for offset in (0, 5):
-            ga, gs = _run(engine, a, geo, offset=offset, passes=passes)
-            _check(ga, gs, wa, ws, f"{name} ({passes} passes, arena at +{offset})")
+            ga, gs = _run(engine, a, geo, offset=offset, passes=passes, variant=variant)
+            _check(ga, gs, wa, ws, f"{name} ({passes} passes, variant {variant}, arena at +{offset})")
 
 
 @pytest.mark.parametrize("tile", [1, 2, 7, 31, 32, 33, 64])
@@ -119,9 +121,10 @@ def test_forced_tiles(engine, oracle_mod, tile):
         geo, total = CASES[name]
         a = _arena(total, geo, seed=tile)
         wa, ws = _want(oracle_mod, a, geo)
-        for passes in (1, 2):
-            ga, gs = _run(engine, a, geo, tile=tile, passes=passes)
-            _check(ga, gs, wa, ws, f"{name} tile {tile}, {passes} passes")
+        # (the tile is the fused pass's and the windowed payload pass's)
+        for passes, variant in ((1, 0), (2, 5)):
+            ga, gs = _run(engine, a, geo, tile=tile, passes=passes, variant=variant)
+            _check(ga, gs, wa, ws, f"{name} tile {tile}, {passes} passes, variant {variant}")
 
 
 @pytest.mark.parametrize("htile", [1, 3, 64, 100, 129, 222])

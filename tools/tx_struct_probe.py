@@ -91,6 +91,18 @@ def main():
     xs = torch.zeros(n, dtype=torch.int16, device=dev)
     sink = torch.zeros(4, dtype=torch.int32, device=dev)
 
+    big = []
+
+    def txv_big(k):
+        """A floor kernel (19-27) over 1 GiB of its own: the asymptotic rate
+        of the same access shape."""
+        def f(r):
+            if not big:
+                big.append(torch.zeros(1 << 30, dtype=torch.uint8, device=dev))
+            t = TxGeo(hdr=big[0].data_ptr(), n=(1 << 30) // geo["slot"], slot=geo["slot"], out=sink.data_ptr())
+            assert TXV.txv_launch(ctypes.byref(t), stream.cuda_stream, k) == 0
+        return f
+
     def txv(k, tile=0):
         def f(r):
             a = batches[r]
@@ -109,6 +121,9 @@ def main():
         "struct_fused": env("NS_CSUM_TX_VARIANT", "1"),
         "struct_ntwb": env("NS_CSUM_TX_VARIANT", "2"),
         "struct_hdr1shot": env("NS_CSUM_TX_VARIANT", "4"),
+        "struct_winpay": env("NS_CSUM_TX_VARIANT", "5"),
+        "txv_pay_group": txv(28),
+        "txv_pay_window": txv(29),
         "struct_fields": lambda r: eng.tcp_tx(batches[r], geo, stream=stream, fields_only=True),
         "struct_hdr_only": lambda r: eng.tcp_tx(batches[r], geo, stream=stream, mode="partial"),
         "txv_stream_t8": txv(5, 8),
@@ -133,6 +148,10 @@ def main():
         "floor_slots_wr_a1": txv(22),
         "floor_slots_wr_a2": txv(23),
         "floor_slots_wr_a3": txv(24),
+        "floor_1g_rw": txv_big(19),
+        "floor_1g_rd": txv_big(20),
+        "floor_1g_wr": txv_big(21),
+        "floor_1g_wr_a2": txv_big(23),
         "floor_slots_rw_a1": txv(25),
         "floor_slots_rw_a2": txv(26),
         "floor_slots_rw_a3": txv(27),

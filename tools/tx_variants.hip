@@ -14,7 +14,8 @@
 //   19 / 20 / 21 = floors over the header slots' bytes [hdr, hdr + n slot):
 //   copied onto themselves (read + write), read only, written only (16-B
 //   lane accesses, 4 per lane, one-shot grid); 22-24 / 25-27 = written only /
-//   copied with store cache policy 1 / 2 / 3.
+//   copied with store cache policy 1 / 2 / 3; 28 / 29 = the payload pass
+//   alone, in 8-lane groups (product) / windowed (round 4).
 // Not part of the product ABI.
 #include "../netstack_amd/csrc/tcp_tx.hip"
 
@@ -94,6 +95,8 @@ extern "C" int txv_launch(const nsk::TxGeo* g, void* stream, int k) {
     case 25: e = launch_floor<0, 1>(*g, s); break;
     case 26: e = launch_floor<0, 2>(*g, s); break;
     case 27: e = launch_floor<0, 3>(*g, s); break;
+    case 28: e = nsk::launch_payload_pass<16, 2, 0, 1, 1>(*g, s); break;
+    case 29: e = nsk::launch_payload_pass<16, 2, 0, 1, 0>(*g, s); break;
     default: e = nsk::launch_tcp_tx_t<16, 2, 0, 1>(*g, s); break;
   }
   return (int)e;
