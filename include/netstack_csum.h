@@ -151,9 +151,13 @@ typedef struct ns_csum_ctx ns_csum_ctx;
 
 typedef struct ns_csum_opts {
   int32_t device;          /* HIP device ordinal                            */
-  uint32_t flags;          /* reserved, 0                                   */
+  uint32_t flags;          /* 0, or NS_OPT_* below (others: NS_EINVAL)      */
   uint64_t staging_bytes;  /* pinned host staging per buffer (0 = 64 MiB)   */
 } ns_csum_opts;
+/* Tests only: chained batches fold their runs with no look-back, every
+ * block deriving its carry-in by walking its run (the path a block takes
+ * when a predecessor is not running).  Results are the same.               */
+#define NS_OPT_FOLD_WALK 0x1u
 
 int ns_csum_abi_version(void);
 /* hipError_t of the last failed HIP call on this thread (0 if none); set

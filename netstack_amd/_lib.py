@@ -33,6 +33,7 @@ NS_DESC_STORE_RAW = 0x8
 NS_DESC_STORE_SHIFT = 4
 NS_BATCH_CHAINED = 0x1
 NS_BATCH_PAIRED = 0x2
+NS_OPT_FOLD_WALK = 0x1
 
 # Every symbol include/netstack_csum.h declares (checked by the CPU tests).
 EXPORTED = (

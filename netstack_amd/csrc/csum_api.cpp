@@ -207,7 +207,7 @@ struct ChainBuf {
     if (rc == NS_OK) rc = status.ensure_async((size_t)nsk::chain_blocks(n), true, s);
     return rc;
   }
-  nsk::ChainScratch get() const { return nsk::ChainScratch{part.p, status.p}; }
+  nsk::ChainScratch get(bool walk = false) const { return nsk::ChainScratch{part.p, status.p, walk}; }
   void release() {
     part.release();
     status.release();
@@ -309,6 +309,7 @@ constexpr uint32_t kHostChunkDesc = 1u << 17;
 
 struct ns_csum_ctx {
   int device = 0;
+  bool fold_walk = false;  // NS_OPT_FOLD_WALK
   uint64_t staging = kDefaultStaging;
   // The host-batch DMA pipeline (ns_csum_batch_host, gathers above
   // kZeroCopyMax): its streams, slots and g_arena, under pmu.  It never
@@ -343,7 +344,10 @@ struct ns_csum_ctx {
   DevBuf<uint16_t> d_out[kMaxHostSlots];
   ChainBuf d_chain[kMaxHostSlots];
   PinBuf<ns_pkt_desc> h_desc[kMaxHostSlots];
-  PinBuf<uint16_t> h_out[kMaxHostSlots];
+  // results: written by the kernel straight into mapped pinned memory (no
+  // D2H copy on the DMA engine; NS_CSUM_HOST_D2H=1 copies them instead, A/B)
+  PinBuf<uint16_t, hipHostMallocMapped | hipHostMallocNonCoherent | hipHostMallocPortable> h_out[kMaxHostSlots];
+  bool host_d2h = false;
   // zero-copy pass buffers for small calls: the table (read by the kernel),
   // the results and the completion word (written by it)
   BarBuf z_buf;
@@ -552,7 +556,7 @@ int run_zero_copy(ns_csum_ctx* ctx, SmallReq* const* reqs, size_t nreq) {
   if (self) zc = nsk::ZcSignal{ctx->z_ctr.p, done_dev, seq};
   HIP_TRY(nsk::launch_batch(nullptr, kWholeSpace, ctx->z_buf.dev, (uint32_t)nd,
                             reinterpret_cast<uint16_t*>(ctx->z_res.dev),
-                            chained ? ctx->z_chain.get() : nsk::ChainScratch{}, ctx->d_err, s,
+                            chained ? ctx->z_chain.get(ctx->fold_walk) : nsk::ChainScratch{}, ctx->d_err, s,
                             std::max<uint64_t>(nb, 1), 0, nullptr, zc));
   if (!self) HIP_TRY(nsk::launch_signal(done_dev, seq, s));
   ctx->st.zc_passes.fetch_add(1, std::memory_order_relaxed);
@@ -765,7 +769,7 @@ int run_host_batch(ns_csum_ctx* ctx, const uint8_t* h_arena, uint64_t arena_byte
       int rc;
       if ((rc = ctx->d_arena[slot].ensure(std::max<uint64_t>(span, 16))) != NS_OK) return rc;
       if ((rc = ctx->d_desc[slot].ensure(cnt)) != NS_OK) return rc;
-      if ((rc = ctx->d_out[slot].ensure(cnt)) != NS_OK) return rc;
+      if (ctx->host_d2h && (rc = ctx->d_out[slot].ensure(cnt)) != NS_OK) return rc;
       if (!desc_pinned && (rc = ctx->h_desc[slot].ensure(cnt)) != NS_OK) return rc;
       if ((rc = ctx->h_out[slot].ensure(cnt)) != NS_OK) return rc;
       if (chained && (rc = ctx->d_chain[slot].ensure(cnt)) != NS_OK) return rc;
@@ -782,10 +786,16 @@ int run_host_batch(ns_csum_ctx* ctx, const uint8_t* h_arena, uint64_t arena_byte
       if (span) HIP_TRY(hipMemcpyAsync(ctx->d_arena[slot].p, h_arena + cut_lo, span, hipMemcpyHostToDevice, s));
       HIP_TRY(hipMemcpyAsync(ctx->d_desc[slot].p, hd, cnt * sizeof(ns_pkt_desc), hipMemcpyHostToDevice, s));
       HIP_TRY(nsk::launch_rebase(ctx->d_desc[slot].p, cnt, cut_lo, s));
-      HIP_TRY(nsk::launch_batch(ctx->d_arena[slot].p, span, ctx->d_desc[slot].p, cnt, ctx->d_out[slot].p,
-                                chained ? ctx->d_chain[slot].get() : nsk::ChainScratch{}, ctx->d_err, s));
-      HIP_TRY(hipMemcpyAsync(ctx->h_out[slot].p, ctx->d_out[slot].p, cnt * sizeof(uint16_t), hipMemcpyDeviceToHost,
-                             s));
+      // The results go straight to mapped host memory: a D2H copy would sit
+      // on the DMA engine's ring waiting for this kernel, and every later
+      // chunk's H2D copies queue behind it (a rocprofv3 copy trace of cfg3
+      // showed the slots' streams fully serialised that way).
+      uint16_t* dst = ctx->host_d2h ? ctx->d_out[slot].p : ctx->h_out[slot].dev;
+      HIP_TRY(nsk::launch_batch(ctx->d_arena[slot].p, span, ctx->d_desc[slot].p, cnt, dst,
+                                chained ? ctx->d_chain[slot].get(ctx->fold_walk) : nsk::ChainScratch{}, ctx->d_err, s));
+      if (ctx->host_d2h)
+        HIP_TRY(hipMemcpyAsync(ctx->h_out[slot].p, ctx->d_out[slot].p, cnt * sizeof(uint16_t), hipMemcpyDeviceToHost,
+                               s));
       HIP_TRY(hipEventRecord(ctx->done[slot], s));
       return NS_OK;
     };
@@ -1037,12 +1047,14 @@ int ns_csum_init(const ns_csum_opts* opts, ns_csum_ctx** out) {
   int ndev = 0;
   int rc = ns_csum_device_count(&ndev);
   if (rc != NS_OK) return rc;
+  if (opts && (opts->flags & ~NS_OPT_FOLD_WALK)) return NS_EINVAL;
   const int dev = opts ? opts->device : 0;
   if (dev < 0 || dev >= ndev) return NS_ENODEV;
   ns_csum_ctx* ctx = new (std::nothrow) ns_csum_ctx();
   if (!ctx) return NS_ENOMEM;
   ctx->device = dev;
   if (opts && opts->staging_bytes) ctx->staging = opts->staging_bytes;
+  ctx->fold_walk = opts && (opts->flags & NS_OPT_FOLD_WALK);
   DeviceGuard g(dev);
   // The context's own streams serve synchronous callers only (zero-copy
   // passes, the DMA pipeline, ns_csum_sync), so they take the device's
@@ -1064,6 +1076,7 @@ int ns_csum_init(const ns_csum_opts* opts, ns_csum_ctx** out) {
     const long x = std::strtol(v, nullptr, 10);
     if (x >= 1 && x <= (long)kMaxHostSlots) ctx->nslots = (uint32_t)x;
   }
+  ctx->host_d2h = std::getenv("NS_CSUM_HOST_D2H") != nullptr;
   if (const char* v = std::getenv("NS_CSUM_HOST_CHUNK")) {
     const long x = std::strtol(v, nullptr, 10);
     if (x >= 1024 && x <= (1l << 22)) ctx->chunk_desc = (uint32_t)x;
@@ -1211,7 +1224,7 @@ int batch_dev(ns_csum_ctx* ctx, const uint8_t* d_arena, uint64_t arena_bytes, co
     uint32_t* split = nullptr;
     const size_t caps = sc->chain.part.cap + sc->chain.status.cap + sc->split.cap;
     const uint64_t t0 = now_ns();
-    if (need_chain && (rc = sc->chain.ensure_async(n, s)) == NS_OK) chain = sc->chain.get();
+    if (need_chain && (rc = sc->chain.ensure_async(n, s)) == NS_OK) chain = sc->chain.get(ctx->fold_walk);
     // split accumulators: zero once, the kernel leaves them so
     if (rc == NS_OK && need_split && (rc = sc->split.ensure_async(nsk::split_words(n), true, s)) == NS_OK)
       split = sc->split.p;

@@ -40,6 +40,7 @@ constexpr uint64_t chain_scratch_words(uint64_t n) { return (chain_flag_word(n) 
 struct ChainScratch {
   uint32_t* partial = nullptr;  // chain_scratch_words(n) u32
   uint64_t* status = nullptr;   // chain_blocks(n) u64, zeroed at allocation
+  bool walk = false;            // NS_OPT_FOLD_WALK (tests): no look-back, every carry-in walked
 };
 
 // A self-signalling launch (`zc.flag` set; unchained checksum tiles only, no

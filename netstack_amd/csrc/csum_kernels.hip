@@ -1686,7 +1686,8 @@ hipError_t launch_batch(const uint8_t* arena, uint64_t arena_bytes,
   }
   if (e != hipSuccess || part == nullptr) return e;
   // run folding: one pass over 6 B per descriptor, any run length
-  launch_fold<>(chain, n, out, desc, arena, stream);
+  if (chain.walk) launch_fold<0>(chain, n, out, desc, arena, stream);
+  else launch_fold<>(chain, n, out, desc, arena, stream);
   return hipGetLastError();
 }
 

@@ -604,11 +604,14 @@ __global__ __launch_bounds__(256) void tcp_tx_pay(TxGeo g) {
   const uint64_t tail0 = (g.n - 1) * (uint64_t)g.mss;  // where the last segment starts
   const uint32_t sz = s < g.n ? (s + 1 < g.n ? g.mss : (uint32_t)(g.size - tail0)) : 0u;
   // wave-relative 32-bit coordinates: one resource over the wave's bytes
-  // (< 8 * 65,535 + 128)
+  // (< 8 * 65,535 + 144), rounded up to whole 16-B chunks: a load whose 16 B
+  // reach past the resource's end reads zeros, so the chunk holding the last
+  // byte must lie inside it (its bytes past the end are in the same aligned
+  // chunk, never another page)
   const uint64_t wbase = (g.pay + s0 * g.mss) & ~127ull;
   const uint64_t s_end = s0 + 8u < g.n ? s0 + 8u : g.n;
   const uint64_t w_end = g.pay + (s_end < g.n ? s_end * (uint64_t)g.mss : g.size);
-  const uint32_t nrec = (uint32_t)(w_end - wbase);
+  const uint32_t nrec = (uint32_t)((w_end - wbase + 15u) & ~15ull);
   const __amdgpu_buffer_rsrc_t r = tx_srd(wbase, nrec);
   const uint32_t pa = sz ? (uint32_t)(g.pay + s * g.mss - wbase) : 0u;  // the segment's first byte
   const uint32_t pe = pa + sz;

@@ -53,9 +53,9 @@ def _views(views):
 class Engine:
     """One ns_csum_ctx bound to a HIP device."""
 
-    def __init__(self, device: int = 0, staging_bytes: int = 0):
+    def __init__(self, device: int = 0, staging_bytes: int = 0, flags: int = 0):
         self.device = device
-        opts = NsOpts(device, 0, staging_bytes)
+        opts = NsOpts(device, flags, staging_bytes)
         h = ctypes.c_void_p()
         check(lib().ns_csum_init(ctypes.byref(opts), ctypes.byref(h)), "ns_csum_init")
         self._h = h

@@ -943,24 +943,18 @@ def test_chain_wrap_fallback(engine):
 
 
 def test_fold_carry_walk_path(engine):
-    """fold_scan's no-wait path: with the look-back disabled (the tuning
-    library's `chained_fold_walk`, SPINS = 0) every block derives its carry-in
-    by walking its run, as a block does when a predecessor is not running.
-    Long runs, short runs and wrapping pieces, against the oracle."""
-    import ctypes
-    import os
-
+    """fold_scan's no-wait path in the product library: a context made with
+    NS_OPT_FOLD_WALK folds chained runs with no look-back, every block
+    deriving its carry-in by walking its run, as a block does when a
+    predecessor is not running (libnetstack_csum.so's own fold_scan
+    instance, through ns_csum_batch_dev).  Long runs, short runs and wrapping
+    pieces, against the oracle; the same table through the default context
+    gives the same results."""
     import oracle as O
+    from netstack_amd import Engine, _lib
     from netstack_amd import workloads as W
 
     torch = _torch()
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    L = ctypes.CDLL(os.path.join(root, "netstack_amd", "lib", "libns_tune.so"))
-    L.nsk_tune_name.restype = ctypes.c_char_p
-    v = [i for i in range(L.nsk_tune_count()) if L.nsk_tune_name(i) == b"chained_fold_walk"]
-    assert v, "libns_tune.so lacks chained_fold_walk"
-    L.nsk_tune_launch.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
-                                  ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
     rng = np.random.default_rng(31)
     n = 60_000
     lengths = rng.integers(256, 400, n).astype(np.uint32)  # the big-packet kernel instance
@@ -977,14 +971,17 @@ def test_fold_carry_walk_path(engine):
     assert bad == 0
     a = torch.from_numpy(arena).cuda()
     dd = torch.from_numpy(d.view(np.uint8).copy()).cuda()
-    out = torch.empty(n, dtype=torch.int16, device="cuda")
-    err = torch.zeros(1, dtype=torch.int64, device="cuda")
-    assert L.nsk_tune_launch(v[0], a.data_ptr(), a.numel(), dd.data_ptr(), n, out.data_ptr(), err.data_ptr(),
-                             None) == 0
-    torch.cuda.synchronize()
-    assert int(err.item()) == 0
-    got = out.cpu().numpy().view(np.uint16)
-    assert np.array_equal(got, want), np.flatnonzero(got != want)[:8]
+    with Engine(0, flags=_lib.NS_OPT_FOLD_WALK) as walk:
+        for eng in (walk, engine):
+            out = torch.empty(n, dtype=torch.int16, device="cuda")
+            eng.batch_tensors(a, dd, out, chained=True)
+            torch.cuda.synchronize()
+            assert eng.sync() == 0
+            got = out.cpu().numpy().view(np.uint16)
+            assert np.array_equal(got, want), np.flatnonzero(got != want)[:8]
+    # an unknown option is refused
+    with pytest.raises(Exception):
+        Engine(0, flags=0x80)
 
 
 @pytest.mark.parametrize("chained", [False, True])

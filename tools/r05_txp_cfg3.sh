@@ -9,7 +9,7 @@ R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 cd "$R"
 export TMPDIR=/tmp
 mkdir -p gpurun_out/txp gpurun_out/c3
-timeout -k 10 400 python -u -m pytest -x -q --timeout 180 --timeout-method thread tests/test_gpu_tx_struct.py > gpurun_out/txp/t.log 2>&1
+timeout -k 10 400 python -u -m pytest -x -q --timeout 180 --timeout-method thread tests/test_gpu_tx_struct.py tests/test_gpu_parity.py::test_fold_carry_walk_path > gpurun_out/txp/t.log 2>&1
 timeout -k 10 300 python3 tools/tx_struct_probe.py --rounds 7 --only struct,struct_winpay,txv_pay_group,txv_pay_window,txv_hdr_pass > gpurun_out/txp/probe.json 2> gpurun_out/txp/probe.err
 timeout -k 10 200 python3 bench.py --config 8 > gpurun_out/txp/bench8.json 2> gpurun_out/txp/bench8.err
 timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/c3/trace -o run -- python3 tools/pmc_run.py --set cfg3probe > gpurun_out/c3/trace.log 2>&1
