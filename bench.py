@@ -786,7 +786,7 @@ def packet_mode(args, dist, eng, dev, tx: bool):
                    "packets_per_gpu": RX_N, "descriptors_per_gpu": n_desc},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
-                     "kernel": ("nsk::tcp_tx<16,2,0,1,0,1> (payload pass) + nsk::tcp_tx<16,2,0,1,0,2> (header pass)"
+                     "kernel": ("nsk::tcp_tx_pay<13> (payload pass, 8-lane groups) + nsk::tcp_tx_hdr<4,0> (header pass)"
                                 if struct else kernel_name(arena.numel(), n_desc, chained=chained)
                                 + (" + nsk::fold_scan" if chained else "")),
                      "layout": ("struct (sendTCPBatch: header slots + payload view, ns_csum_tcp_tx)" if struct

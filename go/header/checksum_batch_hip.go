@@ -416,7 +416,10 @@ const (
 // (tools/crossover.cc on MI355X, profiles/r04/crossover.json; INTEGRATION.md
 // §2 "When offload pays").  The build-tagged callers offload only calls at
 // or above them; smaller calls take the reference's unmodified Go code.
-const (
+// Variables, not constants, so the callers' tests can open the gates and
+// run the engine path at the reference's own sizes (set them before any
+// traffic; they are read without synchronisation).
+var (
 	// ChainsOffloadMinBytes is the payload of one sendTCPBatch
 	// (ChecksumChains): at 64 KiB the engine took 1.57x one core's time,
 	// at 128 KiB 0.91x, at 256 KiB 0.57x.

@@ -419,3 +419,39 @@ def test_go_offload_gates_sit_at_the_measured_crossover():
     assert rx.index("VerifyOffloadMinBytes") < rx.index("header.VerifyPacketBuffersErr(")
     patch = open(GO_PATCH).read()
     assert "+\tdeferCsum := deferTCPBatchChecksums(data.Size()) &&" in patch
+
+GO_GATE_TESTS = {  # Go tests of the engine paths behind the gates -> (package, build tag, gate)
+    "go/transport/tcp/csum_batch_hip_test.go": ("tcp", "hipcsum", "ChainsOffloadMinBytes"),
+    "go/link/fdbased/csum_rx_hip_test.go": ("fdbased", "linux,hipcsum", "VerifyOffloadMinBytes"),
+}
+
+
+def test_go_gate_tests_open_the_gates_and_compare_with_the_reference():
+    """with the measured gates the hooks never reach the engine
+    at the reference's sizes, so Go tests open each gate (a package
+    variable, restored after) and check the engine path against the
+    reference's own decision: finishTCPBatchChecksums against
+    tcpBatchChecksumsRef byte for byte, verifyRXChecksums' verdicts against
+    segment.parse's rule, with no engine fallback counted.  Checked
+    statically (no Go toolchain): Go <= 1.14 forms, the tag before the
+    package clause, the gate set and restored, the functions they test
+    exist in the paired hipcsum files."""
+    shim = _go_code(open(GO_SHIM).read())
+    assert re.search(r"^var \(.*?^\s*ChainsOffloadMinBytes\s*=.*?^\s*VerifyOffloadMinBytes\s*=.*?^\)", shim,
+                     flags=re.M | re.S), "the gates must be variables a test can set"
+    for rel, (pkg, tag, gate) in GO_GATE_TESTS.items():
+        raw = open(os.path.join(ROOT, rel)).read()
+        code = _go_code(raw)
+        for pat in POST_GO114:
+            assert not re.search(pat, code), (rel, pat)
+        assert f"\n\n// +build {tag}\n\npackage {pkg}\n" in raw, rel
+        assert re.search(rf"defer func\(v int\) {{ header\.{gate} = v }}\(header\.{gate}\)", code), rel
+        assert re.search(rf"header\.{gate} = 0", code), rel
+        assert "header.EngineFallbacks()" in code, rel
+        tested = {"tcp": ("deferTCPBatchChecksums", "finishTCPBatchChecksums", "tcpBatchChecksumsRef"),
+                  "fdbased": ("verifyRXChecksums",)}[pkg]
+        for fn in tested:
+            assert re.search(rf"\b{fn}\(", code), (rel, fn)
+        for name in set(re.findall(r"\bheader\.(\w+)", code)):
+            assert name in _top_level(shim) or name in REF_HEADER_NAMES or not os.path.isdir("/root/reference"), \
+                (rel, name)

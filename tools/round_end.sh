@@ -6,7 +6,7 @@
 #      for roofline.traffic), also kept as gpurun_out/prof_TAG/pmc_traffic.json;
 #   3. tools/final_round.sh TAG: every bench line, now carrying that traffic.
 set -euo pipefail
-TAG=${1:-r04}
+TAG=${1:-r05}
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 cd "$R"
 bash tools/profile.sh "$TAG"
