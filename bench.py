@@ -694,10 +694,16 @@ def packet_mode(args, dist, eng, dev, tx: bool):
     stream = torch.cuda.current_stream(dev)
     ev = [torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)]
     state = {"i": 0}
+    # The structured fill alternates between two batches of the same packets:
+    # each call fills header slots the previous call did not write, as
+    # sendTCPBatch's fresh NewPacketDescriptors buffers are (re-filling one
+    # batch leaves its 57 MB of slot writes in the MALL between calls; DESIGN
+    # §4.7).  The checks below run on the first batch.
+    arenas = [arena, W.tx_split_batch(RX_N, seed, dev)[0]] if struct else [arena]
 
-    def fill():
+    def fill(j=0):
         if struct:
-            eng.tcp_tx(arena, geo, out=out, stream=stream)
+            eng.tcp_tx(arenas[j % len(arenas)], geo, out=out, stream=stream)
         else:
             eng.batch_tensors(arena, desc, out, chained=chained, stream=stream, store=tx, paired=split)
 
@@ -705,7 +711,7 @@ def packet_mode(args, dist, eng, dev, tx: bool):
         k = state["i"]
         if k == args.warmup:
             ev[0].record(stream)
-        fill()
+        fill(k)
         state["i"] = k + 1
         if state["i"] == args.warmup + args.steps:
             ev[1].record(stream)
@@ -783,10 +789,11 @@ def packet_mode(args, dist, eng, dev, tx: bool):
                       "(IPv4 header; payload + pseudo-header addresses and TCP header, NS_BATCH_PAIRED)" if split
                       else "2 descriptors each (IPv4 header; pseudo-header addresses + TCP segment)" if fused
                       else "3 chained descriptors each") + (", 2 checksum stores" if tx else ""),
-                   "packets_per_gpu": RX_N, "descriptors_per_gpu": n_desc},
+                   "packets_per_gpu": RX_N, "descriptors_per_gpu": n_desc,
+                   **({"rotating_batches": 2} if struct else {})},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
-                     "kernel": ("nsk::tcp_tx_pay<13> (payload pass, 8-lane groups) + nsk::tcp_tx_hdr<4,0> (header pass)"
+                     "kernel": ("nsk::tcp_tx<16,2,0,1,0,1> (payload pass) + nsk::tcp_tx_hdr<4,0> (header pass)"
                                 if struct else kernel_name(arena.numel(), n_desc, chained=chained)
                                 + (" + nsk::fold_scan" if chained else "")),
                      "layout": ("struct (sendTCPBatch: header slots + payload view, ns_csum_tcp_tx)" if struct

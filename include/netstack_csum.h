@@ -485,7 +485,8 @@ int ns_csum_get_stats(ns_csum_ctx* ctx, ns_csum_stats* out, int reset);
 /* A/B and test knobs of ns_csum_tcp_tx on this context (no reference
  * counterpart; every result is the same whatever they are): variant (0 =
  * production; 1 one fused pass, 2 nontemporal write-back, 3 segments reduced
- * over the wave, 4 the one-shot header pass, 5 the windowed payload pass),
+ * over the wave, 4 the one-shot header pass, 5 the payload pass in 8-lane
+ * groups),
  * tile / htile (segments per wave of the fused pass or the windowed payload
  * pass, and of the header pass; 0 = the launcher's choice), passes (0 = by
  * size, 1 = fused, 2 = two passes).  Read by each call without a lock; set

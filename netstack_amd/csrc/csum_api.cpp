@@ -301,10 +301,13 @@ void bump_max(std::atomic<uint64_t>& m, uint64_t v) {
 }  // namespace
 
 // The host-batch pipeline's shape: chunks in flight and descriptors per chunk
-// (cfg3, 1M x 64 B, two slots: 64K 3.11 ms, 128K 2.18, 256K 2.16, 512K 2.52
-// ms per call).
+// (cfg3, 1M x 64 B, two slots with a D2H copy per chunk: 64K 3.11 ms, 128K
+// 2.18, 256K 2.16, 512K 2.52 ms per call).  Results written straight to
+// mapped memory, 128K-descriptor chunks (round 5, profiles/r05/host/): 2 /
+// 3 / 4 slots 1.86 / 1.80 / 1.72 ms per call, against 2.03 / 1.90 / 1.88 ms
+// with the D2H copy.
 constexpr uint32_t kMaxHostSlots = 4;
-constexpr uint32_t kHostSlots = 2;
+constexpr uint32_t kHostSlots = 4;
 constexpr uint32_t kHostChunkDesc = 1u << 17;
 
 struct ns_csum_ctx {

@@ -117,7 +117,7 @@ constexpr uint64_t kTxTwoPassMinBytes = 64ull << 20;
 // variant (A/B diagnostics; 0 = production): 1 = one fused pass,
 // 2 = nontemporal write-back, 3 = segments reduced over the wave in the loop,
 // 4 = the one-shot header pass (tcp_tx PH = 2) instead of the persistent one,
-// 5 = the windowed payload pass (tcp_tx PH = 1) instead of the group one.
+// 5 = the payload pass in 8-lane groups (tcp_tx_pay) instead of the windowed one.
 hipError_t launch_tcp_tx(TxGeo g, hipStream_t stream, uint32_t variant = 0);
 // Many batches in one fused launch (ns_csum_tcp_tx_multi).  calls[] (host)
 // hold each batch's geometry with n, mode and out set; tx_multi_prepare sets

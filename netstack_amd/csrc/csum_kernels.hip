@@ -475,22 +475,43 @@ __device__ __forceinline__ uint32_t quad_sum(const Srd& r, const PktInfo& p) {
 // after them.  spec_check: every packet of the wave is where predicted and
 // spans <= 4 chunks (then the loaded chunks cover it), else the wave takes
 // quad_sum / direct_sum as without speculation.
+// (32-bit arithmetic: the arena is n * spec bytes under one SRD, < 4 GiB,
+// and a tile's first packet index is below n.)
 __device__ __forceinline__ void spec_load(const Srd& r, uint64_t tile0, uint32_t n, uint32_t spec, uint4 (&v)[4]) {
   const uint32_t l = threadIdx.x & 63u, c = l & 3u;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const uint64_t k = tile0 + 16u * j + (l >> 2);
-    v[j] = bload<2>(r.rsrc, k < n ? (uint32_t)(k * spec) + 16u * c : r.oob);
+    const uint32_t k = (uint32_t)tile0 + 16u * j + (l >> 2);
+    v[j] = bload<2>(r.rsrc, k < n ? k * spec + 16u * c : r.oob);
   }
 }
 
 __device__ __forceinline__ bool spec_check(const PktInfo& p, uint64_t i, uint32_t spec) {
-  return __all(p.nch == 0u || (p.nch <= 4u && (uint64_t)p.first == i * spec)) != 0;
+  return __all(p.nch == 0u || (p.nch <= 4u && p.first == (uint32_t)i * spec)) != 0;
+}
+
+// quad_reduce for a wave in which no chunk needs a mask (every packet whole
+// 16-B-aligned chunks, 4 of them: cfg3's dense 64-B slots): no geometry
+// shuffles and no per-chunk mask tests (round 5: the SQ counters put cfg3's
+// distance to its floor kernels on VALU issue).
+__device__ __forceinline__ uint32_t quad_reduce_whole(const uint4 (&v)[4], uint32_t phase) {
+  const uint32_t l = threadIdx.x & 63u, c = l & 3u;
+  uint32_t sv[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    uint32_t T = 0, W = 0;
+    acc_chunk<false>(v[j], T, W);
+    sv[j] = group_sum<4>(W);
+  }
+  const uint32_t mine = c == 0u ? sv[0] : c == 1u ? sv[1] : c == 2u ? sv[2] : sv[3];
+  const uint32_t W = (uint32_t)__shfl((int)mine, (int)(4u * (l & 15u) + (l >> 4)), 64);
+  return s_class(W, phase);
 }
 
 __device__ __forceinline__ uint32_t spec_sum(const PktInfo& p, const uint4 (&v)[4]) {
   const uint32_t l = threadIdx.x & 63u;
   const uint32_t geo = quad_geo(p);
+  if (!__any(geo >> 13)) return quad_reduce_whole(v, p.ew >> 31);  // no packet's chunk needs a mask
   uint32_t g[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) g[j] = (uint32_t)__shfl((int)geo, (int)(16 * j + (l >> 2)), 64);

@@ -594,7 +594,7 @@ __device__ __forceinline__ uint32_t tx_bytes_from(const uint4 v, int c) {  // W 
   return wsum4(make_uint4(v.x & ~below(c), v.y & ~below(c - 4), v.z & ~below(c - 8), v.w & ~below(c - 12)), 0u);
 }
 
-template <int NB>
+template <int NB, int A0 = 0>
 __global__ __launch_bounds__(256) void tcp_tx_pay(TxGeo g) {
   const uint32_t lane = threadIdx.x & 63u, grp = lane >> 3, li = lane & 7u;
   const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -625,7 +625,7 @@ __global__ __launch_bounds__(256) void tcp_tx_pay(TxGeo g) {
   const uint32_t tc = (pe - 1u) & ~15u;
   const bool owner = sz && ((tc >> 4) & 7u) == li;
   uint4 v[NB];
-  v[0] = tx_load<0>(r, in0 ? cl : nrec);
+  v[0] = tx_load<A0>(r, in0 ? cl : nrec);
   const uint4 t = tx_load<0>(r, owner ? tc : nrec);
 #pragma unroll
   for (int k = 1; k < NB; ++k) v[k] = tx_load<2>(r, ((uint32_t)k <= klast ? cl1 : nrec) + 128u * k);
@@ -653,25 +653,27 @@ static int tx_pay_lines(uint32_t mss) {
   return lines <= 2 ? 2 : lines <= 4 ? 4 : lines <= 8 ? 8 : lines <= 13 ? 13 : 16;
 }
 
-template <int NB>
+template <int NB, int A0>
 static hipError_t launch_tx_pay_t(const TxGeo& g, hipStream_t stream) {
   const uint64_t wgs = (g.n + 31) / 32;  // 4 waves x 8 segments
-  hipLaunchKernelGGL((tcp_tx_pay<NB>), dim3((uint32_t)wgs), dim3(256), 0, stream, g);
+  hipLaunchKernelGGL((tcp_tx_pay<NB, A0>), dim3((uint32_t)wgs), dim3(256), 0, stream, g);
   return hipGetLastError();
 }
 
-// The payload pass: the group shape above, or tcp_tx PH = 1 (GP = 0, the
-// round-4 shape, kept for A/B).
+// The payload pass: the group shape above (GP = 1; GP = 2: line 0
+// nontemporal too, A/B only), or tcp_tx PH = 1 (GP = 0, the round-4 shape,
+// kept for A/B).
 template <int U, int AUX, int SP, int RED, int GP = 1>
 static hipError_t launch_payload_pass(const TxGeo& g, hipStream_t stream) {
   if (g.n == 0) return hipSuccess;
   if (!GP || (g.n + 31) / 32 >= (1ull << 31)) return launch_tcp_tx_t<U, AUX, SP, RED, 0, 1>(g, stream);
+  constexpr int A0 = GP == 2 ? 2 : 0;
   switch (tx_pay_lines(g.mss)) {
-    case 2: return launch_tx_pay_t<2>(g, stream);
-    case 4: return launch_tx_pay_t<4>(g, stream);
-    case 8: return launch_tx_pay_t<8>(g, stream);
-    case 13: return launch_tx_pay_t<13>(g, stream);
-    default: return launch_tx_pay_t<16>(g, stream);
+    case 2: return launch_tx_pay_t<2, A0>(g, stream);
+    case 4: return launch_tx_pay_t<4, A0>(g, stream);
+    case 8: return launch_tx_pay_t<8, A0>(g, stream);
+    case 13: return launch_tx_pay_t<13, A0>(g, stream);
+    default: return launch_tx_pay_t<16, A0>(g, stream);
   }
 }
 
@@ -719,7 +721,16 @@ static hipError_t launch_header_pass(TxGeo h, hipStream_t stream, uint32_t per_c
 // (interleaving the slot write-back with the payload stream
 // cost ~45 us on 1M segments).  One fused pass otherwise.  HP: the header
 // pass persistent (tcp_tx_hdr) or one-shot (tcp_tx PH = 2).
-template <int U, int AUX, int SP, int RED, int HP = 1, int GP = 1>
+// GP: the payload pass windowed (0, production) or in 8-lane groups (1).
+// Alone the group pass is faster (1M x 1460 B: 208.6 vs 222.9 us), but with
+// the header pass between calls it is not: over two rotating batches (fresh
+// header slots each call, as sendTCPBatch's NewPacketDescriptors gives)
+// 262.4 vs 245.4 us per call; re-using one batch's slots, 228.5 vs 244.7
+// (tools/tx_struct_probe.py, profiles/r05/tx_pay/).  The header pass leaves
+// 57 MB of dirty lines that reach HBM during the next payload pass; the
+// windowed pass, 6% short of the read ceiling, absorbs those writes, the
+// group pass, at it, pays for them.
+template <int U, int AUX, int SP, int RED, int HP = 1, int GP = 0>
 static hipError_t launch_passes(TxGeo g, hipStream_t stream, uint32_t per_cu = 0) {
   if (!(g.mode & kTxTcpFull) || g.xs == nullptr) return launch_tcp_tx_t<U, AUX, SP, RED>(g, stream);
   TxGeo h = g;
@@ -770,7 +781,7 @@ hipError_t launch_tcp_tx(TxGeo g, hipStream_t stream, uint32_t variant) {
     case 2: return launch_passes<16, 2, 1, 1>(g, stream);
     case 3: return launch_passes<16, 2, 0, 0>(g, stream);
     case 4: return launch_passes<16, 2, 0, 1, 0>(g, stream);  // the one-shot header pass (round 4)
-    case 5: return launch_passes<16, 2, 0, 1, 1, 0>(g, stream);  // the windowed payload pass (round 4)
+    case 5: return launch_passes<16, 2, 0, 1, 1, 1>(g, stream);  // the payload pass in 8-lane groups
     default: return launch_passes<16, 2, 0, 1>(g, stream);
   }
 }

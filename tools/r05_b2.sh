@@ -9,6 +9,8 @@ cd "$R"
 export TMPDIR=/tmp
 mkdir -p gpurun_out/b2
 timeout -k 10 500 python -u -m pytest -x -q --timeout 180 --timeout-method thread tests/test_gpu_parity.py > gpurun_out/b2/t.log 2>&1
+timeout -k 10 600 bash tools/ab_lib.sh 3 4 > gpurun_out/b2/ab_cfg3.log 2>&1
+timeout -k 10 200 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD -d gpurun_out/b2/c3sq -o run --output-format csv -- python3 tools/pmc_run.py --set cfg3probe > gpurun_out/b2/c3sq.log 2>&1
 for sl in 2 3 4; do
   NS_CSUM_HOST_SLOTS=$sl timeout -k 10 120 python3 bench.py --mode host --config 3 --steps 20 --warmup 3 --no-cpu > gpurun_out/b2/h3_s${sl}.json 2> gpurun_out/b2/h3_s${sl}.err
   NS_CSUM_HOST_D2H=1 NS_CSUM_HOST_SLOTS=$sl timeout -k 10 120 python3 bench.py --mode host --config 3 --steps 20 --warmup 3 --no-cpu > gpurun_out/b2/h3_s${sl}_d2h.json 2> gpurun_out/b2/h3_s${sl}_d2h.err

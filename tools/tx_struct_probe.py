@@ -7,6 +7,9 @@
                           pass, then a header pass writing the slots back whole
   struct_v1..v3           its A/B variants (ns_csum_set_tx_tuning variant: one
                           fused pass, nontemporal write-back, wave reductions)
+  struct_grppay           variant 5: the payload pass in 8-lane groups
+  struct_norot            the product on one batch every call (its header
+                          slots re-used: their writes stay in the MALL)
   struct_hdr1shot         the header pass one-shot (round 4's), not persistent
   struct_pP_hH            P segments per wave in the payload pass, H in the
                           header pass (NS_CSUM_TX_TILE / _HTILE)
@@ -47,6 +50,8 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--n", type=int, default=1 << 20)
     ap.add_argument("--only", default="", help="comma-separated variant names")
+    ap.add_argument("--trend", type=int, default=0,
+                    help="then time this many back-to-back product calls one by one (rotating batches)")
     args = ap.parse_args()
     n = args.n
     dev = torch.device("cuda", 0)
@@ -103,14 +108,14 @@ def main():
             assert TXV.txv_launch(ctypes.byref(t), stream.cuda_stream, k) == 0
         return f
 
-    def txv(k, tile=0):
+    def txv(k, tile=0, rot=True):
         def f(r):
-            a = batches[r]
+            a = batches[r if rot else 0]
             t = TxGeo(hdr=a.data_ptr() + geo["hdr_off"], pay=a.data_ptr() + geo["pay_off"], size=geo["size"], n=n,
                       mss=geo["mss"], slot=geo["slot"], tile=tile, ip_at=geo["ip_at"], ip_len=geo["ip_len"],
                       tcp_at=geo["tcp_at"], tcp_len=geo["tcp_len"], addr_sum=addr_sum(geo["src"], geo["dst"]),
                       proto=6, mode=3, xs=xs.data_ptr() if k >= 8 else None, xstride=1,
-                      out=sink.data_ptr() if k >= 19 else None)
+                      out=sink.data_ptr() if 19 <= k <= 27 else None)  # the floor kernels' sink only
             assert TXV.txv_launch(ctypes.byref(t), stream.cuda_stream, k) == 0
         return f
 
@@ -121,9 +126,18 @@ def main():
         "struct_fused": env("NS_CSUM_TX_VARIANT", "1"),
         "struct_ntwb": env("NS_CSUM_TX_VARIANT", "2"),
         "struct_hdr1shot": env("NS_CSUM_TX_VARIANT", "4"),
-        "struct_winpay": env("NS_CSUM_TX_VARIANT", "5"),
+        "struct_grppay": env("NS_CSUM_TX_VARIANT", "5"),
         "txv_pay_group": txv(28),
         "txv_pay_window": txv(29),
+        "txv_2p_grp_nt": txv(30),
+        "txv_2p_grp_ntwb": txv(31),
+        "txv_2p_grp_nt_ntwb": txv(32),
+        "txv_pay_group_nt": txv(33),
+        "txv_2p_window": txv(9),
+        "txv_2p_window_norot": txv(9, rot=False),
+        "txv_2p_group_norot": txv(35, rot=False),
+        "txv_2p_group": txv(35),
+        "txv_2p_grp_ntwb_norot": txv(31, rot=False),
         "struct_fields": lambda r: eng.tcp_tx(batches[r], geo, stream=stream, fields_only=True),
         "struct_hdr_only": lambda r: eng.tcp_tx(batches[r], geo, stream=stream, mode="partial"),
         "txv_stream_t8": txv(5, 8),
@@ -195,7 +209,19 @@ def main():
             b.synchronize()
             times[name].append(a.elapsed_time(b) * 1e3 / args.reps)
     med = {k: round(float(np.median(v)), 2) for k, v in times.items()}
-    print(json.dumps({"packets": n, "median_us": med, "fill_bit_exact": checks,
+    trend = None
+    if args.trend:
+        evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.trend + 1)]
+        evs[0].record(stream)
+        for i in range(args.trend):
+            eng.tcp_tx(batches[i % 2], geo, stream=stream)
+            evs[i + 1].record(stream)
+        torch.cuda.synchronize()
+        t = [evs[i].elapsed_time(evs[i + 1]) * 1e3 for i in range(args.trend)]
+        q = max(1, args.trend // 10)
+        trend = {"per_call_us": [round(x, 1) for x in t], "first_decile_us": round(float(np.median(t[:q])), 2),
+                 "last_decile_us": round(float(np.median(t[-q:])), 2), "median_us": round(float(np.median(t)), 2)}
+    print(json.dumps({"packets": n, "median_us": med, "fill_bit_exact": checks, "trend": trend,
                       "host_enqueue_us_per_call": {k: round(float(np.median(v)), 1) for k, v in host.items()},
                       "rounds_us": {k: [round(x, 2) for x in v] for k, v in times.items()}}, indent=1))
 

@@ -6,7 +6,8 @@
 //   5 = neither reductions nor write-back (the bare stream + header reads),
 //   6 = 12 windows in flight, 7 = 6 without the write-back; 8 / 9 / 10 = the
 //   two-pass shape (g->xs set) with 12 / 16 / 8 windows in flight; 11 = the
-//   two passes with no header write-back (fields unwritten); 12 / 13 / 14 =
+//   two passes with no header write-back (fields unwritten); (8-17 with
+//   the windowed payload pass, round 4's); 12 / 13 / 14 =
 //   the two passes with the persistent header pass at 4 / 16 / 2 waves per CU
 //   (the product runs 24); 15 = the two passes, one-shot header pass;
 //   16 / 17 = the persistent header pass at 24 / 32 waves per CU;
@@ -15,7 +16,11 @@
 //   copied onto themselves (read + write), read only, written only (16-B
 //   lane accesses, 4 per lane, one-shot grid); 22-24 / 25-27 = written only /
 //   copied with store cache policy 1 / 2 / 3; 28 / 29 = the payload pass
-//   alone, in 8-lane groups (product) / windowed (round 4).
+//   alone, in 8-lane groups (product) / windowed (round 4); 30 / 31 / 32 =
+//   both passes with the group payload pass all nontemporal / with
+//   nontemporal header stores / both; 33 = the all-nontemporal group
+//   payload pass alone; 34 / 35 = both passes, windowed / group payload
+//   pass (whatever the product's default).
 // Not part of the product ABI.
 #include "../netstack_amd/csrc/tcp_tx.hip"
 
@@ -64,9 +69,9 @@ extern "C" int txv_launch(const nsk::TxGeo* g, void* stream, int k) {
     case 5: e = nsk::launch_tcp_tx_t<16, 2, 0, 2, 1>(*g, s); break;
     case 6: e = nsk::launch_tcp_tx_t<12, 2, 0, 1>(*g, s); break;
     case 7: e = nsk::launch_tcp_tx_t<12, 2, 0, 1, 1>(*g, s); break;
-    case 8: e = nsk::launch_passes<12, 2, 0, 1>(*g, s); break;
-    case 9: e = nsk::launch_passes<16, 2, 0, 1>(*g, s); break;
-    case 10: e = nsk::launch_passes<8, 2, 0, 1>(*g, s); break;
+    case 8: e = nsk::launch_passes<12, 2, 0, 1, 1, 0>(*g, s); break;
+    case 9: e = nsk::launch_passes<16, 2, 0, 1, 1, 0>(*g, s); break;
+    case 10: e = nsk::launch_passes<8, 2, 0, 1, 1, 0>(*g, s); break;
     case 11: {  // the two passes, the header pass without its write-back (timing only)
       nsk::TxGeo h = *g;
       h.tile = g->htile;
@@ -74,12 +79,12 @@ extern "C" int txv_launch(const nsk::TxGeo* g, void* stream, int k) {
       if (e == hipSuccess) e = nsk::launch_tcp_tx_t<16, 2, 0, 1, 1, 2>(h, s);
       break;
     }
-    case 12: e = nsk::launch_passes<16, 2, 0, 1, 1>(*g, s, 4); break;
-    case 13: e = nsk::launch_passes<16, 2, 0, 1, 1>(*g, s, 16); break;
-    case 14: e = nsk::launch_passes<16, 2, 0, 1, 1>(*g, s, 2); break;
-    case 15: e = nsk::launch_passes<16, 2, 0, 1, 0>(*g, s); break;
-    case 16: e = nsk::launch_passes<16, 2, 0, 1, 1>(*g, s, 24); break;
-    case 17: e = nsk::launch_passes<16, 2, 0, 1, 1>(*g, s, 32); break;
+    case 12: e = nsk::launch_passes<16, 2, 0, 1, 1, 0>(*g, s, 4); break;
+    case 13: e = nsk::launch_passes<16, 2, 0, 1, 1, 0>(*g, s, 16); break;
+    case 14: e = nsk::launch_passes<16, 2, 0, 1, 1, 0>(*g, s, 2); break;
+    case 15: e = nsk::launch_passes<16, 2, 0, 1, 0, 0>(*g, s); break;
+    case 16: e = nsk::launch_passes<16, 2, 0, 1, 1, 0>(*g, s, 24); break;
+    case 17: e = nsk::launch_passes<16, 2, 0, 1, 1, 0>(*g, s, 32); break;
     case 18: {
       nsk::TxGeo h = *g;
       h.tile = g->htile;
@@ -97,6 +102,12 @@ extern "C" int txv_launch(const nsk::TxGeo* g, void* stream, int k) {
     case 27: e = launch_floor<0, 3>(*g, s); break;
     case 28: e = nsk::launch_payload_pass<16, 2, 0, 1, 1>(*g, s); break;
     case 29: e = nsk::launch_payload_pass<16, 2, 0, 1, 0>(*g, s); break;
+    case 30: e = nsk::launch_passes<16, 2, 0, 1, 1, 2>(*g, s); break;
+    case 31: e = nsk::launch_passes<16, 2, 1, 1, 1, 1>(*g, s); break;
+    case 32: e = nsk::launch_passes<16, 2, 1, 1, 1, 2>(*g, s); break;
+    case 33: e = nsk::launch_payload_pass<16, 2, 0, 1, 2>(*g, s); break;
+    case 34: e = nsk::launch_passes<16, 2, 0, 1, 1, 0>(*g, s); break;
+    case 35: e = nsk::launch_passes<16, 2, 0, 1, 1, 1>(*g, s); break;
     default: e = nsk::launch_tcp_tx_t<16, 2, 0, 1>(*g, s); break;
   }
   return (int)e;
