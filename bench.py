@@ -411,7 +411,7 @@ def parity_sample(batch, out_dev, k: int = 65536) -> dict:
             "which": "first and last 65536 packets of the timed batch, results of the measured kernel"}
 
 
-def kernel_name(arena_bytes: int, n: int, chained: bool = False) -> str:
+def kernel_name(arena_bytes: int, n: int, chained: bool = False, store: bool = False) -> str:
     """The csum_hyb instance launch_batch picks (csum_kernels.hip
     launch_batch / launch_hyb / launch_hyb_tp), as rocprofv3 names it."""
     win = "true" if arena_bytes + 64 >= 0xFFFF0000 else "false"
@@ -794,7 +794,7 @@ def packet_mode(args, dist, eng, dev, tx: bool):
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                      "kernel": ("nsk::tcp_tx<16,2,0,1,0,1> (payload pass) + nsk::tcp_tx_hdr<4,0> (header pass)"
-                                if struct else kernel_name(arena.numel(), n_desc, chained=chained)
+                                if struct else kernel_name(arena.numel(), n_desc, chained=chained, store=tx or split)
                                 + (" + nsk::fold_scan" if chained else "")),
                      "layout": ("struct (sendTCPBatch: header slots + payload view, ns_csum_tcp_tx)" if struct
                                 else "split (sendTCPBatch: header slots + payload view)" if split else "wire"),

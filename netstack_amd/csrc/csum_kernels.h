@@ -128,6 +128,15 @@ uint32_t tx_multi_prepare(TxGeo* calls, uint32_t ncalls, TxGeo* launch, uint32_t
 hipError_t launch_tcp_tx_multi(const TxGeo& launch, uint32_t grid, const TxGeo* d_calls, const uint32_t* d_first,
                                uint32_t ncalls, hipStream_t stream);
 
+// The receive ring's shape for descriptor tables (tbl_ring.hip): one 8-lane
+// group per descriptor.  Measured against csum_hyb's big-packet instance on
+// cfg2 and not taken (tools/grp_probe.py); built only into
+// the timing-variants library.
+bool tbl_ring_eligible(const uint8_t* arena, uint64_t arena_bytes, uint32_t n, uint64_t sizing_bytes);
+hipError_t launch_tbl_ring(const uint8_t* arena, uint64_t arena_bytes, const void* desc, uint32_t n, uint16_t* out,
+                      unsigned long long* err, hipStream_t stream, uint32_t lines = 0);
+constexpr uint64_t kGrpMinAvg = 1024, kGrpMaxAvg = 16384;
+
 // A receive ring verified on the device (rx_ring.hip, ns_csum_rx_ring).
 // Absolute device addresses; validated by the caller: ring and stride
 // 16-B aligned, stride < 2^24, frame_at + link even, view0 = 0 or >= 64 and

@@ -1,0 +1,26 @@
+// grp_variants.hip — the receive ring's shape for descriptor tables
+// (tbl_ring.hip, one 8-lane group per descriptor) beside csum_hyb's
+// big-packet instance, for tools/grp_probe.py.  grpv_launch(k, ...):
+//   0 tbl_ring     1 csum_hyb<...,8,16,4,2,0,2> (what launch_batch runs for
+//   such tables)     2 tbl_ring with no descriptor read (packets at i * 1504,
+//   1500 B: timing only, the floor of its payload loads)
+// Not part of the product ABI.
+#include "../netstack_amd/csrc/csum_kernels.hip"
+#include "../netstack_amd/csrc/tbl_ring.hip"
+
+extern "C" int grpv_launch(int k, const uint8_t* arena, uint64_t bytes, const void* desc, uint32_t n, uint16_t* out,
+                           unsigned long long* err, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  switch (k) {
+    case 1:
+      return (int)nsk::launch_hyb<8, 16, 4, 2, 0, 2>(arena, bytes, desc, n, out, nullptr, err, s, nsk::kBigChunks,
+                                                      bytes, nsk::kTileBytes);
+    case 2: {
+      hipLaunchKernelGGL((nsk::tbl_ring<13, 1504>), dim3((n + 31) / 32), dim3(256), 0, s, arena, bytes,
+                         reinterpret_cast<const uint4*>(desc), n, out, err);
+      return (int)hipGetLastError();
+    }
+    default:
+      return (int)nsk::launch_tbl_ring(arena, bytes, desc, n, out, err, s);
+  }
+}

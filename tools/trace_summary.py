@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Per-launch durations of the checksum kernel from a rocprofv3 kernel trace
 of `bench.py` (tools/profile.sh), summarised the way bench.py times it: the
-launches of the timed region are launches [W, W+K) of csum_hyb in dispatch
+launches of the timed region are launches [W, W+K) of csum_hyb or csum_grp in dispatch
 order (W warm-up launches before them, one parity launch after).
 
   python tools/trace_summary.py TRACE_DIR --warmup W --steps K > summary.json
@@ -22,7 +22,7 @@ def main():
     a = ap.parse_args()
     rows = []
     for f in glob.glob(os.path.join(a.trace_dir, "**", "*kernel_trace.csv"), recursive=True):
-        rows += [r for r in csv.DictReader(open(f)) if "csum_hyb" in r["Kernel_Name"]]
+        rows += [r for r in csv.DictReader(open(f)) if "csum_hyb" in r["Kernel_Name"] or "csum_grp" in r["Kernel_Name"]]
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     dur = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in rows]
     timed = dur[a.warmup:a.warmup + a.steps]
