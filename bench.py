@@ -694,18 +694,26 @@ def packet_mode(args, dist, eng, dev, tx: bool):
     stream = torch.cuda.current_stream(dev)
     ev = [torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)]
     state = {"i": 0}
-    # The structured fill alternates between two batches of the same packets:
-    # each call fills header slots the previous call did not write, as
-    # sendTCPBatch's fresh NewPacketDescriptors buffers are (re-filling one
-    # batch leaves its 57 MB of slot writes in the MALL between calls; DESIGN
-    # §4.7).  The checks below run on the first batch.
-    arenas = [arena, W.tx_split_batch(RX_N, seed, dev)[0]] if struct else [arena]
+    # Every layout alternates between two batches of the same packets (3.2 GB
+    # > the 256 MiB MALL), as cfg2's rotating batches: no launch re-reads what
+    # the one before it left in the MALL, and the structured fill writes header
+    # slots the previous call did not, as sendTCPBatch's fresh
+    # NewPacketDescriptors buffers are (re-filling one batch leaves its 57 MB
+    # of slot writes in the MALL between calls).  The checks
+    # below run on the first batch.
+    if split:
+        arenas = [arena, W.tx_split_batch(RX_N, seed, dev)[0]]
+    elif tx:
+        arenas = [arena, W.tx_batch(RX_N, seed, dev, fused=fused)[0]]
+    else:
+        arenas = [arena, W.rx_batch(RX_N, seed, dev, corrupt_every=1000, fused=fused)[0]]
 
     def fill(j=0):
+        a = arenas[j % 2]
         if struct:
-            eng.tcp_tx(arenas[j % len(arenas)], geo, out=out, stream=stream)
+            eng.tcp_tx(a, geo, out=out, stream=stream)
         else:
-            eng.batch_tensors(arena, desc, out, chained=chained, stream=stream, store=tx, paired=split)
+            eng.batch_tensors(a, desc, out, chained=chained, stream=stream, store=tx, paired=split)
 
     def step():
         k = state["i"]
@@ -789,8 +797,7 @@ def packet_mode(args, dist, eng, dev, tx: bool):
                       "(IPv4 header; payload + pseudo-header addresses and TCP header, NS_BATCH_PAIRED)" if split
                       else "2 descriptors each (IPv4 header; pseudo-header addresses + TCP segment)" if fused
                       else "3 chained descriptors each") + (", 2 checksum stores" if tx else ""),
-                   "packets_per_gpu": RX_N, "descriptors_per_gpu": n_desc,
-                   **({"rotating_batches": 2} if struct else {})},
+                   "packets_per_gpu": RX_N, "descriptors_per_gpu": n_desc, "rotating_batches": 2},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                      "kernel": ("nsk::tcp_tx<16,2,0,1,0,1> (payload pass) + nsk::tcp_tx_hdr<4,0> (header pass)"
@@ -869,6 +876,10 @@ def ring_mode(args, dist, eng, dev, seed):
     from netstack_amd import workloads as W
 
     arena, lens, bad_idx = W.rx_ring_batch(RX_N, seed, dev, corrupt_every=1000)
+    # two rings of the same frames, alternating (3.2 GB > the 256 MiB MALL, as
+    # cfg2's rotating batches: no launch re-reads what the one before it left
+    # in the MALL)
+    rings = [arena, W.rx_ring_batch(RX_N, seed, dev, corrupt_every=1000)[0]]
     ring = dict(stride=W.RX_STRIDE, n=RX_N)
     verdict = torch.empty(RX_N, dtype=torch.uint8, device=dev)
     sums = torch.empty(2 * RX_N, dtype=torch.int16, device=dev)
@@ -880,7 +891,7 @@ def ring_mode(args, dist, eng, dev, seed):
         k = state["i"]
         if k == args.warmup:
             ev[0].record(stream)
-        eng.rx_ring(arena, ring, lens, sums=sums, verdict=verdict, stream=stream)
+        eng.rx_ring(rings[k % 2], ring, lens, sums=sums, verdict=verdict, stream=stream)
         state["i"] = k + 1
         if state["i"] == args.warmup + args.steps:
             ev[1].record(stream)
@@ -911,7 +922,7 @@ def ring_mode(args, dist, eng, dev, seed):
         "data": "synthetic received packets (valid IPv4/TCP checksums, 1 in 1000 corrupted), resident in HBM",
         "config": {"workload": "rx ring: 1,048,576 x 1500-B IPv4/TCP packets per GPU in 1504-B slots, parsed and "
                                "verified on the device from the slots' lengths (ns_csum_rx_ring, no table)",
-                   "packets_per_gpu": RX_N, "descriptors_per_gpu": 0},
+                   "packets_per_gpu": RX_N, "descriptors_per_gpu": 0, "rotating_batches": 2},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                      "kernel": "nsk::rx_ring<13>", "layout": "ring (1504-B slots, u32 lengths)",
@@ -1057,7 +1068,8 @@ def host_mode(args, dist, eng, batch, dev):
             "n_gpus": dist.world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": wall / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
             "config": {"workload": WORKLOADS[args.config], "packets_per_gpu": batch.n,
-                       "staging": "64 MiB / 128K-descriptor chunks, 2 streams; arena and table pinned"},
+                       "staging": "64 MiB / 128K-descriptor chunks, 4 in flight (one stream each), results written to mapped "
+                                  "memory; arena and table pinned"},
         }), flush=True)
     eng.close()
     dist.close()

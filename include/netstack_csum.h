@@ -273,9 +273,10 @@ int ns_csum_tcp_tx_multi(ns_csum_ctx* ctx, uint8_t* d_arena, uint64_t arena_byte
 int ns_csum_stream_release(ns_csum_ctx* ctx, void* stream);
 int ns_csum_scratch_count(ns_csum_ctx* ctx, uint32_t* count);
 
-/* Host-memory batch: H2D of arena and table, kernels, D2H of results,
- * pipelined over two streams in chunks; synchronous.  Pageable host memory is
- * bounced through the context's pinned staging.                             */
+/* Host-memory batch: H2D of arena and table, kernels writing the results
+ * into mapped pinned memory, pipelined in chunks over the context's streams
+ * (four in flight); synchronous.  Pageable host memory is bounced through
+ * the context's pinned staging.                                             */
 int ns_csum_batch_host(ns_csum_ctx* ctx, const uint8_t* h_arena,
                        uint64_t arena_bytes, const ns_pkt_desc* h_desc,
                        uint32_t n, uint16_t* h_out, uint32_t batch_flags);

@@ -339,7 +339,6 @@ struct ns_csum_ctx {
   hipStream_t retire = nullptr;  // frees retired scratch after its last use
   // ns_csum_sync's exchanged error count (mapped: written by take_err)
   MappedPin err_taken;
-  // host-path slots (double-buffered)
   ChainBuf z_chain;  // a chained zero-copy pass's scratch
   // host-path slots (nslots in flight; pmu)
   DevBuf<uint8_t> d_arena[kMaxHostSlots];

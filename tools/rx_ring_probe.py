@@ -46,6 +46,7 @@ def main():
     ap.add_argument("--prev", default="",
                     help="a variants library built from an earlier rx_ring.hip: its product shape is timed "
                          "beside the others as 'prev' (an A/B on one box)")
+    ap.add_argument("--rotate", type=int, default=1, help="alternate two rings (1) or re-read one (0)")
     ap.add_argument("--trend", type=int, default=0,
                     help="then time this many back-to-back launches of the product one by one (run-long drift)")
     args = ap.parse_args()
@@ -63,8 +64,12 @@ def main():
     err = torch.zeros(1, dtype=torch.int64, device=dev)
     verdict = torch.empty(n, dtype=torch.uint8, device=dev)
     sums = torch.empty(2 * n, dtype=torch.int16, device=dev)
-    g = RxGeo(arena.data_ptr(), W.RX_STRIDE, lens.data_ptr(), sums.data_ptr(), verdict.data_ptr(), err.data_ptr(),
-              n, 0, 0, 0)
+    # two rings of the same frames, alternating (3.2 GB > the MALL), as
+    # bench.py runs it
+    arena2 = W.rx_ring_batch(n, 9, dev, corrupt_every=1000)[0] if args.rotate else arena
+    gs = [RxGeo(a.data_ptr(), W.RX_STRIDE, lens.data_ptr(), sums.data_ptr(), verdict.data_ptr(), err.data_ptr(),
+                n, 0, 0, 0) for a in (arena, arena2)]
+    g = gs[0]
     algo = n * (W.RX_PKT + 9)
     ks = [int(k) for k in args.only.split(",")] if args.only else sorted(NAMES)
     libs = {k: lib for k in ks}
@@ -87,11 +92,11 @@ def main():
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     for _ in range(args.rounds):
         for k in ks:
-            for _ in range(3):
-                libs[k].rxv_launch(ctypes.byref(g), stream.cuda_stream, max(k, 0))
+            for j in range(3):
+                libs[k].rxv_launch(ctypes.byref(gs[j % 2]), stream.cuda_stream, max(k, 0))
             ev[0].record(stream)
-            for _ in range(args.reps):
-                libs[k].rxv_launch(ctypes.byref(g), stream.cuda_stream, max(k, 0))
+            for j in range(args.reps):
+                libs[k].rxv_launch(ctypes.byref(gs[j % 2]), stream.cuda_stream, max(k, 0))
             ev[1].record(stream)
             torch.cuda.synchronize()
             res[k].append(ev[0].elapsed_time(ev[1]) * 1e3 / args.reps)
@@ -105,14 +110,14 @@ def main():
         evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.trend + 1)]
         evs[0].record(stream)
         for i in range(args.trend):
-            lib.rxv_launch(ctypes.byref(g), stream.cuda_stream, 0)
+            lib.rxv_launch(ctypes.byref(gs[i % 2]), stream.cuda_stream, 0)
             evs[i + 1].record(stream)
         torch.cuda.synchronize()
         t = [evs[i].elapsed_time(evs[i + 1]) * 1e3 for i in range(args.trend)]
         q = max(1, args.trend // 10)
         trend = {"per_launch_us": [round(x, 1) for x in t],
                  "first_decile_us": round(float(np.median(t[:q])), 2), "last_decile_us": round(float(np.median(t[-q:])), 2)}
-    print(json.dumps({"workload": "1M x 1500-B IPv4/TCP in 1504-B slots", "algo_bytes": algo, "variants": out,
+    print(json.dumps({"workload": "1M x 1500-B IPv4/TCP in 1504-B slots" + (", 2 rotating rings" if args.rotate else ", one ring re-read"), "algo_bytes": algo, "variants": out,
                       "trend": trend}, indent=1))
 
 
