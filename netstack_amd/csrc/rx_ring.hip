@@ -128,7 +128,7 @@ __device__ __forceinline__ uint4 rx_load(__amdgpu_buffer_rsrc_t r, uint32_t off)
 // line 1 re-reads those lines with the range check.  F = 0: every chunk
 // range-checked.  The product runs <NB, 0, 2, 4, 1, 1>;
 // tools/rx_ring_variants.hip times the others.
-template <int NB, int A0 = 0, int AN = 2, int WV = kWaves, int OCC = 1, int F = 1>
+template <int NB, int A0 = 0, int AN = 2, int WV = kWaves, int OCC = 1, int F = 1, int SPEC = 0>
 __global__ __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(OCC))) void rx_ring(RxGeo g) {
   __shared__ uint4 rx_lds[WV * kPerWave * kRowBytes / 16];
   const uint32_t lane = threadIdx.x & 63u, grp = lane >> 3, li = lane & 7u;
@@ -143,10 +143,7 @@ __global__ __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(OCC))) 
   // malformed and counted (ns_csum_sync), a frame of no more than its link
   // header is dropped by the link (packet_dispatchers.go:268-270).
   const uint32_t rlen = live ? g.len[s] : 0u;
-  const bool over = (uint64_t)rlen > g.stride;
   const uint32_t pre = g.frame_at + g.link;
-  const uint32_t P = (!over && rlen > pre) ? rlen - pre : 0u;  // Data.Size()
-  const uint32_t Pl = P < kMaxIp ? P : kMaxIp;                  // bytes any header can cover
   const uint64_t slot = g.ring + s * g.stride;
 
   // Wave-relative 32-bit coordinates: one buffer resource from the 128-B
@@ -158,6 +155,16 @@ __global__ __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(OCC))) 
   const uint32_t pa = (uint32_t)(slot + pre - wbase);  // the IP packet's first byte
   const uint32_t po = pa & 15u;                         // its offset in its 16-B chunk (even)
   const uint32_t cl = (pa & ~127u) + 16u * li;          // lane li's chunk of line 0
+  uint4 v[NB];
+  // SPEC (timing variants): line 0 (1: and line 1, 2) loaded before the
+  // length arrives: bytes past the frame only ever reach the LDS row, whose
+  // reads the parse gates by the lengths, and the sums range-check lines 0-1
+  if constexpr (SPEC >= 1) v[0] = rx_load<A0>(rsrc, live ? cl : nrec);
+  if constexpr (SPEC >= 2) v[1] = rx_load<AN>(rsrc, live ? cl + 128u : nrec);
+  if constexpr (SPEC >= 1) __builtin_amdgcn_sched_barrier(0);
+  const bool over = (uint64_t)rlen > g.stride;
+  const uint32_t P = (!over && rlen > pre) ? rlen - pre : 0u;  // Data.Size()
+  const uint32_t Pl = P < kMaxIp ? P : kMaxIp;                  // bytes any header can cover
   // chunk at o: loaded only where it holds packet bytes, else the range
   // check returns zeros without touching memory
   const uint32_t lim = Pl ? Pl + 15u : 0u;
@@ -170,13 +177,12 @@ __global__ __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(OCC))) 
   const bool any1 = Pl && pe > cl + 128u;  // some line k >= 1 holds packet bytes for this lane
   const uint32_t cl1 = any1 ? cl : nrec;
 
-  uint4 v[NB];
-  v[0] = rx_load<A0>(rsrc, off_of(cl));
+  if constexpr (SPEC < 1) v[0] = rx_load<A0>(rsrc, off_of(cl));
   auto line = [&](int k) {
     if constexpr (F) v[k] = rx_load<AN>(rsrc, ((uint32_t)k <= klast ? cl1 : nrec) + 128u * k);
     else v[k] = rx_load<AN>(rsrc, off_of(cl + 128u * k));
   };
-  line(1);
+  if constexpr (SPEC < 2) line(1);
   // The EtherType (the link header's bytes 12-13, pa - 2): a buffer load on
   // a resource one line lower (pa - 2 may precede wbase), issued after the
   // lines the parse reads, so waiting for it waits for nothing more.
@@ -368,11 +374,11 @@ static int rx_batch_lines(const RxGeo& g) {
   return lines <= 2 ? 2 : lines <= 4 ? 4 : lines <= 8 ? 8 : lines <= 13 ? 13 : 16;
 }
 
-template <int NB, int A0 = 0, int AN = 2, int WV = kWaves, int OCC = 1, int F = 1>
+template <int NB, int A0 = 0, int AN = 2, int WV = kWaves, int OCC = 1, int F = 1, int SPEC = 0>
 static hipError_t launch_rx_ring_t(const RxGeo& g, hipStream_t stream) {
   if (g.n == 0) return hipSuccess;
   const uint64_t per_wg = (uint64_t)WV * kPerWave;
-  hipLaunchKernelGGL((rx_ring<NB, A0, AN, WV, OCC, F>), dim3((uint32_t)((g.n + per_wg - 1) / per_wg)), dim3(64 * WV), 0,
+  hipLaunchKernelGGL((rx_ring<NB, A0, AN, WV, OCC, F, SPEC>), dim3((uint32_t)((g.n + per_wg - 1) / per_wg)), dim3(64 * WV), 0,
                      stream, g);
   return hipGetLastError();
 }

@@ -27,7 +27,7 @@ from netstack_amd import Engine  # noqa: E402
 from netstack_amd import workloads as W  # noqa: E402
 
 NAMES = {0: "product", 1: "all_default", 2: "all_nt", 3: "wg2", 4: "wg8", 5: "wg1", 6: "nb16", 7: "nb8",
-         8: "occ6", 9: "nb12", 10: "checked_f0", 11: "f1_nb8"}
+         8: "occ6", 9: "nb12", 10: "checked_f0", 11: "f1_nb8", 12: "spec_line0", 13: "spec_lines01"}
 
 
 class RxGeo(ctypes.Structure):

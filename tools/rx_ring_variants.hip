@@ -9,6 +9,7 @@
 //   9 12 lines per batch
 //  10 every chunk range-checked (F = 0: round 5's first product shape)
 //  11 F with 8 lines per batch
+//  12 / 13 line 0 / lines 0-1 loaded before the slot's length arrives
 // Every variant computes the same verdicts and sums.  Not part of the ABI.
 #include "../netstack_amd/csrc/rx_ring.hip"
 
@@ -26,6 +27,8 @@ extern "C" int rxv_launch(const nsk::RxGeo* g, void* stream, int k) {
     case 9: return (int)nsk::launch_rx_ring_t<12>(*g, s);
     case 10: return (int)nsk::launch_rx_ring_t<13, 0, 2, 4, 1, 0>(*g, s);
     case 11: return (int)nsk::launch_rx_ring_t<8, 0, 2, 4, 1, 1>(*g, s);
+    case 12: return (int)nsk::launch_rx_ring_t<13, 0, 2, 4, 1, 1, 1>(*g, s);
+    case 13: return (int)nsk::launch_rx_ring_t<13, 0, 2, 4, 1, 1, 2>(*g, s);
     default: return (int)nsk::launch_rx_ring_t<13>(*g, s);
   }
 }
