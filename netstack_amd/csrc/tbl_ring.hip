@@ -145,8 +145,9 @@ __device__ __forceinline__ uint32_t grp_packet(__amdgpu_buffer_rsrc_t r, uint32_
 // FX > 0 (timing probes only, tools/grp_variants.hip): no descriptor read,
 // packet i at arena byte i * FX, 1,500 B long — the payload loads' floor
 // without the descriptor -> payload dependency.
-template <int NB, int FX = 0>
-__global__ __launch_bounds__(64 * kGrpWaves) void tbl_ring(const uint8_t* __restrict__ arena, uint64_t arena_bytes,
+// OCC: a waves-per-SIMD floor for the register allocator (timing probes).
+template <int NB, int FX = 0, int OCC = 1, int FL = 1500>
+__global__ __launch_bounds__(64 * kGrpWaves) __attribute__((amdgpu_waves_per_eu(OCC))) void tbl_ring(const uint8_t* __restrict__ arena, uint64_t arena_bytes,
                                                            const uint4* __restrict__ desc, uint32_t n,
                                                            uint16_t* __restrict__ out,
                                                            unsigned long long* __restrict__ err) {
@@ -159,7 +160,7 @@ __global__ __launch_bounds__(64 * kGrpWaves) void tbl_ring(const uint8_t* __rest
   // every lane of the group loads its packet's descriptor (8 descriptors =
   // 128 B per wave instruction)
   const uint4 raw = !live ? make_uint4(0, 0, 0, 0)
-                   : FX ? make_uint4((uint32_t)(i * FX), (uint32_t)((i * FX) >> 32), 1500u, 0u)
+                   : FX ? make_uint4((uint32_t)(i * FX), (uint32_t)((i * FX) >> 32), (uint32_t)FL, 0u)
                         : desc[i];
   const uint64_t off = (uint64_t)raw.x | ((uint64_t)raw.y << 32);
   uint32_t len = raw.z;

@@ -23,7 +23,7 @@ import torch  # noqa: E402
 
 from netstack_amd import workloads as W  # noqa: E402
 
-NAMES = {0: "tbl_ring", 1: "hyb", 2: "tbl_ring_no_desc"}
+NAMES = {0: "tbl_ring", 1: "hyb", 2: "tbl_ring_no_desc", 3: "no_desc_1460_contig", 4: "no_desc_occ8"}
 
 
 def main():
