@@ -108,14 +108,15 @@ def main():
             assert TXV.txv_launch(ctypes.byref(t), stream.cuda_stream, k) == 0
         return f
 
-    def txv(k, tile=0, rot=True):
+    def txv(k, tile=0, rot=True, htile=0):
         def f(r):
             a = batches[r if rot else 0]
             t = TxGeo(hdr=a.data_ptr() + geo["hdr_off"], pay=a.data_ptr() + geo["pay_off"], size=geo["size"], n=n,
                       mss=geo["mss"], slot=geo["slot"], tile=tile, ip_at=geo["ip_at"], ip_len=geo["ip_len"],
                       tcp_at=geo["tcp_at"], tcp_len=geo["tcp_len"], addr_sum=addr_sum(geo["src"], geo["dst"]),
                       proto=6, mode=3, xs=xs.data_ptr() if k >= 8 else None, xstride=1,
-                      out=sink.data_ptr() if 19 <= k <= 27 else None)  # the floor kernels' sink only
+                      out=sink.data_ptr() if 19 <= k <= 27 or 36 <= k <= 38 else None,  # the floor kernels' sink only
+                      htile=htile)
             assert TXV.txv_launch(ctypes.byref(t), stream.cuda_stream, k) == 0
         return f
 
@@ -166,6 +167,16 @@ def main():
         "floor_1g_rd": txv_big(20),
         "floor_1g_wr": txv_big(21),
         "floor_1g_wr_a2": txv_big(23),
+        "hdr_pc8": txv(40), "hdr_pc16": txv(41), "hdr_pc32": txv(42), "hdr_pc48": txv(43), "hdr_1shot": txv(44),
+        "hdr_t32": txv(18, htile=32), "hdr_t48": txv(18, htile=48), "hdr_1shot_t32": txv(44, htile=32),
+        "hdr_t128": txv(18, htile=128), "hdr_t128_pc12": txv(45, htile=128), "hdr_t128_pc16": txv(41, htile=128),
+        "hdr_t96_pc12": txv(45, htile=96),
+        "floor_1g_rw_co": txv_big(36),
+        "floor_1g_rd_co": txv_big(37),
+        "floor_1g_wr_co": txv_big(38),
+        "floor_slots_rw_co": txv(36),
+        "floor_slots_rd_co": txv(37),
+        "floor_slots_wr_co": txv(38),
         "floor_slots_rw_a1": txv(25),
         "floor_slots_rw_a2": txv(26),
         "floor_slots_rw_a3": txv(27),
@@ -182,7 +193,7 @@ def main():
     want = W.tx_split_expected(n, 7000, dev)
     for name, f in variants.items():
         if name.endswith("_rx") or name in ("struct_hdr_only", "txv_noreduce") or "nowb" in name or "stream" in name \
-                or name.startswith(("floor_", "txv_hdr_pass")):
+                or name.startswith(("floor_", "txv_hdr_pass", "hdr_")):
             continue
         h = batches[0][:n * W.TX_HDR].view(n, W.TX_HDR)
         h[:, W.TX_IP_AT + 10:W.TX_IP_AT + 12] = 0

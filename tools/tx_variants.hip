@@ -20,7 +20,10 @@
 //   both passes with the group payload pass all nontemporal / with
 //   nontemporal header stores / both; 33 = the all-nontemporal group
 //   payload pass alone; 34 / 35 = both passes, windowed / group payload
-//   pass (whatever the product's default).
+//   pass (whatever the product's default); 36 / 37 / 38 = the floors of
+//   19 / 20 / 21 with lane-consecutive chunks (1 KiB per wave instruction);
+//   40-43 = the persistent header pass alone at 8 / 16 / 32 / 48 waves per
+//   CU, 44 = the one-shot header pass alone (htile: the header tile).
 // Not part of the product ABI.
 #include "../netstack_amd/csrc/tcp_tx.hip"
 
@@ -46,6 +49,41 @@ __global__ __launch_bounds__(256) void slot_floor(uint64_t base, uint32_t bytes,
   }
 #pragma unroll
   for (int i = 0; i < 4; ++i) __builtin_amdgcn_raw_buffer_store_b128(v[i], r, (int)((c0 + (uint32_t)i) * 16u), 0, SA);
+}
+
+// The same with each store / load instruction covering 1 KiB contiguous per
+// wave (lane-consecutive chunks; slot_floor gives each lane 4 consecutive
+// chunks, so one instruction touches 4 KiB at a 64-B stride).
+template <int FL>
+__global__ __launch_bounds__(256) void slot_floor_co(uint64_t base, uint32_t bytes, uint32_t* sink) {
+  const __amdgpu_buffer_rsrc_t r = nsk::tx_srd(base, bytes);
+  __attribute__((ext_vector_type(4))) uint32_t v[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const uint32_t o = ((blockIdx.x * 4u + (uint32_t)i) * 256u + threadIdx.x) * 16u;
+    if (FL != 2) v[i] = __builtin_amdgcn_raw_buffer_load_b128(r, (int)o, 0, 0);
+    else v[i] = (__attribute__((ext_vector_type(4))) uint32_t){o, o, o, o};
+  }
+  if (FL == 1) {
+    uint32_t a = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) a ^= v[i].x ^ v[i].y ^ v[i].z ^ v[i].w;
+    if (a == 0x9E3779B9u) sink[0] = a;
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    __builtin_amdgcn_raw_buffer_store_b128(v[i], r, (int)(((blockIdx.x * 4u + (uint32_t)i) * 256u + threadIdx.x) * 16u),
+                                           0, 0);
+}
+
+template <int FL>
+hipError_t launch_floor_co(const nsk::TxGeo& g, hipStream_t s) {
+  const uint32_t bytes = (uint32_t)((g.n * (uint64_t)g.slot) & ~15ull);
+  const uint32_t chunks = bytes / 16u;
+  hipLaunchKernelGGL((slot_floor_co<FL>), dim3((chunks + 1023u) / 1024u), dim3(256), 0, s, g.hdr & ~15ull, bytes,
+                     reinterpret_cast<uint32_t*>(g.out));
+  return hipGetLastError();
 }
 
 template <int FL, int SA = 0>
@@ -107,6 +145,22 @@ extern "C" int txv_launch(const nsk::TxGeo* g, void* stream, int k) {
     case 32: e = nsk::launch_passes<16, 2, 1, 1, 1, 2>(*g, s); break;
     case 33: e = nsk::launch_payload_pass<16, 2, 0, 1, 2>(*g, s); break;
     case 34: e = nsk::launch_passes<16, 2, 0, 1, 1, 0>(*g, s); break;
+    case 40: case 41: case 42: case 43: case 45: {  // the persistent header pass alone at 8 / 16 / 32 / 48 / 12 waves per CU
+      nsk::TxGeo h = *g;
+      h.tile = g->htile;
+      const uint32_t pc[] = {8, 16, 32, 48, 0, 12};
+      e = nsk::launch_header_pass<0>(h, s, pc[k - 40]);
+      break;
+    }
+    case 44: {  // the one-shot header pass alone (round 4's)
+      nsk::TxGeo h = *g;
+      h.tile = g->htile;
+      e = nsk::launch_tcp_tx_t<16, 2, 0, 1, 0, 2>(h, s);
+      break;
+    }
+    case 36: e = launch_floor_co<0>(*g, s); break;
+    case 37: e = launch_floor_co<1>(*g, s); break;
+    case 38: e = launch_floor_co<2>(*g, s); break;
     case 35: e = nsk::launch_passes<16, 2, 0, 1, 1, 1>(*g, s); break;
     default: e = nsk::launch_tcp_tx_t<16, 2, 0, 1>(*g, s); break;
   }
