@@ -138,30 +138,6 @@ __device__ __forceinline__ uint32_t lds_wsum_loop(const uint8_t* L, uint32_t a, 
   return w;
 }
 
-// lds_wsum_loop four dwords at a time: the four LDS reads of an iteration are
-// independent, so a 20-B header costs two LDS round trips instead of six
-// (tcp_tx_hdr's tiles wait on this chain between their load and store).
-__device__ __forceinline__ uint32_t lds_wsum_loop4(const uint8_t* L, uint32_t a, uint32_t len, uint32_t zero) {
-  const uint32_t* D = reinterpret_cast<const uint32_t*>(L);
-  const uint32_t d0 = a >> 2;
-  const uint32_t nd = ((a + len + 3) >> 2) - d0;
-  uint32_t w = 0;
-#pragma nounroll
-  for (uint32_t k0 = 0; k0 < nd; k0 += 4) {
-    uint32_t x[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) x[j] = k0 + j < nd ? D[d0 + k0 + j] : 0u;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int b = (int)(4 * (d0 + k0 + j));
-      uint32_t m = below((int)(a + len) - b) & ~below((int)a - b);
-      m &= ~(below((int)(zero + 2) - b) & ~below((int)zero - b));
-      w = __builtin_amdgcn_sad_u16(x[j] & m, 0u, w);
-    }
-  }
-  return w;
-}
-
 __device__ __forceinline__ void lds_put_be16(uint8_t* L, uint32_t at, uint32_t v) {
   L[at] = (uint8_t)(v >> 8);
   L[at + 1] = (uint8_t)v;
@@ -447,23 +423,17 @@ __global__ __launch_bounds__(256) void tcp_tx_hdr(TxGeo g, uint32_t ntiles) {
   // the payload values and the sums, through resources of their own
   const __amdgpu_buffer_rsrc_t xr = tx_srd((uint64_t)(uintptr_t)g.xs, (uint32_t)(g.n * g.xstride * 2u));
   const __amdgpu_buffer_rsrc_t orr = tx_srd((uint64_t)(uintptr_t)g.out, g.out ? (uint32_t)(g.n * 4u) : 0u);
-  constexpr int SPL = CPL / 4;  // segments per lane: a tile holds at most 64 SPL
-  auto fetch = [&](uint32_t tt, uint4* v, uint32_t* pv) {
+  auto fetch = [&](uint32_t tt, uint4* v, uint32_t& pv) {
     const bool live = tt < ntiles;
     const uint64_t lo = g.hdr + (uint64_t)(live ? tt : 0u) * region;
     const uint32_t bytes = live ? (uint32_t)(end - lo < region ? ((end - lo + 15) & ~15ull) : region) : 0u;
     const __amdgpu_buffer_rsrc_t hr = tx_srd(lo, bytes);
 #pragma unroll
     for (int i = 0; i < CPL; ++i) v[i] = tx_load<0>(hr, (lane + 64u * i) * 16u);
-#pragma unroll
-    for (int q = 0; q < SPL; ++q) {
-      const uint32_t j = lane + 64u * q;
-      const uint64_t si = (uint64_t)tt * g.tile + j;
-      pv[q] = __builtin_amdgcn_raw_buffer_load_b16(
-          xr, (int)(live && j < g.tile && si < g.n ? si * g.xstride * 2u : 0xFFFFFFF0u), 0, 0);
-    }
+    const uint64_t si = (uint64_t)tt * g.tile + lane;
+    pv = __builtin_amdgcn_raw_buffer_load_b16(xr, (int)(live && si < g.n ? si * g.xstride * 2u : 0xFFFFFFF0u), 0, 0);
   };
-  auto finish = [&](uint32_t t, const uint4* v, const uint32_t* pv) {
+  auto finish = [&](uint32_t t, const uint4* v, uint32_t pv) {
     const uint64_t s0 = (uint64_t)t * g.tile;
     const uint32_t nseg = g.n - s0 < g.tile ? (uint32_t)(g.n - s0) : g.tile;
     const uint64_t lo = g.hdr + s0 * g.slot, hi = lo + (uint64_t)nseg * g.slot;
@@ -474,31 +444,27 @@ __global__ __launch_bounds__(256) void tcp_tx_hdr(TxGeo g, uint32_t ntiles) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    // the fields (tx_fields' arithmetic), segments lane, lane + 64, ...
-#pragma unroll
-    for (int q = 0; q < SPL; ++q) {
-      const uint32_t j = lane + 64u * q;
-      uint32_t ipv = 0, tcpv = 0;
-      if (j < nseg) {
-        const uint32_t o = j * g.slot;
-        const uint64_t si = s0 + j;
-        const uint32_t size = si + 1 < g.n ? g.mss : (uint32_t)(g.size - (g.n - 1) * (uint64_t)g.mss);
-        if (g.mode & kTxIp) {
-          const uint32_t a = o + g.ip_at;
-          ipv = tx_fold(tx_class(lds_wsum_loop4(L, a, g.ip_len, a + 10u), a & 1u));  // Checksum(ip[:IHL], 0)
-          lds_put_be16(L, a + 10u, ~ipv & 0xFFFFu);
-        }
-        uint32_t x = tx_fold(g.addr_sum + ((g.tcp_len + size) & 0xFFFFu));  // PseudoHeaderChecksum
-        x = tx_fold(x + g.proto);
-        const uint32_t a = o + g.tcp_at;
-        x = tx_fold(x + (pv[q] & 0xFFFFu));                                             // ChecksumVVWithOffset
-        x = tx_fold(x + tx_class(lds_wsum_loop4(L, a, g.tcp_len, a + 16u), a & 1u));    // CalculateChecksum
-        lds_put_be16(L, a + 16u, ~x & 0xFFFFu);
-        tcpv = x;
+    // the fields (tx_fields' arithmetic for the lane's one segment)
+    uint32_t ipv = 0, tcpv = 0;
+    if (lane < nseg) {
+      const uint32_t o = lane * g.slot;
+      const uint64_t si = s0 + lane;
+      const uint32_t size = si + 1 < g.n ? g.mss : (uint32_t)(g.size - (g.n - 1) * (uint64_t)g.mss);
+      if (g.mode & kTxIp) {
+        const uint32_t a = o + g.ip_at;
+        ipv = tx_fold(tx_class(lds_wsum_loop(L, a, g.ip_len, a + 10u), a & 1u));  // Checksum(ip[:IHL], 0)
+        lds_put_be16(L, a + 10u, ~ipv & 0xFFFFu);
       }
-      __builtin_amdgcn_raw_buffer_store_b32(ipv | (tcpv << 16), orr, (int)(j < nseg ? (s0 + j) * 4u : 0xFFFFFFF0u), 0,
-                                            0);
+      uint32_t x = tx_fold(g.addr_sum + ((g.tcp_len + size) & 0xFFFFu));  // PseudoHeaderChecksum
+      x = tx_fold(x + g.proto);
+      const uint32_t a = o + g.tcp_at;
+      x = tx_fold(x + (pv & 0xFFFFu));                                               // ChecksumVVWithOffset
+      x = tx_fold(x + tx_class(lds_wsum_loop(L, a, g.tcp_len, a + 16u), a & 1u));    // CalculateChecksum
+      lds_put_be16(L, a + 16u, ~x & 0xFFFFu);
+      tcpv = x;
     }
+    __builtin_amdgcn_raw_buffer_store_b32(ipv | (tcpv << 16), orr, (int)(lane < nseg ? (s0 + lane) * 4u : 0xFFFFFFF0u), 0,
+                                          0);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -522,7 +488,7 @@ __global__ __launch_bounds__(256) void tcp_tx_hdr(TxGeo g, uint32_t ntiles) {
     if (lane < (uint32_t)((hi - lo) & 15u)) reinterpret_cast<uint8_t*>((uintptr_t)(lo + full * 16u))[lane] = L[full * 16u + lane];
   };
   uint4 x[CPL], y[CPL];
-  uint32_t px[SPL], py[SPL];
+  uint32_t px = 0, py = 0;
   fetch(t0, x, px);
   fetch(t0 + NW, y, py);
   for (uint32_t t = t0;; t += 2 * NW) {
@@ -738,20 +704,14 @@ static hipError_t launch_header_pass(TxGeo h, hipStream_t stream, uint32_t per_c
   // the persistent kernel's conditions (tcp_tx_hdr): full TCP mode with whole
   // write-back, tiles of <= 64 segments starting 16-B aligned, <= 4 KiB of
   // slots each, d_out 4-B aligned
-  const uint64_t region = (uint64_t)h.tile * h.slot;
-  const bool c4 = h.tile <= 64 && region <= 4096, c8 = h.tile <= 128 && region <= 8192;
-  if (!(c4 || c8) || region % 16 || (h.hdr & 15) || !(h.mode & kTxTcpFull) || (h.mode & kTxFieldsOnly) ||
-      ((uintptr_t)h.out & 3) || h.xs == nullptr)
+  if (h.tile > 64 || (uint64_t)h.tile * h.slot > 4096 || ((uint64_t)h.tile * h.slot) % 16 || (h.hdr & 15) ||
+      !(h.mode & kTxTcpFull) || (h.mode & kTxFieldsOnly) || ((uintptr_t)h.out & 3) || h.xs == nullptr)
     return launch_tcp_tx_t<16, 2, SP, 1, 0, 2>(h, stream);
   const uint64_t tiles = (h.n + h.tile - 1) / h.tile;
   const uint64_t waves = std::min<uint64_t>(tiles, (uint64_t)tx_cu_count() * (per_cu ? per_cu : 24u));
   const uint32_t wgs = (uint32_t)((waves + h.wpg - 1) / h.wpg);
-  if (c4)
-    hipLaunchKernelGGL((tcp_tx_hdr<4, SP>), dim3(wgs), dim3(64 * h.wpg), (size_t)h.lds_wave * h.wpg, stream, h,
-                       (uint32_t)tiles);
-  else
-    hipLaunchKernelGGL((tcp_tx_hdr<8, SP>), dim3(wgs), dim3(64 * h.wpg), (size_t)h.lds_wave * h.wpg, stream, h,
-                       (uint32_t)tiles);
+  hipLaunchKernelGGL((tcp_tx_hdr<4, SP>), dim3(wgs), dim3(64 * h.wpg), (size_t)h.lds_wave * h.wpg, stream, h,
+                     (uint32_t)tiles);
   return hipGetLastError();
 }
 
