@@ -115,7 +115,7 @@ def main():
                       mss=geo["mss"], slot=geo["slot"], tile=tile, ip_at=geo["ip_at"], ip_len=geo["ip_len"],
                       tcp_at=geo["tcp_at"], tcp_len=geo["tcp_len"], addr_sum=addr_sum(geo["src"], geo["dst"]),
                       proto=6, mode=3, xs=xs.data_ptr() if k >= 8 else None, xstride=1,
-                      out=sink.data_ptr() if 19 <= k <= 27 or 36 <= k <= 38 else None,  # the floor kernels' sink only
+                      out=sink.data_ptr() if 19 <= k <= 27 or 36 <= k <= 38 or k == 47 else None,  # the floor kernels' sink only
                       htile=htile)
             assert TXV.txv_launch(ctypes.byref(t), stream.cuda_stream, k) == 0
         return f
@@ -171,6 +171,7 @@ def main():
         "hdr_t32": txv(18, htile=32), "hdr_t48": txv(18, htile=48), "hdr_1shot_t32": txv(44, htile=32),
         "hdr_t128": txv(18, htile=128), "hdr_t128_pc12": txv(45, htile=128), "hdr_t128_pc16": txv(41, htile=128),
         "hdr_t96_pc12": txv(45, htile=96),
+        "hdr_nt": txv(46), "floor_slots_wr_co_nt": txv(47), "floor_1g_wr_co_nt": txv_big(47),
         "floor_1g_rw_co": txv_big(36),
         "floor_1g_rd_co": txv_big(37),
         "floor_1g_wr_co": txv_big(38),

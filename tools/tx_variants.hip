@@ -61,7 +61,7 @@ __global__ __launch_bounds__(256) void slot_floor_co(uint64_t base, uint32_t byt
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const uint32_t o = ((blockIdx.x * 4u + (uint32_t)i) * 256u + threadIdx.x) * 16u;
-    if (FL != 2) v[i] = __builtin_amdgcn_raw_buffer_load_b128(r, (int)o, 0, 0);
+    if (FL < 2) v[i] = __builtin_amdgcn_raw_buffer_load_b128(r, (int)o, 0, 0);
     else v[i] = (__attribute__((ext_vector_type(4))) uint32_t){o, o, o, o};
   }
   if (FL == 1) {
@@ -74,7 +74,7 @@ __global__ __launch_bounds__(256) void slot_floor_co(uint64_t base, uint32_t byt
 #pragma unroll
   for (int i = 0; i < 4; ++i)
     __builtin_amdgcn_raw_buffer_store_b128(v[i], r, (int)(((blockIdx.x * 4u + (uint32_t)i) * 256u + threadIdx.x) * 16u),
-                                           0, 0);
+                                           0, FL == 3 ? 2 : 0);
 }
 
 template <int FL>
@@ -152,6 +152,13 @@ extern "C" int txv_launch(const nsk::TxGeo* g, void* stream, int k) {
       e = nsk::launch_header_pass<0>(h, s, pc[k - 40]);
       break;
     }
+    case 46: {  // the persistent header pass alone, nontemporal stores
+      nsk::TxGeo h = *g;
+      h.tile = g->htile;
+      e = nsk::launch_header_pass<1>(h, s, 0);
+      break;
+    }
+    case 47: e = launch_floor_co<3>(*g, s); break;  // written only, lane-consecutive, nontemporal
     case 44: {  // the one-shot header pass alone (round 4's)
       nsk::TxGeo h = *g;
       h.tile = g->htile;
