@@ -60,6 +60,9 @@ def parse():
                     help="--config 8 packets: as sendTCPBatch builds them (header slots + payload view) "
                          "filled from the batch geometry by ns_csum_tcp_tx (struct) or through an "
                          "NS_BATCH_PAIRED descriptor table (split), or wire-contiguous like config 7")
+    ap.add_argument("--tx-calls", type=int, default=1,
+                    help="--mode host --config 8: the 1M segments as this many sendTCPBatch calls in one "
+                         "ns_csum_tcp_tx_host (23832: one per 64 KiB GSO write)")
     ap.add_argument("--rotate", type=int, default=0,
                     help="distinct batches cycled per step (0 = auto: enough to exceed the 256 MiB MALL)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline time budget")
@@ -472,6 +475,8 @@ def main():
     eng = Engine(ordinal)
 
     cfg = args.config
+    if cfg == 8 and args.mode == "host":
+        return tx_host_mode(args, dist, eng, dev)
     if cfg in (7, 8):
         return packet_mode(args, dist, eng, dev, tx=cfg == 8)
     if cfg == 1:
@@ -837,22 +842,99 @@ def packet_mode(args, dist, eng, dev, tx: bool):
             # CPU leg: the same 65,536 segments through the oracle's C
             # restatement of sendTCPBatch's checksum steps, one core, timed
             # (bounded by --cpu-seconds); value in packet bytes per second
-            g = geo
-            work = np.ascontiguousarray(src).copy()
-            reps, t0 = 0, time.perf_counter()
-            while True:
-                O.c_send_tcp_batch(work, g["hdr_off"], g["pay_off"], 65536 * g["mss"], g["mss"], g["slot"],
-                                   g["ip_at"], g["ip_len"], g["tcp_at"], g["tcp_len"], g["src"], g["dst"],
-                                   copy=False)
-                reps += 1
-                el = time.perf_counter() - t0
-                if el >= args.cpu_seconds:
-                    break
-            result["cpu_baseline"] = {
-                "value": 65536 * W.RX_PKT * reps / el / GIB, "unit": "GiB/s", "cores": 1, "kind": "port",
-                "sample": f"65,536 segments ({65536 * W.RX_PKT} packet bytes) of the rank-0 batch x {reps} passes, "
-                          f"{el:.1f} s; oracle_send_tcp_batch (sendTCPBatch + buildTCPHdr + addIPHeader's checksum "
-                          f"steps over oracle/csum_oracle.c's scalar loop), single thread"}
+            result["cpu_baseline"] = send_tcp_batch_cpu(O, src, geo, args.cpu_seconds)
+    if dist.rank == 0:
+        print(json.dumps(result), flush=True)
+    eng.close()
+    dist.close()
+
+
+def send_tcp_batch_cpu(O, src, g, seconds):
+    """CPU leg of config 8: the first 65,536 segments through the oracle's C
+    restatement of sendTCPBatch's checksum steps, one core, timed for about
+    `seconds`; value in packet bytes per second."""
+    from netstack_amd import workloads as W
+
+    work = np.ascontiguousarray(src).copy()
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        O.c_send_tcp_batch(work, g["hdr_off"], g["pay_off"], 65536 * g["mss"], g["mss"], g["slot"],
+                           g["ip_at"], g["ip_len"], g["tcp_at"], g["tcp_len"], g["src"], g["dst"], copy=False)
+        reps += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return {"value": 65536 * W.RX_PKT * reps / el / GIB, "unit": "GiB/s", "cores": 1, "kind": "port",
+            "sample": f"65,536 segments ({65536 * W.RX_PKT} packet bytes) of the rank-0 batch x {reps} passes, "
+                      f"{el:.1f} s; oracle_send_tcp_batch (sendTCPBatch + buildTCPHdr + addIPHeader's checksum "
+                      f"steps over oracle/csum_oracle.c's scalar loop), single thread"}
+
+
+def tx_calls(geo, calls):
+    """cfg8's geometry as `calls` sendTCPBatch calls of consecutive segments
+    (each its own geometry: the fill is affine in the segment index)."""
+    n = -(-geo["size"] // geo["mss"])
+    per = -(-n // calls)
+    out = []
+    for a in range(0, n, per):
+        out.append(dict(geo, hdr_off=geo["hdr_off"] + a * geo["slot"], pay_off=geo["pay_off"] + a * geo["mss"],
+                        size=min(geo["size"] - a * geo["mss"], per * geo["mss"])))
+    return out
+
+
+def tx_host_mode(args, dist, eng, dev):
+    """`--mode host --config 8`: sendTCPBatch's fill over HOST memory
+    (ns_csum_tcp_tx_host), config 8's 1M x 1460-B segments per GPU in
+    sendTCPBatch's layout (54-B header slots + the payload view) in a pinned
+    host arena, as --tx-calls calls (1, or e.g. 23,832 = one per 64 KiB GSO
+    write: many connections' calls in one).  Each step is one synchronous
+    call: the slots and payload go to the device, the fill runs there, and
+    the fields are written into the host slots.  The refills are idempotent
+    (the fields are summed as zero).  After the timed region the host arena
+    must equal tx_split_expected's (torch integer ops).  Recorded in DESIGN.md
+    as the PCIe-inclusive rate; the device-resident line is --mode dev."""
+    import torch
+
+    from netstack_amd import workloads as W
+    from netstack_amd.engine import tx_table
+
+    seed = 7000 + dist.rank
+    geo = W.tx_struct_geometry(RX_N)
+    src = W.tx_split_batch(RX_N, seed, dev)[0].cpu()
+    arena = torch.empty(src.numel(), dtype=torch.uint8).pin_memory()
+    arena.copy_(src)
+    del src
+    a = arena.numpy()
+    before = a[:geo["pay_off"] + 65536 * geo["mss"]].copy() if dist.rank == 0 and not args.no_cpu else None
+    calls = tx_calls(geo, max(1, args.tx_calls))
+    table = tx_table(calls)
+
+    def step():
+        eng.tcp_tx_host(a, table)
+
+    wall, _ = timed_region(step, lambda: None, dist, args.steps, args.warmup, dev)
+    want = W.tx_split_expected(RX_N, seed, dev)
+    ok = bool(torch.equal(arena.to(dev), want))
+    del want
+    fails = dist.sum(0.0 if ok else 1.0, dev)
+    total = dist.sum(float(RX_N * W.RX_PKT), dev)
+    result = {
+        "metric": "TX checksum fill GiB/s host-inclusive (H2D + fill + fields written back; IPv4 + TCP, 1500-B packets)",
+        "value": total * args.steps / wall / GIB, "unit": "GiB/s", "n_gpus": dist.world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": wall / args.steps * 1e3,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic packets to send (checksum fields zero before the first call), pinned host memory",
+        "config": {"workload": "tx: 1,048,576 x 1500-B IPv4/TCP packets per GPU in sendTCPBatch's layout "
+                               "(54-B header slots + a payload view) in host memory, ns_csum_tcp_tx_host",
+                   "calls": len(calls), "segments_per_call": -(-RX_N // len(calls)),
+                   "staging": "64 MiB chunks, 4 in flight (one stream each); sums to mapped memory, fields "
+                              "written by the host"},
+        "property_check": {"arena_equals_expected": ok, "ranks_failed": int(fails)},
+    }
+    if dist.rank == 0 and not args.no_cpu:
+        import oracle as O
+
+        result["cpu_baseline"] = send_tcp_batch_cpu(O, before, geo, args.cpu_seconds)
     if dist.rank == 0:
         print(json.dumps(result), flush=True)
     eng.close()

@@ -64,13 +64,14 @@
 extern "C" {
 #endif
 
-#define NS_CSUM_ABI_VERSION 8  /* 2: ns_csum_batch_dev_store, NS_DESC_STORE*;
+#define NS_CSUM_ABI_VERSION 9  /* 2: ns_csum_batch_dev_store, NS_DESC_STORE*;
                                   3: ns_csum_stage_*, ns_csum_packet_buffers;
                                   4: ns_csum_stream_release, _scratch_count;
                                   5: ns_csum_get_stats;
                                   6: ns_csum_tcp_tx;
                                   7: ns_csum_tcp_tx_multi;
-                                  8: ns_csum_rx_ring, ns_csum_set_tx_tuning */
+                                  8: ns_csum_rx_ring, ns_csum_set_tx_tuning;
+                                  9: ns_csum_tcp_tx_host */
 
 /* ---- status codes ------------------------------------------------------- */
 #define NS_OK 0
@@ -263,6 +264,23 @@ int ns_csum_tcp_tx(ns_csum_ctx* ctx, uint8_t* d_arena, uint64_t arena_bytes,
 int ns_csum_tcp_tx_multi(ns_csum_ctx* ctx, uint8_t* d_arena, uint64_t arena_bytes,
                          const ns_tcp_tx* txs, uint32_t count, uint16_t* d_out,
                          void* stream);
+/* The same calls over HOST memory (sendTCPBatch as netstack runs it: the
+ * header slots and payload views in host memory, possibly many connections'
+ * calls at once): h_arena as d_arena above, txs[0..count) checked as for
+ * ns_csum_tcp_tx_multi.  Synchronous.  The bytes the calls read (their slots,
+ * and the payload of full-mode calls) go to the device in chunks of at most
+ * the context's staging size (ns_csum_opts.staging_bytes; a call larger than
+ * that is split by segments), four chunks in flight; ranges closer than 4 KiB
+ * travel together, so bytes between them are uploaded too.  Each segment's
+ * fields are then written into h_arena's slots, the same values
+ * ns_csum_tcp_tx_multi stores: only the 2-byte fields change, every other
+ * byte is left as it was.  h_out (2 * sum n_k u16, or NULL) gets the sums as
+ * d_out does.  Pinned memory (ns_csum_stage_acquire) is copied by DMA
+ * directly; pageable memory is bounced by the HIP runtime.  Errors as for
+ * ns_csum_tcp_tx_multi, returned before any byte is written; on an engine
+ * error later (NS_ENOMEM, NS_EHIP) some fields may already be written.     */
+int ns_csum_tcp_tx_host(ns_csum_ctx* ctx, uint8_t* h_arena, uint64_t arena_bytes,
+                        const ns_tcp_tx* txs, uint32_t count, uint16_t* h_out);
 
 /* Frees the scratch the context keeps for `stream` (see ns_csum_batch_dev),
  * after the stream's last launch that used it; nothing waits.  Call it

@@ -350,6 +350,10 @@ struct ns_csum_ctx {
   // D2H copy on the DMA engine; NS_CSUM_HOST_D2H=1 copies them instead, A/B)
   PinBuf<uint16_t, hipHostMallocMapped | hipHostMallocNonCoherent | hipHostMallocPortable> h_out[kMaxHostSlots];
   bool host_d2h = false;
+  // ns_csum_tcp_tx_host: each slot's geometry table (TxGeo[] + first[]),
+  // pinned for its upload and on the device
+  PinBuf<uint8_t> h_txtab[kMaxHostSlots];
+  DevBuf<uint8_t> d_txtab[kMaxHostSlots];
   // zero-copy pass buffers for small calls: the table (read by the kernel),
   // the results and the completion word (written by it)
   BarBuf z_buf;
@@ -815,6 +819,111 @@ int run_host_batch(ns_csum_ctx* ctx, const uint8_t* h_arena, uint64_t arena_byte
   return drain(slot);
 }
 
+inline void put_be16(uint8_t* p, uint32_t v) {
+  p[0] = (uint8_t)(v >> 8);
+  p[1] = (uint8_t)v;
+}
+
+// ns_csum_tcp_tx_host's pipeline over nsh::tx_host_plan's chunks, nslots in
+// flight on the host pipeline's streams.  Per chunk: one H2D copy per merged
+// byte range into the slot's staging, the geometry table, and one
+// tcp_tx_multi launch (fields-only: its stores stay in the staging) whose sums
+// go straight to mapped pinned memory.  When a chunk is done the host writes
+// its fields into the caller's slots from those sums, the values the kernel
+// stores (2 x 2 B per segment instead of copying the slots back), while the
+// later chunks are in flight.
+int run_tx_host(ns_csum_ctx* ctx, uint8_t* h_arena, const nsh::TxHostPlan& plan, uint16_t* h_out) {
+  const uint32_t nslots = ctx->nslots;
+  int64_t pend[kMaxHostSlots];
+  std::fill(pend, pend + kMaxHostSlots, (int64_t)-1);
+  auto finish = [&](uint32_t sl) -> int {
+    if (pend[sl] < 0) return NS_OK;
+    const nsh::TxChunk& c = plan.chunks[(size_t)pend[sl]];
+    pend[sl] = -1;
+    HIP_TRY(hipEventSynchronize(ctx->done[sl]));
+    const uint16_t* res = ctx->h_out[sl].p;
+    for (uint32_t j = c.p0; j < c.p0 + c.np; ++j) {
+      const nsh::TxPiece& q = plan.pieces[j];
+      const uint16_t* r = res + 2 * (q.out0 - c.out0);
+      uint8_t* s = h_arena + q.t.hdr_off;
+      for (uint64_t i = 0; i < q.nseg; ++i, s += q.t.slot) {
+        if (q.mode & nsk::kTxIp) put_be16(s + q.t.ip_at + 10u, ~r[2 * i] & 0xFFFFu);
+        if (q.mode & nsk::kTxTcpFull) put_be16(s + q.t.tcp_at + 16u, ~r[2 * i + 1] & 0xFFFFu);
+        if (q.mode & nsk::kTxTcpPartial) put_be16(s + q.t.tcp_at + 16u, r[2 * i + 1]);
+      }
+      if (h_out) std::memcpy(h_out + 2 * q.out0, r, 4 * q.nseg);
+    }
+    return NS_OK;
+  };
+  std::vector<nsk::TxGeo> calls;
+  std::vector<uint32_t> first;
+  auto enqueue = [&](const nsh::TxChunk& c, uint32_t sl) -> int {
+    int rc;
+    if ((rc = ctx->d_arena[sl].ensure(c.staging + 256)) != NS_OK) return rc;
+    if ((rc = ctx->h_out[sl].ensure(2 * c.nout)) != NS_OK) return rc;
+    const uint64_t base = (uint64_t)(uintptr_t)ctx->d_arena[sl].p;
+    calls.assign(c.np, nsk::TxGeo{});
+    for (uint32_t j = 0; j < c.np; ++j) {
+      const nsh::TxPiece& q = plan.pieces[c.p0 + j];
+      nsk::TxGeo& geo = calls[j];
+      geo.hdr = base + plan.map(c, q.t.hdr_off);
+      // a payload only full-mode pieces read (and upload)
+      geo.pay = (q.mode & nsk::kTxTcpFull) ? base + plan.map(c, q.t.pay_off) : geo.hdr;
+      geo.size = q.t.size;
+      geo.n = q.nseg;
+      geo.mss = q.t.mss;
+      geo.slot = q.t.slot;
+      geo.ip_at = q.t.ip_at;
+      geo.ip_len = q.t.ip_len;
+      geo.tcp_at = q.t.tcp_at;
+      geo.tcp_len = q.t.tcp_len;
+      geo.addr_sum = q.t.addr_sum;
+      geo.proto = q.t.protocol;
+      geo.mode = q.mode | nsk::kTxFieldsOnly;
+      geo.out = ctx->h_out[sl].dev + 2 * (q.out0 - c.out0);
+    }
+    first.assign(c.np + 1, 0);
+    nsk::TxGeo launch{};
+    const uint32_t grid = nsk::tx_multi_prepare(calls.data(), c.np, &launch, first.data());
+    if (grid == 0) return NS_EINVAL;  // more than 2^31 tiles
+    const size_t tab = ((size_t)c.np * sizeof(nsk::TxGeo) + 15) & ~(size_t)15;
+    const size_t bytes = tab + first.size() * sizeof(uint32_t);
+    if ((rc = ctx->h_txtab[sl].ensure(bytes)) != NS_OK) return rc;
+    if ((rc = ctx->d_txtab[sl].ensure(bytes)) != NS_OK) return rc;
+    std::memcpy(ctx->h_txtab[sl].p, calls.data(), (size_t)c.np * sizeof(nsk::TxGeo));
+    std::memcpy(ctx->h_txtab[sl].p + tab, first.data(), first.size() * sizeof(uint32_t));
+    hipStream_t s = ctx->stream[sl];
+    for (uint32_t j = c.r0; j < c.r0 + c.nr; ++j) {
+      const nsh::TxRange& r = plan.ranges[j];
+      HIP_TRY(hipMemcpyAsync(ctx->d_arena[sl].p + r.at, h_arena + r.lo, r.hi - r.lo, hipMemcpyHostToDevice, s));
+    }
+    HIP_TRY(hipMemcpyAsync(ctx->d_txtab[sl].p, ctx->h_txtab[sl].p, bytes, hipMemcpyHostToDevice, s));
+    HIP_TRY(nsk::launch_tcp_tx_multi(launch, grid, reinterpret_cast<const nsk::TxGeo*>(ctx->d_txtab[sl].p),
+                                     reinterpret_cast<const uint32_t*>(ctx->d_txtab[sl].p + tab), c.np, s));
+    HIP_TRY(hipEventRecord(ctx->done[sl], s));
+    return NS_OK;
+  };
+  int rc = NS_OK;
+  uint32_t slot = 0;
+  for (size_t ci = 0; ci < plan.chunks.size(); ++ci) {
+    if ((rc = finish(slot)) != NS_OK) break;
+    if ((rc = enqueue(plan.chunks[ci], slot)) != NS_OK) {
+      // copies of this chunk may be in flight: the caller's memory and the
+      // staging must be idle before returning
+      (void)hipStreamSynchronize(ctx->stream[slot]);
+      (void)hipGetLastError();
+      break;
+    }
+    pend[slot] = (int64_t)ci;
+    slot = (slot + 1) % nslots;
+  }
+  for (uint32_t k = 0; k < nslots; ++k) {
+    const int r = finish((slot + k) % nslots);
+    if (rc == NS_OK) rc = r;
+  }
+  return rc;
+}
+
 // Caller-acquired staging (ns_csum_stage_acquire): mapped pinned buffers a
 // caller fills itself — the Go shim, which may not hand C memory holding Go
 // pointers to the library, copies its views there once.  Gathers whose bytes
@@ -1158,6 +1267,8 @@ void ns_csum_destroy(ns_csum_ctx* ctx) {
       ctx->d_chain[s].release();
       ctx->h_desc[s].release();
       ctx->h_out[s].release();
+      ctx->h_txtab[s].release();
+      ctx->d_txtab[s].release();
       if (ctx->done[s]) (void)hipEventDestroy(ctx->done[s]);
       if (ctx->stream[s]) (void)hipStreamDestroy(ctx->stream[s]);
     }
@@ -1452,6 +1563,21 @@ int ns_csum_tcp_tx_multi(ns_csum_ctx* ctx, uint8_t* d_arena, uint64_t arena_byte
   }
   ctx->scratch.unpin(sc);
   return rc;
+}
+
+int ns_csum_tcp_tx_host(ns_csum_ctx* ctx, uint8_t* h_arena, uint64_t arena_bytes, const ns_tcp_tx* txs,
+                        uint32_t count, uint16_t* h_out) {
+  if (!ctx || (count && !txs) || (arena_bytes && !h_arena)) return NS_EINVAL;
+  CallClock clk(ctx);
+  nsh::TxHostPlan plan;
+  const int vr = nsh::tx_host_plan(txs, count, arena_bytes, ctx->staging, &plan);
+  if (vr != NS_OK) return vr;
+  if (h_out)
+    for (const auto& z : plan.zeros) std::memset(h_out + 2 * z.first, 0, 4 * z.second);
+  if (plan.chunks.empty()) return NS_OK;
+  std::lock_guard<std::mutex> lk(ctx->pmu);
+  DeviceGuard g(ctx->device);
+  return run_tx_host(ctx, h_arena, plan, h_out);
 }
 
 int ns_csum_set_tx_tuning(ns_csum_ctx* ctx, uint32_t variant, uint32_t tile, uint32_t htile, uint32_t passes) {

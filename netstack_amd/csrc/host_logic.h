@@ -840,6 +840,128 @@ inline int tx_multi_plan(const ns_tcp_tx* t, uint32_t count, uint64_t arena_byte
   return NS_OK;
 }
 
+// ns_csum_tcp_tx_host's plan (sendTCPBatch calls over host memory).  The
+// geometry is affine in the segment index (segment i's payload starts at
+// pay_off + i*mss, its slot at hdr_off + i*slot; connect.go:679-691), so a run
+// [a, b) of one call's segments is itself a call — hdr_off + a*slot, pay_off +
+// a*mss, size min(size - a*mss, (b-a)*mss) — with the same segment lengths,
+// pseudo-header length words and sums.  Each call is cut into such pieces of
+// at most `budget` bytes (its slots plus the payload a full-mode call reads;
+// one segment may exceed it), consecutive pieces are grouped into chunks of
+// at most `budget` bytes and kMaxTxHostPieces pieces, and a chunk uploads
+// its pieces' byte ranges merged where they overlap or lie within kTxHostGap
+// bytes of each other.  Each merged range goes to the chunk's staging at its
+// arena offset modulo 256, so the kernel meets the alignments it would meet
+// in the arena.
+constexpr uint64_t kTxHostGap = 4096;
+constexpr uint32_t kMaxTxHostPieces = 1u << 16;
+struct TxPiece {
+  ns_tcp_tx t;       // the run as a call (arena offsets)
+  uint64_t nseg;     // its segments
+  uint64_t out0;     // its first segment's index over all calls' segments
+  uint32_t mode;     // TxPlan::mode
+};
+struct TxRange {
+  uint64_t lo, hi;  // arena bytes [lo, hi)
+  uint64_t at;      // their staging offset
+};
+struct TxChunk {
+  uint32_t p0 = 0, np = 0;  // pieces [p0, p0 + np)
+  uint32_t r0 = 0, nr = 0;  // ranges [r0, r0 + nr), sorted by lo
+  uint64_t staging = 0;     // staging bytes the ranges take
+  uint64_t out0 = 0;        // its pieces' segments are [out0, out0 + nout) over all calls
+  uint64_t nout = 0;
+};
+struct TxHostPlan {
+  std::vector<TxPiece> pieces;
+  std::vector<TxRange> ranges;
+  std::vector<TxChunk> chunks;
+  // calls with segments but nothing to compute (TX offload, no IPv4
+  // header): their sums are 0, as ns_csum_tcp_tx_multi writes them
+  std::vector<std::pair<uint64_t, uint64_t>> zeros;  // (first segment, segments)
+  uint64_t nseg = 0;                                 // all calls' segments
+
+  // The staging offset of arena byte x, which lies in one of chunk c's ranges.
+  uint64_t map(const TxChunk& c, uint64_t x) const {
+    const TxRange* b = ranges.data() + c.r0;
+    const TxRange* e = b + c.nr;
+    const TxRange* r = std::upper_bound(b, e, x, [](uint64_t v, const TxRange& q) { return v < q.lo; }) - 1;
+    return r->at + (x - r->lo);
+  }
+};
+
+inline int tx_host_plan(const ns_tcp_tx* t, uint32_t count, uint64_t arena_bytes, uint64_t budget,
+                        TxHostPlan* out) {
+  std::vector<TxPlan> plans;
+  const int vr = tx_multi_plan(t, count, arena_bytes, &plans);
+  if (vr != NS_OK) return vr;
+  if (budget == 0) return NS_EINVAL;
+  out->pieces.clear();
+  out->ranges.clear();
+  out->chunks.clear();
+  out->zeros.clear();
+  uint64_t seg = 0;
+  std::vector<uint64_t> bytes;  // per piece
+  for (uint32_t k = 0; k < count; ++k) {
+    const ns_tcp_tx& c = t[k];
+    const TxPlan& p = plans[k];
+    if (p.n && !(p.mode & 7u)) out->zeros.emplace_back(seg, p.n);
+    if (p.n && (p.mode & 7u)) {
+      const bool full = (p.mode & 2u) != 0;
+      const uint64_t per = (uint64_t)c.slot + (full ? c.mss : 0u);
+      const uint64_t run = std::max<uint64_t>(1, budget / per);
+      for (uint64_t a = 0; a < p.n; a += run) {
+        TxPiece q;
+        q.nseg = std::min(run, p.n - a);
+        q.t = c;
+        q.t.hdr_off = c.hdr_off + a * c.slot;
+        q.t.pay_off = c.pay_off + a * c.mss;
+        q.t.size = std::min<uint64_t>(c.size - a * c.mss, q.nseg * c.mss);
+        q.out0 = seg + a;
+        q.mode = p.mode;
+        out->pieces.push_back(q);
+        bytes.push_back(q.nseg * c.slot + (full ? q.t.size : 0u));
+      }
+    }
+    seg += p.n;
+  }
+  out->nseg = seg;
+  std::vector<TxRange> iv;
+  const uint32_t np = (uint32_t)out->pieces.size();
+  for (uint32_t i = 0; i < np;) {
+    TxChunk ch;
+    ch.p0 = i;
+    uint64_t sum = 0;
+    while (i < np && ch.np < kMaxTxHostPieces && (ch.np == 0 || sum + bytes[i] <= budget)) {
+      sum += bytes[i++];
+      ++ch.np;
+    }
+    iv.clear();
+    for (uint32_t j = ch.p0; j < i; ++j) {
+      const TxPiece& q = out->pieces[j];
+      iv.push_back({q.t.hdr_off, q.t.hdr_off + q.nseg * q.t.slot, 0});
+      if ((q.mode & 2u) && q.t.size) iv.push_back({q.t.pay_off, q.t.pay_off + q.t.size, 0});
+    }
+    std::sort(iv.begin(), iv.end(), [](const TxRange& a, const TxRange& b) { return a.lo < b.lo; });
+    ch.r0 = (uint32_t)out->ranges.size();
+    uint64_t at = 0;
+    for (size_t j = 0; j < iv.size();) {
+      TxRange m = iv[j++];
+      while (j < iv.size() && iv[j].lo <= m.hi + kTxHostGap) m.hi = std::max(m.hi, iv[j++].hi);
+      m.at = ((at + 255) & ~255ull) + (m.lo & 255u);
+      at = m.at + (m.hi - m.lo);
+      out->ranges.push_back(m);
+    }
+    ch.nr = (uint32_t)(out->ranges.size() - ch.r0);
+    ch.staging = at;
+    const TxPiece& last = out->pieces[i - 1];
+    ch.out0 = out->pieces[ch.p0].out0;
+    ch.nout = last.out0 + last.nseg - ch.out0;
+    out->chunks.push_back(ch);
+  }
+  return NS_OK;
+}
+
 // ns_csum_rx_ring's geometry, validated (include/netstack_csum.h).  `base`
 // is the device address of the arena (its alignment matters: 16-B loads).
 inline int rx_plan(const ns_rx_ring& r, uint64_t base, uint64_t arena_bytes) {

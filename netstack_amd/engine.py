@@ -167,6 +167,24 @@ class Engine:
                                          getattr(stream, "cuda_stream", stream)), "ns_csum_tcp_tx_multi")
         return out
 
+    def tcp_tx_host(self, arena: np.ndarray, geos, mode: str = "full") -> np.ndarray:
+        """sendTCPBatch calls over host memory (ns_csum_tcp_tx_host): `arena`
+        a writable, contiguous uint8 numpy array (pageable, or a stage from
+        stage_acquire) holding the calls' header slots and payloads; `geos`
+        as for tcp_tx_multi.  Synchronous: the fields are written into
+        `arena` in place; returns the 2 * sum(n_k) un-complemented sums."""
+        if not (isinstance(arena, np.ndarray) and arena.dtype == np.uint8 and arena.flags.c_contiguous
+                and arena.flags.writeable):
+            raise ValueError("arena must be a writable, contiguous uint8 numpy array")
+        arr = geos if isinstance(geos, ctypes.Array) else tx_table(geos, mode)
+        count = len(arr) if len(geos) else 0
+        t = np.ctypeslib.as_array(arr)[:count]
+        total = int((-(-t["size"].astype(np.int64) // np.maximum(t["mss"], 1))).sum()) if count else 0
+        out = np.zeros(max(2 * total, 1), dtype=np.uint16)
+        check(lib().ns_csum_tcp_tx_host(self._h, _ptr(arena), arena.size, arr, count, _ptr(out)),
+              "ns_csum_tcp_tx_host")
+        return out[:2 * total]
+
     def set_tx_tuning(self, variant: int = 0, tile: int = 0, htile: int = 0, passes: int = 0) -> None:
         """ns_csum_tcp_tx's A/B and test knobs on this context
         (ns_csum_set_tx_tuning; all zero = production)."""

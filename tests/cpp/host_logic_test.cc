@@ -14,6 +14,10 @@
 //   cut_chunk     chunks tile the table, never end inside a chained run,
 //                 spans within budget, NS_ERANGE on a bad descriptor;
 //   shard_plan    contiguous, ordered, whole runs, byte-balanced;
+//   tx_plan, tx_multi_plan, rx_plan  geometry checks: whatever they accept
+//                 stays inside the arena and apart where the kernels need it;
+//   tx_host_plan  pieces tile each call's segments as valid calls, chunks
+//                 within budget, the staged ranges hold every byte read;
 //   FlatCombiner  many threads x many requests: every request done once
 //                 with its own result (the point of the -fsanitize=thread
 //                 build).
@@ -663,6 +667,133 @@ static void TestTxMultiPlan(Rng& rng, int rounds) {
   CHECK(nsh::tx_multi_plan(two, 2, 1 << 20, &p) == NS_OK, "no payload read");
 }
 
+// nsh::tx_host_plan (ns_csum_tcp_tx_host): random call sets and staging
+// budgets.  The pieces tile each call's segments in order, each a valid call
+// with the segment lengths of the run it stands for; chunks tile the pieces
+// within the budget; and a staging buffer filled from the chunk's ranges
+// holds, at map(x), arena byte x for every slot and payload byte a piece
+// reads, at the arena's alignment modulo 256.
+static void TestTxHostPlan(Rng& rng, int rounds) {
+  int accepted = 0, multi_chunk = 0, split = 0;
+  for (int round = 0; round < rounds * 10; ++round) {
+    const uint32_t count = (uint32_t)(rng() % 7);
+    const uint64_t arena = 1u << 18;
+    std::vector<uint8_t> a(arena);
+    for (auto& b : a) b = (uint8_t)rng();
+    std::vector<ns_tcp_tx> t(count);
+    uint64_t pos = rng() % 300;
+    for (auto& x : t) {  // side by side with random gaps, as a caller packs them
+      x = ns_tcp_tx{};
+      x.mss = rng() % 4 == 0 ? 1 + (uint32_t)(rng() % 16) : 100 + (uint32_t)(rng() % 1500);
+      x.slot = 40 + (uint32_t)(rng() % 40);
+      x.ip_at = 0, x.ip_len = (uint16_t)(rng() % 4 == 0 ? 0 : 20), x.tcp_at = 20, x.tcp_len = 20;
+      x.size = rng() % 8 == 0 ? 0 : rng() % 12000;
+      x.flags = (uint32_t)(rng() % 3);
+      const uint64_t n = (x.size + x.mss - 1) / x.mss;
+      const bool pay_first = rng() % 2;
+      if (pay_first) {
+        x.pay_off = pos, x.hdr_off = pos + x.size + rng() % 6000;
+        pos = x.hdr_off + n * x.slot + rng() % 9000;
+      } else {
+        x.hdr_off = pos, x.pay_off = pos + n * x.slot + rng() % 6000;
+        pos = x.pay_off + x.size + rng() % 9000;
+      }
+    }
+    if (pos > arena) continue;
+    const uint64_t budget = rng() % 3 == 0 ? 1 + rng() % 3000 : 1 + rng() % 60000;
+    nsh::TxHostPlan plan;
+    const int rc = nsh::tx_host_plan(t.data(), count, arena, budget, &plan);
+    CHECK(rc == NS_OK, "rc %d for a packed call set", rc);
+    if (rc != NS_OK) continue;
+    ++accepted;
+    multi_chunk += plan.chunks.size() > 1;
+    // pieces tile every call's segments
+    std::vector<uint64_t> bytes;
+    size_t pi = 0;
+    uint64_t seg = 0, zeros = 0;
+    for (uint32_t k = 0; k < count; ++k) {
+      nsh::TxPlan p;
+      CHECK(nsh::tx_plan(t[k], arena, &p) == NS_OK, "call %u", k);
+      if (p.n && !(p.mode & 7u)) {
+        CHECK(zeros < plan.zeros.size() && plan.zeros[zeros].first == seg && plan.zeros[zeros].second == p.n,
+              "zero sums of call %u", k);
+        ++zeros;
+      }
+      if (p.n && (p.mode & 7u)) {
+        uint64_t next = 0;
+        int pieces = 0;
+        while (next < p.n) {
+          CHECK(pi < plan.pieces.size(), "pieces end inside call %u", k);
+          if (pi >= plan.pieces.size()) return;
+          const nsh::TxPiece& q = plan.pieces[pi++];
+          ++pieces;
+          CHECK(q.out0 == seg + next && q.mode == p.mode, "piece of call %u at segment %llu", k,
+                (unsigned long long)next);
+          const uint64_t want = next + q.nseg == p.n ? t[k].size - next * t[k].mss : q.nseg * t[k].mss;
+          CHECK(q.nseg >= 1 && next + q.nseg <= p.n && q.t.size == want, "piece size");
+          CHECK(q.t.hdr_off == t[k].hdr_off + next * t[k].slot && q.t.pay_off == t[k].pay_off + next * t[k].mss,
+                "piece offsets");
+          nsh::TxPlan qp;
+          CHECK(nsh::tx_plan(q.t, arena, &qp) == NS_OK && qp.n == q.nseg && qp.mode == q.mode, "piece as a call");
+          const uint64_t b = q.nseg * q.t.slot + ((q.mode & 2u) ? q.t.size : 0u);
+          CHECK(b <= budget || q.nseg == 1, "piece of %llu bytes over budget %llu", (unsigned long long)b,
+                (unsigned long long)budget);
+          bytes.push_back(b);
+          next += q.nseg;
+        }
+        split += pieces > 1;
+      }
+      seg += p.n;
+    }
+    CHECK(pi == plan.pieces.size() && zeros == plan.zeros.size() && plan.nseg == seg, "no stray pieces");
+    // chunks tile the pieces; the staging image matches the arena
+    uint32_t next = 0;
+    for (const nsh::TxChunk& c : plan.chunks) {
+      CHECK(c.p0 == next && c.np >= 1 && c.np <= nsh::kMaxTxHostPieces, "chunk pieces");
+      next = c.p0 + c.np;
+      uint64_t sum = 0;
+      for (uint32_t j = c.p0; j < next; ++j) sum += bytes[j];
+      CHECK(sum <= budget || c.np == 1, "chunk over budget");
+      std::vector<uint8_t> st(c.staging + 16, 0xEE);
+      uint64_t end = 0;
+      for (uint32_t j = c.r0; j < c.r0 + c.nr; ++j) {
+        const nsh::TxRange& r = plan.ranges[j];
+        CHECK(r.lo < r.hi && r.hi <= arena && (r.at & 255u) == (r.lo & 255u) && r.at >= end, "range");
+        if (j > c.r0) CHECK(r.lo > plan.ranges[j - 1].hi + nsh::kTxHostGap, "ranges merged");
+        std::memcpy(st.data() + r.at, a.data() + r.lo, r.hi - r.lo);
+        end = r.at + (r.hi - r.lo);
+      }
+      CHECK(end == c.staging, "staging size");
+      const nsh::TxPiece& last = plan.pieces[next - 1];
+      CHECK(c.out0 == plan.pieces[c.p0].out0 && c.nout == last.out0 + last.nseg - c.out0, "chunk sums");
+      for (uint32_t j = c.p0; j < next; ++j) {
+        const nsh::TxPiece& q = plan.pieces[j];
+        auto same = [&](uint64_t lo, uint64_t len) {
+          const uint64_t m = plan.map(c, lo);
+          return m + len <= c.staging && std::memcmp(st.data() + m, a.data() + lo, len) == 0;
+        };
+        CHECK(same(q.t.hdr_off, q.nseg * q.t.slot), "slots staged");
+        if (q.mode & 2u) CHECK(same(q.t.pay_off, q.t.size), "payload staged");
+      }
+    }
+    CHECK(next == plan.pieces.size(), "chunks tile the pieces");
+  }
+  CHECK(accepted > 0 && multi_chunk > 0 && split > 0, "coverage: %d accepted, %d multi-chunk, %d split", accepted,
+        multi_chunk, split);
+  // refused as tx_multi_plan refuses, and a zero budget
+  ns_tcp_tx two[2]{};
+  for (auto& x : two) x.mss = 1460, x.slot = 54, x.ip_at = 14, x.ip_len = 20, x.tcp_at = 34, x.tcp_len = 20;
+  two[0].size = two[1].size = 14600;
+  two[0].hdr_off = 0, two[0].pay_off = 4096, two[1].hdr_off = 539, two[1].pay_off = 20000;
+  nsh::TxHostPlan plan;
+  CHECK(nsh::tx_host_plan(two, 2, 1 << 20, 1 << 20, &plan) == NS_EINVAL, "overlapping slots");
+  two[1].hdr_off = 540;
+  CHECK(nsh::tx_host_plan(two, 2, 1 << 20, 0, &plan) == NS_EINVAL, "zero budget");
+  CHECK(nsh::tx_host_plan(two, 2, 1 << 20, 1 << 20, &plan) == NS_OK && plan.chunks.size() == 1 &&
+            plan.pieces.size() == 2 && plan.nseg == 20,
+        "two calls, one chunk");
+}
+
 int main(int argc, char** argv) {
   const bool quick = argc > 1 && std::strcmp(argv[1], "--quick") == 0;
   Rng rng(20261016);
@@ -674,6 +805,7 @@ int main(int argc, char** argv) {
   TestShardPlan(rng, r);
   TestTxPlan(rng, r);
   TestTxMultiPlan(rng, r);
+  TestTxHostPlan(rng, r);
   TestRxPlan(rng, r);
   TestCombiner(16, quick ? 200 : 2000);
   TestScratchRegistry(8, 1000, quick ? 2000 : 20000);

@@ -43,7 +43,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_strerror():
     L = _lib.lib()
-    assert L.ns_csum_abi_version() == _lib.ABI_VERSION == 8
+    assert L.ns_csum_abi_version() == _lib.ABI_VERSION == 9
     for code in (0, -1, -2, -3, -4, -5):
         assert L.ns_csum_strerror(code)
 

@@ -1,0 +1,167 @@
+"""GPU: ns_csum_tcp_tx_host — sendTCPBatch calls over HOST memory
+(transport/tcp/connect.go:668-702, buildTCPHdr :634-666, addIPHeader
+network/ipv4/ipv4.go:217-238), many connections' calls in one synchronous
+call — against the oracle's C restatement (oracle.c_send_tcp_batch),
+bit-exact: the whole host arena afterwards (both fields of every segment
+written, every other byte unchanged) and the un-complemented sums.
+
+Covered: the geometries of test_gpu_tx_struct.py side by side in one arena
+(odd slots and MSS, options, IPv6, MSS 7, partial / offload modes, no
+segments), pageable and pinned (stage_acquire) arenas, a staging budget so
+small that calls are split by segments and chunks cycle through all four
+pipeline slots, a 95 MB call in several chunks, and the error paths."""
+
+import numpy as np
+import pytest
+
+from test_gpu_tx_struct import CASES
+
+pytestmark = pytest.mark.gpu
+
+SPECS = [("netstack_default", "full"), ("odd_slots_odd_mss", "full"), ("ipv6_route", "full"),
+         ("options_32b_tcp", "partial"), ("mss_7", "full"), ("size_below_mss", "none"),
+         ("ip_header_with_options", "full"), ("last_is_one_byte", "full"), ("payload_before_slots", "full"),
+         ("jumbo_9000", "full"), ("gso_64k", "full"), ("mss_1", "full")]
+
+
+def _layout(seed, reps=2, gap=40):
+    """Calls of SPECS laid out side by side (random gaps), an empty call, and
+    the arena with the route's addresses in every IPv4 header."""
+    rng = np.random.default_rng(seed)
+    geos, pos = [], 3
+    for name, mode in SPECS * reps:
+        geo, total = CASES[name]
+        g = dict(geo, mode=mode)
+        g["hdr_off"] += pos
+        g["pay_off"] += pos
+        geos.append(g)
+        pos += total + int(rng.integers(0, gap))
+    geos.insert(len(geos) // 2, dict(CASES["netstack_default"][0], size=0, hdr_off=0, pay_off=0))
+    a = rng.integers(0, 256, pos + 64, dtype=np.uint8)
+    for g in geos:
+        n = -(-g["size"] // g["mss"])
+        if g["ip_len"]:
+            for i in range(n):
+                at = g["hdr_off"] + i * g["slot"] + g["ip_at"]
+                a[at + 12:at + 16] = np.frombuffer(g["src"], np.uint8)
+                a[at + 16:at + 20] = np.frombuffer(g["dst"], np.uint8)
+    return geos, a
+
+
+def _want(oracle_mod, a, geos):
+    want = a.copy()
+    sums = []
+    for g in geos:
+        _, ws = oracle_mod.c_send_tcp_batch(want, g["hdr_off"], g["pay_off"], g["size"], g["mss"], g["slot"],
+                                            g["ip_at"], g["ip_len"], g["tcp_at"], g["tcp_len"], g["src"], g["dst"],
+                                            g["protocol"], g.get("mode", "full"), copy=False)
+        sums.append(np.asarray(ws, dtype=np.uint16))
+    return want, np.concatenate(sums) if sums else np.zeros(0, np.uint16)
+
+
+def _check(got, sums, want, want_sums, what):
+    bad = np.flatnonzero(got != want)
+    assert bad.size == 0, f"{what}: {bad.size} arena bytes differ, first at {bad[:8]}"
+    diff = np.flatnonzero(sums != want_sums)
+    assert diff.size == 0, f"{what}: {diff.size} sums differ, first at {diff[:8]}"
+
+
+def test_calls_side_by_side_bit_exact(engine, oracle_mod):
+    geos, a = _layout(7)
+    want, ws = _want(oracle_mod, a, geos)
+    got = a.copy()
+    sums = engine.tcp_tx_host(got, geos)
+    _check(got, sums, want, ws, "pageable arena")
+    # again over the filled arena: the fields are summed as zero, so a refill
+    # is idempotent
+    sums = engine.tcp_tx_host(got, geos)
+    _check(got, sums, want, ws, "refill")
+
+
+def test_pinned_stage_arena(engine, oracle_mod):
+    """The Go shim's shape: the calls packed into an acquired stage (pinned,
+    device-mapped host memory), copied by DMA without a bounce."""
+    geos, a = _layout(11, reps=1)
+    want, ws = _want(oracle_mod, a, geos)
+    st = engine.stage_acquire(a.size)
+    try:
+        st[:] = a
+        sums = engine.tcp_tx_host(st, geos)
+        _check(st.copy(), sums, want, ws, "stage arena")
+    finally:
+        engine.stage_release(st)
+
+
+@pytest.mark.parametrize("staging", [4096, 70_000, 1 << 20])
+def test_small_staging_splits_calls(oracle_mod, staging):
+    """A staging budget below one call's bytes: calls are cut into runs of
+    segments (each its own sendTCPBatch geometry) and the chunks cycle
+    through the four pipeline slots; the result is the same bytes."""
+    from netstack_amd import Engine
+
+    geos, a = _layout(13 + staging)
+    want, ws = _want(oracle_mod, a, geos)
+    with Engine(0, staging_bytes=staging) as eng:
+        got = a.copy()
+        sums = eng.tcp_tx_host(got, geos)
+        _check(got, sums, want, ws, f"staging {staging}")
+        assert eng.sync() == 0
+
+
+def test_one_large_call_in_chunks(oracle_mod):
+    """65,536 x 1460-B segments (95 MB of payload) through 16 MiB of staging:
+    one call split over six chunks, against the oracle."""
+    from netstack_amd import Engine
+
+    from test_gpu_tx_struct import _arena, _geo
+
+    geo, total = _geo(1460 * 65536 - 333, 1460, hdr_off=5)
+    a = _arena(total, geo, seed=5)
+    want, ws = _want(oracle_mod, a, [geo])
+    with Engine(0, staging_bytes=16 << 20) as eng:
+        sums = eng.tcp_tx_host(a, [geo])
+    _check(a, sums, want, ws, "95 MB call")
+
+
+def test_same_as_device_multi(engine, oracle_mod):
+    """The host entry writes exactly what ns_csum_tcp_tx_multi writes over a
+    device copy of the same arena."""
+    import torch
+
+    geos, a = _layout(17, reps=1)
+    buf = torch.from_numpy(a).cuda()
+    ntot = sum(-(-g["size"] // g["mss"]) for g in geos)
+    out = torch.full((2 * ntot,), -1, dtype=torch.int16, device="cuda")
+    engine.tcp_tx_multi(buf, geos, out=out)
+    torch.cuda.synchronize()
+    got = a.copy()
+    sums = engine.tcp_tx_host(got, geos)
+    assert np.array_equal(got, buf.cpu().numpy())
+    assert np.array_equal(sums, out.cpu().numpy().view(np.uint16))
+
+
+def test_errors(engine):
+    from netstack_amd import _lib
+    from netstack_amd.engine import tx_table
+
+    geos, a = _layout(19, reps=1)
+    before = a.copy()
+    L, h = _lib.lib(), engine._h
+    clash = [geos[0], dict(geos[1], hdr_off=geos[0]["hdr_off"] + 10)]
+    with pytest.raises(ValueError):  # NS_EINVAL: slots of two calls overlap
+        engine.tcp_tx_host(a, clash)
+    with pytest.raises(_lib.ChecksumError) as e:  # NS_ERANGE: past the arena
+        engine.tcp_tx_host(a[:geos[0]["pay_off"] + 10], geos[:1])
+    assert e.value.status == _lib.NS_ERANGE
+    with pytest.raises(ValueError):
+        engine.tcp_tx_host(np.frombuffer(bytes(a), dtype=np.uint8), geos)  # read-only
+    assert np.array_equal(a, before), "a refused call wrote nothing"
+    arr = tx_table(geos)
+    assert L.ns_csum_tcp_tx_host(None, a.ctypes.data, a.size, arr, len(geos), None) == _lib.NS_EINVAL
+    assert L.ns_csum_tcp_tx_host(h, None, a.size, arr, len(geos), None) == _lib.NS_EINVAL
+    assert L.ns_csum_tcp_tx_host(h, a.ctypes.data, a.size, None, 3, None) == _lib.NS_EINVAL
+    assert L.ns_csum_tcp_tx_host(h, a.ctypes.data, a.size, arr, 0, None) == _lib.NS_OK
+    # no sums wanted: the fields are still written
+    assert L.ns_csum_tcp_tx_host(h, a.ctypes.data, a.size, arr, len(geos), None) == _lib.NS_OK
+    assert not np.array_equal(a, before)
+    assert engine.tcp_tx_host(a, []).size == 0
