@@ -413,7 +413,7 @@ const (
 // Offload thresholds.  A synchronous engine call costs one GPU round trip
 // (~11 us) plus its bytes; below these sizes one core running the
 // reference's own loop (checksum.go:26-46) on the same bytes finishes first
-// (tools/crossover.cc on MI355X, profiles/r04/crossover.json; INTEGRATION.md
+// (tools/crossover.cc on MI355X, profiles/r05/crossover.json; INTEGRATION.md
 // §2 "When offload pays").  The build-tagged callers offload only calls at
 // or above them; smaller calls take the reference's unmodified Go code.
 // Variables, not constants, so the callers' tests can open the gates and
@@ -428,6 +428,11 @@ var (
 	// (VerifyPacketBuffers): 64 x 1500 B took 1.31x one core's time,
 	// 128 x 1500 B 0.88x, 256 x 1500 B 0.70x.
 	VerifyOffloadMinBytes = 128 * 1500
+	// TxBatchOffloadMinBytes is the payload of all the batches one
+	// FillTCPBatches call fills (profiles/r05/crossover.json "tx_host",
+	// 64 KiB sendTCPBatch calls, stage copies included): 4 calls took 1.09x
+	// one core's time, 8 calls (512 KiB) 0.67x, 64 calls 0.31x.
+	TxBatchOffloadMinBytes = 512 << 10
 )
 
 // VerifyPacketBuffers runs the receive path's checksum checks over a batch
@@ -595,6 +600,166 @@ func packetBuffers(pkts []tcpip.PacketBuffer, op C.uint32_t, verdict []uint8) er
 		}
 	}
 	return nil
+}
+
+// TCPBatch is one sendTCPBatch call's checksum work (connect.go:668-702) in
+// the form ns_csum_tcp_tx_host takes it: Slots is the call's
+// NewPacketDescriptors buffer (n slots of SlotSize bytes, route.go:181-188),
+// each holding the segment's encoded headers — the IPv4 header at IPAt (IPLen
+// bytes, IHL*4; 0: none, as before WritePackets or on an IPv6 route) and the
+// TCP header at TCPAt (TCPLen = DataOffset) — and Payload is the data view,
+// cut into MSS-byte segments (:679-691).  Src and Dst are the route's
+// addresses (4 or 16 bytes), Protocol its transport protocol (6), Mode what
+// buildTCPHdr does with the TCP field (:652-663).
+type TCPBatch struct {
+	Slots                      []byte
+	SlotSize                   int
+	Payload                    buffer.VectorisedView
+	MSS                        int
+	IPAt, IPLen, TCPAt, TCPLen int
+	Src, Dst                   tcpip.Address
+	Protocol                   tcpip.TransportProtocolNumber
+	Mode                       int
+}
+
+// TCPBatch.Mode: the full checksum (buildTCPHdr's default), the
+// pseudo-header sum only (gso.NeedsCsum, CHECKSUM_PARTIAL), or nothing
+// (CapabilityTXChecksumOffload); the IPv4 field is filled in every mode.
+const (
+	TxCsumFull    = 0
+	TxCsumPartial = 1
+	TxCsumOffload = 2
+)
+
+// FillTCPBatches writes the checksum fields of every segment of every batch —
+// buildTCPHdr's TCP checksum (connect.go:652-663) and addIPHeader's IPv4
+// header checksum (ipv4.go:236) — in one engine call, ns_csum_tcp_tx_host:
+// the batches' slots and payloads are packed into one engine stage, the fields
+// are computed on the device and written into the stage, and each batch's
+// slots are copied back.  Many connections' sendTCPBatch calls can go in
+// one call; that is the shape the engine pays off for at netstack's 64 KiB
+// GSO writes (INTEGRATION.md §2).  Fields are summed as zero, as freshly
+// encoded headers hold them.  Below TxBatchOffloadMinBytes of payload in
+// all, and whenever the engine cannot run the call (counted in
+// EngineFallbacks), the same fields are computed by the reference's Go code
+// (fillTCPBatchGo).
+func FillTCPBatches(batches []TCPBatch) {
+	total := 0
+	for i := range batches {
+		total += batches[i].Payload.Size()
+	}
+	// below the measured crossover one core is faster: the reference's code
+	if total < TxBatchOffloadMinBytes {
+		for i := range batches {
+			fillTCPBatchGo(&batches[i])
+		}
+		return
+	}
+	if err := FillTCPBatchesErr(batches); err != nil {
+		for i := range batches {
+			fillTCPBatchGo(&batches[i])
+		}
+	}
+}
+
+// FillTCPBatchesErr is FillTCPBatches without the fallback: on an engine
+// failure nothing is written and the error is returned (and counted).
+func FillTCPBatchesErr(batches []TCPBatch) error {
+	if len(batches) == 0 {
+		return nil
+	}
+	ctx, rc := csumEngine()
+	if rc != C.NS_OK {
+		return engineFailed("ns_csum_init", rc)
+	}
+	need := 0
+	for i := range batches {
+		b := &batches[i]
+		need += tcpBatchSegments(b)*b.SlotSize + b.Payload.Size()
+	}
+	st, rc := acquireStage(ctx, need)
+	if rc != C.NS_OK {
+		return engineFailed("ns_csum_stage_acquire", rc)
+	}
+	defer st.release()
+	txs := make([]C.ns_tcp_tx, len(batches))
+	slotAt := make([]int, len(batches))
+	for i := range batches {
+		b := &batches[i]
+		n := tcpBatchSegments(b)
+		_, slotAt[i] = st.put(b.Slots[:n*b.SlotSize])
+		payAt := st.used
+		for _, v := range b.Payload.Views() {
+			st.put(v)
+		}
+		var flags C.uint32_t
+		switch b.Mode {
+		case TxCsumPartial:
+			flags = C.NS_TX_TCP_PARTIAL
+		case TxCsumOffload:
+			flags = C.NS_TX_TCP_NONE
+		}
+		// Checksum(dst, Checksum(src, 0)): PseudoHeaderChecksum's address part
+		// (checksum.go:113-114); the kernel adds the protocol and length words
+		txs[i] = C.ns_tcp_tx{hdr_off: C.uint64_t(slotAt[i]), pay_off: C.uint64_t(payAt),
+			size: C.uint64_t(b.Payload.Size()), mss: C.uint32_t(b.MSS), slot: C.uint32_t(b.SlotSize),
+			ip_at: C.uint16_t(b.IPAt), ip_len: C.uint16_t(b.IPLen), tcp_at: C.uint16_t(b.TCPAt),
+			tcp_len: C.uint16_t(b.TCPLen), addr_sum: C.uint16_t(Checksum([]byte(b.Dst), Checksum([]byte(b.Src), 0))),
+			protocol: C.uint16_t(b.Protocol), flags: flags}
+	}
+	if rc := C.ns_csum_tcp_tx_host(ctx, st.base, C.uint64_t(st.used), &txs[0], C.uint32_t(len(txs)), nil); rc != C.NS_OK {
+		return engineFailed("ns_csum_tcp_tx_host", rc)
+	}
+	for i := range batches {
+		b := &batches[i]
+		n := tcpBatchSegments(b) * b.SlotSize
+		copy(b.Slots[:n], st.mem[slotAt[i]:slotAt[i]+n])
+	}
+	return nil
+}
+
+// tcpBatchSegments is sendTCPBatch's n = ceil(data.Size() / mss)
+// (connect.go:675); 0 for an MSS the engine refuses anyway.
+func tcpBatchSegments(b *TCPBatch) int {
+	if b.MSS <= 0 {
+		return 0
+	}
+	return (b.Payload.Size() + b.MSS - 1) / b.MSS
+}
+
+// fillTCPBatchGo is the reference's own computation of the same fields, in
+// its order: per segment, buildTCPHdr's PseudoHeaderChecksum, then
+// ChecksumVVWithOffset over the payload and TCP.CalculateChecksum
+// (connect.go:652-663), then addIPHeader's IPv4 CalculateChecksum
+// (ipv4.go:236).  Both fields are cleared first, as Encode leaves them.
+func fillTCPBatchGo(b *TCPBatch) {
+	n := tcpBatchSegments(b)
+	size, off := b.Payload.Size(), 0
+	for i := 0; i < n; i++ {
+		slot := b.Slots[i*b.SlotSize:][:b.SlotSize]
+		packetSize := b.MSS
+		if packetSize > size {
+			packetSize = size
+		}
+		size -= packetSize
+		if b.Mode != TxCsumOffload {
+			tcp := TCP(slot[b.TCPAt:][:b.TCPLen])
+			tcp.SetChecksum(0)
+			xsum := PseudoHeaderChecksum(b.Protocol, b.Src, b.Dst, uint16(b.TCPLen+packetSize))
+			if b.Mode == TxCsumPartial {
+				tcp.SetChecksum(xsum)
+			} else {
+				xsum = ChecksumVVWithOffset(b.Payload, xsum, off, packetSize)
+				tcp.SetChecksum(^tcp.CalculateChecksum(xsum))
+			}
+		}
+		if b.IPLen > 0 {
+			ip := IPv4(slot[b.IPAt:][:b.IPLen])
+			ip.SetChecksum(0)
+			ip.SetChecksum(^ip.CalculateChecksum())
+		}
+		off += packetSize
+	}
 }
 
 // RxRing is a receive ring resident in device memory (ns_rx_ring): n slots

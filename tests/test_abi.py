@@ -198,7 +198,8 @@ def test_go_shim_builds_with_the_reference_go_version_and_adds_only_new_names():
     declared |= set(re.findall(r"^\s*(\w+)\s*=", code[code.index("const ("):] if "const (" in code else "",
                                flags=re.M))
     assert declared and not (declared & CHECKSUM_GO_NAMES), declared & CHECKSUM_GO_NAMES
-    for name in ("ChecksumVVBatch", "ChecksumChains", "ChecksumBatch", "VerifyPacketBuffers", "FillPacketBuffers"):
+    for name in ("ChecksumVVBatch", "ChecksumChains", "ChecksumBatch", "VerifyPacketBuffers", "FillPacketBuffers",
+                 "FillTCPBatches", "VerifyRingDevice"):
         assert name in declared, name
     called = set(re.findall(r"C\.(ns_csum_\w+)\(", code))
     assert called and called <= declared_symbols(), called - declared_symbols()
@@ -376,7 +377,7 @@ def test_go_engine_errors_fall_back_to_the_reference_go():
     assert shim.count("engineFailed(") >= len(set(checked)) and "func EngineFallbacks() uint64" in shim
     for fn, ref in (("ChecksumVVBatch", "ChecksumVVWithOffset(vv"), ("ChecksumChains", "checksumChainsGo(chains"),
                     ("ChecksumBatch", "calculateChecksum(b"), ("VerifyPacketBuffers", "PacketChecksumUnchecked"),
-                    ("FillPacketBuffers", "fillPacketGo(")):
+                    ("FillPacketBuffers", "fillPacketGo("), ("FillTCPBatches", "fillTCPBatchGo(&batches[i])")):
         body = re.search(rf"^func {fn}\(.*?^}}", shim, flags=re.M | re.S).group(0)
         assert ref in body, fn
     tx = _go_code(open(os.path.join(ROOT, "go/transport/tcp/csum_batch_hip.go")).read())
@@ -392,7 +393,7 @@ def test_go_engine_errors_fall_back_to_the_reference_go():
 def test_go_offload_gates_sit_at_the_measured_crossover():
     """The build-tagged callers offload only calls at or above the sizes
     where one engine call beat one core (tools/crossover.cc on MI355X,
-    profiles/r04/crossover.json); below them the reference's own Go code runs
+    profiles/r05/crossover.json); below them the reference's own Go code runs
     (INTEGRATION.md §2).  Each gate is a measured point no smaller than the
     measured crossover and no more than 2x it, and each caller tests it
     before calling the engine."""
@@ -400,14 +401,14 @@ def test_go_offload_gates_sit_at_the_measured_crossover():
 
     code = _go_code(open(GO_SHIM).read())
     env = {}
-    for name in ("ChainsOffloadMinBytes", "VerifyOffloadMinBytes"):
+    for name in ("ChainsOffloadMinBytes", "VerifyOffloadMinBytes", "TxBatchOffloadMinBytes"):
         m = re.search(rf"^\s*{name}\s*=\s*([0-9<>* ]+)$", code, flags=re.M)
         assert m, name
         env[name] = int(eval(m.group(1), {}))  # a constant expression of integers
-    with open(os.path.join(ROOT, "profiles", "r04", "crossover.json")) as f:
+    with open(os.path.join(ROOT, "profiles", "r05", "crossover.json")) as f:
         xo = json.load(f)
     for gate, shape in (("ChainsOffloadMinBytes", "chains"), ("ChainsOffloadMinBytes", "vv_batch"),
-                        ("VerifyOffloadMinBytes", "verify")):
+                        ("VerifyOffloadMinBytes", "verify"), ("TxBatchOffloadMinBytes", "tx_host")):
         x = xo[shape]["crossover"]
         assert x is not None, shape
         assert x["bytes"] <= env[gate] <= 2 * x["bytes"], (gate, shape, x, env[gate])
@@ -417,6 +418,8 @@ def test_go_offload_gates_sit_at_the_measured_crossover():
     rx = _go_code(open(os.path.join(ROOT, "go/link/fdbased/csum_rx_hip.go")).read())
     assert re.search(r"if total < header\.VerifyOffloadMinBytes \{\s*return\s*\}", rx)
     assert rx.index("VerifyOffloadMinBytes") < rx.index("header.VerifyPacketBuffersErr(")
+    body = re.search(r"^func FillTCPBatches\(.*?^}", code, flags=re.M | re.S).group(0)
+    assert body.index("TxBatchOffloadMinBytes") < body.index("FillTCPBatchesErr(")
     patch = open(GO_PATCH).read()
     assert "+\tdeferCsum := deferTCPBatchChecksums(data.Size()) &&" in patch
 
@@ -455,3 +458,28 @@ def test_go_gate_tests_open_the_gates_and_compare_with_the_reference():
         for name in set(re.findall(r"\bheader\.(\w+)", code)):
             assert name in _top_level(shim) or name in REF_HEADER_NAMES or not os.path.isdir("/root/reference"), \
                 (rel, name)
+
+
+def test_go_tx_host_test_compares_with_the_reference_go():
+    """FillTCPBatches (ns_csum_tcp_tx_host) has a Go test in package header
+    that fills many batches through the engine and through fillTCPBatchGo
+    (the reference's buildTCPHdr / addIPHeader arithmetic) and compares the
+    slot bytes, with no fallback counted.  fillTCPBatchGo itself calls only
+    the reference's package-header functions.  Checked statically."""
+    raw = open(os.path.join(ROOT, "go/header/checksum_batch_hip_test.go")).read()
+    code = _go_code(raw)
+    for pat in POST_GO114:
+        assert not re.search(pat, code), pat
+    assert "\n\n// +build hipcsum\n\npackage header\n" in raw
+    for call in ("FillTCPBatchesErr(got)", "FillTCPBatches(got)", "fillTCPBatchGo(&want[i])", "EngineFallbacks()",
+                 "bytes.Equal(", "defer func(v int) { TxBatchOffloadMinBytes = v }(TxBatchOffloadMinBytes)"):
+        assert call in code, call
+    for mode in ("TxCsumFull", "TxCsumPartial", "TxCsumOffload"):
+        assert mode in code, mode
+    shim = _go_code(open(GO_SHIM).read())
+    body = re.search(r"^func fillTCPBatchGo\(.*?^}", shim, flags=re.M | re.S).group(0)
+    for ref in ("PseudoHeaderChecksum(", "ChecksumVVWithOffset(", "tcp.CalculateChecksum(", "ip.CalculateChecksum()"):
+        assert ref in body, ref
+        if os.path.isdir("/root/reference/tcpip/header"):
+            assert ref.split("(")[0].split(".")[-1] in REF_HEADER_NAMES | {"CalculateChecksum"}, ref
+    assert "C.ns_csum_tcp_tx_host(" in shim and "ns_csum_tcp_tx_host" in declared_symbols()

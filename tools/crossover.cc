@@ -13,6 +13,10 @@
 //   vv_batch      ChecksumVVWithOffset per MSS segment         sendTCPBatch payload
 //   chains        pseudo-header + payload + TCP header chains  finishTCPBatchChecksums
 //   verify        segment.parse's check per received packet    recvmmsg batch (VerifyPacketBuffers)
+//   tx_host       K sendTCPBatch calls of 64 KiB (45 segments, 54-B slots),
+//                 both fields of every segment (FillTCPBatches: the calls
+//                 copied into an engine stage, ns_csum_tcp_tx_host, the slots
+//                 copied back) against buildTCPHdr + addIPHeader per segment
 // The scalar loop is compiled without auto-vectorisation, as the Go compiler
 // emits it.  Output: one JSON object; "crossover" is the smallest size from
 // which the engine is faster at every larger size measured (null if never).
@@ -245,7 +249,78 @@ int main(int argc, char** argv) {
       });
       pts.push_back({n, (uint64_t)n * 1500, g, c});
     }
-    emit("verify", "packets", pts, true);
+    emit("verify", "packets", pts, false);
+  }
+  {  // FillTCPBatches: K connections' 64 KiB sendTCPBatch calls in one engine call
+    const uint32_t slot = 54, ip_at = 14, tcp_at = 34, seg = 45, csize = 65536;
+    const uint32_t per = seg * slot + csize;  // one call's slots, then its payload
+    auto be16 = [](uint8_t* p, uint32_t v) {
+      p[0] = (uint8_t)(v >> 8);
+      p[1] = (uint8_t)v;
+    };
+    const uint8_t src[4] = {10, 0, 0, 1}, dst[4] = {10, 0, 0, 2};
+    const uint16_t addr_sum = go_sum(dst, 4, false, go_sum(src, 4, false, 0, nullptr), nullptr);
+    std::vector<Point> pts;
+    const uint32_t counts[] = {1, 2, 4, 8, 16, 32, 64, 128, 256, 512, 1024};
+    for (uint32_t k : counts) {
+      // the callers' memory: K calls side by side, fresh headers (fields 0)
+      std::vector<uint8_t> mem((size_t)k * per);
+      for (uint32_t c = 0; c < k; ++c) {
+        uint8_t* base = mem.data() + (size_t)c * per;
+        for (uint32_t i = 0; i < seg; ++i) {
+          uint8_t* s = base + i * slot;
+          std::memset(s, 0, slot);
+          const uint8_t ip[20] = {0x45, 0, 0x05, 0xDC, (uint8_t)(c >> 8), (uint8_t)c, 0x40, 0, 64, 6, 0, 0,
+                                  10, 0, 0, 1, 10, 0, 0, 2};
+          std::memcpy(s + ip_at, ip, 20);
+          be16(s + tcp_at, 40000 + (c & 0x3FFF));
+          be16(s + tcp_at + 2, 443);
+          be16(s + tcp_at + 4, i);
+          s[tcp_at + 12] = 5 << 4;
+          s[tcp_at + 13] = 0x10;
+          be16(s + tcp_at + 14, 65535);
+        }
+        std::memcpy(base + seg * slot, payload.data() + (size_t)(c % 64) * 4096, csize);
+      }
+      std::vector<ns_tcp_tx> txs(k);
+      for (uint32_t c = 0; c < k; ++c)
+        txs[c] = ns_tcp_tx{(uint64_t)c * per, (uint64_t)c * per + seg * slot, csize, 1460, slot, ip_at, 20, tcp_at, 20,
+                           addr_sum, 6, 0};
+      uint8_t* stage = nullptr;
+      check(ns_csum_stage_acquire(ctx, mem.size(), &stage), "stage_acquire");
+      const double g = median_us(std::max(20, iters / 4), [&] {
+        for (uint32_t c = 0; c < k; ++c)  // the shim packs each call into the stage
+          std::memcpy(stage + (size_t)c * per, mem.data() + (size_t)c * per, per);
+        check(ns_csum_tcp_tx_host(ctx, stage, mem.size(), txs.data(), k, nullptr), "tcp_tx_host");
+        for (uint32_t c = 0; c < k; ++c)  // and copies the slots back
+          std::memcpy(mem.data() + (size_t)c * per, stage + (size_t)c * per, seg * slot);
+      });
+      // buildTCPHdr (connect.go:652-663) and addIPHeader (ipv4.go:236) per
+      // segment, on the callers' memory
+      auto cpu = [&](uint8_t* m) {
+        for (uint32_t c = 0; c < k; ++c) {
+          uint8_t* base = m + (size_t)c * per;
+          for (uint32_t i = 0; i < seg; ++i) {
+            uint8_t* s = base + i * slot;
+            const uint32_t len = std::min<uint32_t>(1460, csize - i * 1460);
+            s[tcp_at + 16] = s[tcp_at + 17] = 0;
+            const uint8_t lw[4] = {0, 6, (uint8_t)((20 + len) >> 8), (uint8_t)(20 + len)};
+            uint16_t x = go_sum(lw, 4, false, addr_sum, nullptr);  // PseudoHeaderChecksum
+            x = go_sum(base + seg * slot + i * 1460, len, false, x, nullptr);  // ChecksumVVWithOffset
+            be16(s + tcp_at + 16, ~go_sum(s + tcp_at, 20, false, x, nullptr) & 0xFFFF);
+            s[ip_at + 10] = s[ip_at + 11] = 0;
+            be16(s + ip_at + 10, ~go_sum(s + ip_at, 20, false, 0, nullptr) & 0xFFFF);
+          }
+        }
+      };
+      std::vector<uint8_t> ref = mem;
+      cpu(ref.data());
+      if (ref != mem) check(NS_EHIP, "tx_host parity");
+      const double c = median_us(std::max(20, iters / 4), [&] { cpu(ref.data()); });
+      check(ns_csum_stage_release(ctx, stage), "stage_release");
+      pts.push_back({k, (uint64_t)k * csize, g, c});
+    }
+    emit("tx_host", "calls", pts, true);
   }
   std::printf("}\n");
   ns_csum_destroy(ctx);
