@@ -807,6 +807,18 @@ inline int tx_plan(const ns_tcp_tx& t, uint64_t arena_bytes, TxPlan* out) {
   return NS_OK;
 }
 
+// Two interval lists merged into one sorted by lo.  Callers usually pack
+// their calls side by side, so each list is sorted only if it is not already:
+// O(n) instead of a sort for packed calls (23,832 calls: a 4-5 ms plan).
+template <typename Iv>
+inline void merge_by_lo(std::vector<Iv>& a, std::vector<Iv>& b, std::vector<Iv>* out) {
+  auto lt = [](const Iv& x, const Iv& y) { return x.lo < y.lo; };
+  if (!std::is_sorted(a.begin(), a.end(), lt)) std::sort(a.begin(), a.end(), lt);
+  if (!std::is_sorted(b.begin(), b.end(), lt)) std::sort(b.begin(), b.end(), lt);
+  out->resize(a.size() + b.size());
+  std::merge(a.begin(), a.end(), b.begin(), b.end(), out->begin(), lt);
+}
+
 // ns_csum_tcp_tx_multi: every call checked as above, then the ranges the
 // one launch touches: no call's slots may overlap another's slots, nor any
 // payload a full-mode call reads (waves of other calls write slots back while
@@ -817,16 +829,17 @@ inline int tx_multi_plan(const ns_tcp_tx* t, uint32_t count, uint64_t arena_byte
     uint64_t lo, hi;
     bool slots;
   };
-  std::vector<Iv> iv;
+  std::vector<Iv> sl, pl, iv;
+  sl.reserve(count);
   for (uint32_t k = 0; k < count; ++k) {
     const int rc = tx_plan(t[k], arena_bytes, &(*plans)[k]);
     if (rc != NS_OK) return rc;
     const TxPlan& p = (*plans)[k];
     if (p.n == 0 || !(p.mode & 7u)) continue;
-    iv.push_back({t[k].hdr_off, t[k].hdr_off + p.n * t[k].slot, true});
-    if ((p.mode & 2u) && t[k].size) iv.push_back({t[k].pay_off, t[k].pay_off + t[k].size, false});
+    sl.push_back({t[k].hdr_off, t[k].hdr_off + p.n * t[k].slot, true});
+    if ((p.mode & 2u) && t[k].size) pl.push_back({t[k].pay_off, t[k].pay_off + t[k].size, false});
   }
-  std::sort(iv.begin(), iv.end(), [](const Iv& a, const Iv& b) { return a.lo < b.lo; });
+  merge_by_lo(sl, pl, &iv);
   uint64_t slot_end = 0, pay_end = 0;
   for (const Iv& v : iv) {
     if (v.slots) {
@@ -926,7 +939,7 @@ inline int tx_host_plan(const ns_tcp_tx* t, uint32_t count, uint64_t arena_bytes
     seg += p.n;
   }
   out->nseg = seg;
-  std::vector<TxRange> iv;
+  std::vector<TxRange> sl, pl, iv;
   const uint32_t np = (uint32_t)out->pieces.size();
   for (uint32_t i = 0; i < np;) {
     TxChunk ch;
@@ -936,13 +949,14 @@ inline int tx_host_plan(const ns_tcp_tx* t, uint32_t count, uint64_t arena_bytes
       sum += bytes[i++];
       ++ch.np;
     }
-    iv.clear();
+    sl.clear();
+    pl.clear();
     for (uint32_t j = ch.p0; j < i; ++j) {
       const TxPiece& q = out->pieces[j];
-      iv.push_back({q.t.hdr_off, q.t.hdr_off + q.nseg * q.t.slot, 0});
-      if ((q.mode & 2u) && q.t.size) iv.push_back({q.t.pay_off, q.t.pay_off + q.t.size, 0});
+      sl.push_back({q.t.hdr_off, q.t.hdr_off + q.nseg * q.t.slot, 0});
+      if ((q.mode & 2u) && q.t.size) pl.push_back({q.t.pay_off, q.t.pay_off + q.t.size, 0});
     }
-    std::sort(iv.begin(), iv.end(), [](const TxRange& a, const TxRange& b) { return a.lo < b.lo; });
+    merge_by_lo(sl, pl, &iv);
     ch.r0 = (uint32_t)out->ranges.size();
     uint64_t at = 0;
     for (size_t j = 0; j < iv.size();) {
