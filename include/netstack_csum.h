@@ -24,6 +24,7 @@
  *   (connect.go:663, ipv4.go:236; tcp.go:252, ipv4.go:223)        -> ns_csum_batch_dev_store
  *   sendTCPBatch's whole batch from its geometry: buildTCPHdr for every
  *   segment (connect.go:668-702) and addIPHeader (ipv4.go:217-238)  -> ns_csum_tcp_tx
+ *   ... for calls in host memory, many at once                    -> ns_csum_tcp_tx_host
  *   any composition of Checksum(v, xsum) / view chaining (a whole
  *   TCP/UDP/ICMP/IPv4 checksum per chain)                         -> ns_csum_chains
  *   the checksum steps of a batch of tcpip.PacketBuffer
@@ -71,7 +72,7 @@ extern "C" {
                                   6: ns_csum_tcp_tx;
                                   7: ns_csum_tcp_tx_multi;
                                   8: ns_csum_rx_ring, ns_csum_set_tx_tuning;
-                                  9: ns_csum_tcp_tx_host */
+                                  9: ns_csum_tcp_tx_host, _host_multi */
 
 /* ---- status codes ------------------------------------------------------- */
 #define NS_OK 0
@@ -467,6 +468,16 @@ int ns_csum_batch_multi(ns_csum_ctx* const* ctxs, uint32_t nctx,
                         const uint8_t* h_arena, uint64_t arena_bytes,
                         const ns_pkt_desc* h_desc, uint32_t n, uint16_t* h_out,
                         uint32_t batch_flags);
+/* ns_csum_tcp_tx_host_multi: ns_csum_tcp_tx_host's calls over nctx contexts
+ * (normally one per device, each with its own PCIe link): the calls are cut
+ * into nctx consecutive parts balanced by the bytes each uploads (a call may
+ * be split between segments), each part runs ns_csum_tcp_tx_host on its own
+ * context from its own host thread, and h_out (or NULL) holds the sums in
+ * call order as for one context.  No collective.  Synchronous.             */
+int ns_csum_tcp_tx_host_multi(ns_csum_ctx* const* ctxs, uint32_t nctx,
+                              uint8_t* h_arena, uint64_t arena_bytes,
+                              const ns_tcp_tx* txs, uint32_t count,
+                              uint16_t* h_out);
 
 /* ---- (sharding plan) ----------------------------------------------------
  * Splits n descriptors into `parts` contiguous ranges with near-equal payload

@@ -1860,6 +1860,36 @@ int ns_csum_batch_multi(ns_csum_ctx* const* ctxs, uint32_t nctx, const uint8_t* 
   return NS_OK;
 }
 
+int ns_csum_tcp_tx_host_multi(ns_csum_ctx* const* ctxs, uint32_t nctx, uint8_t* h_arena, uint64_t arena_bytes,
+                              const ns_tcp_tx* txs, uint32_t count, uint16_t* h_out) {
+  if (!ctxs || nctx == 0 || (count && !txs) || (arena_bytes && !h_arena)) return NS_EINVAL;
+  for (uint32_t c = 0; c < nctx; ++c)
+    if (!ctxs[c]) return NS_EINVAL;
+  std::vector<nsh::TxPlan> plans;
+  const int vr = nsh::tx_multi_plan(txs, count, arena_bytes, &plans);
+  if (vr != NS_OK) return vr;
+  std::vector<std::vector<ns_tcp_tx>> parts;
+  std::vector<uint64_t> seg0;
+  nsh::tx_shard_calls(txs, count, plans, nctx, &parts, &seg0);
+  // One host thread per part (per device context), each running the host TX
+  // pipeline on its own context's streams.  Parts are independent (each
+  // segment's fields depend on its own bytes): no collective.
+  std::vector<int> status(nctx, NS_OK);
+  std::vector<std::thread> th;
+  th.reserve(nctx);
+  for (uint32_t c = 0; c < nctx; ++c) {
+    if (parts[c].empty()) continue;
+    th.emplace_back([&, c]() {
+      status[c] = ns_csum_tcp_tx_host(ctxs[c], h_arena, arena_bytes, parts[c].data(), (uint32_t)parts[c].size(),
+                                      h_out ? h_out + 2 * seg0[c] : nullptr);
+    });
+  }
+  for (auto& t : th) t.join();
+  for (uint32_t c = 0; c < nctx; ++c)
+    if (status[c] != NS_OK) return status[c];
+  return NS_OK;
+}
+
 int ns_csum_get_stats(ns_csum_ctx* ctx, ns_csum_stats* out, int reset) {
   if (!ctx || !out) return NS_EINVAL;
   StatCounters& c = ctx->st;

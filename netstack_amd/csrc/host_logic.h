@@ -903,6 +903,61 @@ struct TxHostPlan {
   }
 };
 
+// Segments [a, a + nseg) of call c as a call of their own.
+inline ns_tcp_tx tx_run(const ns_tcp_tx& c, uint64_t a, uint64_t nseg) {
+  ns_tcp_tx r = c;
+  r.hdr_off = c.hdr_off + a * c.slot;
+  r.pay_off = c.pay_off + a * c.mss;
+  r.size = std::min<uint64_t>(c.size - a * c.mss, nseg * c.mss);
+  return r;
+}
+
+// ns_csum_tcp_tx_host_multi's split: the calls (checked by tx_multi_plan)
+// cut into `parts` consecutive lists of runs, balanced by the bytes each
+// uploads (slots, and the payload of full-mode calls): a list ends once it
+// holds ceil(total / parts) bytes, cutting a call between segments where
+// needed.  Calls with nothing to compute stay whole in the list they fall
+// in.  seg0[p] = the index over all calls' segments of list p's first
+// segment, so list p's sums are h_out[2 seg0[p] ...].  Lists may be empty.
+inline void tx_shard_calls(const ns_tcp_tx* t, uint32_t count, const std::vector<TxPlan>& plans, uint32_t parts,
+                           std::vector<std::vector<ns_tcp_tx>>* out, std::vector<uint64_t>* seg0) {
+  out->assign(parts, {});
+  seg0->assign(parts, 0);
+  auto per_seg = [&](uint32_t k) {
+    return (plans[k].n && (plans[k].mode & 7u)) ? (uint64_t)t[k].slot + ((plans[k].mode & 2u) ? t[k].mss : 0u) : 0u;
+  };
+  uint64_t total = 0;
+  for (uint32_t k = 0; k < count; ++k)
+    if (per_seg(k)) total += plans[k].n * t[k].slot + ((plans[k].mode & 2u) ? t[k].size : 0u);
+  const uint64_t quota = std::max<uint64_t>(1, (total + parts - 1) / parts);
+  uint32_t p = 0;
+  uint64_t have = 0, seg = 0;
+  for (uint32_t k = 0; k < count; ++k) {
+    const uint64_t n = plans[k].n, b = per_seg(k);
+    if (!b) {  // whole, wherever it falls
+      (*out)[p].push_back(t[k]);
+      seg += n;
+      continue;
+    }
+    for (uint64_t a = 0; a < n;) {
+      if (have >= quota && p + 1 < parts) {
+        ++p;
+        have = 0;
+        (*seg0)[p] = seg;
+      }
+      // segments that fit the part's quota (at least one; the last part takes the rest)
+      const uint64_t room = p + 1 < parts ? (quota - have + b - 1) / b : n - a;
+      const uint64_t m = std::min<uint64_t>(n - a, std::max<uint64_t>(1, room));
+      const ns_tcp_tx r = tx_run(t[k], a, m);
+      (*out)[p].push_back(r);
+      have += m * t[k].slot + ((plans[k].mode & 2u) ? r.size : 0u);
+      a += m;
+      seg += m;
+    }
+  }
+  for (uint32_t q = p + 1; q < parts; ++q) (*seg0)[q] = seg;
+}
+
 inline int tx_host_plan(const ns_tcp_tx* t, uint32_t count, uint64_t arena_bytes, uint64_t budget,
                         TxHostPlan* out) {
   std::vector<TxPlan> plans;
@@ -926,10 +981,7 @@ inline int tx_host_plan(const ns_tcp_tx* t, uint32_t count, uint64_t arena_bytes
       for (uint64_t a = 0; a < p.n; a += run) {
         TxPiece q;
         q.nseg = std::min(run, p.n - a);
-        q.t = c;
-        q.t.hdr_off = c.hdr_off + a * c.slot;
-        q.t.pay_off = c.pay_off + a * c.mss;
-        q.t.size = std::min<uint64_t>(c.size - a * c.mss, q.nseg * c.mss);
+        q.t = tx_run(c, a, q.nseg);
         q.out0 = seg + a;
         q.mode = p.mode;
         out->pieces.push_back(q);

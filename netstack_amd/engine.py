@@ -394,6 +394,25 @@ def batch_multi(engines, arena, desc: np.ndarray, chained: bool = False) -> np.n
     return out
 
 
+def tcp_tx_host_multi(engines, arena: np.ndarray, geos, mode: str = "full") -> np.ndarray:
+    """sendTCPBatch calls over host memory sharded over several engines
+    (devices) by ns_csum_tcp_tx_host_multi: byte-balanced consecutive parts,
+    one host thread and one device per part, no collective.  Fields written
+    into `arena` in place; returns the 2 * sum(n_k) sums in call order."""
+    if not (isinstance(arena, np.ndarray) and arena.dtype == np.uint8 and arena.flags.c_contiguous
+            and arena.flags.writeable):
+        raise ValueError("arena must be a writable, contiguous uint8 numpy array")
+    arr = geos if isinstance(geos, ctypes.Array) else tx_table(geos, mode)
+    count = len(arr) if len(geos) else 0
+    t = np.ctypeslib.as_array(arr)[:count]
+    total = int((-(-t["size"].astype(np.int64) // np.maximum(t["mss"], 1))).sum()) if count else 0
+    out = np.zeros(max(2 * total, 1), dtype=np.uint16)
+    hs = (ctypes.c_void_p * len(engines))(*[e._h for e in engines])
+    check(lib().ns_csum_tcp_tx_host_multi(hs, len(engines), _ptr(arena), arena.size, arr, count, _ptr(out)),
+          "ns_csum_tcp_tx_host_multi")
+    return out[:2 * total]
+
+
 _engines: dict[int, Engine] = {}
 _elock = threading.Lock()
 

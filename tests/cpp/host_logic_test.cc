@@ -18,6 +18,7 @@
 //                 stays inside the arena and apart where the kernels need it;
 //   tx_host_plan  pieces tile each call's segments as valid calls, chunks
 //                 within budget, the staged ranges hold every byte read;
+//   tx_shard_calls  parts tile the calls' segments in order, balanced;
 //   FlatCombiner  many threads x many requests: every request done once
 //                 with its own result (the point of the -fsanitize=thread
 //                 build).
@@ -794,6 +795,86 @@ static void TestTxHostPlan(Rng& rng, int rounds) {
         "two calls, one chunk");
 }
 
+// nsh::tx_shard_calls (ns_csum_tcp_tx_host_multi): random call sets and part
+// counts.  The parts, in order, hold every call's segments in order as runs
+// that are valid calls, seg0 follows the segment counts, and every part but
+// the last stays within one segment of the byte quota.
+static void TestTxShardCalls(Rng& rng, int rounds) {
+  int checked = 0;
+  for (int round = 0; round < rounds * 10; ++round) {
+    const uint32_t count = (uint32_t)(rng() % 9);
+    const uint64_t arena = 1u << 20;
+    std::vector<ns_tcp_tx> t(count);
+    uint64_t pos = 0;
+    for (auto& x : t) {
+      x = ns_tcp_tx{};
+      x.mss = rng() % 4 == 0 ? 1 + (uint32_t)(rng() % 16) : 100 + (uint32_t)(rng() % 1500);
+      x.slot = 40 + (uint32_t)(rng() % 40);
+      x.ip_at = 0, x.ip_len = (uint16_t)(rng() % 4 == 0 ? 0 : 20), x.tcp_at = 20, x.tcp_len = 20;
+      x.size = rng() % 8 == 0 ? 0 : rng() % 40000;
+      x.flags = (uint32_t)(rng() % 3);
+      const uint64_t n = (x.size + x.mss - 1) / x.mss;
+      x.hdr_off = pos, x.pay_off = pos + n * x.slot + rng() % 100;
+      pos = x.pay_off + x.size + rng() % 100;
+    }
+    if (pos > arena) continue;
+    std::vector<nsh::TxPlan> plans;
+    CHECK(nsh::tx_multi_plan(t.data(), count, arena, &plans) == NS_OK, "packed calls");
+    const uint32_t parts = 1 + (uint32_t)(rng() % 9);
+    std::vector<std::vector<ns_tcp_tx>> out;
+    std::vector<uint64_t> seg0;
+    nsh::tx_shard_calls(t.data(), count, plans, parts, &out, &seg0);
+    CHECK(out.size() == parts && seg0.size() == parts, "part count");
+    uint64_t total = 0, maxper = 0;
+    for (uint32_t k = 0; k < count; ++k)
+      if (plans[k].n && (plans[k].mode & 7u)) {
+        total += plans[k].n * t[k].slot + ((plans[k].mode & 2u) ? t[k].size : 0u);
+        maxper = std::max<uint64_t>(maxper, t[k].slot + ((plans[k].mode & 2u) ? t[k].mss : 0u));
+      }
+    const uint64_t quota = std::max<uint64_t>(1, (total + parts - 1) / parts);
+    // walk the parts against the calls
+    uint32_t k = 0;
+    uint64_t a = 0, seg = 0, sum = 0;
+    for (uint32_t p = 0; p < parts; ++p) {
+      CHECK(seg0[p] == seg, "seg0 of part %u", p);
+      uint64_t bytes = 0;
+      for (const ns_tcp_tx& r : out[p]) {
+        while (k < count && a == plans[k].n && !(plans[k].n == 0 && a == 0 && r.hdr_off == t[k].hdr_off &&
+                                                  r.size == t[k].size)) {
+          ++k;
+          a = 0;
+        }
+        CHECK(k < count, "run past the calls");
+        if (k >= count) return;
+        const bool work = plans[k].n && (plans[k].mode & 7u);
+        nsh::TxPlan rp;
+        CHECK(nsh::tx_plan(r, arena, &rp) == NS_OK && rp.mode == plans[k].mode, "run as a call");
+        const ns_tcp_tx want = nsh::tx_run(t[k], a, rp.n);
+        CHECK(r.hdr_off == want.hdr_off && r.pay_off == want.pay_off && r.size == want.size, "run %llu of call %u",
+              (unsigned long long)a, k);
+        CHECK(work || (a == 0 && rp.n == plans[k].n), "a call without work stays whole");
+        if (work) bytes += rp.n * r.slot + ((rp.mode & 2u) ? r.size : 0u);
+        a += rp.n;
+        seg += rp.n;
+        if (plans[k].n == 0) {  // no segments: one run, then the next call
+          ++k;
+          a = 0;
+        }
+      }
+      if (p + 1 < parts) CHECK(bytes <= quota + maxper, "part %u: %llu bytes, quota %llu", p,
+                               (unsigned long long)bytes, (unsigned long long)quota);
+      sum += bytes;
+    }
+    while (k < count && a == plans[k].n) {
+      ++k;
+      a = 0;
+    }
+    CHECK(k == count && sum == total, "every segment placed once");
+    ++checked;
+  }
+  CHECK(checked > 0, "no call set checked");
+}
+
 int main(int argc, char** argv) {
   const bool quick = argc > 1 && std::strcmp(argv[1], "--quick") == 0;
   Rng rng(20261016);
@@ -806,6 +887,7 @@ int main(int argc, char** argv) {
   TestTxPlan(rng, r);
   TestTxMultiPlan(rng, r);
   TestTxHostPlan(rng, r);
+  TestTxShardCalls(rng, r);
   TestRxPlan(rng, r);
   TestCombiner(16, quick ? 200 : 2000);
   TestScratchRegistry(8, 1000, quick ? 2000 : 20000);

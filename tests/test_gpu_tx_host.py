@@ -165,3 +165,24 @@ def test_errors(engine):
     assert L.ns_csum_tcp_tx_host(h, a.ctypes.data, a.size, arr, len(geos), None) == _lib.NS_OK
     assert not np.array_equal(a, before)
     assert engine.tcp_tx_host(a, []).size == 0
+
+
+@pytest.mark.parametrize("parts", [2, 3])
+def test_multi_context_split(oracle_mod, parts):
+    """ns_csum_tcp_tx_host_multi: the calls split by bytes over several
+    contexts (on the box's one device; one per GPU in production), each part
+    on its own host thread, calls cut between segments where a part ends;
+    the same bytes and sums as one context."""
+    from netstack_amd import Engine
+    from netstack_amd.engine import tcp_tx_host_multi
+
+    geos, a = _layout(23 + parts)
+    want, ws = _want(oracle_mod, a, geos)
+    engines = [Engine(0, staging_bytes=1 << 20) for _ in range(parts)]
+    try:
+        got = a.copy()
+        sums = tcp_tx_host_multi(engines, got, geos)
+        _check(got, sums, want, ws, f"{parts} contexts")
+    finally:
+        for e in engines:
+            e.close()
