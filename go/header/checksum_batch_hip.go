@@ -421,17 +421,17 @@ const (
 // traffic; they are read without synchronisation).
 var (
 	// ChainsOffloadMinBytes is the payload of one sendTCPBatch
-	// (ChecksumChains): at 64 KiB the engine took 1.57x one core's time,
-	// at 128 KiB 0.91x, at 256 KiB 0.57x.
+	// (ChecksumChains): at 64 KiB the engine took 1.63x one core's time,
+	// at 128 KiB 0.94x, at 256 KiB 0.61x.
 	ChainsOffloadMinBytes = 128 << 10
 	// VerifyOffloadMinBytes is the Data bytes of one recvmmsg batch
-	// (VerifyPacketBuffers): 64 x 1500 B took 1.31x one core's time,
-	// 128 x 1500 B 0.88x, 256 x 1500 B 0.70x.
+	// (VerifyPacketBuffers): 64 x 1500 B took 1.38x one core's time,
+	// 128 x 1500 B 0.95x, 256 x 1500 B 0.76x.
 	VerifyOffloadMinBytes = 128 * 1500
 	// TxBatchOffloadMinBytes is the payload of all the batches one
 	// FillTCPBatches call fills (profiles/r05/crossover.json "tx_host",
-	// 64 KiB sendTCPBatch calls, stage copies included): 4 calls took 1.09x
-	// one core's time, 8 calls (512 KiB) 0.67x, 64 calls 0.31x.
+	// 64 KiB sendTCPBatch calls, stage copies included): 4 calls took 1.19x
+	// one core's time, 8 calls (512 KiB) 0.74x, 64 calls 0.34x.
 	TxBatchOffloadMinBytes = 512 << 10
 )
 
@@ -792,6 +792,47 @@ func VerifyRingDevice(arena uintptr, arenaBytes uint64, r RxRing, lens, sums, ve
 		(*C.uint32_t)(unsafe.Pointer(lens)), (*C.uint16_t)(unsafe.Pointer(sums)),
 		(*C.uint8_t)(unsafe.Pointer(verdict)), unsafe.Pointer(stream)); rc != C.NS_OK {
 		return engineFailed("ns_csum_rx_ring", rc)
+	}
+	return nil
+}
+
+// VerifyRingHost is VerifyRingDevice for a ring in host memory: arena holds
+// r.N slots of r.Stride bytes from r.RingOff (recvmmsg's buffers laid out
+// at a fixed stride), lens their received lengths; verdict (or nil) and sums
+// (or nil, 2 per slot) receive the results (ns_csum_rx_ring_host).  The parse
+// runs on the device: no per-packet host planning, unlike
+// VerifyPacketBuffers.  On an error (counted in EngineFallbacks) the outputs
+// are not to be used: the caller delivers the frames unverified
+// (RXChecksumUnknown), as the default build does.
+func VerifyRingHost(arena []byte, r RxRing, lens []uint32, sums []uint16, verdict []uint8) error {
+	n := int(r.N)
+	if len(lens) < n || (sums != nil && len(sums) < 2*n) || (verdict != nil && len(verdict) < n) {
+		panic("netstack_csum: VerifyRingHost: lens, sums or verdict too short")
+	}
+	if n == 0 {
+		return nil
+	}
+	ctx, rc := csumEngine()
+	if rc != C.NS_OK {
+		return engineFailed("ns_csum_init", rc)
+	}
+	cr := C.ns_rx_ring{ring_off: C.uint64_t(r.RingOff), stride: C.uint64_t(r.Stride), n: C.uint32_t(r.N),
+		frame_at: C.uint16_t(r.FrameAt), link_hdr: C.uint16_t(r.LinkHdr), first_view: C.uint32_t(r.FirstView)}
+	var ap *C.uint8_t
+	if len(arena) > 0 {
+		ap = (*C.uint8_t)(unsafe.Pointer(&arena[0]))
+	}
+	var sp *C.uint16_t
+	if sums != nil {
+		sp = (*C.uint16_t)(unsafe.Pointer(&sums[0]))
+	}
+	var vp *C.uint8_t
+	if verdict != nil {
+		vp = (*C.uint8_t)(unsafe.Pointer(&verdict[0]))
+	}
+	if rc := C.ns_csum_rx_ring_host(ctx, ap, C.uint64_t(len(arena)), &cr, (*C.uint32_t)(unsafe.Pointer(&lens[0])),
+		sp, vp); rc != C.NS_OK {
+		return engineFailed("ns_csum_rx_ring_host", rc)
 	}
 	return nil
 }

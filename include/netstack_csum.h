@@ -41,6 +41,7 @@
  *   (network/ipv4/ipv4.go:341-394, header/ipv4.go:280-296; network/ipv6/
  *   ipv6.go:168-188, header/ipv6.go:207-222), segment.parse
  *   (tcp/segment.go:145-181), handleICMP                         -> ns_csum_rx_ring
+ *   ... for a ring in host memory                                 -> ns_csum_rx_ring_host
  *
  * Semantics (bit-exact with checksum.go, including its un-folded uint32 wrap for
  * buffers > 128 KiB): every descriptor d is one calculateChecksum call over
@@ -72,7 +73,8 @@ extern "C" {
                                   6: ns_csum_tcp_tx;
                                   7: ns_csum_tcp_tx_multi;
                                   8: ns_csum_rx_ring, ns_csum_set_tx_tuning;
-                                  9: ns_csum_tcp_tx_host, _host_multi */
+                                  9: ns_csum_tcp_tx_host, _host_multi,
+                                     ns_csum_rx_ring_host */
 
 /* ---- status codes ------------------------------------------------------- */
 #define NS_OK 0
@@ -454,6 +456,16 @@ typedef struct ns_rx_ring {
 int ns_csum_rx_ring(ns_csum_ctx* ctx, const uint8_t* d_arena, uint64_t arena_bytes,
                     const ns_rx_ring* ring, const uint32_t* d_len, uint16_t* d_sums,
                     uint8_t* d_verdict, void* stream);
+/* The same ring in HOST memory (recvmmsg's buffers as the link endpoint
+ * fills them): h_arena, h_len, h_sums and h_verdict are host pointers, the
+ * ring's own alignment is free (ring_off need not be 16-B aligned; the stride
+ * still must be a multiple of 16).  The slots go to the device in chunks of
+ * whole slots (up to the context's staging size), four in flight; verdicts
+ * and sums come back through mapped memory.  No host planning: the parse
+ * runs on the device.  Synchronous.  Errors as for ns_csum_rx_ring.        */
+int ns_csum_rx_ring_host(ns_csum_ctx* ctx, const uint8_t* h_arena, uint64_t arena_bytes,
+                         const ns_rx_ring* ring, const uint32_t* h_len, uint16_t* h_sums,
+                         uint8_t* h_verdict);
 
 /* header.ChecksumCombine(a, b)                     checksum.go:104-107      */
 uint16_t ns_csum_combine(uint16_t a, uint16_t b);

@@ -354,6 +354,10 @@ struct ns_csum_ctx {
   // pinned for its upload and on the device
   PinBuf<uint8_t> h_txtab[kMaxHostSlots];
   DevBuf<uint8_t> d_txtab[kMaxHostSlots];
+  // ns_csum_rx_ring_host: each slot's received lengths on the device and its
+  // verdicts (mapped, written by the kernel; the sums go to h_out)
+  DevBuf<uint32_t> d_len[kMaxHostSlots];
+  MappedPin h_verd[kMaxHostSlots];
   // zero-copy pass buffers for small calls: the table (read by the kernel),
   // the results and the completion word (written by it)
   BarBuf z_buf;
@@ -924,6 +928,76 @@ int run_tx_host(ns_csum_ctx* ctx, uint8_t* h_arena, const nsh::TxHostPlan& plan,
   return rc;
 }
 
+// ns_csum_rx_ring_host's pipeline: the ring in chunks of whole slots (as
+// many as the staging budget holds), nslots in flight on the host pipeline's
+// streams.  Per chunk: the slots and their lengths go to the device, rx_ring
+// parses and verifies them there and writes verdicts and sums straight to
+// mapped pinned memory; when the chunk is done they are copied to the
+// caller's arrays while later chunks are in flight.  No host planning.
+int run_rx_host(ns_csum_ctx* ctx, const uint8_t* h_arena, const ns_rx_ring& r, const uint32_t* h_len,
+                uint16_t* h_sums, uint8_t* h_verdict) {
+  const uint32_t nslots = ctx->nslots;
+  const uint32_t per = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(1, ctx->staging / r.stride), 1u << 24);
+  struct Pending {
+    bool live = false;
+    uint32_t first = 0, count = 0;
+  } pend[kMaxHostSlots];
+  auto finish = [&](uint32_t sl) -> int {
+    if (!pend[sl].live) return NS_OK;
+    pend[sl].live = false;
+    HIP_TRY(hipEventSynchronize(ctx->done[sl]));
+    if (h_sums) std::memcpy(h_sums + 2 * (uint64_t)pend[sl].first, ctx->h_out[sl].p, 4 * (size_t)pend[sl].count);
+    if (h_verdict) std::memcpy(h_verdict + pend[sl].first, ctx->h_verd[sl].p, pend[sl].count);
+    return NS_OK;
+  };
+  auto enqueue = [&](uint32_t first, uint32_t cnt, uint32_t sl) -> int {
+    int rc;
+    const uint64_t bytes = (uint64_t)cnt * r.stride;
+    if ((rc = ctx->d_arena[sl].ensure(bytes)) != NS_OK) return rc;
+    if ((rc = ctx->d_len[sl].ensure(cnt)) != NS_OK) return rc;
+    if ((rc = ctx->h_out[sl].ensure(2 * (size_t)cnt)) != NS_OK) return rc;
+    if ((rc = ctx->h_verd[sl].ensure(cnt)) != NS_OK) return rc;
+    hipStream_t s = ctx->stream[sl];
+    HIP_TRY(hipMemcpyAsync(ctx->d_arena[sl].p, h_arena + r.ring_off + (uint64_t)first * r.stride, bytes,
+                           hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(ctx->d_len[sl].p, h_len + first, 4 * (size_t)cnt, hipMemcpyHostToDevice, s));
+    nsk::RxGeo geo{};
+    geo.ring = (uint64_t)(uintptr_t)ctx->d_arena[sl].p;
+    geo.stride = r.stride;
+    geo.len = ctx->d_len[sl].p;
+    geo.sums = ctx->h_out[sl].dev;
+    geo.verdict = ctx->h_verd[sl].dev;
+    geo.err = ctx->d_err;
+    geo.n = cnt;
+    geo.frame_at = r.frame_at;
+    geo.link = r.link_hdr;
+    geo.view0 = r.first_view ? r.first_view - r.link_hdr : 0u;
+    HIP_TRY(nsk::launch_rx_ring(geo, s));
+    HIP_TRY(hipEventRecord(ctx->done[sl], s));
+    return NS_OK;
+  };
+  int rc = NS_OK;
+  uint32_t slot = 0;
+  for (uint32_t first = 0; first < r.n; first += per) {
+    const uint32_t cnt = std::min(per, r.n - first);
+    if ((rc = finish(slot)) != NS_OK) break;
+    if ((rc = enqueue(first, cnt, slot)) != NS_OK) {
+      (void)hipStreamSynchronize(ctx->stream[slot]);
+      (void)hipGetLastError();
+      break;
+    }
+    pend[slot].live = true;
+    pend[slot].first = first;
+    pend[slot].count = cnt;
+    slot = (slot + 1) % nslots;
+  }
+  for (uint32_t k = 0; k < nslots; ++k) {
+    const int e = finish((slot + k) % nslots);
+    if (rc == NS_OK) rc = e;
+  }
+  return rc;
+}
+
 // Caller-acquired staging (ns_csum_stage_acquire): mapped pinned buffers a
 // caller fills itself — the Go shim, which may not hand C memory holding Go
 // pointers to the library, copies its views there once.  Gathers whose bytes
@@ -1269,6 +1343,8 @@ void ns_csum_destroy(ns_csum_ctx* ctx) {
       ctx->h_out[s].release();
       ctx->h_txtab[s].release();
       ctx->d_txtab[s].release();
+      ctx->d_len[s].release();
+      ctx->h_verd[s].release();
       if (ctx->done[s]) (void)hipEventDestroy(ctx->done[s]);
       if (ctx->stream[s]) (void)hipStreamDestroy(ctx->stream[s]);
     }
@@ -1612,6 +1688,24 @@ int ns_csum_rx_ring(ns_csum_ctx* ctx, const uint8_t* d_arena, uint64_t arena_byt
   geo.view0 = r.first_view ? r.first_view - r.link_hdr : 0u;
   HIP_TRY(nsk::launch_rx_ring(geo, (hipStream_t)stream));
   return NS_OK;
+}
+
+int ns_csum_rx_ring_host(ns_csum_ctx* ctx, const uint8_t* h_arena, uint64_t arena_bytes, const ns_rx_ring* ring,
+                         const uint32_t* h_len, uint16_t* h_sums, uint8_t* h_verdict) {
+  if (!ctx || !ring || (arena_bytes && !h_arena) || (!h_sums && !h_verdict)) return NS_EINVAL;
+  const ns_rx_ring& r = *ring;
+  if (r.n && !h_len) return NS_EINVAL;
+  if (r.ring_off > arena_bytes) return NS_ERANGE;
+  // the slots go to 16-B-aligned staging: the host ring's own alignment is free
+  ns_rx_ring r0 = r;
+  r0.ring_off = 0;
+  const int vr = nsh::rx_plan(r0, 0, arena_bytes - r.ring_off);
+  if (vr != NS_OK) return vr;
+  CallClock clk(ctx);
+  if (r.n == 0) return NS_OK;
+  std::lock_guard<std::mutex> lk(ctx->pmu);
+  DeviceGuard g(ctx->device);
+  return run_rx_host(ctx, h_arena, r, h_len, h_sums, h_verdict);
 }
 
 int ns_csum_batch_host(ns_csum_ctx* ctx, const uint8_t* h_arena, uint64_t arena_bytes,

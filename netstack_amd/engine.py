@@ -222,6 +222,24 @@ class Engine:
                                     getattr(stream, "cuda_stream", stream)), "ns_csum_rx_ring")
         return verdict, sums
 
+    def rx_ring_host(self, arena, ring: dict, lens):
+        """Verify a receive ring in HOST memory (ns_csum_rx_ring_host):
+        `arena` a contiguous uint8 numpy array, `ring` as for rx_ring, `lens`
+        the n received lengths (uint32).  Synchronous; returns (verdict,
+        sums) as numpy arrays of n bytes and 2n u16."""
+        a = _u8(arena)
+        n = int(ring["n"])
+        ln = np.ascontiguousarray(lens, dtype=np.uint32)
+        if ln.size < n:
+            raise ValueError("lens must hold n received lengths")
+        verdict = np.zeros(max(n, 1), dtype=np.uint8)
+        sums = np.zeros(max(2 * n, 1), dtype=np.uint16)
+        r = _lib.NsRxRing(int(ring.get("ring_off", 0)), int(ring["stride"]), n, int(ring.get("frame_at", 0)),
+                          int(ring.get("link_hdr", 0)), int(ring.get("first_view", 0)), int(ring.get("flags", 0)))
+        check(lib().ns_csum_rx_ring_host(self._h, _ptr(a), a.size, ctypes.byref(r), _ptr(ln), _ptr(sums),
+                                         _ptr(verdict)), "ns_csum_rx_ring_host")
+        return verdict[:n], sums[:2 * n]
+
     def stream_release(self, stream) -> None:
         """Free the scratch this context keeps for `stream` (a torch.cuda.Stream
         or a raw hipStream_t) after its last launch (ns_csum_stream_release);

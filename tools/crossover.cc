@@ -13,6 +13,8 @@
 //   vv_batch      ChecksumVVWithOffset per MSS segment         sendTCPBatch payload
 //   chains        pseudo-header + payload + TCP header chains  finishTCPBatchChecksums
 //   verify        segment.parse's check per received packet    recvmmsg batch (VerifyPacketBuffers)
+//   verify_ring_host  the same packets copied into a 1504-B-stride ring
+//                 stage, parsed on the device (ns_csum_rx_ring_host)
 //   tx_host       K sendTCPBatch calls of 64 KiB (45 segments, 54-B slots),
 //                 both fields of every segment (FillTCPBatches: the calls
 //                 copied into an engine stage, ns_csum_tcp_tx_host, the slots
@@ -191,7 +193,7 @@ int main(int argc, char** argv) {
       p[0] = (uint8_t)(v >> 8);
       p[1] = (uint8_t)v;
     };
-    std::vector<Point> pts;
+    std::vector<Point> pts, rpts;
     const uint32_t counts[] = {1, 2, 4, 8, 16, 32, 64, 128, 256, 512, 1024, 2048};
     for (uint32_t n : counts) {
       std::vector<uint8_t> pk((size_t)n * 1500);
@@ -248,8 +250,34 @@ int main(int argc, char** argv) {
         g_sink += ok;
       });
       pts.push_back({n, (uint64_t)n * 1500, g, c});
+      // the same packets as a receive ring in an engine stage: each packet's
+      // views copied into its 1504-B slot (what a caller does with recvmmsg's
+      // buffers), then ns_csum_rx_ring_host parses and verifies them on the
+      // device, no host planning
+      uint8_t* stage = nullptr;
+      check(ns_csum_stage_acquire(ctx, (uint64_t)n * 1504, &stage), "stage_acquire");
+      std::vector<uint32_t> lens(n, 1500);
+      std::vector<uint8_t> rv(n);
+      const ns_rx_ring ring{0, 1504, n, 0, 0, 128, 0};
+      const double gr = median_us(std::max(20, iters / 2), [&] {
+        for (uint32_t i = 0; i < n; ++i) {
+          uint8_t* dst = stage + (size_t)i * 1504;
+          for (int k = 0; k < 5; ++k) {
+            const ns_view& v = views[(size_t)i * 5 + k];
+            std::memcpy(dst, v.data, v.len);
+            dst += v.len;
+          }
+        }
+        check(ns_csum_rx_ring_host(ctx, stage, (uint64_t)n * 1504, &ring, lens.data(), nullptr, rv.data()),
+              "rx_ring_host");
+      });
+      for (uint8_t v : rv)
+        if (v != NS_PKB_VALID) check(NS_EHIP, "ring verify parity");
+      check(ns_csum_stage_release(ctx, stage), "stage_release");
+      rpts.push_back({n, (uint64_t)n * 1500, gr, c});
     }
     emit("verify", "packets", pts, false);
+    emit("verify_ring_host", "packets", rpts, false);
   }
   {  // FillTCPBatches: K connections' 64 KiB sendTCPBatch calls in one engine call
     const uint32_t slot = 54, ip_at = 14, tcp_at = 34, seg = 45, csize = 65536;

@@ -16,6 +16,9 @@ echo "host modes"
 for c in 2 3 4; do
   timeout -k 10 200 python bench.py --mode host --config $c --no-cpu --no-parity > $OUT/bench_host$c.json 2>/dev/null
 done
+echo "host RX ring (ns_csum_rx_ring_host)"
+timeout -k 10 300 python bench.py --mode host --config 7 --rx-layout ring --steps 10 --warmup 2 \
+  > $OUT/bench_host7_ring.json 2>/dev/null
 echo "host TX (ns_csum_tcp_tx_host): one call, and one call per 64 KiB GSO write"
 timeout -k 10 300 python bench.py --mode host --config 8 --steps 10 --warmup 2 --cpu-seconds 5 > $OUT/bench_host8.json 2>/dev/null
 timeout -k 10 300 python bench.py --mode host --config 8 --tx-calls 23832 --steps 10 --warmup 2 --no-cpu \
