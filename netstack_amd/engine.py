@@ -173,13 +173,7 @@ class Engine:
         stage_acquire) holding the calls' header slots and payloads; `geos`
         as for tcp_tx_multi.  Synchronous: the fields are written into
         `arena` in place; returns the 2 * sum(n_k) un-complemented sums."""
-        if not (isinstance(arena, np.ndarray) and arena.dtype == np.uint8 and arena.flags.c_contiguous
-                and arena.flags.writeable):
-            raise ValueError("arena must be a writable, contiguous uint8 numpy array")
-        arr = geos if isinstance(geos, ctypes.Array) else tx_table(geos, mode)
-        count = len(arr) if len(geos) else 0
-        t = np.ctypeslib.as_array(arr)[:count]
-        total = int((-(-t["size"].astype(np.int64) // np.maximum(t["mss"], 1))).sum()) if count else 0
+        arr, count, total = _tx_host_args(arena, geos, mode)
         out = np.zeros(max(2 * total, 1), dtype=np.uint16)
         check(lib().ns_csum_tcp_tx_host(self._h, _ptr(arena), arena.size, arr, count, _ptr(out)),
               "ns_csum_tcp_tx_host")
@@ -371,6 +365,20 @@ def tx_table(geos, mode: str = "full"):
     return arr
 
 
+def _tx_host_args(arena, geos, mode):
+    """Checks a host arena for the host TX entry points and returns the
+    ns_tcp_tx table, the call count and the calls' total segments
+    (n_k = ceil(size / mss), connect.go:675; the C side refuses mss 0)."""
+    if not (isinstance(arena, np.ndarray) and arena.dtype == np.uint8 and arena.flags.c_contiguous
+            and arena.flags.writeable):
+        raise ValueError("arena must be a writable, contiguous uint8 numpy array")
+    arr = geos if isinstance(geos, ctypes.Array) else tx_table(geos, mode)
+    count = len(arr) if len(geos) else 0
+    t = np.ctypeslib.as_array(arr)[:count]
+    total = int((-(-t["size"].astype(np.int64) // np.maximum(t["mss"], 1))).sum()) if count else 0
+    return arr, count, total
+
+
 @functools.lru_cache(maxsize=1024)
 def addr_sum(src: bytes, dst: bytes) -> int:
     """Checksum(dst, Checksum(src, 0)) (checksum.go:113-114): the address part
@@ -417,13 +425,7 @@ def tcp_tx_host_multi(engines, arena: np.ndarray, geos, mode: str = "full") -> n
     (devices) by ns_csum_tcp_tx_host_multi: byte-balanced consecutive parts,
     one host thread and one device per part, no collective.  Fields written
     into `arena` in place; returns the 2 * sum(n_k) sums in call order."""
-    if not (isinstance(arena, np.ndarray) and arena.dtype == np.uint8 and arena.flags.c_contiguous
-            and arena.flags.writeable):
-        raise ValueError("arena must be a writable, contiguous uint8 numpy array")
-    arr = geos if isinstance(geos, ctypes.Array) else tx_table(geos, mode)
-    count = len(arr) if len(geos) else 0
-    t = np.ctypeslib.as_array(arr)[:count]
-    total = int((-(-t["size"].astype(np.int64) // np.maximum(t["mss"], 1))).sum()) if count else 0
+    arr, count, total = _tx_host_args(arena, geos, mode)
     out = np.zeros(max(2 * total, 1), dtype=np.uint16)
     hs = (ctypes.c_void_p * len(engines))(*[e._h for e in engines])
     check(lib().ns_csum_tcp_tx_host_multi(hs, len(engines), _ptr(arena), arena.size, arr, count, _ptr(out)),
