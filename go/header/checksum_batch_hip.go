@@ -421,18 +421,18 @@ const (
 // traffic; they are read without synchronisation).
 var (
 	// ChainsOffloadMinBytes is the payload of one sendTCPBatch
-	// (ChecksumChains): at 64 KiB the engine took 1.63x one core's time,
-	// at 128 KiB 0.94x, at 256 KiB 0.61x.
+	// (ChecksumChains; medians of six runs): at 64 KiB the engine took 1.70x
+	// one core's time, at 128 KiB 0.98x, at 256 KiB 0.62x.
 	ChainsOffloadMinBytes = 128 << 10
 	// VerifyOffloadMinBytes is the Data bytes of one recvmmsg batch
-	// (VerifyPacketBuffers): 64 x 1500 B took 1.38x one core's time,
-	// 128 x 1500 B 0.95x, 256 x 1500 B 0.76x.
+	// (VerifyPacketBuffers): 64 x 1500 B took 1.41x one core's time,
+	// 128 x 1500 B 0.98x, 256 x 1500 B 0.74x.
 	VerifyOffloadMinBytes = 128 * 1500
 	// TxBatchOffloadMinBytes is the payload of all the batches one
 	// FillTCPBatches call fills (profiles/r05/crossover.json "tx_host",
-	// 64 KiB sendTCPBatch calls, stage copies included): 4 calls took 1.19x
-	// one core's time, 8 calls (512 KiB) 0.74x, 64 calls 0.34x.
-	TxBatchOffloadMinBytes = 512 << 10
+	// 64 KiB sendTCPBatch calls, stage copies included): 2 calls took 1.32x
+	// one core's time, 4 calls (256 KiB) 0.82x, 64 calls 0.39x.
+	TxBatchOffloadMinBytes = 256 << 10
 )
 
 // VerifyPacketBuffers runs the receive path's checksum checks over a batch

@@ -358,6 +358,11 @@ struct ns_csum_ctx {
   // verdicts (mapped, written by the kernel; the sums go to h_out)
   DevBuf<uint32_t> d_len[kMaxHostSlots];
   MappedPin h_verd[kMaxHostSlots];
+  // the small host paths' results and completion word (coherent: written
+  // through, visible once the signal is; pmu)
+  CoherentPin p_res;
+  CoherentPin p_done;
+  uint32_t p_seq = 0;
   // zero-copy pass buffers for small calls: the table (read by the kernel),
   // the results and the completion word (written by it)
   BarBuf z_buf;
@@ -836,7 +841,132 @@ inline void put_be16(uint8_t* p, uint32_t v) {
 // its fields into the caller's slots from those sums, the values the kernel
 // stores (2 x 2 B per segment instead of copying the slots back), while the
 // later chunks are in flight.
+// A finished chunk's fields, written into the caller's slots from the sums
+// the kernel left in `res` (the values it stores), and its sums to h_out.
+void patch_tx_fields(const nsh::TxHostPlan& plan, const nsh::TxChunk& c, const uint16_t* res, uint8_t* h_arena,
+                     uint16_t* h_out) {
+  for (uint32_t j = c.p0; j < c.p0 + c.np; ++j) {
+    const nsh::TxPiece& q = plan.pieces[j];
+    const uint16_t* r = res + 2 * (q.out0 - c.out0);
+    uint8_t* s = h_arena + q.t.hdr_off;
+    for (uint64_t i = 0; i < q.nseg; ++i, s += q.t.slot) {
+      if (q.mode & nsk::kTxIp) put_be16(s + q.t.ip_at + 10u, ~r[2 * i] & 0xFFFFu);
+      if (q.mode & nsk::kTxTcpFull) put_be16(s + q.t.tcp_at + 16u, ~r[2 * i + 1] & 0xFFFFu);
+      if (q.mode & nsk::kTxTcpPartial) put_be16(s + q.t.tcp_at + 16u, r[2 * i + 1]);
+    }
+    if (h_out) std::memcpy(h_out + 2 * q.out0, r, 4 * q.nseg);
+  }
+}
+
+// Chunk c's geometry table for tcp_tx_multi over staging at device address
+// `base`, sums to `out`: calls[np] and first[np + 1], the launch shape; the
+// grid (0: too many tiles).
+uint32_t tx_chunk_table(const nsh::TxHostPlan& plan, const nsh::TxChunk& c, uint64_t base, uint16_t* out,
+                        std::vector<nsk::TxGeo>* calls, std::vector<uint32_t>* first, nsk::TxGeo* launch) {
+  calls->assign(c.np, nsk::TxGeo{});
+  for (uint32_t j = 0; j < c.np; ++j) {
+    const nsh::TxPiece& q = plan.pieces[c.p0 + j];
+    nsk::TxGeo& geo = (*calls)[j];
+    geo.hdr = base + plan.map(c, q.t.hdr_off);
+    // a payload only full-mode pieces read (and upload)
+    geo.pay = (q.mode & nsk::kTxTcpFull) ? base + plan.map(c, q.t.pay_off) : geo.hdr;
+    geo.size = q.t.size;
+    geo.n = q.nseg;
+    geo.mss = q.t.mss;
+    geo.slot = q.t.slot;
+    geo.ip_at = q.t.ip_at;
+    geo.ip_len = q.t.ip_len;
+    geo.tcp_at = q.t.tcp_at;
+    geo.tcp_len = q.t.tcp_len;
+    geo.addr_sum = q.t.addr_sum;
+    geo.proto = q.t.protocol;
+    geo.mode = q.mode | nsk::kTxFieldsOnly;
+    geo.out = out + 2 * (q.out0 - c.out0);
+  }
+  first->assign(c.np + 1, 0);
+  *launch = nsk::TxGeo{};
+  return nsk::tx_multi_prepare(calls->data(), c.np, launch, first->data());
+}
+
+// Host TX calls whose bytes and table fit kTxSmallBytes take no DMA: the
+// ranges and the table are written through the BAR into a leased gather
+// stage (fine-grained VRAM on large-BAR parts), one launch reads them there
+// and writes its sums to mapped memory, then one wait, as the small checksum
+// calls do.  Above that size the DMA pipeline's ~55 GB/s beats the BAR's ~23.
+constexpr uint64_t kTxSmallBytes = 1ull << 20;
+
+// Completes a small host-path launch on stream s (pmu held): a one-wave
+// kernel behind it stores this call's sequence number into coherent host
+// memory and the caller spins on that word, as the zero-copy passes do (the
+// stream's own completion arrives some microseconds later).
+// Past 2 ms it waits on the stream, which also reports a failed kernel.
+int wait_small(ns_csum_ctx* ctx, hipStream_t s) {
+  int rc;
+  if (ctx->p_done.cap == 0) {  // zeroed once: no stale word may equal a sequence number
+    if ((rc = ctx->p_done.ensure(64)) != NS_OK) return rc;
+    __atomic_store_n(reinterpret_cast<uint32_t*>(ctx->p_done.p), 0u, __ATOMIC_RELEASE);
+  }
+  uint32_t seq = ++ctx->p_seq;
+  if (seq == 0) seq = ++ctx->p_seq;
+  uint32_t* done = reinterpret_cast<uint32_t*>(ctx->p_done.p);
+  HIP_TRY(nsk::launch_signal(reinterpret_cast<uint32_t*>(ctx->p_done.dev), seq, s));
+  const auto t0 = std::chrono::steady_clock::now();
+  for (uint32_t spin = 0; __atomic_load_n(done, __ATOMIC_ACQUIRE) != seq; ++spin) {
+    if ((spin & 255u) == 255u && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) {
+      HIP_TRY(hipStreamSynchronize(s));
+      if (__atomic_load_n(done, __ATOMIC_ACQUIRE) != seq) return NS_EHIP;
+      break;
+    }
+  }
+  return NS_OK;
+}
+
+int run_tx_small(ns_csum_ctx* ctx, uint8_t* h_arena, const nsh::TxHostPlan& plan, uint16_t* h_out) {
+  const nsh::TxChunk& c = plan.chunks[0];
+  int rc = NS_OK;
+  if ((rc = ctx->p_res.ensure(4 * c.nout)) != NS_OK) return rc;
+  uint16_t* res = reinterpret_cast<uint16_t*>(ctx->p_res.p);
+  const uint64_t tab_at = (c.staging + 255) & ~255ull;
+  const size_t tab = ((size_t)c.np * sizeof(nsk::TxGeo) + 15) & ~(size_t)15;
+  const uint64_t need = tab_at + tab + ((size_t)c.np + 1) * sizeof(uint32_t);
+  BarBuf* st = lease_gather_stage(ctx, &rc, need);
+  if (!st) return rc;
+  for (uint32_t j = c.r0; j < c.r0 + c.nr; ++j) {
+    const nsh::TxRange& r = plan.ranges[j];
+    std::memcpy(st->p + r.at, h_arena + r.lo, r.hi - r.lo);
+  }
+  std::vector<nsk::TxGeo> calls;
+  std::vector<uint32_t> first;
+  nsk::TxGeo launch{};
+  const uint32_t grid = tx_chunk_table(plan, c, (uint64_t)(uintptr_t)st->dev,
+                                       reinterpret_cast<uint16_t*>(ctx->p_res.dev), &calls, &first, &launch);
+  if (grid == 0) {
+    return_gather_stage(ctx, st);
+    return NS_EINVAL;
+  }
+  // written once, never read back (the stage may be VRAM behind the BAR)
+  std::memcpy(st->p + tab_at, calls.data(), (size_t)c.np * sizeof(nsk::TxGeo));
+  std::memcpy(st->p + tab_at + tab, first.data(), first.size() * sizeof(uint32_t));
+  __builtin_ia32_sfence();  // drain the write-combined BAR stores before the launch
+  hipStream_t s = ctx->stream[0];
+  const hipError_t e = nsk::launch_tcp_tx_multi(launch, grid, reinterpret_cast<const nsk::TxGeo*>(st->dev + tab_at),
+                                                reinterpret_cast<const uint32_t*>(st->dev + tab_at + tab), c.np, s);
+  rc = e == hipSuccess ? wait_small(ctx, s) : report_hip(e, "run_tx_small", __FILE__, __LINE__);
+  return_gather_stage(ctx, st);
+  if (rc != NS_OK) return rc;
+  patch_tx_fields(plan, c, res, h_arena, h_out);
+  return NS_OK;
+}
+
 int run_tx_host(ns_csum_ctx* ctx, uint8_t* h_arena, const nsh::TxHostPlan& plan, uint16_t* h_out) {
+  if (plan.chunks.size() == 1 && zero_copy_enabled()) {
+    // (within the context's staging budget too: a context created with a
+    // small budget sends everything through the pipeline)
+    const nsh::TxChunk& c = plan.chunks[0];
+    const uint64_t tab = ((uint64_t)c.np * sizeof(nsk::TxGeo) + 15) & ~15ull;
+    const uint64_t need = ((c.staging + 255) & ~255ull) + tab + 4ull * (c.np + 1);
+    if (need <= std::min<uint64_t>(kTxSmallBytes, ctx->staging)) return run_tx_small(ctx, h_arena, plan, h_out);
+  }
   const uint32_t nslots = ctx->nslots;
   int64_t pend[kMaxHostSlots];
   std::fill(pend, pend + kMaxHostSlots, (int64_t)-1);
@@ -845,18 +975,7 @@ int run_tx_host(ns_csum_ctx* ctx, uint8_t* h_arena, const nsh::TxHostPlan& plan,
     const nsh::TxChunk& c = plan.chunks[(size_t)pend[sl]];
     pend[sl] = -1;
     HIP_TRY(hipEventSynchronize(ctx->done[sl]));
-    const uint16_t* res = ctx->h_out[sl].p;
-    for (uint32_t j = c.p0; j < c.p0 + c.np; ++j) {
-      const nsh::TxPiece& q = plan.pieces[j];
-      const uint16_t* r = res + 2 * (q.out0 - c.out0);
-      uint8_t* s = h_arena + q.t.hdr_off;
-      for (uint64_t i = 0; i < q.nseg; ++i, s += q.t.slot) {
-        if (q.mode & nsk::kTxIp) put_be16(s + q.t.ip_at + 10u, ~r[2 * i] & 0xFFFFu);
-        if (q.mode & nsk::kTxTcpFull) put_be16(s + q.t.tcp_at + 16u, ~r[2 * i + 1] & 0xFFFFu);
-        if (q.mode & nsk::kTxTcpPartial) put_be16(s + q.t.tcp_at + 16u, r[2 * i + 1]);
-      }
-      if (h_out) std::memcpy(h_out + 2 * q.out0, r, 4 * q.nseg);
-    }
+    patch_tx_fields(plan, c, ctx->h_out[sl].p, h_arena, h_out);
     return NS_OK;
   };
   std::vector<nsk::TxGeo> calls;
@@ -865,30 +984,9 @@ int run_tx_host(ns_csum_ctx* ctx, uint8_t* h_arena, const nsh::TxHostPlan& plan,
     int rc;
     if ((rc = ctx->d_arena[sl].ensure(c.staging + 256)) != NS_OK) return rc;
     if ((rc = ctx->h_out[sl].ensure(2 * c.nout)) != NS_OK) return rc;
-    const uint64_t base = (uint64_t)(uintptr_t)ctx->d_arena[sl].p;
-    calls.assign(c.np, nsk::TxGeo{});
-    for (uint32_t j = 0; j < c.np; ++j) {
-      const nsh::TxPiece& q = plan.pieces[c.p0 + j];
-      nsk::TxGeo& geo = calls[j];
-      geo.hdr = base + plan.map(c, q.t.hdr_off);
-      // a payload only full-mode pieces read (and upload)
-      geo.pay = (q.mode & nsk::kTxTcpFull) ? base + plan.map(c, q.t.pay_off) : geo.hdr;
-      geo.size = q.t.size;
-      geo.n = q.nseg;
-      geo.mss = q.t.mss;
-      geo.slot = q.t.slot;
-      geo.ip_at = q.t.ip_at;
-      geo.ip_len = q.t.ip_len;
-      geo.tcp_at = q.t.tcp_at;
-      geo.tcp_len = q.t.tcp_len;
-      geo.addr_sum = q.t.addr_sum;
-      geo.proto = q.t.protocol;
-      geo.mode = q.mode | nsk::kTxFieldsOnly;
-      geo.out = ctx->h_out[sl].dev + 2 * (q.out0 - c.out0);
-    }
-    first.assign(c.np + 1, 0);
     nsk::TxGeo launch{};
-    const uint32_t grid = nsk::tx_multi_prepare(calls.data(), c.np, &launch, first.data());
+    const uint32_t grid = tx_chunk_table(plan, c, (uint64_t)(uintptr_t)ctx->d_arena[sl].p, ctx->h_out[sl].dev,
+                                         &calls, &first, &launch);
     if (grid == 0) return NS_EINVAL;  // more than 2^31 tiles
     const size_t tab = ((size_t)c.np * sizeof(nsk::TxGeo) + 15) & ~(size_t)15;
     const size_t bytes = tab + first.size() * sizeof(uint32_t);
@@ -934,8 +1032,46 @@ int run_tx_host(ns_csum_ctx* ctx, uint8_t* h_arena, const nsh::TxHostPlan& plan,
 // parses and verifies them there and writes verdicts and sums straight to
 // mapped pinned memory; when the chunk is done they are copied to the
 // caller's arrays while later chunks are in flight.  No host planning.
+// A small ring (its slots and lengths within kTxSmallBytes and the staging
+// budget) takes no DMA either: written through the BAR into a gather stage,
+// one launch, one wait.
+int run_rx_small(ns_csum_ctx* ctx, const uint8_t* h_arena, const ns_rx_ring& r, const uint32_t* h_len,
+                 uint16_t* h_sums, uint8_t* h_verdict) {
+  const uint64_t bytes = (uint64_t)r.n * r.stride, len_at = (bytes + 255) & ~255ull;
+  int rc = NS_OK;
+  // results: the sums, then the verdicts
+  if ((rc = ctx->p_res.ensure(5 * (size_t)r.n)) != NS_OK) return rc;
+  BarBuf* st = lease_gather_stage(ctx, &rc, len_at + 4ull * r.n);
+  if (!st) return rc;
+  std::memcpy(st->p, h_arena + r.ring_off, bytes);
+  std::memcpy(st->p + len_at, h_len, 4 * (size_t)r.n);
+  __builtin_ia32_sfence();  // drain the write-combined BAR stores before the launch
+  nsk::RxGeo geo{};
+  geo.ring = (uint64_t)(uintptr_t)st->dev;
+  geo.stride = r.stride;
+  geo.len = reinterpret_cast<const uint32_t*>(st->dev + len_at);
+  geo.sums = reinterpret_cast<uint16_t*>(ctx->p_res.dev);
+  geo.verdict = ctx->p_res.dev + 4 * (size_t)r.n;
+  geo.err = ctx->d_err;
+  geo.n = r.n;
+  geo.frame_at = r.frame_at;
+  geo.link = r.link_hdr;
+  geo.view0 = r.first_view ? r.first_view - r.link_hdr : 0u;
+  hipStream_t s = ctx->stream[0];
+  const hipError_t e = nsk::launch_rx_ring(geo, s);
+  rc = e == hipSuccess ? wait_small(ctx, s) : report_hip(e, "run_rx_small", __FILE__, __LINE__);
+  return_gather_stage(ctx, st);
+  if (rc != NS_OK) return rc;
+  if (h_sums) std::memcpy(h_sums, ctx->p_res.p, 4 * (size_t)r.n);
+  if (h_verdict) std::memcpy(h_verdict, ctx->p_res.p + 4 * (size_t)r.n, r.n);
+  return NS_OK;
+}
+
 int run_rx_host(ns_csum_ctx* ctx, const uint8_t* h_arena, const ns_rx_ring& r, const uint32_t* h_len,
                 uint16_t* h_sums, uint8_t* h_verdict) {
+  const uint64_t small = (((uint64_t)r.n * r.stride + 255) & ~255ull) + 4ull * r.n;
+  if (zero_copy_enabled() && small <= std::min<uint64_t>(kTxSmallBytes, ctx->staging))
+    return run_rx_small(ctx, h_arena, r, h_len, h_sums, h_verdict);
   const uint32_t nslots = ctx->nslots;
   const uint32_t per = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(1, ctx->staging / r.stride), 1u << 24);
   struct Pending {
@@ -1345,6 +1481,10 @@ void ns_csum_destroy(ns_csum_ctx* ctx) {
       ctx->d_txtab[s].release();
       ctx->d_len[s].release();
       ctx->h_verd[s].release();
+      if (s == 0) {
+        ctx->p_res.release();
+        ctx->p_done.release();
+      }
       if (ctx->done[s]) (void)hipEventDestroy(ctx->done[s]);
       if (ctx->stream[s]) (void)hipStreamDestroy(ctx->stream[s]);
     }

@@ -4,9 +4,9 @@ and verified on the device with no host planning.  Every slot's verdict and
 sums against oracle/packets.py verify_frame (the CPU restatement of the
 receive dispatch, HandlePacket/IsValid and segment.parse) and against
 ns_csum_rx_ring over a device copy of the same ring: link headers, first
-views, padded frames, unaligned ring offsets, a staging budget of a few
-slots (chunks cycling through the four pipeline slots), outputs one at a
-time, and the error paths."""
+views, padded frames, unaligned ring offsets, small rings (written through
+the BAR, no DMA), a staging budget of a few slots (chunks cycling through the
+four pipeline slots), outputs one at a time, and the error paths."""
 
 import ctypes
 
@@ -37,6 +37,20 @@ def test_host_ring_matches_oracle_and_device(engine, link_hdr, first_view, frame
     dv, ds = _run(engine, arena, ln, ring)
     assert np.array_equal(verdict, dv) and np.array_equal(sums, ds)
     assert {0, 1, 2, 3} <= set(verdict.tolist())
+
+
+@pytest.mark.parametrize("n", [1, 8, 200])
+def test_small_ring_through_a_bar_stage(engine, n):
+    """Rings of up to ~1 MiB go through a gather stage written through the
+    BAR (no DMA): the same verdicts and sums as the oracle and the device
+    ring."""
+    rng = np.random.default_rng(5600 + n)
+    _, frames = _frames(rng, n, 14, max_payload=1400)
+    arena, ln = _ring(frames, 1504, ring_off=5)
+    ring = dict(ring_off=5, stride=1504, n=n, link_hdr=14, first_view=128)
+    verdict, sums = engine.rx_ring_host(arena, ring, ln)
+    wv, ws = _want(arena, ln, ring)
+    assert np.array_equal(verdict, wv) and np.array_equal(sums, ws)
 
 
 @pytest.mark.parametrize("ring_off", [0, 3, 1000])
