@@ -52,7 +52,7 @@ def parse():
                     help="BASELINE.json configs[k-1]; 7 = device-resident RX verification, "
                          "8 = device-resident TX checksum fill (SURVEY §8(f) ranks 2 and 1)")
     ap.add_argument("--mode", default="dev", choices=("dev", "host"))
-    ap.add_argument("--rx-layout", default="fused", choices=("fused", "chained", "ring"),
+    ap.add_argument("--rx-layout", default="fused", choices=("fused", "chained", "ring", "bufs"),
                     help="--config 7 (and 8 with --tx-layout wire) descriptor table: 2 independent descriptors "
                          "per packet, or 3 chained; --config 7 ring: no table, a receive ring parsed and verified "
                          "on the device (ns_csum_rx_ring)")
@@ -60,6 +60,8 @@ def parse():
                     help="--config 8 packets: as sendTCPBatch builds them (header slots + payload view) "
                          "filled from the batch geometry by ns_csum_tcp_tx (struct) or through an "
                          "NS_BATCH_PAIRED descriptor table (split), or wire-contiguous like config 7")
+    ap.add_argument("--bufs-order", default="shuffled", choices=("shuffled", "ring"),
+                    help="--rx-layout bufs: buffers handed over in shuffled order, or in ring order")
     ap.add_argument("--tx-calls", type=int, default=1,
                     help="--mode host --config 8: the 1M segments as this many sendTCPBatch calls in one "
                          "ns_csum_tcp_tx_host (23832: one per 64 KiB GSO write)")
@@ -477,7 +479,7 @@ def main():
     cfg = args.config
     if cfg == 8 and args.mode == "host":
         return tx_host_mode(args, dist, eng, dev)
-    if cfg == 7 and args.mode == "host" and args.rx_layout != "ring":
+    if cfg == 7 and args.mode == "host" and args.rx_layout != "ring":  # (bufs: device-resident only)
         raise SystemExit("--mode host --config 7 takes --rx-layout ring (ns_csum_rx_ring_host)")
     if cfg in (7, 8):
         return packet_mode(args, dist, eng, dev, tx=cfg == 8)
@@ -677,7 +679,7 @@ def packet_mode(args, dist, eng, dev, tx: bool):
     from netstack_amd import workloads as W
 
     seed = 7000 + dist.rank
-    if not tx and args.rx_layout == "ring":
+    if not tx and args.rx_layout in ("ring", "bufs"):
         return ring_host_mode(args, dist, eng, dev, seed) if args.mode == "host" else \
             ring_mode(args, dist, eng, dev, seed)
     struct = tx and args.tx_layout == "struct"
@@ -966,6 +968,17 @@ def ring_mode(args, dist, eng, dev, seed):
     # in the MALL)
     rings = [arena, W.rx_ring_batch(RX_N, seed, dev, corrupt_every=1000)[0]]
     ring = dict(stride=W.RX_STRIDE, n=RX_N)
+    bufs = args.rx_layout == "bufs"
+    if bufs:
+        # `--rx-layout bufs` (ns_csum_rx_bufs): the same buffers handed over in
+        # a shuffled order, as a NIC's buffer pool returns them: packet k is
+        # the frame in slot perm[k], found through an offset table
+        perm = np.random.default_rng(seed).permutation(RX_N) if args.bufs_order == "shuffled" else np.arange(RX_N)
+        offs = torch.from_numpy((perm.astype(np.int64) * W.RX_STRIDE).astype(np.int32)).to(dev)
+        lens = lens[torch.from_numpy(perm).to(dev)].contiguous()
+        inv = np.empty(RX_N, dtype=np.int64)
+        inv[perm] = np.arange(RX_N)
+        bad_idx = np.sort(inv[bad_idx])
     verdict = torch.empty(RX_N, dtype=torch.uint8, device=dev)
     sums = torch.empty(2 * RX_N, dtype=torch.int16, device=dev)
     stream = torch.cuda.current_stream(dev)
@@ -976,7 +989,10 @@ def ring_mode(args, dist, eng, dev, seed):
         k = state["i"]
         if k == args.warmup:
             ev[0].record(stream)
-        eng.rx_ring(rings[k % 2], ring, lens, sums=sums, verdict=verdict, stream=stream)
+        if bufs:
+            eng.rx_bufs(rings[k % 2], ring, offs, lens, sums=sums, verdict=verdict, stream=stream)
+        else:
+            eng.rx_ring(rings[k % 2], ring, lens, sums=sums, verdict=verdict, stream=stream)
         state["i"] = k + 1
         if state["i"] == args.warmup + args.steps:
             ev[1].record(stream)
@@ -994,30 +1010,35 @@ def ring_mode(args, dist, eng, dev, seed):
     fails = dist.sum(0.0 if prop_ok else 1.0, dev)
     pkt_bytes = RX_N * W.RX_PKT
     total = dist.sum(float(pkt_bytes), dev)
-    # per slot: the packet's bytes and its u32 length read; its verdict (1 B)
-    # and its two u16 sums written
-    algo = pkt_bytes + RX_N * (4 + 1 + 4)
+    # per slot: the packet's bytes and its u32 length read (bufs: and its u32
+    # offset); its verdict (1 B) and its two u16 sums written
+    algo = pkt_bytes + RX_N * (4 + 1 + 4 + (4 if bufs else 0))
     achieved = algo / kern_avg_s / 1e9
-    traffic, traffic_src = pmc_traffic(args.pmc_json, "7ring")
+    traffic, traffic_src = pmc_traffic(args.pmc_json, "7bufs" if bufs else "7ring")
     result = {
         "metric": "RX checksum verification GiB/s device-resident (IPv4 + TCP, 1500-B packets)",
         "value": total * args.steps / wall / GIB, "unit": "GiB/s", "n_gpus": dist.world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": wall / args.steps * 1e3,
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
         "data": "synthetic received packets (valid IPv4/TCP checksums, 1 in 1000 corrupted), resident in HBM",
-        "config": {"workload": "rx ring: 1,048,576 x 1500-B IPv4/TCP packets per GPU in 1504-B slots, parsed and "
-                               "verified on the device from the slots' lengths (ns_csum_rx_ring, no table)",
+        "config": {"workload": (f"rx buffer list: 1,048,576 x 1500-B IPv4/TCP packets per GPU in 1504-B buffers "
+                                f"handed over in {args.bufs_order} order through an offset table, parsed and verified "
+                                "on the device (ns_csum_rx_bufs)" if bufs else
+                                "rx ring: 1,048,576 x 1500-B IPv4/TCP packets per GPU in 1504-B slots, parsed and "
+                                "verified on the device from the slots' lengths (ns_csum_rx_ring, no table)"),
                    "packets_per_gpu": RX_N, "descriptors_per_gpu": 0, "rotating_batches": 2},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
-                     "kernel": "nsk::rx_ring<13>", "layout": "ring (1504-B slots, u32 lengths)",
+                     "kernel": "nsk::rx_ring<13,0,2,4,1,1,0,1>" if bufs else "nsk::rx_ring<13>",
+                     "layout": "buffer list (shuffled 1504-B buffers, u32 offsets and lengths)" if bufs
+                     else "ring (1504-B slots, u32 lengths)",
                      "algorithmic_bytes_per_launch": algo, "avg_launch_us": kern_avg_s * 1e6},
         "bad_descriptors": bad,
         "property_check": {"ipv4_all_valid": ip_ok, "tcp_failures": int(tcp_fail.size),
                            "expected_failures": int(bad_idx.size), "verdicts_as_expected": bool((v == want).all()),
                            "ok": prop_ok, "ranks_failed": int(fails)},
     }
-    if dist.rank == 0 and not args.no_cpu:
+    if dist.rank == 0 and not args.no_cpu and not bufs:
         import oracle as O
 
         k = 65536

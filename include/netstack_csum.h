@@ -74,7 +74,7 @@ extern "C" {
                                   7: ns_csum_tcp_tx_multi;
                                   8: ns_csum_rx_ring, ns_csum_set_tx_tuning;
                                   9: ns_csum_tcp_tx_host, _host_multi,
-                                     ns_csum_rx_ring_host */
+                                     ns_csum_rx_ring_host, ns_csum_rx_bufs */
 
 /* ---- status codes ------------------------------------------------------- */
 #define NS_OK 0
@@ -456,6 +456,18 @@ typedef struct ns_rx_ring {
 int ns_csum_rx_ring(ns_csum_ctx* ctx, const uint8_t* d_arena, uint64_t arena_bytes,
                     const ns_rx_ring* ring, const uint32_t* d_len, uint16_t* d_sums,
                     uint8_t* d_verdict, void* stream);
+/* The same checks over buffers at per-packet offsets in one device arena
+ * (a NIC's buffer pool, not a fixed-stride ring): packet k's frame is in the
+ * buffer at d_arena + ring->ring_off + d_off[k] (16-B aligned) of
+ * ring->stride bytes (the buffers' capacity, a multiple of 16), with d_len[k]
+ * bytes received; the other ns_rx_ring fields as above (n, frame_at,
+ * link_hdr, first_view).  arena_bytes - ring_off must be below 4 GiB - 512
+ * (32-bit offsets).  A buffer not 16-B aligned or not inside the arena gets
+ * NS_PKB_MALFORMED and sums 0, and is counted by ns_csum_sync.  Asynchronous
+ * on `stream`.                                                              */
+int ns_csum_rx_bufs(ns_csum_ctx* ctx, const uint8_t* d_arena, uint64_t arena_bytes,
+                    const ns_rx_ring* ring, const uint32_t* d_off, const uint32_t* d_len,
+                    uint16_t* d_sums, uint8_t* d_verdict, void* stream);
 /* The same ring in HOST memory (recvmmsg's buffers as the link endpoint
  * fills them): h_arena, h_len, h_sums and h_verdict are host pointers, the
  * ring's own alignment is free (ring_off need not be 16-B aligned; the stride

@@ -45,7 +45,7 @@ EXPORTED = (
     "ns_csum_stage_acquire", "ns_csum_stage_release", "ns_csum_packet_buffers",
     "ns_csum_stream_release", "ns_csum_scratch_count", "ns_csum_get_stats", "ns_csum_tcp_tx",
     "ns_csum_tcp_tx_multi", "ns_csum_rx_ring", "ns_csum_set_tx_tuning", "ns_csum_tcp_tx_host",
-    "ns_csum_tcp_tx_host_multi", "ns_csum_rx_ring_host",
+    "ns_csum_tcp_tx_host_multi", "ns_csum_rx_ring_host", "ns_csum_rx_bufs",
 )
 NS_PIECE_RESTART = 0x1
 NS_PIECE_END = 0x2
@@ -179,6 +179,7 @@ def _declare(lib):
         "ns_csum_tcp_tx_multi": (c.c_int, [vp, u8p, c.c_uint64, c.POINTER(NsTcpTx), c.c_uint32, vp, vp]),
         "ns_csum_rx_ring": (c.c_int, [vp, u8p, c.c_uint64, c.POINTER(NsRxRing), vp, vp, vp, vp]),
         "ns_csum_rx_ring_host": (c.c_int, [vp, u8p, c.c_uint64, c.POINTER(NsRxRing), vp, vp, vp]),
+        "ns_csum_rx_bufs": (c.c_int, [vp, u8p, c.c_uint64, c.POINTER(NsRxRing), vp, vp, vp, vp, vp]),
         "ns_csum_set_tx_tuning": (c.c_int, [vp, c.c_uint32, c.c_uint32, c.c_uint32, c.c_uint32]),
         "ns_csum_tcp_tx_host": (c.c_int, [vp, u8p, c.c_uint64, c.POINTER(NsTcpTx), c.c_uint32, vp]),
         "ns_csum_tcp_tx_host_multi": (c.c_int, [c.POINTER(vp), c.c_uint32, u8p, c.c_uint64, c.POINTER(NsTcpTx),

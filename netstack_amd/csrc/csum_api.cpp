@@ -1830,6 +1830,40 @@ int ns_csum_rx_ring(ns_csum_ctx* ctx, const uint8_t* d_arena, uint64_t arena_byt
   return NS_OK;
 }
 
+int ns_csum_rx_bufs(ns_csum_ctx* ctx, const uint8_t* d_arena, uint64_t arena_bytes, const ns_rx_ring* ring,
+                    const uint32_t* d_off, const uint32_t* d_len, uint16_t* d_sums, uint8_t* d_verdict, void* stream) {
+  if (!ctx || !ring || (arena_bytes && !d_arena) || (!d_sums && !d_verdict)) return NS_EINVAL;
+  const ns_rx_ring& r = *ring;
+  if (r.n && (!d_len || !d_off)) return NS_EINVAL;
+  const uint64_t base = (uint64_t)(uintptr_t)d_arena;
+  if (r.ring_off > arena_bytes) return NS_ERANGE;
+  // the ring's shape rules with no slots to place (the buffers are wherever
+  // the offsets say; the kernel checks each against the arena)
+  ns_rx_ring r0 = r;
+  r0.n = 0;
+  const int vr = nsh::rx_plan(r0, base, arena_bytes);
+  if (vr != NS_OK) return vr;
+  const uint64_t limit = arena_bytes - r.ring_off;
+  if (limit > (1ull << 32) - 512) return NS_EINVAL;  // 32-bit offsets under one buffer resource
+  if (r.n == 0) return NS_OK;
+  DeviceGuard g(ctx->device);
+  nsk::RxGeo geo{};
+  geo.ring = base + r.ring_off;
+  geo.stride = r.stride;
+  geo.len = d_len;
+  geo.sums = d_sums;
+  geo.verdict = d_verdict;
+  geo.err = ctx->d_err;
+  geo.n = r.n;
+  geo.frame_at = r.frame_at;
+  geo.link = r.link_hdr;
+  geo.view0 = r.first_view ? r.first_view - r.link_hdr : 0u;
+  geo.off = d_off;
+  geo.limit = limit;
+  HIP_TRY(nsk::launch_rx_ring(geo, (hipStream_t)stream));
+  return NS_OK;
+}
+
 int ns_csum_rx_ring_host(ns_csum_ctx* ctx, const uint8_t* h_arena, uint64_t arena_bytes, const ns_rx_ring* ring,
                          const uint32_t* h_len, uint16_t* h_sums, uint8_t* h_verdict) {
   if (!ctx || !ring || (arena_bytes && !h_arena) || (!h_sums && !h_verdict)) return NS_EINVAL;

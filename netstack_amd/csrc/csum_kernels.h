@@ -152,6 +152,11 @@ struct RxGeo {
   uint32_t frame_at;  // bytes before the link frame in a slot (a virtio-net header)
   uint32_t link;      // 0: the frame is the IP packet; 14: Ethernet
   uint32_t view0;     // the IP packet's first view (BufConfig[0] - link), 0: one view
+  // A buffer list instead of a ring (ns_csum_rx_bufs): packet s in the buffer
+  // at ring + off[s] (16-B aligned) of `stride` bytes, inside `limit` bytes
+  // from `ring` (< 4 GiB); nullptr: the ring's slots.
+  const uint32_t* off;
+  uint64_t limit;
 };
 hipError_t launch_rx_ring(const RxGeo& g, hipStream_t stream);
 

@@ -26,6 +26,9 @@
 //            header/icmpv6.go:202-221).
 // oracle/packets.py (verify, verify_frame) restates the same rules on the CPU.
 //
+// A buffer list (ns_csum_rx_bufs, LIST = 1) is the same parse over buffers at
+// per-packet offsets in one arena (a NIC's buffer pool) instead of slots.
+//
 // Shape.  A wave owns 8 consecutive slots, one 8-lane group per packet.  The
 // group's instruction k reads the packet's k-th 128-B HBM line whole (lane i:
 // 16 B at line + 16 i), so every load instruction reads exactly one line per
@@ -128,7 +131,10 @@ __device__ __forceinline__ uint4 rx_load(__amdgpu_buffer_rsrc_t r, uint32_t off)
 // line 1 re-reads those lines with the range check.  F = 0: every chunk
 // range-checked.  The product runs <NB, 0, 2, 4, 1, 1>;
 // tools/rx_ring_variants.hip times the others.
-template <int NB, int A0 = 0, int AN = 2, int WV = kWaves, int OCC = 1, int F = 1, int SPEC = 0>
+// LIST = 1: a buffer list (g.off): packet s's buffer at g.ring + g.off[s]; one
+// buffer resource over the whole arena (< 4 GiB, 32-bit offsets).  A buffer
+// that is misaligned or not inside the arena is malformed and counted.
+template <int NB, int A0 = 0, int AN = 2, int WV = kWaves, int OCC = 1, int F = 1, int SPEC = 0, int LIST = 0>
 __global__ __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(OCC))) void rx_ring(RxGeo g) {
   __shared__ uint4 rx_lds[WV * kPerWave * kRowBytes / 16];
   const uint32_t lane = threadIdx.x & 63u, grp = lane >> 3, li = lane & 7u;
@@ -142,15 +148,28 @@ __global__ __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(OCC))) 
   // net header) and the link header.  A slot longer than the ring's stride is
   // malformed and counted (ns_csum_sync), a frame of no more than its link
   // header is dropped by the link (packet_dispatchers.go:268-270).
-  const uint32_t rlen = live ? g.len[s] : 0u;
+  uint32_t rlen = live ? g.len[s] : 0u;
   const uint32_t pre = g.frame_at + g.link;
-  const uint64_t slot = g.ring + s * g.stride;
-
-  // Wave-relative 32-bit coordinates: one buffer resource from the 128-B
-  // line of the wave's first packet over its slots (< 8 strides + a line).
-  const uint64_t wbase = (g.ring + s0 * g.stride + pre) & ~127ull;
-  const uint64_t s_end = s0 + kPerWave < g.n ? s0 + kPerWave : g.n;
-  const uint32_t nrec = (uint32_t)(g.ring + s_end * g.stride - wbase);
+  uint64_t slot;
+  uint64_t wbase;
+  uint32_t nrec;
+  bool bad = false;  // LIST: a buffer not 16-B aligned or not inside the arena
+  if constexpr (LIST) {
+    const uint32_t o = live ? g.off[s] : 0u;
+    bad = live && ((o & 15u) || (uint64_t)o + g.stride > g.limit);
+    if (bad) rlen = 0;  // parsed as an empty frame: malformed
+    slot = g.ring + (bad ? 0u : o);
+    // arena-relative 32-bit coordinates: one resource over the whole arena
+    wbase = g.ring & ~127ull;
+    nrec = (uint32_t)(g.ring + g.limit - wbase);
+  } else {
+    slot = g.ring + s * g.stride;
+    // Wave-relative 32-bit coordinates: one buffer resource from the 128-B
+    // line of the wave's first packet over its slots (< 8 strides + a line).
+    wbase = (g.ring + s0 * g.stride + pre) & ~127ull;
+    const uint64_t s_end = s0 + kPerWave < g.n ? s0 + kPerWave : g.n;
+    nrec = (uint32_t)(g.ring + s_end * g.stride - wbase);
+  }
   const __amdgpu_buffer_rsrc_t rsrc = rx_srd(wbase, nrec);
   const uint32_t pa = (uint32_t)(slot + pre - wbase);  // the IP packet's first byte
   const uint32_t po = pa & 15u;                         // its offset in its 16-B chunk (even)
@@ -362,7 +381,7 @@ __global__ __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(OCC))) 
       g.sums[2 * s] = (uint16_t)(v4 ? rx_class(rs) : 0u);
       g.sums[2 * s + 1] = (uint16_t)tr;
     }
-    if (over) atomicAdd(g.err, 1ull);
+    if (over || bad) atomicAdd(g.err, 1ull);
   }
 }
 
@@ -374,23 +393,28 @@ static int rx_batch_lines(const RxGeo& g) {
   return lines <= 2 ? 2 : lines <= 4 ? 4 : lines <= 8 ? 8 : lines <= 13 ? 13 : 16;
 }
 
-template <int NB, int A0 = 0, int AN = 2, int WV = kWaves, int OCC = 1, int F = 1, int SPEC = 0>
+template <int NB, int A0 = 0, int AN = 2, int WV = kWaves, int OCC = 1, int F = 1, int SPEC = 0, int LIST = 0>
 static hipError_t launch_rx_ring_t(const RxGeo& g, hipStream_t stream) {
   if (g.n == 0) return hipSuccess;
   const uint64_t per_wg = (uint64_t)WV * kPerWave;
-  hipLaunchKernelGGL((rx_ring<NB, A0, AN, WV, OCC, F, SPEC>), dim3((uint32_t)((g.n + per_wg - 1) / per_wg)), dim3(64 * WV), 0,
-                     stream, g);
+  hipLaunchKernelGGL((rx_ring<NB, A0, AN, WV, OCC, F, SPEC, LIST>), dim3((uint32_t)((g.n + per_wg - 1) / per_wg)),
+                     dim3(64 * WV), 0, stream, g);
   return hipGetLastError();
 }
 
-hipError_t launch_rx_ring(const RxGeo& g, hipStream_t stream) {
+template <int LIST>
+static hipError_t launch_rx_ring_l(const RxGeo& g, hipStream_t stream) {
   switch (rx_batch_lines(g)) {
-    case 2: return launch_rx_ring_t<2>(g, stream);
-    case 4: return launch_rx_ring_t<4>(g, stream);
-    case 8: return launch_rx_ring_t<8>(g, stream);
-    case 13: return launch_rx_ring_t<13>(g, stream);
-    default: return launch_rx_ring_t<16>(g, stream);
+    case 2: return launch_rx_ring_t<2, 0, 2, kWaves, 1, 1, 0, LIST>(g, stream);
+    case 4: return launch_rx_ring_t<4, 0, 2, kWaves, 1, 1, 0, LIST>(g, stream);
+    case 8: return launch_rx_ring_t<8, 0, 2, kWaves, 1, 1, 0, LIST>(g, stream);
+    case 13: return launch_rx_ring_t<13, 0, 2, kWaves, 1, 1, 0, LIST>(g, stream);
+    default: return launch_rx_ring_t<16, 0, 2, kWaves, 1, 1, 0, LIST>(g, stream);
   }
+}
+
+hipError_t launch_rx_ring(const RxGeo& g, hipStream_t stream) {
+  return g.off ? launch_rx_ring_l<1>(g, stream) : launch_rx_ring_l<0>(g, stream);
 }
 
 }  // namespace nsk

@@ -216,6 +216,37 @@ class Engine:
                                     getattr(stream, "cuda_stream", stream)), "ns_csum_rx_ring")
         return verdict, sums
 
+    def rx_bufs(self, arena, ring: dict, offs, lens, sums=None, verdict=None, stream=None):
+        """Verify received frames in buffers at per-packet offsets of a device
+        arena (ns_csum_rx_bufs): `ring` as for rx_ring with `stride` the
+        buffers' capacity; `offs` and `lens` uint32/int32 CUDA tensors of n
+        offsets (from ring_off, 16-B aligned) and received lengths.  Launches
+        on `stream` without synchronising; returns (verdict, sums)."""
+        import torch
+
+        n = int(ring["n"])
+        if not (arena.is_cuda and lens.is_cuda and offs.is_cuda):
+            raise ValueError("arena, offs and lens must be device tensors")
+        for t, what in ((lens, "lens"), (offs, "offs")):
+            if t.element_size() != 4 or t.numel() < n or not t.is_contiguous():
+                raise ValueError(f"{what} must be a contiguous tensor of n 32-bit values")
+        if verdict is None:
+            verdict = torch.empty(max(n, 1), dtype=torch.uint8, device=arena.device)
+        if sums is None:
+            sums = torch.empty(max(2 * n, 1), dtype=torch.int16, device=arena.device)
+        if not verdict.is_cuda or verdict.element_size() != 1 or verdict.numel() < n:
+            raise ValueError("verdict must be a device tensor of n bytes")
+        if not sums.is_cuda or sums.element_size() != 2 or sums.numel() < 2 * n:
+            raise ValueError("sums must be a device tensor of 2n 16-bit sums")
+        r = _lib.NsRxRing(int(ring.get("ring_off", 0)), int(ring["stride"]), n, int(ring.get("frame_at", 0)),
+                          int(ring.get("link_hdr", 0)), int(ring.get("first_view", 0)), int(ring.get("flags", 0)))
+        if stream is None:
+            stream = torch.cuda.current_stream(arena.device)
+        check(lib().ns_csum_rx_bufs(self._h, arena.data_ptr(), arena.numel() * arena.element_size(),
+                                    ctypes.byref(r), offs.data_ptr(), lens.data_ptr(), sums.data_ptr(),
+                                    verdict.data_ptr(), getattr(stream, "cuda_stream", stream)), "ns_csum_rx_bufs")
+        return verdict, sums
+
     def rx_ring_host(self, arena, ring: dict, lens):
         """Verify a receive ring in HOST memory (ns_csum_rx_ring_host):
         `arena` a contiguous uint8 numpy array, `ring` as for rx_ring, `lens`

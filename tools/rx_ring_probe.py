@@ -34,7 +34,7 @@ class RxGeo(ctypes.Structure):
     _fields_ = [("ring", ctypes.c_uint64), ("stride", ctypes.c_uint64), ("len", ctypes.c_void_p),
                 ("sums", ctypes.c_void_p), ("verdict", ctypes.c_void_p), ("err", ctypes.c_void_p),
                 ("n", ctypes.c_uint32), ("frame_at", ctypes.c_uint32), ("link", ctypes.c_uint32),
-                ("view0", ctypes.c_uint32)]
+                ("view0", ctypes.c_uint32), ("off", ctypes.c_void_p), ("limit", ctypes.c_uint64)]
 
 
 def main():
