@@ -796,6 +796,26 @@ func VerifyRingDevice(arena uintptr, arenaBytes uint64, r RxRing, lens, sums, ve
 	return nil
 }
 
+// VerifyBufsDevice is VerifyRingDevice over buffers at per-packet offsets
+// of one device arena (a GPU-attached NIC's buffer pool; ns_csum_rx_bufs):
+// packet k's frame is in the buffer at arena + r.RingOff + offs[k], of
+// r.Stride bytes (the buffers' capacity).  offs, lens, sums (or 0) and
+// verdict (or 0) are device addresses.  Errors as for VerifyRingDevice.
+func VerifyBufsDevice(arena uintptr, arenaBytes uint64, r RxRing, offs, lens, sums, verdict, stream uintptr) error {
+	ctx, rc := csumEngine()
+	if rc != C.NS_OK {
+		return engineFailed("ns_csum_init", rc)
+	}
+	cr := C.ns_rx_ring{ring_off: C.uint64_t(r.RingOff), stride: C.uint64_t(r.Stride), n: C.uint32_t(r.N),
+		frame_at: C.uint16_t(r.FrameAt), link_hdr: C.uint16_t(r.LinkHdr), first_view: C.uint32_t(r.FirstView)}
+	if rc := C.ns_csum_rx_bufs(ctx, (*C.uint8_t)(unsafe.Pointer(arena)), C.uint64_t(arenaBytes), &cr,
+		(*C.uint32_t)(unsafe.Pointer(offs)), (*C.uint32_t)(unsafe.Pointer(lens)), (*C.uint16_t)(unsafe.Pointer(sums)),
+		(*C.uint8_t)(unsafe.Pointer(verdict)), unsafe.Pointer(stream)); rc != C.NS_OK {
+		return engineFailed("ns_csum_rx_bufs", rc)
+	}
+	return nil
+}
+
 // VerifyRingHost is VerifyRingDevice for a ring in host memory: arena holds
 // r.N slots of r.Stride bytes from r.RingOff (recvmmsg's buffers laid out
 // at a fixed stride), lens their received lengths; verdict (or nil) and sums
