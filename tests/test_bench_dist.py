@@ -225,3 +225,27 @@ def test_cfg8_defaults_to_the_structured_tx_fill():
     pay, total = W.tx_split_layout(1 << 20)
     assert g["pay_off"] == pay and g["hdr_off"] + (1 << 20) * g["slot"] <= pay
     assert g["pay_off"] + g["size"] == total and g["tcp_at"] + g["tcp_len"] == g["slot"]
+
+
+@pytest.mark.parametrize("calls", [1, 7, 23832, 1 << 20])
+def test_tx_calls_tile_the_batch(calls):
+    """bench.py --mode host --config 8 --tx-calls K cuts cfg8's geometry into
+    K sendTCPBatch calls of consecutive segments: together they cover every
+    segment once, with sendTCPBatch's own segment lengths (connect.go:679-691),
+    and each call's slots and payload follow the previous call's."""
+    import bench
+    from netstack_amd import workloads as W
+
+    g = W.tx_struct_geometry(1 << 20)
+    parts = bench.tx_calls(g, calls)
+    n = -(-g["size"] // g["mss"])
+    segs = [-(-p["size"] // p["mss"]) for p in parts]
+    assert sum(segs) == n and len(parts) <= calls
+    assert sum(p["size"] for p in parts) == g["size"]
+    hdr, pay = g["hdr_off"], g["pay_off"]
+    for p, k in zip(parts, segs):
+        assert p["hdr_off"] == hdr and p["pay_off"] == pay
+        assert all(p[f] == g[f] for f in ("mss", "slot", "ip_at", "ip_len", "tcp_at", "tcp_len", "src", "dst"))
+        hdr += k * g["slot"]
+        pay += p["size"]
+    assert all(p["size"] % g["mss"] == 0 for p in parts[:-1])
