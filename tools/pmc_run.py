@@ -176,6 +176,17 @@ def rx_set(dev, L):
     torch.cuda.synchronize()
     print(f"LABEL cfg7ring algorithmic_bytes={n * (W.RX_PKT + 9)} payload={n * W.RX_PKT} arena={arena.numel()} "
           f"n={n} shape=calib2164", flush=True)
+    # the same frames through a buffer list (bench.py --rx-layout bufs), in
+    # ring order and shuffled: the offset table adds 4 B per packet
+    for order in ("ring", "shuffled"):
+        perm = np.random.default_rng(7000).permutation(n) if order == "shuffled" else np.arange(n)
+        offs = torch.from_numpy((perm.astype(np.int64) * W.RX_STRIDE).astype(np.int32)).to(dev)
+        ln = lens[torch.from_numpy(perm).to(dev)].contiguous()
+        for _ in range(REPS):
+            eng.rx_bufs(arena, dict(stride=W.RX_STRIDE, n=n), offs, ln, sums=sums, verdict=verdict)
+        torch.cuda.synchronize()
+        print(f"LABEL cfg7bufs_{order} algorithmic_bytes={n * (W.RX_PKT + 13)} payload={n * W.RX_PKT} "
+              f"arena={arena.numel()} n={n} shape=calib2164", flush=True)
 
 
 def cfg3probe_set(dev, L):
