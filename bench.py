@@ -62,6 +62,8 @@ def parse():
                          "NS_BATCH_PAIRED descriptor table (split), or wire-contiguous like config 7")
     ap.add_argument("--bufs-order", default="shuffled", choices=("shuffled", "ring"),
                     help="--rx-layout bufs: buffers handed over in shuffled order, or in ring order")
+    ap.add_argument("--bufs-stride", type=int, default=0,
+                    help="--rx-layout bufs: buffer spacing in the pool (a multiple of 16 >= 1504; 0: the ring's 1504)")
     ap.add_argument("--tx-calls", type=int, default=1,
                     help="--mode host --config 8: the 1M segments as this many sendTCPBatch calls in one "
                          "ns_csum_tcp_tx_host (23832: one per 64 KiB GSO write)")
@@ -967,14 +969,30 @@ def ring_mode(args, dist, eng, dev, seed):
     # cfg2's rotating batches: no launch re-reads what the one before it left
     # in the MALL)
     rings = [arena, W.rx_ring_batch(RX_N, seed, dev, corrupt_every=1000)[0]]
-    ring = dict(stride=W.RX_STRIDE, n=RX_N)
     bufs = args.rx_layout == "bufs"
+    stride = W.RX_STRIDE
+    if bufs and args.bufs_stride and args.bufs_stride != W.RX_STRIDE:
+        # the same slots spread to a wider spacing (a pool of line-aligned
+        # buffers when it is a multiple of 128): the frames do not move
+        # within their buffers
+        stride = args.bufs_stride
+        if stride % 16 or stride < W.RX_STRIDE:
+            raise SystemExit("--bufs-stride must be a multiple of 16 and at least 1504")
+
+        def spread(a):
+            b = torch.zeros(RX_N, stride, dtype=torch.uint8, device=dev)
+            b[:, :W.RX_STRIDE] = a.view(RX_N, W.RX_STRIDE)
+            return b.view(-1)
+
+        rings = [spread(r) for r in rings]
+        arena = rings[0]
+    ring = dict(stride=stride, n=RX_N)
     if bufs:
         # `--rx-layout bufs` (ns_csum_rx_bufs): the same buffers handed over in
         # a shuffled order, as a NIC's buffer pool returns them: packet k is
         # the frame in slot perm[k], found through an offset table
         perm = np.random.default_rng(seed).permutation(RX_N) if args.bufs_order == "shuffled" else np.arange(RX_N)
-        offs = torch.from_numpy((perm.astype(np.int64) * W.RX_STRIDE).astype(np.int32)).to(dev)
+        offs = torch.from_numpy((perm.astype(np.int64) * stride).astype(np.int32)).to(dev)
         lens = lens[torch.from_numpy(perm).to(dev)].contiguous()
         inv = np.empty(RX_N, dtype=np.int64)
         inv[perm] = np.arange(RX_N)
@@ -1021,9 +1039,9 @@ def ring_mode(args, dist, eng, dev, seed):
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": wall / args.steps * 1e3,
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
         "data": "synthetic received packets (valid IPv4/TCP checksums, 1 in 1000 corrupted), resident in HBM",
-        "config": {"workload": (f"rx buffer list: 1,048,576 x 1500-B IPv4/TCP packets per GPU in 1504-B buffers "
-                                f"handed over in {args.bufs_order} order through an offset table, parsed and verified "
-                                "on the device (ns_csum_rx_bufs)" if bufs else
+        "config": {"workload": (f"rx buffer list: 1,048,576 x 1500-B IPv4/TCP packets per GPU in buffers spaced "
+                                f"{stride} B apart, handed over in {args.bufs_order} order through an offset table, "
+                                "parsed and verified on the device (ns_csum_rx_bufs)" if bufs else
                                 "rx ring: 1,048,576 x 1500-B IPv4/TCP packets per GPU in 1504-B slots, parsed and "
                                 "verified on the device from the slots' lengths (ns_csum_rx_ring, no table)"),
                    "packets_per_gpu": RX_N, "descriptors_per_gpu": 0, "rotating_batches": 2},
