@@ -63,7 +63,7 @@ def parse():
     ap.add_argument("--bufs-order", default="shuffled", choices=("shuffled", "ring"),
                     help="--rx-layout bufs: buffers handed over in shuffled order, or in ring order")
     ap.add_argument("--bufs-stride", type=int, default=0,
-                    help="--rx-layout bufs: buffer spacing in the pool (a multiple of 16 >= 1504; 0: the ring's 1504)")
+                    help="--rx-layout ring / bufs: slot or buffer spacing (a multiple of 16 >= 1504; 0: 1504)")
     ap.add_argument("--tx-calls", type=int, default=1,
                     help="--mode host --config 8: the 1M segments as this many sendTCPBatch calls in one "
                          "ns_csum_tcp_tx_host (23832: one per 64 KiB GSO write)")
@@ -971,7 +971,7 @@ def ring_mode(args, dist, eng, dev, seed):
     rings = [arena, W.rx_ring_batch(RX_N, seed, dev, corrupt_every=1000)[0]]
     bufs = args.rx_layout == "bufs"
     stride = W.RX_STRIDE
-    if bufs and args.bufs_stride and args.bufs_stride != W.RX_STRIDE:
+    if args.bufs_stride and args.bufs_stride != W.RX_STRIDE:
         # the same slots spread to a wider spacing (a pool of line-aligned
         # buffers when it is a multiple of 128): the frames do not move
         # within their buffers
@@ -1042,8 +1042,8 @@ def ring_mode(args, dist, eng, dev, seed):
         "config": {"workload": (f"rx buffer list: 1,048,576 x 1500-B IPv4/TCP packets per GPU in buffers spaced "
                                 f"{stride} B apart, handed over in {args.bufs_order} order through an offset table, "
                                 "parsed and verified on the device (ns_csum_rx_bufs)" if bufs else
-                                "rx ring: 1,048,576 x 1500-B IPv4/TCP packets per GPU in 1504-B slots, parsed and "
-                                "verified on the device from the slots' lengths (ns_csum_rx_ring, no table)"),
+                                f"rx ring: 1,048,576 x 1500-B IPv4/TCP packets per GPU in {stride}-B slots, parsed "
+                                "and verified on the device from the slots' lengths (ns_csum_rx_ring, no table)"),
                    "packets_per_gpu": RX_N, "descriptors_per_gpu": 0, "rotating_batches": 2},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
@@ -1056,7 +1056,7 @@ def ring_mode(args, dist, eng, dev, seed):
                            "expected_failures": int(bad_idx.size), "verdicts_as_expected": bool((v == want).all()),
                            "ok": prop_ok, "ranks_failed": int(fails)},
     }
-    if dist.rank == 0 and not args.no_cpu and not bufs:
+    if dist.rank == 0 and not args.no_cpu and not bufs and stride == W.RX_STRIDE:
         import oracle as O
 
         k = 65536
