@@ -134,7 +134,12 @@ __device__ __forceinline__ uint4 rx_load(__amdgpu_buffer_rsrc_t r, uint32_t off)
 // LIST = 1: a buffer list (g.off): packet s's buffer at g.ring + g.off[s]; one
 // buffer resource over the whole arena (< 4 GiB, 32-bit offsets).  A buffer
 // that is misaligned or not inside the arena is malformed and counted.
-template <int NB, int A0 = 0, int AN = 2, int WV = kWaves, int OCC = 1, int F = 1, int SPEC = 0, int LIST = 0>
+// ROT = 1 (timing variant, tools/rx_ring_variants.hip): load slot k >= 2 of
+// group g reads line 2 + (k - 2 + 3 g) mod (NB - 2), so the eight groups of
+// a wave do not all ask for line k of their slots at once (the same lines
+// are loaded and summed whole: the sums do not change).
+template <int NB, int A0 = 0, int AN = 2, int WV = kWaves, int OCC = 1, int F = 1, int SPEC = 0, int LIST = 0,
+          int ROT = 0>
 __global__ __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(OCC))) void rx_ring(RxGeo g) {
   __shared__ uint4 rx_lds[WV * kPerWave * kRowBytes / 16];
   const uint32_t lane = threadIdx.x & 63u, grp = lane >> 3, li = lane & 7u;
@@ -197,7 +202,16 @@ __global__ __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(OCC))) 
   const uint32_t cl1 = any1 ? cl : nrec;
 
   if constexpr (SPEC < 1) v[0] = rx_load<A0>(rsrc, off_of(cl));
+  const uint32_t rot = ROT && NB > 3 ? (3u * grp) % (uint32_t)(NB > 3 ? NB - 2 : 1) : 0u;
   auto line = [&](int k) {
+    if constexpr (F && ROT && NB > 3) {
+      if (k >= 2) {
+        uint32_t kk = (uint32_t)k + rot;
+        if (kk >= (uint32_t)NB) kk -= (uint32_t)(NB - 2);
+        v[k] = rx_load<AN>(rsrc, (kk <= klast ? cl1 : nrec) + 128u * kk);
+        return;
+      }
+    }
     if constexpr (F) v[k] = rx_load<AN>(rsrc, ((uint32_t)k <= klast ? cl1 : nrec) + 128u * k);
     else v[k] = rx_load<AN>(rsrc, off_of(cl + 128u * k));
   };
@@ -400,12 +414,13 @@ static int rx_batch_lines(const RxGeo& g) {
   return lines <= 2 ? 2 : lines <= 4 ? 4 : lines <= 8 ? 8 : lines <= 13 ? 13 : 16;
 }
 
-template <int NB, int A0 = 0, int AN = 2, int WV = kWaves, int OCC = 1, int F = 1, int SPEC = 0, int LIST = 0>
+template <int NB, int A0 = 0, int AN = 2, int WV = kWaves, int OCC = 1, int F = 1, int SPEC = 0, int LIST = 0,
+          int ROT = 0>
 static hipError_t launch_rx_ring_t(const RxGeo& g, hipStream_t stream) {
   if (g.n == 0) return hipSuccess;
   const uint64_t per_wg = (uint64_t)WV * kPerWave;
-  hipLaunchKernelGGL((rx_ring<NB, A0, AN, WV, OCC, F, SPEC, LIST>), dim3((uint32_t)((g.n + per_wg - 1) / per_wg)),
-                     dim3(64 * WV), 0, stream, g);
+  hipLaunchKernelGGL((rx_ring<NB, A0, AN, WV, OCC, F, SPEC, LIST, ROT>),
+                     dim3((uint32_t)((g.n + per_wg - 1) / per_wg)), dim3(64 * WV), 0, stream, g);
   return hipGetLastError();
 }
 

@@ -27,7 +27,8 @@ from netstack_amd import Engine  # noqa: E402
 from netstack_amd import workloads as W  # noqa: E402
 
 NAMES = {0: "product", 1: "all_default", 2: "all_nt", 3: "wg2", 4: "wg8", 5: "wg1", 6: "nb16", 7: "nb8",
-         8: "occ6", 9: "nb12", 10: "checked_f0", 11: "f1_nb8", 12: "spec_line0", 13: "spec_lines01"}
+         8: "occ6", 9: "nb12", 10: "checked_f0", 11: "f1_nb8", 12: "spec_line0", 13: "spec_lines01",
+         14: "rotated_lines"}
 
 
 class RxGeo(ctypes.Structure):
@@ -47,6 +48,7 @@ def main():
                     help="a variants library built from an earlier rx_ring.hip: its product shape is timed "
                          "beside the others as 'prev' (an A/B on one box)")
     ap.add_argument("--rotate", type=int, default=1, help="alternate two rings (1) or re-read one (0)")
+    ap.add_argument("--stride", type=int, default=0, help="slot spacing (a multiple of 16 >= 1504; 0: 1504)")
     ap.add_argument("--trend", type=int, default=0,
                     help="then time this many back-to-back launches of the product one by one (run-long drift)")
     args = ap.parse_args()
@@ -57,8 +59,18 @@ def main():
     lib = ctypes.CDLL(os.path.join(ROOT, "netstack_amd", "lib", "libns_rxv.so"))
     lib.rxv_launch.argtypes = [ctypes.POINTER(RxGeo), ctypes.c_void_p, ctypes.c_int]
     lib.rxv_launch.restype = ctypes.c_int
+    stride = args.stride or W.RX_STRIDE
+
+    def spread(a):  # the same slots at a wider spacing
+        if stride == W.RX_STRIDE:
+            return a
+        b = torch.zeros(n, stride, dtype=torch.uint8, device=dev)
+        b[:, :W.RX_STRIDE] = a.view(n, W.RX_STRIDE)
+        return b.view(-1)
+
     arena, lens, bad = W.rx_ring_batch(n, 9, dev, corrupt_every=1000)
-    ring = dict(stride=W.RX_STRIDE, n=n)
+    arena = spread(arena)
+    ring = dict(stride=stride, n=n)
     v0, s0 = eng.rx_ring(arena, ring, lens)
     torch.cuda.synchronize()
     err = torch.zeros(1, dtype=torch.int64, device=dev)
@@ -66,8 +78,8 @@ def main():
     sums = torch.empty(2 * n, dtype=torch.int16, device=dev)
     # two rings of the same frames, alternating (3.2 GB > the MALL), as
     # bench.py runs it
-    arena2 = W.rx_ring_batch(n, 9, dev, corrupt_every=1000)[0] if args.rotate else arena
-    gs = [RxGeo(a.data_ptr(), W.RX_STRIDE, lens.data_ptr(), sums.data_ptr(), verdict.data_ptr(), err.data_ptr(),
+    arena2 = spread(W.rx_ring_batch(n, 9, dev, corrupt_every=1000)[0]) if args.rotate else arena
+    gs = [RxGeo(a.data_ptr(), stride, lens.data_ptr(), sums.data_ptr(), verdict.data_ptr(), err.data_ptr(),
                 n, 0, 0, 0) for a in (arena, arena2)]
     g = gs[0]
     algo = n * (W.RX_PKT + 9)
@@ -117,7 +129,7 @@ def main():
         q = max(1, args.trend // 10)
         trend = {"per_launch_us": [round(x, 1) for x in t],
                  "first_decile_us": round(float(np.median(t[:q])), 2), "last_decile_us": round(float(np.median(t[-q:])), 2)}
-    print(json.dumps({"workload": "1M x 1500-B IPv4/TCP in 1504-B slots" + (", 2 rotating rings" if args.rotate else ", one ring re-read"), "algo_bytes": algo, "variants": out,
+    print(json.dumps({"workload": f"1M x 1500-B IPv4/TCP in {stride}-B slots" + (", 2 rotating rings" if args.rotate else ", one ring re-read"), "algo_bytes": algo, "variants": out,
                       "trend": trend}, indent=1))
 
 

@@ -10,6 +10,7 @@
 //  10 every chunk range-checked (F = 0: round 5's first product shape)
 //  11 F with 8 lines per batch
 //  12 / 13 line 0 / lines 0-1 loaded before the slot's length arrives
+//  14 the product shape with each group's lines >= 2 in a rotated order
 // Every variant computes the same verdicts and sums.  Not part of the ABI.
 #include "../netstack_amd/csrc/rx_ring.hip"
 
@@ -29,6 +30,7 @@ extern "C" int rxv_launch(const nsk::RxGeo* g, void* stream, int k) {
     case 11: return (int)nsk::launch_rx_ring_t<8, 0, 2, 4, 1, 1>(*g, s);
     case 12: return (int)nsk::launch_rx_ring_t<13, 0, 2, 4, 1, 1, 1>(*g, s);
     case 13: return (int)nsk::launch_rx_ring_t<13, 0, 2, 4, 1, 1, 2>(*g, s);
+    case 14: return (int)nsk::launch_rx_ring_t<13, 0, 2, 4, 1, 1, 0, 0, 1>(*g, s);
     default: return (int)nsk::launch_rx_ring_t<13>(*g, s);
   }
 }
