@@ -1114,8 +1114,9 @@ int run_rx_host(ns_csum_ctx* ctx, const uint8_t* h_arena, const ns_rx_ring& r, c
   };
   int rc = NS_OK;
   uint32_t slot = 0;
-  for (uint32_t first = 0; first < r.n; first += per) {
-    const uint32_t cnt = std::min(per, r.n - first);
+  for (uint64_t f = 0; f < r.n; f += per) {  // 64-bit: first + per may pass 2^32
+    const uint32_t first = (uint32_t)f;
+    const uint32_t cnt = (uint32_t)std::min<uint64_t>(per, r.n - f);
     if ((rc = finish(slot)) != NS_OK) break;
     if ((rc = enqueue(first, cnt, slot)) != NS_OK) {
       (void)hipStreamSynchronize(ctx->stream[slot]);
