@@ -160,6 +160,46 @@ def test_product_kernels_never_spill_and_keep_occupancy():
         assert v["Occupancy"] >= (8 if k.endswith("Li2EEEvNS_5TxGeoE") else 6), (k, v)
 
 
+    # the receive-ring kernels (rx_ring.hip): no scratch; the product's
+    # MTU instance (13 lines per batch, ring and buffer list) keeps 5 waves
+    rx = {}
+    cur = None
+    for line in open(os.path.join(ROOT, "netstack_amd", "lib", "rx_ring.resources.txt")).read().splitlines():
+        m = re.search(r"Function Name: (\S+)", line)
+        if m:
+            cur = m.group(1)
+            rx[cur] = {}
+            continue
+        m = re.search(r"(ScratchSize \[bytes/lane\]|Occupancy \[waves/SIMD\]|VGPRs): (\d+)", line)
+        if m and cur:
+            rx[cur][m.group(1).split()[0]] = int(m.group(2))
+    assert len(rx) >= 10 and all("rx_ring" in k for k in rx), sorted(rx)
+    for k, v in rx.items():
+        assert v["ScratchSize"] == 0, (k, v)
+        if "rx_ringILi13E" in k:
+            assert v["Occupancy"] >= 5, (k, v)
+
+
+def test_host_and_list_entry_points_check_arguments_before_the_device():
+    """The round-5 entry points refuse bad arguments with NS_EINVAL before
+    touching a device (so this runs on a CPU-only host)."""
+    import ctypes
+
+    L = _lib.lib()
+    t = (_lib.NsTcpTx * 1)()
+    r = _lib.NsRxRing(0, 1504, 1, 0, 0, 0, 0)
+    buf = (ctypes.c_uint8 * 4096)()
+    u32 = (ctypes.c_uint32 * 4)()
+    u16 = (ctypes.c_uint16 * 8)()
+    assert L.ns_csum_tcp_tx_host(None, buf, 4096, t, 1, None) == _lib.NS_EINVAL
+    assert L.ns_csum_tcp_tx_host_multi(None, 1, buf, 4096, t, 1, None) == _lib.NS_EINVAL
+    hs = (ctypes.c_void_p * 1)(None)
+    assert L.ns_csum_tcp_tx_host_multi(hs, 0, buf, 4096, t, 1, None) == _lib.NS_EINVAL
+    assert L.ns_csum_tcp_tx_host_multi(hs, 1, buf, 4096, t, 1, None) == _lib.NS_EINVAL  # a NULL context
+    assert L.ns_csum_rx_ring_host(None, buf, 4096, ctypes.byref(r), u32, u16, None) == _lib.NS_EINVAL
+    assert L.ns_csum_rx_bufs(None, buf, 4096, ctypes.byref(r), u32, u32, u16, None, None) == _lib.NS_EINVAL
+
+
 GO_SHIM = os.path.join(ROOT, "go", "header", "checksum_batch_hip.go")
 # Identifiers tcpip/header/checksum.go declares (checksum.go:26-122): the shim
 # is added NEXT to that file, so it must declare none of them.
