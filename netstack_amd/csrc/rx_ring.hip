@@ -424,19 +424,26 @@ static hipError_t launch_rx_ring_t(const RxGeo& g, hipStream_t stream) {
   return hipGetLastError();
 }
 
-template <int LIST>
+template <int LIST, int A0 = 0>
 static hipError_t launch_rx_ring_l(const RxGeo& g, hipStream_t stream) {
   switch (rx_batch_lines(g)) {
-    case 2: return launch_rx_ring_t<2, 0, 2, kWaves, 1, 1, 0, LIST>(g, stream);
-    case 4: return launch_rx_ring_t<4, 0, 2, kWaves, 1, 1, 0, LIST>(g, stream);
-    case 8: return launch_rx_ring_t<8, 0, 2, kWaves, 1, 1, 0, LIST>(g, stream);
-    case 13: return launch_rx_ring_t<13, 0, 2, kWaves, 1, 1, 0, LIST>(g, stream);
-    default: return launch_rx_ring_t<16, 0, 2, kWaves, 1, 1, 0, LIST>(g, stream);
+    case 2: return launch_rx_ring_t<2, A0, 2, kWaves, 1, 1, 0, LIST>(g, stream);
+    case 4: return launch_rx_ring_t<4, A0, 2, kWaves, 1, 1, 0, LIST>(g, stream);
+    case 8: return launch_rx_ring_t<8, A0, 2, kWaves, 1, 1, 0, LIST>(g, stream);
+    case 13: return launch_rx_ring_t<13, A0, 2, kWaves, 1, 1, 0, LIST>(g, stream);
+    default: return launch_rx_ring_t<16, A0, 2, kWaves, 1, 1, 0, LIST>(g, stream);
   }
 }
 
+// Line 0 takes the default cache policy because its first bytes may be the
+// slot before's last ones.  A ring of line-aligned slots whose IP packets
+// start in their slot's first line shares no line between slots: line 0
+// goes nontemporal too (1536-B slots: 236.5 -> 234.2 us per 1M frames,
+// tools/rx_ring_probe.py --stride 1536).
 hipError_t launch_rx_ring(const RxGeo& g, hipStream_t stream) {
-  return g.off ? launch_rx_ring_l<1>(g, stream) : launch_rx_ring_l<0>(g, stream);
+  if (g.off) return launch_rx_ring_l<1>(g, stream);
+  if ((g.ring & 127) == 0 && (g.stride & 127) == 0 && g.frame_at + g.link < 128) return launch_rx_ring_l<0, 2>(g, stream);
+  return launch_rx_ring_l<0>(g, stream);
 }
 
 }  // namespace nsk

@@ -231,6 +231,18 @@ def test_small_and_common_strides(engine, stride):
     assert len(got) == 200
 
 
+@pytest.mark.parametrize("stride,link_hdr,frame_at", [(1536, 0, 0), (2048, 14, 10), (1536, 14, 120), (1664, 14, 2)])
+def test_line_aligned_slots(engine, stride, link_hdr, frame_at):
+    """Rings of 128-B-aligned slots whose packets start in the slot's first
+    line load line 0 nontemporal too (no line is shared between slots); a
+    frame starting past the first line (frame_at + link >= 128) keeps the
+    default shape.  The same verdicts and sums as the oracle either way."""
+    rng = np.random.default_rng(19 + stride + frame_at)
+    _, frames = _frames(rng, 300, link_hdr, max_payload=stride - frame_at - 80)
+    got = _check(engine, frames, stride, frame_at, link_hdr, 128 if link_hdr else 0, ring_off=stride * 2)
+    assert {0, 1} <= set(got)
+
+
 def test_header_fuzz(engine):
     """Random byte flips in the first 80 bytes of valid packets (every
     header field the receive path reads), as TUN and Ethernet frames."""
