@@ -201,7 +201,18 @@ __global__ __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(OCC))) 
   const bool any1 = Pl && pe > cl + 128u;  // some line k >= 1 holds packet bytes for this lane
   const uint32_t cl1 = any1 ? cl : nrec;
 
-  if constexpr (SPEC < 1) v[0] = rx_load<A0>(rsrc, off_of(cl));
+  if constexpr (SPEC < 1 && LIST && A0 == 0) {
+    // a buffer list: line 0 nontemporal for a buffer that starts a line and
+    // whose packet starts in that line (no other buffer can share it), with
+    // the default policy otherwise; the other load reads nothing (offset
+    // nrec: the resource's out-of-range zeros)
+    const bool alone = (slot & 127u) == 0 && pre < 128u;
+    const uint4 a = rx_load<0>(rsrc, alone ? nrec : off_of(cl));
+    const uint4 b = rx_load<2>(rsrc, alone ? off_of(cl) : nrec);
+    v[0] = make_uint4(a.x | b.x, a.y | b.y, a.z | b.z, a.w | b.w);
+  } else if constexpr (SPEC < 1) {
+    v[0] = rx_load<A0>(rsrc, off_of(cl));
+  }
   const uint32_t rot = ROT && NB > 3 ? (3u * grp) % (uint32_t)(NB > 3 ? NB - 2 : 1) : 0u;
   auto line = [&](int k) {
     if constexpr (F && ROT && NB > 3) {
