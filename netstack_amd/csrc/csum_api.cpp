@@ -888,12 +888,12 @@ uint32_t tx_chunk_table(const nsh::TxHostPlan& plan, const nsh::TxChunk& c, uint
   return nsk::tx_multi_prepare(calls->data(), c.np, launch, first->data());
 }
 
-// Host TX calls whose bytes and table fit kTxSmallBytes take no DMA: the
+// Host TX calls whose bytes and table fit kHostSmallBytes take no DMA: the
 // ranges and the table are written through the BAR into a leased gather
 // stage (fine-grained VRAM on large-BAR parts), one launch reads them there
 // and writes its sums to mapped memory, then one wait, as the small checksum
 // calls do.  Above that size the DMA pipeline's ~55 GB/s beats the BAR's ~23.
-constexpr uint64_t kTxSmallBytes = 1ull << 20;
+constexpr uint64_t kHostSmallBytes = 1ull << 20;
 
 // Completes a small host-path launch on stream s (pmu held): a one-wave
 // kernel behind it stores this call's sequence number into coherent host
@@ -965,7 +965,7 @@ int run_tx_host(ns_csum_ctx* ctx, uint8_t* h_arena, const nsh::TxHostPlan& plan,
     const nsh::TxChunk& c = plan.chunks[0];
     const uint64_t tab = ((uint64_t)c.np * sizeof(nsk::TxGeo) + 15) & ~15ull;
     const uint64_t need = ((c.staging + 255) & ~255ull) + tab + 4ull * (c.np + 1);
-    if (need <= std::min<uint64_t>(kTxSmallBytes, ctx->staging)) return run_tx_small(ctx, h_arena, plan, h_out);
+    if (need <= std::min<uint64_t>(kHostSmallBytes, ctx->staging)) return run_tx_small(ctx, h_arena, plan, h_out);
   }
   const uint32_t nslots = ctx->nslots;
   int64_t pend[kMaxHostSlots];
@@ -1032,7 +1032,7 @@ int run_tx_host(ns_csum_ctx* ctx, uint8_t* h_arena, const nsh::TxHostPlan& plan,
 // parses and verifies them there and writes verdicts and sums straight to
 // mapped pinned memory; when the chunk is done they are copied to the
 // caller's arrays while later chunks are in flight.  No host planning.
-// A small ring (its slots and lengths within kTxSmallBytes and the staging
+// A small ring (its slots and lengths within kHostSmallBytes and the staging
 // budget) takes no DMA either: written through the BAR into a gather stage,
 // one launch, one wait.
 int run_rx_small(ns_csum_ctx* ctx, const uint8_t* h_arena, const ns_rx_ring& r, const uint32_t* h_len,
@@ -1070,7 +1070,7 @@ int run_rx_small(ns_csum_ctx* ctx, const uint8_t* h_arena, const ns_rx_ring& r, 
 int run_rx_host(ns_csum_ctx* ctx, const uint8_t* h_arena, const ns_rx_ring& r, const uint32_t* h_len,
                 uint16_t* h_sums, uint8_t* h_verdict) {
   const uint64_t small = (((uint64_t)r.n * r.stride + 255) & ~255ull) + 4ull * r.n;
-  if (zero_copy_enabled() && small <= std::min<uint64_t>(kTxSmallBytes, ctx->staging))
+  if (zero_copy_enabled() && small <= std::min<uint64_t>(kHostSmallBytes, ctx->staging))
     return run_rx_small(ctx, h_arena, r, h_len, h_sums, h_verdict);
   const uint32_t nslots = ctx->nslots;
   const uint32_t per = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(1, ctx->staging / r.stride), 1u << 24);
