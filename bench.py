@@ -581,7 +581,8 @@ def main():
             "avg_launch_us": kern_avg_s * 1e6,
             "rotating_batches": rotate,
             "basis": (f"avg_launch_us over the timed region's back-to-back launches cycling {rotate} distinct "
-                      f"batches ({rotate * batch.arena_bytes / 2**20:.0f} MiB > the 256 MiB MALL)"
+                      f"batches ({rotate * (batch.arena_bytes + 18 * batch.n) / 2**20:.0f} MiB of arenas, "
+                      f"descriptor tables and results > the 256 MiB MALL)"
                       if rotate > 1 else "avg_launch_us over the timed region's back-to-back launches"),
             "unrotated": {"avg_launch_us": unrot_us, "frac": algo_bytes / unrot_us / 1e3 / HBM_PEAK_GBS,
                           "note": "batch 0 re-read back to back, 20 launches: may hit the MALL"},

@@ -274,14 +274,18 @@ int ns_csum_tcp_tx_multi(ns_csum_ctx* ctx, uint8_t* d_arena, uint64_t arena_byte
  * and the payload of full-mode calls) go to the device in chunks of at most
  * the context's staging size (ns_csum_opts.staging_bytes; a call larger than
  * that is split by segments), four chunks in flight; ranges closer than 4 KiB
- * travel together, so bytes between them are uploaded too.  Each segment's
+ * travel together, so bytes between them are uploaded too (and count
+ * against the staging size; only a chunk of one call's run of segments can
+ * exceed it, by that gap and 512 B of alignment).  Each segment's
  * fields are then written into h_arena's slots, the same values
  * ns_csum_tcp_tx_multi stores: only the 2-byte fields change, every other
  * byte is left as it was.  h_out (2 * sum n_k u16, or NULL) gets the sums as
  * d_out does.  Pinned memory (ns_csum_stage_acquire) is copied by DMA
  * directly; pageable memory is bounced by the HIP runtime.  Errors as for
  * ns_csum_tcp_tx_multi, returned before any byte is written; on an engine
- * error later (NS_ENOMEM, NS_EHIP) some fields may already be written.     */
+ * error later (NS_ENOMEM, NS_EHIP) some fields may already be written.
+ * Like ns_csum_rx_ring_host it waits for a host pipeline call running on the
+ * same context, small calls (within 1 MiB, no DMA) included.               */
 int ns_csum_tcp_tx_host(ns_csum_ctx* ctx, uint8_t* h_arena, uint64_t arena_bytes,
                         const ns_tcp_tx* txs, uint32_t count, uint16_t* h_out);
 
@@ -474,7 +478,12 @@ int ns_csum_rx_bufs(ns_csum_ctx* ctx, const uint8_t* d_arena, uint64_t arena_byt
  * still must be a multiple of 16).  The slots go to the device in chunks of
  * whole slots (up to the context's staging size), four in flight; verdicts
  * and sums come back through mapped memory.  No host planning: the parse
- * runs on the device.  Synchronous.  Errors as for ns_csum_rx_ring.        */
+ * runs on the device.  Synchronous.  Errors as for ns_csum_rx_ring.
+ * Calls on one context share its host pipeline: a ring (even one small
+ * enough for the BAR stage, within 1 MiB) waits for any ns_csum_batch_host,
+ * _tcp_tx_host or _rx_ring_host call already running on that context; the
+ * zero-copy passes of the single-buffer calls do not.  Use a context per
+ * thread where that wait matters.                                           */
 int ns_csum_rx_ring_host(ns_csum_ctx* ctx, const uint8_t* h_arena, uint64_t arena_bytes,
                          const ns_rx_ring* ring, const uint32_t* h_len, uint16_t* h_sums,
                          uint8_t* h_verdict);
@@ -523,7 +532,10 @@ typedef struct ns_csum_stats {
   uint64_t lock_ns_max;      /* longest wait for the context lock by a pass   */
   uint64_t zc_passes;        /* zero-copy passes run                          */
   uint64_t zc_late;          /* ...whose completion word was not in after
-                                2 ms (the caller then waited on the stream)   */
+                                2 ms (the caller then waited on the stream);
+                                also counts the small host-ring / host-TX
+                                passes (ns_csum_rx_ring_host, _tcp_tx_host
+                                within 1 MiB) that were late the same way    */
   uint64_t zc_pass_ns_max;   /* longest pass, launch to results               */
   uint64_t growths;          /* stream-ordered scratch growths (batch_dev)    */
   uint64_t growth_ns_total;  /* host time in hipFreeAsync/hipMallocAsync/

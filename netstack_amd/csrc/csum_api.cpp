@@ -913,6 +913,7 @@ int wait_small(ns_csum_ctx* ctx, hipStream_t s) {
   const auto t0 = std::chrono::steady_clock::now();
   for (uint32_t spin = 0; __atomic_load_n(done, __ATOMIC_ACQUIRE) != seq; ++spin) {
     if ((spin & 255u) == 255u && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) {
+      ctx->st.zc_late.fetch_add(1, std::memory_order_relaxed);  // counted like a late zero-copy pass
       HIP_TRY(hipStreamSynchronize(s));
       if (__atomic_load_n(done, __ATOMIC_ACQUIRE) != seq) return NS_EHIP;
       break;

@@ -443,9 +443,10 @@ int plan_packet(Builder& g, const PacketBytes& pb, uint32_t op, PacketPlan* pp) 
       pp->verdict = NS_PKB_INVALID;
     } else if (ip.proto == kProtoICMPv6 && !ip.v4) {
       // handleICMP (network/ipv6/icmp.go:62-84): h = the first view, payload
-      // = the other views, ICMPv6Checksum (header/icmpv6.go:202-221)
+      // = the other views, ICMPv6Checksum (header/icmpv6.go:202-221); a first
+      // view under ICMPv6MinimumSize (8, header/icmpv6.go:35) is dropped (:68)
       uint8_t h[4];
-      if (first_end - t0 < 4 || !pb.read(t0, h, 4)) {
+      if (first_end - t0 < 8 || !pb.read(t0, h, 4)) {
         pp->verdict = NS_PKB_MALFORMED;
         return NS_OK;
       }
@@ -456,6 +457,10 @@ int plan_packet(Builder& g, const PacketBytes& pb, uint32_t op, PacketPlan* pp) 
       pb.pieces(t0 + 4, first_end, false, false, &ps);
       pp->tr_chain = add_chain(init);
       pp->verdict = NS_PKB_INVALID;
+    } else if (ip.proto == kProtoUDP && first_end - t0 < 8) {
+      // stack.DeliverTransportPacket: First() >= UDPMinimumSize (stack/nic.go:
+      // 851); UDP takes no checksum on receive otherwise (UNCHECKED)
+      pp->verdict = NS_PKB_MALFORMED;
     }
     return NS_OK;
   }
@@ -861,9 +866,10 @@ inline int tx_multi_plan(const ns_tcp_tx* t, uint32_t count, uint64_t arena_byte
 // pseudo-header length words and sums.  Each call is cut into such pieces of
 // at most `budget` bytes (its slots plus the payload a full-mode call reads;
 // one segment may exceed it), consecutive pieces are grouped into chunks of
-// at most `budget` bytes and kMaxTxHostPieces pieces, and a chunk uploads
-// its pieces' byte ranges merged where they overlap or lie within kTxHostGap
-// bytes of each other.  Each merged range goes to the chunk's staging at its
+// at most kMaxTxHostPieces pieces whose staging is at most `budget` bytes
+// (a one-piece chunk excepted), and a chunk uploads its pieces' byte ranges
+// merged where they overlap or lie within kTxHostGap bytes of each other —
+// the gap bytes travel and count against the budget.  Each merged range goes to the chunk's staging at its
 // arena offset modulo 256, so the kernel meets the alignments it would meet
 // in the arena.
 constexpr uint64_t kTxHostGap = 4096;
@@ -992,6 +998,28 @@ inline int tx_host_plan(const ns_tcp_tx* t, uint32_t count, uint64_t arena_bytes
   }
   out->nseg = seg;
   std::vector<TxRange> sl, pl, iv;
+  // The staging pieces [p0, p1) take: their ranges merged (the bytes of the
+  // gaps merged in count) at their offsets modulo 256 (the alignment counts);
+  // `emit` appends the ranges to the plan.
+  auto staging_of = [&](uint32_t p0, uint32_t p1, bool emit) -> uint64_t {
+    sl.clear();
+    pl.clear();
+    for (uint32_t j = p0; j < p1; ++j) {
+      const TxPiece& q = out->pieces[j];
+      sl.push_back({q.t.hdr_off, q.t.hdr_off + q.nseg * q.t.slot, 0});
+      if ((q.mode & 2u) && q.t.size) pl.push_back({q.t.pay_off, q.t.pay_off + q.t.size, 0});
+    }
+    merge_by_lo(sl, pl, &iv);
+    uint64_t at = 0;
+    for (size_t j = 0; j < iv.size();) {
+      TxRange m = iv[j++];
+      while (j < iv.size() && iv[j].lo <= m.hi + kTxHostGap) m.hi = std::max(m.hi, iv[j++].hi);
+      m.at = ((at + 255) & ~255ull) + (m.lo & 255u);
+      at = m.at + (m.hi - m.lo);
+      if (emit) out->ranges.push_back(m);
+    }
+    return at;
+  };
   const uint32_t np = (uint32_t)out->pieces.size();
   for (uint32_t i = 0; i < np;) {
     TxChunk ch;
@@ -1001,25 +1029,23 @@ inline int tx_host_plan(const ns_tcp_tx* t, uint32_t count, uint64_t arena_bytes
       sum += bytes[i++];
       ++ch.np;
     }
-    sl.clear();
-    pl.clear();
-    for (uint32_t j = ch.p0; j < i; ++j) {
-      const TxPiece& q = out->pieces[j];
-      sl.push_back({q.t.hdr_off, q.t.hdr_off + q.nseg * q.t.slot, 0});
-      if ((q.mode & 2u) && q.t.size) pl.push_back({q.t.pay_off, q.t.pay_off + q.t.size, 0});
+    // The pieces' own bytes fit the budget; with the gaps and alignment the
+    // staging may not: keep the longest prefix whose staging fits (a single
+    // piece always goes, and may exceed the budget by its own gap and
+    // alignment, under 4.6 KiB).
+    if (ch.np > 1 && staging_of(ch.p0, i, false) > budget) {
+      uint32_t lo = 1, hi = ch.np - 1;  // lo: taken; counts above hi: too big
+      while (lo < hi) {
+        const uint32_t mid = lo + (hi - lo + 1) / 2;
+        if (staging_of(ch.p0, ch.p0 + mid, false) <= budget) lo = mid;
+        else hi = mid - 1;
+      }
+      ch.np = lo;
+      i = ch.p0 + lo;
     }
-    merge_by_lo(sl, pl, &iv);
     ch.r0 = (uint32_t)out->ranges.size();
-    uint64_t at = 0;
-    for (size_t j = 0; j < iv.size();) {
-      TxRange m = iv[j++];
-      while (j < iv.size() && iv[j].lo <= m.hi + kTxHostGap) m.hi = std::max(m.hi, iv[j++].hi);
-      m.at = ((at + 255) & ~255ull) + (m.lo & 255u);
-      at = m.at + (m.hi - m.lo);
-      out->ranges.push_back(m);
-    }
+    ch.staging = staging_of(ch.p0, i, true);
     ch.nr = (uint32_t)(out->ranges.size() - ch.r0);
-    ch.staging = at;
     const TxPiece& last = out->pieces[i - 1];
     ch.out0 = out->pieces[ch.p0].out0;
     ch.nout = last.out0 + last.nseg - ch.out0;

@@ -290,12 +290,17 @@ __global__ __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(OCC))) 
   const uint32_t tfl = (first < tend ? first : tend) - a;  // the transport's first view
   const uint32_t ta = h(a), toff = (h(a + 12) >> 4) * 4u;
   const uint32_t want = (h(a + 2) << 8) | h(a + 3);
-  const bool tcp = ip && proto == 6, icmp4 = ip && v4 && proto == 1, icmp6 = ip && !v4 && proto == 58;
-  const bool tcp_bad = tfl < 20 || toff < 20 || toff > tfl;  // segment.parse (segment.go:160-180)
+  const bool tcp = ip && proto == 6, udp = ip && proto == 17, icmp4 = ip && v4 && proto == 1,
+             icmp6 = ip && !v4 && proto == 58;
+  // The minimum sizes, each against the transport's first view: TCP 20 and
+  // UDP 8 (stack/nic.go:851, header/tcp.go:169, header/udp.go:56), ICMPv4 8
+  // (ipv4/icmp.go:60, header/icmpv4.go:32), ICMPv6 8 (ipv6/icmp.go:68,
+  // ICMPv6MinimumSize, header/icmpv6.go:35).
+  const bool tcp_bad = tfl < 20 || toff < 20 || toff > tfl;  // + segment.parse (segment.go:159)
   // kind: 1 TCP, 2 ICMPv4 echo request (handleICMP, icmp.go:60-80), 3 ICMPv6
-  const uint32_t kind = tcp && !tcp_bad ? 1u : icmp4 && tfl >= 8 && ta == 8 ? 2u : icmp6 && tfl >= 4 ? 3u : 0u;
+  const uint32_t kind = tcp && !tcp_bad ? 1u : icmp4 && tfl >= 8 && ta == 8 ? 2u : icmp6 && tfl >= 8 ? 3u : 0u;
   const bool malformed = !P || (g.link ? np != 0 && !v4 && !v6 : !v4 && !v6) || (frag && fragbad) ||
-                         (tcp && tcp_bad) || (icmp4 && tfl < 8) || (icmp6 && tfl < 4);
+                         (tcp && tcp_bad) || (udp && tfl < 8) || (icmp4 && tfl < 8) || (icmp6 && tfl < 8);
   uint32_t verdict = malformed ? kMalformed : kUnchecked;  // the checked kinds are decided below
   const uint32_t b = kind ? tend : 0u;
   const uint32_t asz = v4 ? 8u : 32u;

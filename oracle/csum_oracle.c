@@ -404,7 +404,7 @@ int oracle_rx_verify(const uint8_t* slot, uint64_t slot_bytes, uint64_t rlen, ui
     return (uint16_t)~s == want ? 1 : 0;
   }
   if (proto == 58 && ver == 6) { /* ICMPv6Checksum(h, src, dst, the other views) */
-    if (tfirst.n < 4) return 3;
+    if (tfirst.n < 8) return 3; /* ICMPv6MinimumSize (ipv6/icmp.go:68, header/icmpv6.go:35) */
     const uint16_t want = (uint16_t)(((uint32_t)tfirst.p[2] << 8) | tfirst.p[3]);
     const uint64_t total = ovv_size(&vv);
     uint16_t xsum = oracle_checksum(src, 16, 0);
@@ -422,6 +422,7 @@ int oracle_rx_verify(const uint8_t* slot, uint64_t slot_bytes, uint64_t rlen, ui
     *tr_out = (uint16_t)~got;
     return got == want ? 1 : 0;
   }
+  if (proto == 17 && tfirst.n < 8) return 3; /* UDPMinimumSize (stack/nic.go:851) */
   return 2;
 }
 

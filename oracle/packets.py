@@ -147,13 +147,18 @@ def verify(hdr: bytes, views, size: int, net_proto: int | None = None):
         got = (~s) & 0xFFFF
         return (VALID if got == want else INVALID), net, s
     if proto == 58 and ver == 6:
-        # handleICMP (network/ipv6/icmp.go:62-84)
-        if len(tfirst) < 4:
+        # handleICMP (network/ipv6/icmp.go:62-84): len(v) < ICMPv6MinimumSize
+        # (= 8, header/icmpv6.go:35) is dropped at :68-71
+        if len(tfirst) < 8:
             return MALFORMED, net, 0
         h = bytearray(tfirst)
         want = (h[2] << 8) | h[3]
         got = _icmpv6_checksum(h, src, dst, data[1:])
         return (VALID if got == want else INVALID), net, (~got) & 0xFFFF
+    if proto == 17 and len(tfirst) < 8:
+        # stack DeliverTransportPacket: First() >= UDPMinimumSize (stack/nic.go:
+        # 851, header/udp.go:56); UDP takes no checksum on receive otherwise
+        return MALFORMED, net, 0
     return UNCHECKED, net, 0
 
 

@@ -755,6 +755,10 @@ static void TestTxHostPlan(Rng& rng, int rounds) {
       uint64_t sum = 0;
       for (uint32_t j = c.p0; j < next; ++j) sum += bytes[j];
       CHECK(sum <= budget || c.np == 1, "chunk over budget");
+      // the staging (merged gaps and alignment included) fits too; a
+      // one-piece chunk by at most its own gap and two ranges' alignment
+      CHECK(c.staging <= budget || (c.np == 1 && c.staging <= sum + nsh::kTxHostGap + 512),
+            "chunk staging %llu over budget %llu", (unsigned long long)c.staging, (unsigned long long)budget);
       std::vector<uint8_t> st(c.staging + 16, 0xEE);
       uint64_t end = 0;
       for (uint32_t j = c.r0; j < c.r0 + c.nr; ++j) {

@@ -125,9 +125,13 @@ def random_packet(rng, max_payload: int = 9000) -> bytearray:
     their TotalLength (Data.CapLength)."""
     r = rng.random()
     kind = "tcp4" if r < 0.45 else "tcp6" if r < 0.65 else "icmp4" if r < 0.72 else \
-        "icmp6" if r < 0.79 else "udp4" if r < 0.85 else "frag" if r < 0.88 else "bad"
+        "icmp6" if r < 0.79 else "udp4" if r < 0.85 else "frag" if r < 0.88 else "bad" if r < 0.96 else "short"
     plen = int(rng.choice([0, 1, 7, int(rng.integers(0, 1460)), int(rng.integers(0, max_payload))]))
-    if kind == "frag":
+    if kind == "short":  # a message around its protocol's minimum size
+        k = ("tcp", "udp", "icmp4", "icmp6")[int(rng.integers(0, 4))]
+        p = short_message(rng, k, int(rng.integers(0, MIN_SIZE[k] + 3)),
+                          None if k.startswith("icmp") else bool(rng.integers(0, 2)))
+    elif kind == "frag":
         p = frag_packet(rng, int(rng.integers(0, 6)), plen)
     elif kind == "bad":
         p = valid_packet(rng, "tcp4", plen)
@@ -156,3 +160,90 @@ def ethernet(pkt: bytes, etype: int | None = None) -> bytes:
     if etype is None:
         etype = 0x86DD if pkt and (pkt[0] >> 4) == 6 else 0x0800
     return bytes(range(1, 13)) + struct.pack(">H", etype) + bytes(pkt)
+
+
+# The receive path's minimum sizes, each checked against the transport's FIRST
+# VIEW (Data.First() after the IP trim) before any checksum is taken:
+#   tcp   TCPMinimumSize 20   stack/nic.go:851 (DeliverTransportPacket),
+#                             header/tcp.go:169; segment.go:159 (DataOffset)
+#   udp   UDPMinimumSize 8    stack/nic.go:851, header/udp.go:56
+#   icmp4 ICMPv4MinimumSize 8 network/ipv4/icmp.go:60, header/icmpv4.go:32
+#   icmp6 ICMPv6MinimumSize 8 network/ipv6/icmp.go:68, header/icmpv6.go:35
+# and the network headers' against the packet's first view:
+#   ip4   IPv4MinimumSize 20  stack/nic.go:774, header/ipv4.go:83, :281
+#   ip6   IPv6MinimumSize 40  stack/nic.go:774, header/ipv6.go:68, :208
+MIN_SIZE = {"tcp": 20, "udp": 8, "icmp4": 8, "icmp6": 8}
+_HDR = {"tcp": 20, "udp": 8, "icmp4": 8, "icmp6": 8}
+_PROTO = {"tcp": 6, "udp": 17, "icmp4": 1, "icmp6": 58}
+
+
+def short_message(rng, kind: str, length: int, v6: bool | None = None) -> bytearray:
+    """An IP packet whose transport message is exactly `length` bytes:
+    `kind` in tcp/udp/icmp4/icmp6 (IPv4 unless v6 or icmp6).  From the
+    protocol's minimum size on it is a well-formed message with correct
+    checksums (oracle/packets.py fill, a 20-B TCP header, an ICMP echo
+    request); below it, the first `length` bytes of one, with the IP length
+    fields saying `length`."""
+    import packets as P
+
+    v6 = kind == "icmp6" if v6 is None else v6
+    alen = 16 if v6 else 4
+    src = bytes(rng.integers(0, 256, alen, dtype=np.uint8))
+    dst = bytes(rng.integers(0, 256, alen, dtype=np.uint8))
+    proto, hl = _PROTO[kind], _HDR[kind]
+    if kind == "tcp":
+        t = tcp_header(rng, 0)
+    elif kind == "udp":
+        from netstack_amd.proto import encode_udp
+
+        t = encode_udp(int(rng.integers(1, 65536)), int(rng.integers(1, 65536)), length)
+    else:
+        t = bytearray(8)
+        t[0] = 128 if kind == "icmp6" else 8  # echo request
+        struct.pack_into(">HH", t, 4, int(rng.integers(0, 65536)), int(rng.integers(0, 65536)))
+    ip = ip6(proto, src, dst, length) if v6 else ip4(proto, src, dst, length, int(rng.integers(0, 65536)))
+    if length < hl:
+        return bytearray(ip + t[:length])
+    payload = bytes(rng.integers(0, 256, length - hl, dtype=np.uint8))
+    hdr, _, _ = P.fill(bytes(ip + t), [payload], length - hl)
+    return bytearray(hdr + payload)
+
+
+def min_size_verdict(kind: str, first_len: int, valid: int = 1) -> int:
+    """The reference's verdict for a message of `kind` whose first view holds
+    `first_len` transport bytes: MALFORMED (3) under the minimum size; at or
+    above it UNCHECKED (2) for UDP (no receive checksum), else `valid` (the
+    checksum's outcome, 1 for the well-formed messages above)."""
+    if first_len < MIN_SIZE[kind]:
+        return 3
+    return 2 if kind == "udp" else valid
+
+
+def short_messages(rng, extra: int = 2):
+    """Every (kind, ip version, length) with length 0 .. minimum + extra:
+    [(kind, v6, length, packet)] — the rows of the minimum-size table."""
+    out = []
+    for kind in ("tcp", "udp", "icmp4", "icmp6"):
+        for v6 in ((False,) if kind == "icmp4" else (True,) if kind == "icmp6" else (False, True)):
+            for length in range(0, MIN_SIZE[kind] + extra + 1):
+                out.append((kind, v6, length, short_message(rng, kind, length, v6)))
+    return out
+
+
+def min_size_frames(rng, link_hdr: int):
+    """The minimum-size rows as a receive batch: every short_messages row
+    (TUN packets, or Ethernet frames when link_hdr) plus, for each row at or
+    above its minimum, a copy with its last byte changed (the checksum's
+    INVALID side).  Returns (frames, the reference's verdicts)."""
+    frames, want = [], []
+    for kind, _, length, p in short_messages(rng):
+        frames.append(p)
+        want.append(min_size_verdict(kind, length))
+        if length >= MIN_SIZE[kind]:
+            q = bytearray(p)
+            q[-1] ^= int(rng.integers(1, 256))
+            frames.append(q)
+            want.append(min_size_verdict(kind, length, valid=0))
+    if link_hdr:
+        frames = [ethernet(bytes(f)) for f in frames]
+    return [bytes(f) for f in frames], want

@@ -88,6 +88,35 @@ def test_verify_packet_buffers_recvmmsg_batches(engine, seed):
         assert all(kinds[k] > 0 for k in kinds), kinds  # every verdict occurs
 
 
+@pytest.mark.parametrize("link_hdr", [0, 14])
+def test_verify_minimum_sizes(engine, link_hdr):
+    """The minimum-size rows (tests/pktgen.py MIN_SIZE; ICMPv6 8 B,
+    network/ipv6/icmp.go:68) as the link hands them up in BufConfig views,
+    plus longer messages whose transport first view is cut at every length
+    up to the minimum + 2 (the gate is on Data.First(), not the message)."""
+    from netstack_amd.buffer import NewVectorisedView, View
+    from netstack_amd.packet import PacketBuffer, verify_packet_buffers
+    from pktgen import MIN_SIZE, min_size_frames, min_size_verdict, short_message
+
+    rng = np.random.default_rng(3200 + link_hdr)
+    frames, want = min_size_frames(rng, 0)
+    pkts = [PacketBuffer(Data=_views_bufconfig(f, link_hdr)) for f in frames]
+    for kind, v6 in (("tcp", False), ("tcp", True), ("udp", True), ("icmp4", False), ("icmp6", True)):
+        ipl = 40 if v6 else 20
+        for cut in range(1, MIN_SIZE[kind] + 3):
+            p = bytes(short_message(rng, kind, MIN_SIZE[kind] + 40, v6))
+            pkts.append(PacketBuffer(Data=NewVectorisedView(len(p), [View(bytearray(p[:ipl + cut])),
+                                                                     View(bytearray(p[ipl + cut:]))])))
+            want.append(min_size_verdict(kind, cut) if cut < MIN_SIZE[kind] or kind != "icmp6" or cut % 2 == 0
+                        else None)
+    verdict, sums = verify_packet_buffers(pkts, engine)
+    for i, pk in enumerate(pkts):
+        w = _oracle_rx(pk)
+        assert (int(verdict[i]), int(sums[2 * i]), int(sums[2 * i + 1])) == w, i
+        if want[i] is not None:
+            assert w[0] == want[i], i
+
+
 def test_verify_single_corrupted_byte_fails(engine):
     """TestReceivedIncorrectChecksumIncrement (tcp_test.go:3246-3254): one
     flipped payload byte fails the segment, anywhere in any view."""

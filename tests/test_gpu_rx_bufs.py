@@ -85,6 +85,23 @@ def test_pool_matches_oracle_and_ring(engine, link_hdr, first_view, ring_off):
     assert engine.sync() == 0
 
 
+@pytest.mark.parametrize("link_hdr,first_view", [(0, 0), (14, 128)])
+def test_minimum_sizes(engine, link_hdr, first_view):
+    """The minimum-size rows (tests/pktgen.py MIN_SIZE; ICMPv6 8 B,
+    network/ipv6/icmp.go:68) from a shuffled pool: the oracle's verdicts and
+    sums, and the reference's verdict table."""
+    from pktgen import min_size_frames
+
+    rng = np.random.default_rng(5950 + link_hdr)
+    frames, want = min_size_frames(rng, link_hdr)
+    arena, offs, lens = _pool(frames, 128, seed=5951, ring_off=16)
+    ring = dict(ring_off=16, stride=128, n=len(frames), link_hdr=link_hdr, first_view=first_view)
+    verdict, sums = _run_bufs(engine, arena, offs, lens, ring)
+    wv, ws = _want(arena, offs, lens, ring)
+    assert np.array_equal(verdict, wv) and np.array_equal(sums, ws)
+    assert verdict.tolist() == want
+
+
 def test_bad_buffers_are_malformed_and_counted(engine):
     rng = np.random.default_rng(5800)
     _, frames = _frames(rng, 64, 14, max_payload=1400)

@@ -141,6 +141,21 @@ def test_reference_packet_fixtures(engine):
     _check(engine, [ethernet(p, 0x0800) for p in pk], stride, link_hdr=14, first_view=128)
 
 
+@pytest.mark.parametrize("link_hdr,first_view", [(0, 0), (0, 128), (0, 64), (14, 128), (14, 0), (14, 78)])
+def test_minimum_sizes(engine, link_hdr, first_view):
+    """Every transport message from 0 to its minimum + 2 bytes (TCP 20, UDP 8,
+    ICMPv4 8, ICMPv6 8 — ICMPv6MinimumSize, network/ipv6/icmp.go:68; the
+    table and its reference lines in tests/pktgen.py MIN_SIZE), intact and
+    with a changed byte: MALFORMED under the minimum, the checksum's verdict
+    from it, as the oracle and the reference give them."""
+    from pktgen import min_size_frames
+
+    rng = np.random.default_rng(5900 + link_hdr + first_view)
+    frames, want = min_size_frames(rng, link_hdr)
+    got = _check(engine, frames, 128, link_hdr=link_hdr, first_view=first_view, seed=3)
+    assert got == want
+
+
 def test_first_view_decides_the_tcp_header_check(engine):
     """segment.parse checks DataOffset against the FIRST view (segment.go:160):
     a 60-B IPv4 header and a 60-B TCP header fit BufConfig's 128-B first view

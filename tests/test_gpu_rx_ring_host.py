@@ -53,6 +53,24 @@ def test_small_ring_through_a_bar_stage(engine, n):
     assert np.array_equal(verdict, wv) and np.array_equal(sums, ws)
 
 
+@pytest.mark.parametrize("link_hdr,first_view,ring_off", [(0, 0, 0), (14, 128, 5)])
+def test_minimum_sizes(engine, link_hdr, first_view, ring_off):
+    """The minimum-size rows (tests/pktgen.py MIN_SIZE; ICMPv6 8 B,
+    network/ipv6/icmp.go:68) in a host ring small enough for the BAR stage:
+    the oracle's verdicts and sums, the device ring's, and the reference's
+    verdict table."""
+    from pktgen import min_size_frames
+
+    rng = np.random.default_rng(5960 + link_hdr)
+    frames, want = min_size_frames(rng, link_hdr)
+    arena, ln = _ring(frames, 128, ring_off=ring_off)
+    ring = dict(ring_off=ring_off, stride=128, n=len(frames), link_hdr=link_hdr, first_view=first_view)
+    verdict, sums = engine.rx_ring_host(arena, ring, ln)
+    wv, ws = _want(arena, ln, ring)
+    assert np.array_equal(verdict, wv) and np.array_equal(sums, ws)
+    assert verdict.tolist() == want
+
+
 @pytest.mark.parametrize("ring_off", [0, 3, 1000])
 def test_small_staging_and_unaligned_ring(oracle_mod, ring_off):
     """A staging budget of 7 slots: the ring goes up in chunks that cycle

@@ -8,7 +8,7 @@
 //   8-waves/SIMD register floor
 // Not part of the product ABI.
 #include "../netstack_amd/csrc/csum_kernels.hip"
-#include "../netstack_amd/csrc/tbl_ring.hip"
+#include "tbl_ring.hip"
 
 extern "C" int grpv_launch(int k, const uint8_t* arena, uint64_t bytes, const void* desc, uint32_t n, uint16_t* out,
                            unsigned long long* err, void* stream) {
