@@ -326,8 +326,14 @@ struct ns_csum_ctx {
   hipEvent_t done[kMaxHostSlots] = {};
   std::mutex pmu;
   // Zero-copy passes and ns_csum_sync run on zstream, a stream of their own
-  // (at the greatest priority like the pipeline's: a hardware queue apart
-  // from callers' streams and from the pipeline), under mu.
+  // at the greatest priority like the pipeline's, under mu.  That puts it on
+  // a hardware queue apart from callers' (normal-priority) streams, but with
+  // four pipeline streams at that priority and GPU_MAX_HW_QUEUES = 4 it
+  // shares one with a pipeline stream: a pass may run behind one chunk's
+  // copy and kernel there.  Measured (profiles/r06/latency/, 1 KiB passes
+  // during 0.6 GB host TX calls): longest pass 29.5-81.8 us with 4 slots,
+  // 33.3-36.3 us with 3 (NS_CSUM_HOST_SLOTS=3), no late pass either way;
+  // tests/test_gpu_tx_host.py asserts the longest pass under 1 ms.
   hipStream_t zstream = nullptr;
   unsigned long long* d_err = nullptr;
   std::mutex mu;  // guards everything below but the pipeline's state
