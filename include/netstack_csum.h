@@ -550,15 +550,18 @@ int ns_csum_get_stats(ns_csum_ctx* ctx, ns_csum_stats* out, int reset);
 
 /* A/B and test knobs of ns_csum_tcp_tx on this context (no reference
  * counterpart; every result is the same whatever they are): variant (0 =
- * production; 1 one fused pass, 2 nontemporal write-back, 3 segments reduced
- * over the wave, 4 the one-shot header pass, 5 the payload pass in 8-lane
- * groups),
+ * production: the payload pass in 8-lane groups, header stores written
+ * through; 1 one fused pass; with the windowed payload pass: 2 nontemporal
+ * write-back, 3 segments reduced over the wave, 4 the one-shot header pass;
+ * 5 the group pass with default-policy header stores; 6 round 5's
+ * production, windowed with default-policy stores),
  * tile / htile (segments per wave of the fused pass or the windowed payload
- * pass, and of the header pass; 0 = the launcher's choice), passes (0 = by
+ * pass — a tile set here selects the windowed pass — and of the header
+ * pass; 0 = the launcher's choice), passes (0 = by
  * size, 1 = fused, 2 = two passes).  Read by each call without a lock; set
  * them while no ns_csum_tcp_tx call runs on the context.  ns_csum_init takes
  * their initial values from NS_CSUM_TX_VARIANT / _TILE / _HTILE / _PASSES,
- * once.  NS_EINVAL for a variant above 5 or passes above 2.                 */
+ * once.  NS_EINVAL for a variant above 6 or passes above 2.                 */
 int ns_csum_set_tx_tuning(ns_csum_ctx* ctx, uint32_t variant, uint32_t tile, uint32_t htile,
                           uint32_t passes);
 

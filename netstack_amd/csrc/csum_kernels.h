@@ -114,10 +114,12 @@ struct TxGeo {
 // against one: 16 MB 15.5 vs 13.1 us, 191 MB 41.2 vs 42.5, 383 MB 72.2 vs
 // 76.6, 1.5 GB 246 vs 271 (profiles/r04/tx_struct/sizes/).
 constexpr uint64_t kTxTwoPassMinBytes = 64ull << 20;
-// variant (A/B diagnostics; 0 = production): 1 = one fused pass,
-// 2 = nontemporal write-back, 3 = segments reduced over the wave in the loop,
-// 4 = the one-shot header pass (tcp_tx PH = 2) instead of the persistent one,
-// 5 = the payload pass in 8-lane groups (tcp_tx_pay) instead of the windowed one.
+// variant (A/B diagnostics; 0 = production: the payload pass in 8-lane
+// groups, the header pass's stores nt sc1): 1 = one fused pass, 2 = windowed
+// payload pass + nontemporal write-back, 3 = windowed, segments reduced over
+// the wave in the loop, 4 = windowed + the one-shot header pass (tcp_tx
+// PH = 2), 5 = group payload pass + default-policy header stores, 6 =
+// round 5's production (windowed + default-policy stores).
 hipError_t launch_tcp_tx(TxGeo g, hipStream_t stream, uint32_t variant = 0);
 // Many batches in one fused launch (ns_csum_tcp_tx_multi).  calls[] (host)
 // hold each batch's geometry with n, mode and out set; tx_multi_prepare sets

@@ -156,6 +156,13 @@ __device__ __forceinline__ void tx_store_be16(uint64_t addr, uint32_t v) {
   }
 }
 
+// The header pass's store cache policy (SP): 0 default, 1 nt, then the
+// scope bits, A/B only: 2 sc1, 3 sc0 sc1, 4 nt sc1, 5 sc0, 6 sc0 nt sc1
+// (buffer aux: 1 = sc0, 2 = nt, 16 = sc1).
+constexpr int tx_store_aux(int sp) {
+  return sp == 1 ? 2 : sp == 2 ? 16 : sp == 3 ? 17 : sp == 4 ? 18 : sp == 5 ? 1 : sp == 6 ? 19 : 0;
+}
+
 }  // namespace
 
 // Step 3 of a tile (below): lane l finishes segments s0 + l, s0 + l + 64, ...
@@ -250,7 +257,7 @@ __device__ __forceinline__ void tx_writeback_buf(const uint8_t* L, __amdgpu_buff
     if (at >= lo && at + 16 <= hi) {
       const uint4 x = L4[c];
       __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const __attribute__((ext_vector_type(4))) uint32_t*>(&x),
-                                             hr, (int)at, 0, SP == 1 ? 2 : 0);
+                                             hr, (int)at, 0, tx_store_aux(SP));
     } else {  // a chunk shared with the neighbouring tile: only this tile's bytes
       for (uint32_t k = 0; k < 16; ++k)
         if (at + k >= lo && at + k < hi) __builtin_amdgcn_raw_buffer_store_b8(L[at + k], hr, (int)(at + k), 0, 0);
@@ -476,7 +483,7 @@ __global__ __launch_bounds__(256) void tcp_tx_hdr(TxGeo g, uint32_t ntiles) {
       const uint32_t c = lane + 64u * i;
       const uint4 x = L4[c < chunks ? c : 0u];
       __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const __attribute__((ext_vector_type(4))) uint32_t*>(&x),
-                                             hr, (int)(c * 16u), 0, SP == 1 ? 2 : 0);
+                                             hr, (int)(c * 16u), 0, tx_store_aux(SP));
     }
     return full < chunks;  // an unaligned end: the last tile
   };
@@ -666,7 +673,9 @@ static hipError_t launch_tx_pay_t(const TxGeo& g, hipStream_t stream) {
 template <int U, int AUX, int SP, int RED, int GP = 1>
 static hipError_t launch_payload_pass(const TxGeo& g, hipStream_t stream) {
   if (g.n == 0) return hipSuccess;
-  if (!GP || (g.n + 31) / 32 >= (1ull << 31)) return launch_tcp_tx_t<U, AUX, SP, RED, 0, 1>(g, stream);
+  // a tile forced through ns_csum_set_tx_tuning selects the windowed pass
+  // (the group pass's shape is fixed: 8 segments per wave)
+  if (!GP || g.tile || (g.n + 31) / 32 >= (1ull << 31)) return launch_tcp_tx_t<U, AUX, SP, RED, 0, 1>(g, stream);
   constexpr int A0 = GP == 2 ? 2 : 0;
   switch (tx_pay_lines(g.mss)) {
     case 2: return launch_tx_pay_t<2, A0>(g, stream);
@@ -721,15 +730,17 @@ static hipError_t launch_header_pass(TxGeo h, hipStream_t stream, uint32_t per_c
 // (interleaving the slot write-back with the payload stream
 // cost ~45 us on 1M segments).  One fused pass otherwise.  HP: the header
 // pass persistent (tcp_tx_hdr) or one-shot (tcp_tx PH = 2).
-// GP: the payload pass windowed (0, production) or in 8-lane groups (1).
-// Alone the group pass is faster (1M x 1460 B: 208.6 vs 222.9 us), but with
-// the header pass between calls it is not: over two rotating batches (fresh
-// header slots each call, as sendTCPBatch's NewPacketDescriptors gives)
-// 262.4 vs 245.4 us per call; re-using one batch's slots, 228.5 vs 244.7
-// (tools/tx_struct_probe.py, profiles/r05/tx_pay/).  The header pass leaves
-// 57 MB of dirty lines that reach HBM during the next payload pass; the
-// windowed pass, 6% short of the read ceiling, absorbs those writes, the
-// group pass, at it, pays for them.
+// GP: the payload pass windowed (0) or in 8-lane groups (1, production).
+// SP: the header pass's store policy (tx_store_aux; production 4, nt sc1).
+// With default-policy stores the header pass's 57 MB of slots leave L2
+// within its own dispatch (WRITE_SIZE, profiles/r06/tx_drain/) but stay
+// dirty in the die-level Infinity Cache, which writes them to HBM only when
+// the next call's payload stream evicts them: that pass then takes 244 us
+// instead of 208 over fresh slots (idle time between calls does not help; a
+// 1 GiB read in between takes the cost instead).  nt sc1 stores write them
+// through: the payload pass stays at 211 us and both passes take 237 against
+// 251 for round 5's windowed pass with default stores (which absorbed the
+// eviction 6% below the read ceiling).  tools/tx_drain_probe.py.
 template <int U, int AUX, int SP, int RED, int HP = 1, int GP = 0>
 static hipError_t launch_passes(TxGeo g, hipStream_t stream, uint32_t per_cu = 0) {
   if (!(g.mode & kTxTcpFull) || g.xs == nullptr) return launch_tcp_tx_t<U, AUX, SP, RED>(g, stream);
@@ -781,8 +792,9 @@ hipError_t launch_tcp_tx(TxGeo g, hipStream_t stream, uint32_t variant) {
     case 2: return launch_passes<16, 2, 1, 1>(g, stream);
     case 3: return launch_passes<16, 2, 0, 0>(g, stream);
     case 4: return launch_passes<16, 2, 0, 1, 0>(g, stream);  // the one-shot header pass (round 4)
-    case 5: return launch_passes<16, 2, 0, 1, 1, 1>(g, stream);  // the payload pass in 8-lane groups
-    default: return launch_passes<16, 2, 0, 1>(g, stream);
+    case 5: return launch_passes<16, 2, 0, 1, 1, 1>(g, stream);  // group payload pass, default-policy stores
+    case 6: return launch_passes<16, 2, 0, 1, 1, 0>(g, stream);  // round 5's: windowed, default-policy stores
+    default: return launch_passes<16, 2, 4, 1, 1, 1>(g, stream);  // group payload pass, nt sc1 header stores
   }
 }
 

@@ -103,13 +103,14 @@ def _check(got_arena, got_sums, want_arena, want_sums, what):
 @pytest.mark.parametrize("name", sorted(CASES))
 def test_geometry_bit_exact(engine, oracle_mod, name):
     """Each geometry in every shape: one fused pass (what batches below
-    kTxTwoPassMinBytes take), the payload + header passes (the payload pass
-    windowed), and the same with the payload pass in 8-lane groups, one
-    segment each (variant 5)."""
+    kTxTwoPassMinBytes take), the payload + header passes (production: the
+    payload pass in 8-lane groups, one segment each, header stores written
+    through), the group pass with default-policy stores (variant 5) and
+    round 5's windowed payload pass (variant 6)."""
     geo, total = CASES[name]
     a = _arena(total, geo, seed=len(name))
     wa, ws = _want(oracle_mod, a, geo)
-    for passes, variant in ((1, 0), (2, 0), (2, 5)):
+    for passes, variant in ((1, 0), (2, 0), (2, 5), (2, 6)):
         for offset in (0, 5):
             ga, gs = _run(engine, a, geo, offset=offset, passes=passes, variant=variant)
             _check(ga, gs, wa, ws, f"{name} ({passes} passes, variant {variant}, arena at +{offset})")
@@ -121,7 +122,8 @@ def test_forced_tiles(engine, oracle_mod, tile):
         geo, total = CASES[name]
         a = _arena(total, geo, seed=tile)
         wa, ws = _want(oracle_mod, a, geo)
-        # (the tile is the fused pass's and the windowed payload pass's)
+        # (the tile is the fused pass's and the windowed payload pass's: a
+        # forced tile selects the windowed pass)
         for passes, variant in ((1, 0), (2, 0)):
             ga, gs = _run(engine, a, geo, tile=tile, passes=passes, variant=variant)
             _check(ga, gs, wa, ws, f"{name} tile {tile}, {passes} passes, variant {variant}")

@@ -189,6 +189,54 @@ def rx_set(dev, L):
               f"arena={arena.numel()} n={n} shape=calib2164", flush=True)
 
 
+def cfg4probe_set(dev, L):
+    """cfg4 as the bench runs it (2 rotating arenas and tables), its two
+    packet classes alone (the other class's lengths set to 0, the arena
+    unchanged: tools/cfg4_split.py), cfg2 rotated, and the calibration reads
+    in the two access shapes cfg4's kernel uses (8-lane nontemporal groups,
+    calib2164; per-lane runs of 4 chunks, calib400): which counter per byte
+    separates cfg4 from a byte-weighted mix of the two reads.
+    Each variant: REPS launches to cycle the arenas in (label _warm), then
+    REPS measured, alternating arenas (batch k's table with arena k)."""
+    sp = torch.cuda.current_stream(dev).cuda_stream
+    buf = torch.ones(CAL_BYTES, dtype=torch.uint8, device=dev)
+    outb = torch.zeros(65536, dtype=torch.int32, device=dev)
+    for mode in (400, 2164):
+        for _ in range(REPS):
+            assert L.nsk_calib_launch(mode, buf.data_ptr(), CAL_BYTES, outb.data_ptr(), 8192, sp) == 0
+        torch.cuda.synchronize()
+        print(f"LABEL calib{mode} bytes={CAL_BYTES}", flush=True)
+    del buf
+    torch.cuda.empty_cache()
+    eng = Engine(0)
+    for cfg in (2, 4):
+        b = W.config(cfg)
+        arenas = [b.arena_device(dev), W.random_bytes_torch(b.seed + 77, b.arena_bytes, dev)]
+        a = b.desc["off"] & np.uint64(15)
+        nch = ((a + b.desc["len"].astype(np.uint64) - np.uint64(1)) >> np.uint64(4)) + np.uint64(1)
+        big = nch >= 40
+        variants = [("all", np.ones(b.n, bool))] + ([("big", big), ("small", ~big)] if cfg == 4 else [])
+        out = torch.empty(b.n, dtype=torch.int16, device=dev)
+        for name, keep in variants:
+            d = b.desc.copy()
+            d["len"] = np.where(keep, d["len"], 0)
+            t = torch.from_numpy(d.view(np.uint8).copy()).to(dev)
+            ts = [t, t.clone()]
+            for k in range(REPS):  # cycle in (tools/pmc_parse.py matches REPS dispatches per label)
+                eng.batch_tensors(arenas[(k + 1) % 2], ts[(k + 1) % 2], out)
+            torch.cuda.synchronize()
+            print(f"LABEL cfg{cfg}_{name}_warm n={b.n}", flush=True)
+            for k in range(REPS):
+                eng.batch_tensors(arenas[k % 2], ts[k % 2], out)
+            torch.cuda.synchronize()
+            payload = int(d["len"].sum(dtype=np.uint64))
+            share = float(d["len"][big].sum(dtype=np.uint64)) / max(payload, 1)
+            print(f"LABEL cfg{cfg}_{name} algorithmic_bytes={payload + 18 * b.n} payload={payload} "
+                  f"arena={b.arena_bytes} n={b.n} big_share={share:.4f} rotated=2", flush=True)
+        del arenas, out
+        torch.cuda.empty_cache()
+
+
 def cfg3probe_set(dev, L):
     names = [L.nsk_tune_name(v).decode() for v in range(L.nsk_tune_count())]
     sp = torch.cuda.current_stream(dev).cuda_stream
@@ -209,7 +257,7 @@ def cfg3probe_set(dev, L):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--set", default="main", choices=("main", "cfg3probe", "rx"))
+    ap.add_argument("--set", default="main", choices=("main", "cfg3probe", "rx", "cfg4probe"))
     args = ap.parse_args()
     L = ctypes.CDLL(os.path.join(ROOT, "netstack_amd", "lib", "libns_tune.so"))
     L.nsk_calib_launch.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
@@ -225,6 +273,8 @@ def main():
         main_set(dev, L)
     elif args.set == "rx":
         rx_set(dev, L)
+    elif args.set == "cfg4probe":
+        cfg4probe_set(dev, L)
     else:
         cfg3probe_set(dev, L)
 

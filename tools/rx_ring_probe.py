@@ -28,7 +28,7 @@ from netstack_amd import workloads as W  # noqa: E402
 
 NAMES = {0: "product", 1: "all_default", 2: "all_nt", 3: "wg2", 4: "wg8", 5: "wg1", 6: "nb16", 7: "nb8",
          8: "occ6", 9: "nb12", 10: "checked_f0", 11: "f1_nb8", 12: "spec_line0", 13: "spec_lines01",
-         14: "rotated_lines"}
+         14: "rotated_lines", 20: "bufs_product", 21: "bufs_nt_sc1", 22: "bufs_all_default", 23: "bufs_sc1"}
 
 
 class RxGeo(ctypes.Structure):
@@ -49,6 +49,9 @@ def main():
                          "beside the others as 'prev' (an A/B on one box)")
     ap.add_argument("--rotate", type=int, default=1, help="alternate two rings (1) or re-read one (0)")
     ap.add_argument("--stride", type=int, default=0, help="slot spacing (a multiple of 16 >= 1504; 0: 1504)")
+    ap.add_argument("--bufs", default="", choices=("", "shuffled", "ring"),
+                    help="the frames as a buffer list (ns_csum_rx_bufs) in shuffled or ring order; variants "
+                         "20-23 then (the ring variants need no list)")
     ap.add_argument("--trend", type=int, default=0,
                     help="then time this many back-to-back launches of the product one by one (run-long drift)")
     args = ap.parse_args()
@@ -71,7 +74,14 @@ def main():
     arena, lens, bad = W.rx_ring_batch(n, 9, dev, corrupt_every=1000)
     arena = spread(arena)
     ring = dict(stride=stride, n=n)
-    v0, s0 = eng.rx_ring(arena, ring, lens)
+    offs = None
+    if args.bufs:  # packet k is the frame in slot perm[k] (bench.py --rx-layout bufs)
+        perm = np.random.default_rng(9).permutation(n) if args.bufs == "shuffled" else np.arange(n)
+        offs = torch.from_numpy((perm.astype(np.int64) * stride).astype(np.int32)).to(dev)
+        lens = lens[torch.from_numpy(perm).to(dev)].contiguous()
+        v0, s0 = eng.rx_bufs(arena, ring, offs, lens)
+    else:
+        v0, s0 = eng.rx_ring(arena, ring, lens)
     torch.cuda.synchronize()
     err = torch.zeros(1, dtype=torch.int64, device=dev)
     verdict = torch.empty(n, dtype=torch.uint8, device=dev)
@@ -80,10 +90,12 @@ def main():
     # bench.py runs it
     arena2 = spread(W.rx_ring_batch(n, 9, dev, corrupt_every=1000)[0]) if args.rotate else arena
     gs = [RxGeo(a.data_ptr(), stride, lens.data_ptr(), sums.data_ptr(), verdict.data_ptr(), err.data_ptr(),
-                n, 0, 0, 0) for a in (arena, arena2)]
+                n, 0, 0, 0, offs.data_ptr() if offs is not None else None, a.numel() if offs is not None else 0)
+          for a in (arena, arena2)]
     g = gs[0]
     algo = n * (W.RX_PKT + 9)
-    ks = [int(k) for k in args.only.split(",")] if args.only else sorted(NAMES)
+    ks = [int(k) for k in args.only.split(",")] if args.only else \
+        sorted(k for k in NAMES if (k >= 20) == bool(args.bufs))
     libs = {k: lib for k in ks}
     names = dict(NAMES)
     if args.prev:
@@ -129,7 +141,7 @@ def main():
         q = max(1, args.trend // 10)
         trend = {"per_launch_us": [round(x, 1) for x in t],
                  "first_decile_us": round(float(np.median(t[:q])), 2), "last_decile_us": round(float(np.median(t[-q:])), 2)}
-    print(json.dumps({"workload": f"1M x 1500-B IPv4/TCP in {stride}-B slots" + (", 2 rotating rings" if args.rotate else ", one ring re-read"), "algo_bytes": algo, "variants": out,
+    print(json.dumps({"workload": f"1M x 1500-B IPv4/TCP in {stride}-B slots" + (", 2 rotating rings" if args.rotate else ", one ring re-read") + (f", a buffer list in {args.bufs} order" if args.bufs else ""), "algo_bytes": algo, "variants": out,
                       "trend": trend}, indent=1))
 
 

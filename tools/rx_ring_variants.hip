@@ -11,6 +11,8 @@
 //  11 F with 8 lines per batch
 //  12 / 13 line 0 / lines 0-1 loaded before the slot's length arrives
 //  14 the product shape with each group's lines >= 2 in a rotated order
+//  20-23 buffer lists (LIST = 1, g.off set): the product shape, then lines
+//        >= 1 with the policy nt sc1 / default / sc1 instead of nt
 // Every variant computes the same verdicts and sums.  Not part of the ABI.
 #include "../netstack_amd/csrc/rx_ring.hip"
 
@@ -31,6 +33,10 @@ extern "C" int rxv_launch(const nsk::RxGeo* g, void* stream, int k) {
     case 12: return (int)nsk::launch_rx_ring_t<13, 0, 2, 4, 1, 1, 1>(*g, s);
     case 13: return (int)nsk::launch_rx_ring_t<13, 0, 2, 4, 1, 1, 2>(*g, s);
     case 14: return (int)nsk::launch_rx_ring_t<13, 0, 2, 4, 1, 1, 0, 0, 1>(*g, s);
+    case 20: return (int)nsk::launch_rx_ring_t<13, 0, 2, 4, 1, 1, 0, 1>(*g, s);
+    case 21: return (int)nsk::launch_rx_ring_t<13, 0, 18, 4, 1, 1, 0, 1>(*g, s);
+    case 22: return (int)nsk::launch_rx_ring_t<13, 0, 0, 4, 1, 1, 0, 1>(*g, s);
+    case 23: return (int)nsk::launch_rx_ring_t<13, 0, 16, 4, 1, 1, 0, 1>(*g, s);
     default: return (int)nsk::launch_rx_ring_t<13>(*g, s);
   }
 }

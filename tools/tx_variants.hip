@@ -23,7 +23,8 @@
 //   pass (whatever the product's default); 36 / 37 / 38 = the floors of
 //   19 / 20 / 21 with lane-consecutive chunks (1 KiB per wave instruction);
 //   40-43 = the persistent header pass alone at 8 / 16 / 32 / 48 waves per
-//   CU, 44 = the one-shot header pass alone (htile: the header tile).
+//   CU, 44 = the one-shot header pass alone (htile: the header tile);
+//   70-76 = the persistent header pass alone, store policies (tx_store_aux).
 // Not part of the product ABI.
 #include "../netstack_amd/csrc/tcp_tx.hip"
 
@@ -169,6 +170,19 @@ extern "C" int txv_launch(const nsk::TxGeo* g, void* stream, int k) {
     case 37: e = launch_floor_co<1>(*g, s); break;
     case 38: e = launch_floor_co<2>(*g, s); break;
     case 35: e = nsk::launch_passes<16, 2, 0, 1, 1, 1>(*g, s); break;
+    // 70-76: the persistent header pass alone with store policy SP = k - 70
+    // (tcp_tx.hip tx_store_aux: default, nt, sc1, sc0 sc1, nt sc1, sc0,
+    // sc0 nt sc1)
+    case 70: case 71: case 72: case 73: case 74: case 75: case 76: {
+      nsk::TxGeo h = *g;
+      h.tile = g->htile;
+      const int sp = k - 70;
+      e = sp == 0 ? nsk::launch_header_pass<0>(h, s, 0) : sp == 1 ? nsk::launch_header_pass<1>(h, s, 0)
+        : sp == 2 ? nsk::launch_header_pass<2>(h, s, 0) : sp == 3 ? nsk::launch_header_pass<3>(h, s, 0)
+        : sp == 4 ? nsk::launch_header_pass<4>(h, s, 0) : sp == 5 ? nsk::launch_header_pass<5>(h, s, 0)
+        : nsk::launch_header_pass<6>(h, s, 0);
+      break;
+    }
     default: e = nsk::launch_tcp_tx_t<16, 2, 0, 1>(*g, s); break;
   }
   return (int)e;
