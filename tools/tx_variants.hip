@@ -24,9 +24,136 @@
 //   19 / 20 / 21 with lane-consecutive chunks (1 KiB per wave instruction);
 //   40-43 = the persistent header pass alone at 8 / 16 / 32 / 48 waves per
 //   CU, 44 = the one-shot header pass alone (htile: the header tile);
-//   70-76 = the persistent header pass alone, store policies (tx_store_aux).
+//   70-76 = the persistent header pass alone, store policies (tx_store_aux);
+//   77 / 78 = one pass in the group shape, slots written through / default.
 // Not part of the product ABI.
 #include "../netstack_amd/csrc/tcp_tx.hip"
+
+
+// Measured (round 6, bench.py --config 8, two rotating batches, three
+// interleaved runs each; profiles/r06/tx_onepass/): 265.8 us with
+// written-through slot stores, 279 us with default-policy ones, against
+// 235.6-236.2 us for the two passes: the slot writes interleaved with the
+// payload stream cost ~56 us, write-through or not.  The product keeps two
+// passes.
+namespace nsk {
+// One pass in the group shape (timing variants 77 / 78; round 6): tcp_tx_pay's payload loop,
+// then the wave finishes its own 8 segments' header slots, which sit back to
+// back (8 x slot bytes from a 16-B-aligned start): the slot chunks are loaded
+// with the payload (lane c: chunk c), parked in the wave's LDS row after the
+// payload sums, segment g's fields computed by lane 8g from there (its
+// group's W in registers: no payload value goes through memory), and the
+// chunks written back with store policy SP.  For regions of at most 1 KiB
+// (slot <= 128) that start 16-B aligned; the last wave's ragged end is
+// written byte by byte.
+template <int NB, int SP>
+__global__ __launch_bounds__(256) void tcp_tx_payhdr(TxGeo g) {
+  __shared__ uint4 ph_lds[4][64];
+  const uint32_t lane = threadIdx.x & 63u, grp = lane >> 3, li = lane & 7u;
+  const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t s0 = ((uint64_t)blockIdx.x * 4u + wv) * 8u;
+  if (s0 >= g.n) return;  // a whole wave leaves together
+  const uint64_t s = s0 + grp;
+  const uint64_t tail0 = (g.n - 1) * (uint64_t)g.mss;
+  const uint32_t sz = s < g.n ? (s + 1 < g.n ? g.mss : (uint32_t)(g.size - tail0)) : 0u;
+  const uint64_t wbase = (g.pay + s0 * g.mss) & ~127ull;
+  const uint64_t s_end = s0 + 8u < g.n ? s0 + 8u : g.n;
+  const uint32_t nseg = (uint32_t)(s_end - s0);
+  const uint64_t w_end = g.pay + (s_end < g.n ? s_end * (uint64_t)g.mss : g.size);
+  const uint32_t nrec = (uint32_t)((w_end - wbase + 15u) & ~15ull);
+  const __amdgpu_buffer_rsrc_t r = tx_srd(wbase, nrec);
+  // the wave's header slots: chunk `lane` (the last chunk may reach up to 15
+  // bytes past the region, inside its own aligned 16 B)
+  const uint64_t h_lo = g.hdr + s0 * g.slot;
+  const uint32_t hbytes = nseg * g.slot, hchunks = (hbytes + 15u) >> 4;
+  const __amdgpu_buffer_rsrc_t hr = tx_srd(h_lo, hchunks * 16u);
+  const uint4 hv = tx_load<0>(hr, lane < hchunks ? lane * 16u : hchunks * 16u);
+  const uint32_t pa = sz ? (uint32_t)(g.pay + s * g.mss - wbase) : 0u;
+  const uint32_t pe = pa + sz;
+  const uint32_t cl = (pa & ~127u) + 16u * li;
+  const uint32_t klast = sz && pe > cl ? (pe - 1u - cl) >> 7 : 0u;
+  const uint32_t cl1 = sz && pe > cl + 128u ? cl : nrec;
+  const bool in0 = sz && cl + 16u > pa && cl < pe;
+  const uint32_t tc = (pe - 1u) & ~15u;
+  const bool owner = sz && ((tc >> 4) & 7u) == li;
+  uint4 v[NB];
+  v[0] = tx_load<0>(r, in0 ? cl : nrec);
+  const uint4 t = tx_load<0>(r, owner ? tc : nrec);
+#pragma unroll
+  for (int k = 1; k < NB; ++k) v[k] = tx_load<2>(r, ((uint32_t)k <= klast ? cl1 : nrec) + 128u * k);
+  uint32_t w = tx_bytes_from(v[0], pa > cl ? (int)(pa - cl) : 0);
+#pragma unroll
+  for (int k = 1; k < NB; ++k) w = wsum4(v[k], w);
+  for (uint32_t k0 = NB; __builtin_amdgcn_ballot_w64(k0 <= klast) != 0; k0 += 4) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) w = wsum4(tx_load<2>(r, ((k0 + k) <= klast ? cl1 : nrec) + 128u * (k0 + k)), w);
+  }
+  if (owner) w -= tx_bytes_from(t, (int)(pe - tc));
+  w += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)w, 0xB1, 0xF, 0xF, false);
+  w += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)w, 0x4E, 0xF, 0xF, false);
+  w += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)w, 0x141, 0xF, 0xF, false);
+  // the slots into the wave's LDS row
+  uint4* L4 = ph_lds[wv];
+  uint8_t* L = reinterpret_cast<uint8_t*>(L4);
+  if (lane < hchunks) L4[lane] = hv;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  if (li == 0 && s < g.n) {  // tcp_tx_hdr's arithmetic for segment s
+    const uint32_t o = grp * g.slot;
+    uint32_t ipv = 0;
+    if (g.mode & kTxIp) {
+      const uint32_t a = o + g.ip_at;
+      ipv = tx_fold(tx_class(lds_wsum_loop(L, a, g.ip_len, a + 10u), a & 1u));  // Checksum(ip[:IHL], 0)
+      lds_put_be16(L, a + 10u, ~ipv & 0xFFFFu);
+    }
+    uint32_t x = tx_fold(g.addr_sum + ((g.tcp_len + sz) & 0xFFFFu));  // PseudoHeaderChecksum
+    x = tx_fold(x + g.proto);
+    const uint32_t a = o + g.tcp_at;
+    x = tx_fold(x + tx_class(w, (uint32_t)((g.pay + s * g.mss) & 1u)));       // ChecksumVVWithOffset
+    x = tx_fold(x + tx_class(lds_wsum_loop(L, a, g.tcp_len, a + 16u), a & 1u));  // CalculateChecksum
+    lds_put_be16(L, a + 16u, ~x & 0xFFFFu);
+    if (g.out) *reinterpret_cast<uint32_t*>(g.out + 2 * s) = ipv | (x << 16);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const uint32_t full = hbytes >> 4;
+  const __amdgpu_buffer_rsrc_t hw = tx_srd(h_lo, full * 16u);
+  const uint4 xv = L4[lane < hchunks ? lane : 0u];
+  __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const __attribute__((ext_vector_type(4))) uint32_t*>(&xv),
+                                         hw, (int)(lane < full ? lane * 16u : full * 16u), 0, tx_store_aux(SP));
+  if (full < hchunks && lane < (hbytes & 15u))  // the last wave's ragged end
+    reinterpret_cast<uint8_t*>((uintptr_t)(h_lo + full * 16u))[lane] = L[full * 16u + lane];
+}
+
+template <int NB, int SP>
+static hipError_t launch_tx_payhdr_t(const TxGeo& g, hipStream_t stream) {
+  const uint64_t wgs = (g.n + 31) / 32;
+  hipLaunchKernelGGL((tcp_tx_payhdr<NB, SP>), dim3((uint32_t)wgs), dim3(256), 0, stream, g);
+  return hipGetLastError();
+}
+
+// 77 / 78's conditions: full TCP mode with whole slots written back, each
+// wave's 8 slots 16-B aligned and at most 1 KiB, d_out 4-B aligned.
+static bool tx_payhdr_ok(const TxGeo& g) {
+  return (g.mode & kTxTcpFull) && !(g.mode & kTxFieldsOnly) && !(g.hdr & 15) && (8u * g.slot) % 16 == 0 &&
+         g.slot <= 128 && !((uintptr_t)g.out & 3) && (g.n + 31) / 32 < (1ull << 31);
+}
+
+template <int SP>
+static hipError_t launch_payhdr(const TxGeo& g, hipStream_t stream) {
+  if (g.n == 0) return hipSuccess;
+  switch (tx_pay_lines(g.mss)) {
+    case 2: return launch_tx_payhdr_t<2, SP>(g, stream);
+    case 4: return launch_tx_payhdr_t<4, SP>(g, stream);
+    case 8: return launch_tx_payhdr_t<8, SP>(g, stream);
+    case 13: return launch_tx_payhdr_t<13, SP>(g, stream);
+    default: return launch_tx_payhdr_t<16, SP>(g, stream);
+  }
+}
+
+}  // namespace nsk
 
 namespace {
 // FL: 0 read + write back, 1 read only (one dword per wave out), 2 write only
@@ -170,6 +297,11 @@ extern "C" int txv_launch(const nsk::TxGeo* g, void* stream, int k) {
     case 37: e = launch_floor_co<1>(*g, s); break;
     case 38: e = launch_floor_co<2>(*g, s); break;
     case 35: e = nsk::launch_passes<16, 2, 0, 1, 1, 1>(*g, s); break;
+    // 77 / 78: one pass, the group payload loop + the wave's own slots,
+    // written through (nt sc1) / default policy (falls back to production
+    // where its conditions fail)
+    case 77: e = nsk::tx_payhdr_ok(*g) ? nsk::launch_payhdr<4>(*g, s) : nsk::launch_tcp_tx(*g, s, 0); break;
+    case 78: e = nsk::tx_payhdr_ok(*g) ? nsk::launch_payhdr<0>(*g, s) : nsk::launch_tcp_tx(*g, s, 0); break;
     // 70-76: the persistent header pass alone with store policy SP = k - 70
     // (tcp_tx.hip tx_store_aux: default, nt, sc1, sc0 sc1, nt sc1, sc0,
     // sc0 nt sc1)
