@@ -138,8 +138,13 @@ __device__ __forceinline__ uint4 rx_load(__amdgpu_buffer_rsrc_t r, uint32_t off)
 // group g reads line 2 + (k - 2 + 3 g) mod (NB - 2), so the eight groups of
 // a wave do not all ask for line k of their slots at once (the same lines
 // are loaded and summed whole: the sums do not change).
+// LL = 1 (timing variant, tools/rx_ring_variants.hip): the packet's last
+// line (the one it may share with the next buffer) with the default cache
+// policy, its other lines >= 1 with AN, through two predicated loads of which
+// one reads nothing; only lines NB - 2 and NB - 1 (where an MTU frame ends)
+// get the pair.
 template <int NB, int A0 = 0, int AN = 2, int WV = kWaves, int OCC = 1, int F = 1, int SPEC = 0, int LIST = 0,
-          int ROT = 0>
+          int ROT = 0, int LL = 0>
 __global__ __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(OCC))) void rx_ring(RxGeo g) {
   __shared__ uint4 rx_lds[WV * kPerWave * kRowBytes / 16];
   const uint32_t lane = threadIdx.x & 63u, grp = lane >> 3, li = lane & 7u;
@@ -214,7 +219,17 @@ __global__ __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(OCC))) 
     v[0] = rx_load<A0>(rsrc, off_of(cl));
   }
   const uint32_t rot = ROT && NB > 3 ? (3u * grp) % (uint32_t)(NB > 3 ? NB - 2 : 1) : 0u;
+  // LL: the group's last line holding packet bytes
+  const uint32_t kgl = LL && Pl ? (pe - 1u - (pa & ~127u)) >> 7 : 0xFFFFFFFFu;
   auto line = [&](int k) {
+    if constexpr (F && LL) if (k >= NB - 2) {  // (the lines an MTU frame can end in: a probe)
+      const uint32_t o = ((uint32_t)k <= klast ? cl1 : nrec) + 128u * k;
+      const bool last = (uint32_t)k == kgl;
+      const uint4 x = rx_load<AN>(rsrc, last ? nrec + 128u * k : o);
+      const uint4 y = rx_load<0>(rsrc, last ? o : nrec + 128u * k);
+      v[k] = make_uint4(x.x | y.x, x.y | y.y, x.z | y.z, x.w | y.w);
+      return;
+    }
     if constexpr (F && ROT && NB > 3) {
       if (k >= 2) {
         uint32_t kk = (uint32_t)k + rot;
@@ -431,11 +446,11 @@ static int rx_batch_lines(const RxGeo& g) {
 }
 
 template <int NB, int A0 = 0, int AN = 2, int WV = kWaves, int OCC = 1, int F = 1, int SPEC = 0, int LIST = 0,
-          int ROT = 0>
+          int ROT = 0, int LL = 0>
 static hipError_t launch_rx_ring_t(const RxGeo& g, hipStream_t stream) {
   if (g.n == 0) return hipSuccess;
   const uint64_t per_wg = (uint64_t)WV * kPerWave;
-  hipLaunchKernelGGL((rx_ring<NB, A0, AN, WV, OCC, F, SPEC, LIST, ROT>),
+  hipLaunchKernelGGL((rx_ring<NB, A0, AN, WV, OCC, F, SPEC, LIST, ROT, LL>),
                      dim3((uint32_t)((g.n + per_wg - 1) / per_wg)), dim3(64 * WV), 0, stream, g);
   return hipGetLastError();
 }

@@ -130,8 +130,9 @@ def main_set(dev, L):
     torch.cuda.empty_cache()
     # cfg 8 as bench.py runs it by default: the same layout filled from its
     # geometry (ns_csum_tcp_tx: a payload pass and a header pass per call, so
-    # 2 dispatches per launch; the payload is read in whole 1-KiB windows per
-    # wave instruction, nontemporal: the coalesced calibration shape)
+    # 2 dispatches per launch; since round 6 the payload is read by 8-lane
+    # groups, one whole 128-B line per group per instruction, nontemporal
+    # past line 0: the group calibration shape)
     arena, _ = W.tx_split_batch(n, 7000, dev)
     geo = W.tx_struct_geometry(n)
     for _ in range(REPS):
@@ -139,7 +140,7 @@ def main_set(dev, L):
     torch.cuda.synchronize()
     algo = n * W.RX_PKT + 4 * n
     print(f"LABEL cfg8struct algorithmic_bytes={algo} payload={n * W.RX_PKT} arena={arena.numel()} n={n} "
-          f"kernels=2 shape=calib102", flush=True)
+          f"kernels=2 shape=calib2164", flush=True)
     del arena
     torch.cuda.empty_cache()
 

@@ -13,6 +13,8 @@
 //  14 the product shape with each group's lines >= 2 in a rotated order
 //  20-23 buffer lists (LIST = 1, g.off set): the product shape, then lines
 //        >= 1 with the policy nt sc1 / default / sc1 instead of nt
+//  24-25 buffer lists with each packet's last line at the default policy
+//        (LL), the other lines >= 1 nt / nt sc1
 // Every variant computes the same verdicts and sums.  Not part of the ABI.
 #include "../netstack_amd/csrc/rx_ring.hip"
 
@@ -37,6 +39,8 @@ extern "C" int rxv_launch(const nsk::RxGeo* g, void* stream, int k) {
     case 21: return (int)nsk::launch_rx_ring_t<13, 0, 18, 4, 1, 1, 0, 1>(*g, s);
     case 22: return (int)nsk::launch_rx_ring_t<13, 0, 0, 4, 1, 1, 0, 1>(*g, s);
     case 23: return (int)nsk::launch_rx_ring_t<13, 0, 16, 4, 1, 1, 0, 1>(*g, s);
+    case 24: return (int)nsk::launch_rx_ring_t<13, 0, 2, 4, 1, 1, 0, 1, 0, 1>(*g, s);
+    case 25: return (int)nsk::launch_rx_ring_t<13, 0, 18, 4, 1, 1, 0, 1, 0, 1>(*g, s);
     default: return (int)nsk::launch_rx_ring_t<13>(*g, s);
   }
 }
