@@ -1,14 +1,16 @@
 set -e
 # Every bench line of a round, on the GPU box: tools/final_round.sh TAG
-TAG=${1:-r05}
+TAG=${1:-r06}
 OUT=gpurun_out/final_$TAG
 mkdir -p $OUT
 for c in 1 2 3 4 5 7 8; do
   echo "bench cfg$c"
   timeout -k 10 300 python bench.py --config $c > $OUT/bench_cfg$c.json 2> $OUT/bench_cfg$c.err
 done
-echo "bench cfg7 as a receive ring (ns_csum_rx_ring)"
+echo "bench cfg7 as a receive ring (ns_csum_rx_ring) and as a buffer list (ns_csum_rx_bufs), shuffled and in ring order"
 timeout -k 10 300 python bench.py --config 7 --rx-layout ring > $OUT/bench_cfg7_ring.json 2> $OUT/bench_cfg7_ring.err
+timeout -k 10 300 python bench.py --config 7 --rx-layout bufs --no-cpu > $OUT/bench_cfg7_bufs.json 2> $OUT/bench_cfg7_bufs.err
+timeout -k 10 300 python bench.py --config 7 --rx-layout bufs --bufs-order ring --no-cpu > $OUT/bench_cfg7_bufs_ring.json 2> $OUT/bench_cfg7_bufs_ring.err
 echo "bench cfg8 paired table and wire layout"
 timeout -k 10 300 python bench.py --config 8 --tx-layout split > $OUT/bench_cfg8_split.json 2> $OUT/bench_cfg8_split.err
 timeout -k 10 300 python bench.py --config 8 --tx-layout wire > $OUT/bench_cfg8_wire.json 2> $OUT/bench_cfg8_wire.err
