@@ -56,6 +56,9 @@ def main():
     ap.add_argument("--n", type=int, default=1 << 20)
     ap.add_argument("--only", default="")
     ap.add_argument("--no-check", action="store_true")
+    ap.add_argument("--htile", type=int, default=0, help="header-pass tile (segments per wave; 0: 64)")
+    ap.add_argument("--per-cu", type=int, default=0,
+                    help="header-pass waves per CU (header policy 4 only, txv 90; 0: 24)")
     args = ap.parse_args()
     n = args.n
     dev = torch.device("cuda", 0)
@@ -71,9 +74,12 @@ def main():
     asum = addr_sum(geo["src"], geo["dst"])
 
     def launch(k, a):
+        if k == 74 and (args.per_cu or args.htile):
+            k = 90
         t = TxGeo(hdr=a.data_ptr() + geo["hdr_off"], pay=a.data_ptr() + geo["pay_off"], size=geo["size"], n=n,
                   mss=geo["mss"], slot=geo["slot"], ip_at=geo["ip_at"], ip_len=geo["ip_len"], tcp_at=geo["tcp_at"],
-                  tcp_len=geo["tcp_len"], addr_sum=asum, proto=6, mode=3, xs=xs.data_ptr(), xstride=1)
+                  tcp_len=geo["tcp_len"], addr_sum=asum, proto=6, mode=3, xs=xs.data_ptr(), xstride=1,
+                  htile=args.htile, pad=args.per_cu)
         assert TXV.txv_launch(ctypes.byref(t), stream.cuda_stream, k) == 0
 
     def flush():  # tools/tx_variants.hip 37: a lane-consecutive read of 1 GiB
@@ -118,7 +124,8 @@ def main():
             ok = bool(torch.equal(b, want))
         med = lambda v: v[len(v) // 2]  # noqa: E731
         mean = lambda v: sum(v) / len(v)  # noqa: E731
-        print(json.dumps({"scenario": sc, "payload_pass": p, "header_store_policy": int(h), "rotating_batches": rot,
+        print(json.dumps({"scenario": sc, "htile": args.htile, "per_cu": args.per_cu,
+                          "payload_pass": p, "header_store_policy": int(h), "rotating_batches": rot,
                           "between_calls": gap, "calls": args.calls,
                           "payload_us": {"median": round(med(pt), 2), "mean": round(mean(pt), 2),
                                          "min": round(pt[0], 2), "max": round(pt[-1], 2)},

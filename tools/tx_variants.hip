@@ -25,7 +25,8 @@
 //   40-43 = the persistent header pass alone at 8 / 16 / 32 / 48 waves per
 //   CU, 44 = the one-shot header pass alone (htile: the header tile);
 //   70-76 = the persistent header pass alone, store policies (tx_store_aux);
-//   77 / 78 = one pass in the group shape, slots written through / default.
+//   77 / 78 = one pass in the group shape, slots written through / default;
+//   90 = the production header pass alone at g->pad waves per CU.
 // Not part of the product ABI.
 #include "../netstack_amd/csrc/tcp_tx.hip"
 
@@ -297,6 +298,12 @@ extern "C" int txv_launch(const nsk::TxGeo* g, void* stream, int k) {
     case 37: e = launch_floor_co<1>(*g, s); break;
     case 38: e = launch_floor_co<2>(*g, s); break;
     case 35: e = nsk::launch_passes<16, 2, 0, 1, 1, 1>(*g, s); break;
+    case 90: {  // the production header pass (nt sc1 stores) at g->pad waves per CU (0: 24), tile g->htile
+      nsk::TxGeo h = *g;
+      h.tile = g->htile;
+      e = nsk::launch_header_pass<4>(h, s, g->pad);
+      break;
+    }
     // 77 / 78: one pass, the group payload loop + the wave's own slots,
     // written through (nt sc1) / default policy (falls back to production
     // where its conditions fail)
