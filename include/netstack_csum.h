@@ -394,7 +394,10 @@ typedef struct ns_pkt_buf {
  * INTEGRATION.md §2 says who checks it then); NS_PKB_MALFORMED where IsValid,
  * HandlePacket's fragment checks (no payload, or a uint16
  * FragmentOffset() + size - 1 that wraps: ipv4.go:357-373) or the
- * transport's length checks drop the packet first.
+ * transport's length checks drop the packet first: a transport first view
+ * under 20 B for TCP (or a DataOffset outside [20, that view]) and under 8 B
+ * for UDP (stack/nic.go:851, segment.go:159), ICMPv4 (ipv4/icmp.go:60) and
+ * ICMPv6 (ICMPv6MinimumSize, ipv6/icmp.go:68; not the 4-B ICMPv6HeaderSize).
  * NS_PKB_FILL — a batch to transmit: Header holds the IP header and the
  * transport header (Data the payload); writes ^sum into the transport
  * checksum field — TCP buildTCPHdr (connect.go:653-663), UDP sendUDP
