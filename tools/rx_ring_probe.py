@@ -29,7 +29,8 @@ from netstack_amd import workloads as W  # noqa: E402
 NAMES = {0: "product", 1: "all_default", 2: "all_nt", 3: "wg2", 4: "wg8", 5: "wg1", 6: "nb16", 7: "nb8",
          8: "occ6", 9: "nb12", 10: "checked_f0", 11: "f1_nb8", 12: "spec_line0", 13: "spec_lines01",
          14: "rotated_lines", 20: "bufs_product", 21: "bufs_nt_sc1", 22: "bufs_all_default", 23: "bufs_sc1",
-         24: "bufs_lastline_default", 25: "bufs_lastline_default_nt_sc1"}
+         24: "bufs_lastline_default", 25: "bufs_lastline_default_nt_sc1", 26: "bufs_ll_sc0_nt",
+         27: "bufs_ll_sc0_sc1", 28: "bufs_ll_sc0_nt_sc1", 29: "bufs_ll_sc0"}
 
 
 class RxGeo(ctypes.Structure):

@@ -13,8 +13,9 @@
 //  14 the product shape with each group's lines >= 2 in a rotated order
 //  20-23 buffer lists (LIST = 1, g.off set): the product shape, then lines
 //        >= 1 with the policy nt sc1 / default / sc1 instead of nt
-//  24-25 buffer lists with each packet's last line at the default policy
-//        (LL), the other lines >= 1 nt / nt sc1
+//  24-29 buffer lists with each packet's last line at the default policy
+//        (LL), the other lines >= 1 nt / nt sc1 / sc0 nt / sc0 sc1 /
+//        sc0 nt sc1 / sc0
 // Every variant computes the same verdicts and sums.  Not part of the ABI.
 #include "../netstack_amd/csrc/rx_ring.hip"
 
@@ -41,6 +42,10 @@ extern "C" int rxv_launch(const nsk::RxGeo* g, void* stream, int k) {
     case 23: return (int)nsk::launch_rx_ring_t<13, 0, 16, 4, 1, 1, 0, 1>(*g, s);
     case 24: return (int)nsk::launch_rx_ring_t<13, 0, 2, 4, 1, 1, 0, 1, 0, 1>(*g, s);
     case 25: return (int)nsk::launch_rx_ring_t<13, 0, 18, 4, 1, 1, 0, 1, 0, 1>(*g, s);
+    case 26: return (int)nsk::launch_rx_ring_t<13, 0, 3, 4, 1, 1, 0, 1, 0, 1>(*g, s);
+    case 27: return (int)nsk::launch_rx_ring_t<13, 0, 17, 4, 1, 1, 0, 1, 0, 1>(*g, s);
+    case 28: return (int)nsk::launch_rx_ring_t<13, 0, 19, 4, 1, 1, 0, 1, 0, 1>(*g, s);
+    case 29: return (int)nsk::launch_rx_ring_t<13, 0, 1, 4, 1, 1, 0, 1, 0, 1>(*g, s);
     default: return (int)nsk::launch_rx_ring_t<13>(*g, s);
   }
 }
