@@ -415,7 +415,8 @@ __global__ __launch_bounds__(256) void tcp_tx(TxGeo g) {
 // for all of them.  For tiles that start 16-B aligned (hdr, tile * slot) and
 // hold at most 64 segments and 64 CPL chunks; the last tile's unaligned end
 // is written with byte stores as the wave's last act.
-template <int CPL, int SP>
+// DEP = tiles in flight per wave (2; 3 as a timing variant).
+template <int CPL, int SP, int DEP = 2>
 __global__ __launch_bounds__(256) void tcp_tx_hdr(TxGeo g, uint32_t ntiles) {
   extern __shared__ uint4 tx_lds[];
   const uint32_t lane = threadIdx.x & 63u;
@@ -498,6 +499,32 @@ __global__ __launch_bounds__(256) void tcp_tx_hdr(TxGeo g, uint32_t ntiles) {
   uint32_t px = 0, py = 0;
   fetch(t0, x, px);
   fetch(t0 + NW, y, py);
+  if constexpr (DEP == 3) {
+    uint4 z[CPL];
+    uint32_t pz = 0;
+    fetch(t0 + 2 * NW, z, pz);
+    for (uint32_t t = t0;; t += 3 * NW) {
+      if (finish(t, x, px)) {
+        tail(t);
+        break;
+      }
+      fetch(t + 3 * NW, x, px);
+      if (t + NW >= ntiles) break;
+      if (finish(t + NW, y, py)) {
+        tail(t + NW);
+        break;
+      }
+      fetch(t + 4 * NW, y, py);
+      if (t + 2 * NW >= ntiles) break;
+      if (finish(t + 2 * NW, z, pz)) {
+        tail(t + 2 * NW);
+        break;
+      }
+      fetch(t + 5 * NW, z, pz);
+      if (t + 3 * NW >= ntiles) break;
+    }
+    return;
+  }
   for (uint32_t t = t0;; t += 2 * NW) {
     // tile t from x, then tile t + 2 NW's fetch into x (x is in LDS by then)
     bool ragged = finish(t, x, px);
@@ -704,7 +731,7 @@ static uint32_t tx_cu_count() {
 // us at 24, 245.2 at 32, 245.6 at 16, 250.7 at 8, 254.6 at 4, against 248.3
 // for the one-shot header pass; profiles/r05/tx_hdr/), or the one-shot
 // kernel where tcp_tx_hdr's conditions do not hold.
-template <int SP>
+template <int SP, int DEP = 2>
 static hipError_t launch_header_pass(TxGeo h, hipStream_t stream, uint32_t per_cu) {
   if (h.n == 0) return hipSuccess;
   uint32_t grid = 0;
@@ -719,7 +746,7 @@ static hipError_t launch_header_pass(TxGeo h, hipStream_t stream, uint32_t per_c
   const uint64_t tiles = (h.n + h.tile - 1) / h.tile;
   const uint64_t waves = std::min<uint64_t>(tiles, (uint64_t)tx_cu_count() * (per_cu ? per_cu : 24u));
   const uint32_t wgs = (uint32_t)((waves + h.wpg - 1) / h.wpg);
-  hipLaunchKernelGGL((tcp_tx_hdr<4, SP>), dim3(wgs), dim3(64 * h.wpg), (size_t)h.lds_wave * h.wpg, stream, h,
+  hipLaunchKernelGGL((tcp_tx_hdr<4, SP, DEP>), dim3(wgs), dim3(64 * h.wpg), (size_t)h.lds_wave * h.wpg, stream, h,
                      (uint32_t)tiles);
   return hipGetLastError();
 }

@@ -26,7 +26,8 @@
 //   CU, 44 = the one-shot header pass alone (htile: the header tile);
 //   70-76 = the persistent header pass alone, store policies (tx_store_aux);
 //   77 / 78 = one pass in the group shape, slots written through / default;
-//   90 = the production header pass alone at g->pad waves per CU.
+//   90 = the production header pass alone at g->pad waves per CU; 91 = the
+//   same with 3 tiles in flight per wave.
 // Not part of the product ABI.
 #include "../netstack_amd/csrc/tcp_tx.hip"
 
@@ -298,6 +299,12 @@ extern "C" int txv_launch(const nsk::TxGeo* g, void* stream, int k) {
     case 37: e = launch_floor_co<1>(*g, s); break;
     case 38: e = launch_floor_co<2>(*g, s); break;
     case 35: e = nsk::launch_passes<16, 2, 0, 1, 1, 1>(*g, s); break;
+    case 91: {  // the same with 3 tiles in flight per wave
+      nsk::TxGeo h = *g;
+      h.tile = g->htile;
+      e = nsk::launch_header_pass<4, 3>(h, s, g->pad);
+      break;
+    }
     case 90: {  // the production header pass (nt sc1 stores) at g->pad waves per CU (0: 24), tile g->htile
       nsk::TxGeo h = *g;
       h.tile = g->htile;
