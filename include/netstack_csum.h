@@ -557,14 +557,15 @@ int ns_csum_get_stats(ns_csum_ctx* ctx, ns_csum_stats* out, int reset);
  * through; 1 one fused pass; with the windowed payload pass: 2 nontemporal
  * write-back, 3 segments reduced over the wave, 4 the one-shot header pass;
  * 5 the group pass with default-policy header stores; 6 round 5's
- * production, windowed with default-policy stores),
+ * production, windowed with default-policy stores; 7 production with the
+ * persistent header pass),
  * tile / htile (segments per wave of the fused pass or the windowed payload
  * pass — a tile set here selects the windowed pass — and of the header
  * pass; 0 = the launcher's choice), passes (0 = by
  * size, 1 = fused, 2 = two passes).  Read by each call without a lock; set
  * them while no ns_csum_tcp_tx call runs on the context.  ns_csum_init takes
  * their initial values from NS_CSUM_TX_VARIANT / _TILE / _HTILE / _PASSES,
- * once.  NS_EINVAL for a variant above 6 or passes above 2.                 */
+ * once.  NS_EINVAL for a variant above 7 or passes above 2.                 */
 int ns_csum_set_tx_tuning(ns_csum_ctx* ctx, uint32_t variant, uint32_t tile, uint32_t htile,
                           uint32_t passes);
 

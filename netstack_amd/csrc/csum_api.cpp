@@ -1805,7 +1805,7 @@ int ns_csum_tcp_tx_host(ns_csum_ctx* ctx, uint8_t* h_arena, uint64_t arena_bytes
 }
 
 int ns_csum_set_tx_tuning(ns_csum_ctx* ctx, uint32_t variant, uint32_t tile, uint32_t htile, uint32_t passes) {
-  if (!ctx || variant > 6 || passes > 2) return NS_EINVAL;
+  if (!ctx || variant > 7 || passes > 2) return NS_EINVAL;
   ctx->tx_variant = variant;
   ctx->tx_tile = tile;
   ctx->tx_htile = htile;

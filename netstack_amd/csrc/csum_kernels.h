@@ -119,7 +119,8 @@ constexpr uint64_t kTxTwoPassMinBytes = 64ull << 20;
 // payload pass + nontemporal write-back, 3 = windowed, segments reduced over
 // the wave in the loop, 4 = windowed + the one-shot header pass (tcp_tx
 // PH = 2), 5 = group payload pass + default-policy header stores, 6 =
-// round 5's production (windowed + default-policy stores).
+// round 5's production (windowed + default-policy stores), 7 = production
+// with the persistent header pass (2 tiles per wave in flight).
 hipError_t launch_tcp_tx(TxGeo g, hipStream_t stream, uint32_t variant = 0);
 // Many batches in one fused launch (ns_csum_tcp_tx_multi).  calls[] (host)
 // hold each batch's geometry with n, mode and out set; tx_multi_prepare sets

@@ -415,7 +415,8 @@ __global__ __launch_bounds__(256) void tcp_tx(TxGeo g) {
 // for all of them.  For tiles that start 16-B aligned (hdr, tile * slot) and
 // hold at most 64 segments and 64 CPL chunks; the last tile's unaligned end
 // is written with byte stores as the wave's last act.
-// DEP = tiles in flight per wave (2; 3 as a timing variant).
+// DEP = tiles in flight per wave (2; 3 as a timing variant); 1: one tile
+// per wave on a one-shot grid (register-staged, no persistence).
 template <int CPL, int SP, int DEP = 2>
 __global__ __launch_bounds__(256) void tcp_tx_hdr(TxGeo g, uint32_t ntiles) {
   extern __shared__ uint4 tx_lds[];
@@ -498,6 +499,10 @@ __global__ __launch_bounds__(256) void tcp_tx_hdr(TxGeo g, uint32_t ntiles) {
   uint4 x[CPL], y[CPL];
   uint32_t px = 0, py = 0;
   fetch(t0, x, px);
+  if constexpr (DEP == 1) {  // one tile per wave (a one-shot grid, NW = ntiles)
+    if (finish(t0, x, px)) tail(t0);
+    return;
+  }
   fetch(t0 + NW, y, py);
   if constexpr (DEP == 3) {
     uint4 z[CPL];
@@ -744,7 +749,8 @@ static hipError_t launch_header_pass(TxGeo h, hipStream_t stream, uint32_t per_c
       !(h.mode & kTxTcpFull) || (h.mode & kTxFieldsOnly) || ((uintptr_t)h.out & 3) || h.xs == nullptr)
     return launch_tcp_tx_t<16, 2, SP, 1, 0, 2>(h, stream);
   const uint64_t tiles = (h.n + h.tile - 1) / h.tile;
-  const uint64_t waves = std::min<uint64_t>(tiles, (uint64_t)tx_cu_count() * (per_cu ? per_cu : 24u));
+  if (DEP == 1 && per_cu >= 1 && per_cu <= 4) h.wpg = per_cu;  // one-shot: per_cu = waves per workgroup (A/B)
+  const uint64_t waves = DEP == 1 ? tiles : std::min<uint64_t>(tiles, (uint64_t)tx_cu_count() * (per_cu ? per_cu : 24u));
   const uint32_t wgs = (uint32_t)((waves + h.wpg - 1) / h.wpg);
   hipLaunchKernelGGL((tcp_tx_hdr<4, SP, DEP>), dim3(wgs), dim3(64 * h.wpg), (size_t)h.lds_wave * h.wpg, stream, h,
                      (uint32_t)tiles);
@@ -756,7 +762,12 @@ static hipError_t launch_header_pass(TxGeo h, hipStream_t stream, uint32_t per_c
 // only payload, the header pass then reads, fills and writes back the slots
 // (interleaving the slot write-back with the payload stream
 // cost ~45 us on 1M segments).  One fused pass otherwise.  HP: the header
-// pass persistent (tcp_tx_hdr) or one-shot (tcp_tx PH = 2).
+// pass one tile per wave on a one-shot grid, register-staged (2, production:
+// tcp_tx_hdr DEP = 1), persistent (1: DEP = 2) or round 4's LDS-DMA one-shot
+// (0: tcp_tx PH = 2).  In situ after the payload pass over fresh slots
+// (profiles/r06/tx_drain/header_oneshot.jsonl): 25.7-26.1 us at 4 waves per
+// workgroup against 27.9-28.3 persistent and 22.2 for a plain copy of the
+// slots with the same stores.
 // GP: the payload pass windowed (0) or in 8-lane groups (1, production).
 // SP: the header pass's store policy (tx_store_aux; production 4, nt sc1).
 // With default-policy stores the header pass's 57 MB of slots leave L2
@@ -774,7 +785,10 @@ static hipError_t launch_passes(TxGeo g, hipStream_t stream, uint32_t per_cu = 0
   TxGeo h = g;
   h.tile = g.htile;
   hipError_t e = launch_payload_pass<U, AUX, SP, RED, GP>(g, stream);
-  if (e == hipSuccess) e = HP ? launch_header_pass<SP>(h, stream, per_cu) : launch_tcp_tx_t<U, AUX, SP, RED, 0, 2>(h, stream);
+  if (e == hipSuccess)
+    e = HP == 2 ? launch_header_pass<SP, 1>(h, stream, 0)
+        : HP    ? launch_header_pass<SP>(h, stream, per_cu)
+                : launch_tcp_tx_t<U, AUX, SP, RED, 0, 2>(h, stream);
   return e;
 }
 
@@ -821,7 +835,8 @@ hipError_t launch_tcp_tx(TxGeo g, hipStream_t stream, uint32_t variant) {
     case 4: return launch_passes<16, 2, 0, 1, 0>(g, stream);  // the one-shot header pass (round 4)
     case 5: return launch_passes<16, 2, 0, 1, 1, 1>(g, stream);  // group payload pass, default-policy stores
     case 6: return launch_passes<16, 2, 0, 1, 1, 0>(g, stream);  // round 5's: windowed, default-policy stores
-    default: return launch_passes<16, 2, 4, 1, 1, 1>(g, stream);  // group payload pass, nt sc1 header stores
+    case 7: return launch_passes<16, 2, 4, 1, 1, 1>(g, stream);  // the header pass persistent (2 tiles per wave in flight)
+    default: return launch_passes<16, 2, 4, 1, 2, 1>(g, stream);  // group payload pass, one-shot header pass, nt sc1 stores
   }
 }
 

@@ -105,12 +105,13 @@ def test_geometry_bit_exact(engine, oracle_mod, name):
     """Each geometry in every shape: one fused pass (what batches below
     kTxTwoPassMinBytes take), the payload + header passes (production: the
     payload pass in 8-lane groups, one segment each, header stores written
-    through), the group pass with default-policy stores (variant 5) and
-    round 5's windowed payload pass (variant 6)."""
+    through, one tile per wave), the group pass with default-policy stores
+    (variant 5), round 5's windowed payload pass (variant 6) and the
+    persistent header pass (variant 7)."""
     geo, total = CASES[name]
     a = _arena(total, geo, seed=len(name))
     wa, ws = _want(oracle_mod, a, geo)
-    for passes, variant in ((1, 0), (2, 0), (2, 5), (2, 6)):
+    for passes, variant in ((1, 0), (2, 0), (2, 5), (2, 6), (2, 7)):
         for offset in (0, 5):
             ga, gs = _run(engine, a, geo, offset=offset, passes=passes, variant=variant)
             _check(ga, gs, wa, ws, f"{name} ({passes} passes, variant {variant}, arena at +{offset})")

@@ -57,7 +57,10 @@ def main():
     ap.add_argument("--only", default="")
     ap.add_argument("--no-check", action="store_true")
     ap.add_argument("--htile", type=int, default=0, help="header-pass tile (segments per wave; 0: 64)")
-    ap.add_argument("--depth", type=int, default=2, help="header-pass tiles in flight per wave (3: txv 91)")
+    ap.add_argument("--hfloor", action="store_true",
+                    help="in place of the header pass (policy 4), a plain copy of the slots onto themselves with "
+                         "the same stores (txv 39; timing only: no fields, use --no-check)")
+    ap.add_argument("--depth", type=int, default=2, help="header-pass tiles in flight per wave (3: txv 91; 1: one tile per wave, one-shot grid, txv 92)")
     ap.add_argument("--per-cu", type=int, default=0,
                     help="header-pass waves per CU (header policy 4 only, txv 90; 0: 24)")
     args = ap.parse_args()
@@ -75,8 +78,12 @@ def main():
     asum = addr_sum(geo["src"], geo["dst"])
 
     def launch(k, a):
-        if k == 74 and args.depth == 3:
+        if k == 74 and args.hfloor:
+            k = 39
+        elif k == 74 and args.depth == 3:
             k = 91
+        elif k == 74 and args.depth == 1:
+            k = 92
         elif k == 74 and (args.per_cu or args.htile):
             k = 90
         t = TxGeo(hdr=a.data_ptr() + geo["hdr_off"], pay=a.data_ptr() + geo["pay_off"], size=geo["size"], n=n,
@@ -127,7 +134,7 @@ def main():
             ok = bool(torch.equal(b, want))
         med = lambda v: v[len(v) // 2]  # noqa: E731
         mean = lambda v: sum(v) / len(v)  # noqa: E731
-        print(json.dumps({"scenario": sc, "htile": args.htile, "per_cu": args.per_cu, "depth": args.depth,
+        print(json.dumps({"scenario": sc, "htile": args.htile, "per_cu": args.per_cu, "depth": args.depth, "hfloor": args.hfloor,
                           "payload_pass": p, "header_store_policy": int(h), "rotating_batches": rot,
                           "between_calls": gap, "calls": args.calls,
                           "payload_us": {"median": round(med(pt), 2), "mean": round(mean(pt), 2),

@@ -22,12 +22,13 @@
 //   payload pass alone; 34 / 35 = both passes, windowed / group payload
 //   pass (whatever the product's default); 36 / 37 / 38 = the floors of
 //   19 / 20 / 21 with lane-consecutive chunks (1 KiB per wave instruction);
+//   39 = 36 with nt sc1 stores;
 //   40-43 = the persistent header pass alone at 8 / 16 / 32 / 48 waves per
 //   CU, 44 = the one-shot header pass alone (htile: the header tile);
 //   70-76 = the persistent header pass alone, store policies (tx_store_aux);
 //   77 / 78 = one pass in the group shape, slots written through / default;
 //   90 = the production header pass alone at g->pad waves per CU; 91 = the
-//   same with 3 tiles in flight per wave.
+//   same with 3 tiles in flight per wave; 92 = one tile per wave, one-shot.
 // Not part of the product ABI.
 #include "../netstack_amd/csrc/tcp_tx.hip"
 
@@ -191,7 +192,7 @@ __global__ __launch_bounds__(256) void slot_floor_co(uint64_t base, uint32_t byt
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const uint32_t o = ((blockIdx.x * 4u + (uint32_t)i) * 256u + threadIdx.x) * 16u;
-    if (FL < 2) v[i] = __builtin_amdgcn_raw_buffer_load_b128(r, (int)o, 0, 0);
+    if (FL < 2 || FL == 4) v[i] = __builtin_amdgcn_raw_buffer_load_b128(r, (int)o, 0, 0);
     else v[i] = (__attribute__((ext_vector_type(4))) uint32_t){o, o, o, o};
   }
   if (FL == 1) {
@@ -204,7 +205,7 @@ __global__ __launch_bounds__(256) void slot_floor_co(uint64_t base, uint32_t byt
 #pragma unroll
   for (int i = 0; i < 4; ++i)
     __builtin_amdgcn_raw_buffer_store_b128(v[i], r, (int)(((blockIdx.x * 4u + (uint32_t)i) * 256u + threadIdx.x) * 16u),
-                                           0, FL == 3 ? 2 : 0);
+                                           0, FL == 3 ? 2 : FL == 4 ? 18 : 0);
 }
 
 template <int FL>
@@ -298,7 +299,14 @@ extern "C" int txv_launch(const nsk::TxGeo* g, void* stream, int k) {
     case 36: e = launch_floor_co<0>(*g, s); break;
     case 37: e = launch_floor_co<1>(*g, s); break;
     case 38: e = launch_floor_co<2>(*g, s); break;
+    case 39: e = launch_floor_co<4>(*g, s); break;  // copied onto themselves, lane-consecutive, nt sc1 stores
     case 35: e = nsk::launch_passes<16, 2, 0, 1, 1, 1>(*g, s); break;
+    case 92: {  // one tile per wave on a one-shot grid (register-staged)
+      nsk::TxGeo h = *g;
+      h.tile = g->htile;
+      e = nsk::launch_header_pass<4, 1>(h, s, g->pad);  // g->pad: waves per workgroup (0: the launcher's)
+      break;
+    }
     case 91: {  // the same with 3 tiles in flight per wave
       nsk::TxGeo h = *g;
       h.tile = g->htile;
