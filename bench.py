@@ -373,8 +373,14 @@ def rank_batch(cfg: int, rank: int, world: int = 1):
 def cpu_baseline(batch, seconds: float, threads: int):
     import oracle as O
 
-    # bounded sample: the first packets of this rank's batch (same bytes)
+    # bounded sample: the first packets of this rank's batch (same bytes);
+    # the threaded leg takes at least 64 MiB of payload per pass, so that
+    # starting its threads (once per pass) is not what it measures (64-B
+    # packets: 65,536 of them are only 4 MiB)
     n_s = min(batch.n, 65536)
+    if threads > 1:
+        mean = max(float(batch.desc["len"][:n_s].mean()), 1.0)
+        n_s = min(batch.n, max(n_s, int((64 << 20) / mean)))
     d = batch.desc[:n_s].copy()
     span = int(d["off"][-1] + d["len"][-1])
     arena = batch.host_bytes(0, span)
