@@ -492,8 +492,9 @@ __device__ __forceinline__ bool spec_check(const PktInfo& p, uint64_t i, uint32_
 
 // quad_reduce for a wave in which no chunk needs a mask (every packet whole
 // 16-B-aligned chunks, 4 of them: cfg3's dense 64-B slots): no geometry
-// shuffles and no per-chunk mask tests (round 5: the SQ counters put cfg3's
-// distance to its floor kernels on VALU issue).
+// shuffles and no per-chunk mask tests (round 5: a first SQ pass put cfg3's
+// distance to its floor kernels on VALU issue; a second did not confirm it,
+// DESIGN.md §4.2b).
 __device__ __forceinline__ uint32_t quad_reduce_whole(const uint4 (&v)[4], uint32_t phase) {
   const uint32_t l = threadIdx.x & 63u, c = l & 3u;
   uint32_t sv[4];

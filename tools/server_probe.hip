@@ -1,5 +1,5 @@
 // server_probe.hip — how fast a resident workgroup answers a small request,
-// against a launch per request (DESIGN.md §10 item 0).  One wave polls a
+// against a launch per request (DESIGN.md §10 item 4).  One wave polls a
 // doorbell word in fine-grained VRAM that the host writes through the BAR;
 // on a new sequence number it (optionally) sums a 1500-B payload staged in
 // VRAM and answers with a system-scope release store into coherent host
