@@ -24,6 +24,21 @@ incorrect_checksum — transport/tcp/tcp_test.go:3232-3259
     {1, 2, 3}) with its first payload byte overwritten with 0x4; expected:
     ChecksumErrors + 1 (stack and endpoint).  The endpoint's port and the
     ack number are chosen by the test at run time; fixed values stand in.
+ipv6_receive      — the IPv6 packets network/ipv6's tests inject and expect to
+    pass the checksum: ipv6_test.go:40-67 testReceiveICMP (a 32-B
+    NeighborAdvert) and :71-125 testReceiveUDP (an 8-B UDP, 5555 -> 80) as
+    TestReceiveOnAllNodesMulticastAddr (:129-155) and
+    TestReceiveOnSolicitedNodeAddr (:160-225) send them; ndp_test.go:75-184
+    TestHopLimitValidation (each NDP type at its table size, lladdr0 ->
+    lladdr1, hop limit 254 and 255) and :189-372 TestRouterAdvertValidation
+    (its seven RAs to ff02::1, 15-B NDPPayloadTooSmall among them).  Each
+    row: the packet, the verdict the receive path owes it (VALID; UNCHECKED
+    for UDP) and what the reference's test then expects — the drops these
+    tests count (hop limit, code, source, RA size) all come after the
+    checksum check (network/ipv6/icmp.go:79-102), so none of them changes
+    the verdict.  The checksums are computed here as those tests compute
+    them (ICMPv6Checksum / PseudoHeaderChecksum over the message with a zero
+    checksum field).
 
 Nothing here is reference source: the file holds values only.
 """
@@ -103,9 +118,76 @@ def incorrect_checksum():
             "source": "transport/tcp/tcp_test.go:3232-3259, testing/context/context.go:311-356"}
 
 
+def _sum16(b: bytes, acc: int = 0) -> int:
+    if len(b) % 2:
+        b += b"\0"
+    for i in range(0, len(b), 2):
+        acc += b[i] << 8 | b[i + 1]
+    while acc > 0xFFFF:
+        acc = (acc & 0xFFFF) + (acc >> 16)
+    return acc
+
+
+def _ipv6(src: bytes, dst: bytes, proto: int, hop: int, msg: bytearray, at: int) -> str:
+    """msg's checksum field (offset at) set from the pseudo-header, then the
+    40-B IPv6 header (IPv6Fields: PayloadLength, NextHeader, HopLimit)."""
+    pseudo = _sum16(src + dst + len(msg).to_bytes(4, "big") + bytes([0, 0, 0, proto]))
+    c = ~_sum16(bytes(msg), pseudo) & 0xFFFF
+    msg[at:at + 2] = c.to_bytes(2, "big")
+    h = bytes([0x60, 0, 0, 0]) + len(msg).to_bytes(2, "big") + bytes([proto, hop]) + src + dst
+    return (h + bytes(msg)).hex()
+
+
+def ipv6_receive():
+    addr1 = b"\x0a" + bytes(14) + b"\x01"
+    addr2 = b"\x0a" + bytes(14) + b"\x02"
+    all_nodes = b"\xff\x02" + bytes(13) + b"\x01"
+    snmc = b"\xff\x02" + bytes(9) + b"\x01\xff" + addr2[-3:]
+
+    def lladdr(mac):  # header/ipv6.go:271-290 LinkLocalAddr
+        return b"\xfe\x80" + bytes(6) + bytes([mac[0] ^ 2, mac[1], mac[2], 0xFF, 0xFE, mac[3], mac[4], mac[5]])
+
+    ll0, ll1 = lladdr(b"\x02\x02\x03\x04\x05\x06"), lladdr(b"\x0a\x0b\x0c\x0d\x0e\x0f")
+    rows = []
+    for dname, dst in (("all_nodes", all_nodes), ("solicited_node", snmc)):
+        na = bytearray(32)
+        na[0] = 136
+        rows.append({"name": f"receive_icmp_{dname}", "packet": _ipv6(addr1, dst, 58, 255, na, 2), "verdict": 1,
+                     "reference": "ICMP.V6PacketsReceived.NeighborAdvert + 1",
+                     "source": "network/ipv6/ipv6_test.go:40-67,129-225"})
+        u = bytearray((5555).to_bytes(2, "big") + (80).to_bytes(2, "big") + (8).to_bytes(2, "big") + bytes(2))
+        rows.append({"name": f"receive_udp_{dname}", "packet": _ipv6(addr1, dst, 17, 255, u, 6), "verdict": 2,
+                     "reference": "UDP.PacketsReceived + 1", "source": "network/ipv6/ipv6_test.go:71-125,129-225"})
+    for tname, typ, size in (("RouterSolicit", 133, 8), ("RouterAdvert", 134, 4 + 12), ("NeighborSolicit", 135, 24),
+                             ("NeighborAdvert", 136, 32), ("RedirectMsg", 137, 8)):
+        for hop in (254, 255):
+            m = bytearray(size)
+            m[0] = typ
+            rows.append({"name": f"hop_limit_{tname}_{hop}", "packet": _ipv6(ll0, ll1, 58, hop, m, 2), "verdict": 1,
+                         "reference": f"ICMP.V6PacketsReceived.{tname} + 1" if hop == 255
+                         else "ICMP.V6PacketsReceived.Invalid + 1 (hop limit, after the checksum)",
+                         "source": "network/ipv6/ndp_test.go:75-184"})
+    ra = bytes(12)
+    opts = bytes([2, 1]) + bytes(6) + bytes([255, 1]) + bytes(6) + bytes([3, 4]) + bytes(30)
+    zero_len = bytes([2, 0]) + opts[2:]
+    for name, src, hop, code, payload, ok in (("OK", ll0, 255, 0, ra, True), ("NonLinkLocalSourceAddr", addr1, 255, 0, ra, False),
+                                              ("HopLimitNot255", ll0, 254, 0, ra, False), ("NonZeroCode", ll0, 255, 1, ra, False),
+                                              ("NDPPayloadTooSmall", ll0, 255, 0, ra[:11], False),
+                                              ("OKWithOptions", ll0, 255, 0, ra + opts, True),
+                                              ("OptionWithZeroLength", ll0, 255, 0, ra + zero_len, False)):
+        m = bytearray([134, code, 0, 0]) + payload
+        rows.append({"name": f"router_advert_{name}", "packet": _ipv6(src, all_nodes, 58, hop, m, 2), "verdict": 1,
+                     "reference": "ICMP.V6PacketsReceived.RouterAdvert + 1" if ok
+                     else "ICMP.V6PacketsReceived.Invalid + 1 (after the checksum)",
+                     "source": "network/ipv6/ndp_test.go:189-372"})
+    assert len(rows) == 4 + 10 + 7
+    return rows
+
+
 def main():
     out = {"invalid_fragments": invalid_fragments(), "holes": holes(), "process": process(),
-           "fragmentation": fragmentation(), "incorrect_checksum": incorrect_checksum()}
+           "fragmentation": fragmentation(), "incorrect_checksum": incorrect_checksum(),
+           "ipv6_receive": ipv6_receive()}
     with open(os.path.join(HERE, "rx_fixtures.json"), "w") as f:
         json.dump(out, f, indent=1)
         f.write("\n")

@@ -114,3 +114,21 @@ def write_packet_fragments(hdr: bytes, data, mtu: int, set_checksums: bool = Tru
             out.append((first_hdr[:outer], []))
             data = [bytes(first_hdr[outer:])] + data
     return [(bytes(h), d) for h, d in out]
+
+
+def ipv6_rows(fx):
+    """tests/golden/rx_fixtures.json ipv6_receive, each packet intact and
+    with its checksum field's low bit flipped (ICMPv6 -> INVALID, as
+    handleICMP counts it, network/ipv6/icmp.go:79-82; UDP stays UNCHECKED)."""
+    import packets as P
+
+    rows = []
+    for c in fx["ipv6_receive"]:
+        b = bytes.fromhex(c["packet"])
+        at = 40 + (6 if b[6] == 17 else 2)
+        bad = bytearray(b)
+        bad[at + 1] ^= 1
+        rows.append((c["name"], b, c["verdict"]))
+        rows.append((c["name"] + "/bad", bytes(bad), P.UNCHECKED if b[6] == 17 else P.INVALID))
+    return rows
+

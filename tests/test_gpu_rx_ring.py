@@ -141,6 +141,27 @@ def test_reference_packet_fixtures(engine):
     _check(engine, [ethernet(p, 0x0800) for p in pk], stride, link_hdr=14, first_view=128)
 
 
+@pytest.mark.parametrize("link_hdr,first_view", [(0, 0), (0, 128), (14, 128), (14, 0)])
+def test_ipv6_receive_fixtures(engine, link_hdr, first_view):
+    """tests/golden/rx_fixtures.json ipv6_receive: the IPv6 packets
+    network/ipv6's tests inject (ipv6_test.go testReceiveICMP/testReceiveUDP,
+    ndp_test.go's NDP hop-limit and RA validation: 8-B, 15-B and 64-B ICMPv6
+    messages, an 8-B UDP), intact and with a flipped checksum bit, in a ring
+    and through ns_csum_packet_buffers: the fixture's verdicts, the oracle's
+    sums."""
+    import rxcases
+
+    from netstack_amd.packet import PacketBuffer, verify_packet_buffers
+
+    rows = rxcases.ipv6_rows(rxcases.fixtures())
+    frames = [ethernet(b) if link_hdr else b for _, b, _ in rows]
+    got = _check(engine, frames, 128, link_hdr=link_hdr, first_view=first_view, seed=4)
+    assert got == [w for _, _, w in rows]
+    pkts = [PacketBuffer(Data=views_bufconfig(b, link_hdr)) for _, b, _ in rows]
+    v2, _ = verify_packet_buffers(pkts, engine)
+    assert list(v2) == got
+
+
 @pytest.mark.parametrize("link_hdr,first_view", [(0, 0), (0, 128), (0, 64), (14, 128), (14, 0), (14, 78)])
 def test_minimum_sizes(engine, link_hdr, first_view):
     """Every transport message from 0 to its minimum + 2 bytes (TCP 20, UDP 8,

@@ -207,3 +207,33 @@ def test_ipv4_header_past_the_first_view_is_malformed():
     for c in cases:
         views = [bytes.fromhex(v) for v in c["views"]]
         assert P.verify(b"", views, c["size"]) == (c["verdict"], c["ipv4_sum"], c["transport_sum"]), c["name"]
+
+
+def test_ipv6_receive_packets_verify(fx):
+    """The IPv6 packets network/ipv6's tests inject (ipv6_test.go:40-225
+    testReceiveICMP/testReceiveUDP, ndp_test.go:75-372 NDP hop-limit and RA
+    validation — odd-length and 8-B ICMPv6 among them) get the fixture's
+    verdict from both restatements, as one view, in the link's BufConfig
+    views (TUN and Ethernet), and the link's sums as the Python oracle's."""
+    import numpy as np
+
+    import oracle as O
+    import packets as P
+    from pktgen import ethernet
+
+    rows = R.ipv6_rows(fx)
+    assert len(rows) == 42 and {r[2] for r in rows} == {P.VALID, P.INVALID, P.UNCHECKED}
+    for name, b, want in rows:
+        assert P.verify(b"", [b], len(b))[0] == want, name
+    for link_hdr in (0, 14):
+        frames = [ethernet(b) if link_hdr else b for _, b, _ in rows]
+        stride = 128
+        arena = np.random.default_rng(6).integers(0, 256, len(frames) * stride, dtype=np.uint8)
+        lens = np.zeros(len(frames), dtype=np.uint32)
+        for k, f in enumerate(frames):
+            arena[k * stride:k * stride + len(f)] = np.frombuffer(f, dtype=np.uint8)
+            lens[k] = len(f)
+        v, s = O.c_rx_ring(arena, lens, stride, len(frames), link_hdr=link_hdr, first_view=128)
+        for k, (name, _, want) in enumerate(rows):
+            py = P.verify_frame(bytes(arena[k * stride:(k + 1) * stride]), int(lens[k]), 0, link_hdr, 128)
+            assert py[0] == want and (int(v[k]), int(s[2 * k]), int(s[2 * k + 1])) == py, (name, link_hdr)
