@@ -39,6 +39,16 @@ ipv6_receive      — the IPv6 packets network/ipv6's tests inject and expect to
     the verdict.  The checksums are computed here as those tests compute
     them (ICMPv6Checksum / PseudoHeaderChecksum over the message with a zero
     checksum field).
+receive_control   — network/ip_test.go:293-398 TestIPv4ReceiveControl and
+    :534-650 TestIPv6ReceiveControl: an ICMP error (outer header, ICMP
+    header with ident 0xdead / sequence 0xbeef, the inner header, 8 payload
+    bytes i & 0xff) cut short by each case's trunc, and the case's
+    expectedCount.  The verdict each row owes follows from the rules these
+    packets meet first: the IP header against the packet (IsValid), the
+    8-B ICMP minimum (ipv4/icmp.go:60, ipv6/icmp.go:68), then for ICMPv6
+    the checksum (set over the untruncated message, so a cut one is
+    INVALID) and for a non-echo ICMPv4 none (UNCHECKED).  Every row the
+    reference counts (expectedCount 1) is VALID or UNCHECKED.
 
 Nothing here is reference source: the file holds values only.
 """
@@ -184,10 +194,72 @@ def ipv6_receive():
     return rows
 
 
+def receive_control():
+    rows = []
+    src4, local4, remote4 = bytes([10, 0, 0, 0xbb]), bytes([10, 0, 0, 1]), bytes([10, 0, 0, 2])
+
+    def ipv4(total, proto, frag, src, dst):  # IPv4Fields: IHL 20, TTL 20, no checksum
+        return bytes([0x45, 0]) + total.to_bytes(2, "big") + bytes(2) + (frag >> 3).to_bytes(2, "big") + \
+            bytes([20, proto, 0, 0]) + src + dst
+
+    # (name, expectedCount, inner fragment offset, code, trunc, verdict)
+    for name, count, fo, code, trunc, verdict in (
+            ("FragmentationNeeded", 1, 0, 4, 0, 2), ("Truncated (10 bytes missing)", 0, 0, 4, 10, 2),
+            ("Truncated (missing IPv4 header)", 0, 0, 4, 28, 2),
+            ("Truncated (missing 'extra info')", 0, 0, 4, 32, 3),
+            ("Truncated (missing ICMP header)", 0, 0, 4, 36, 3), ("Port unreachable", 1, 0, 3, 0, 2),
+            ("Non-zero fragment offset", 0, 100, 3, 0, 2), ("Zero-length packet", 0, 0, 3, 56, 3)):
+        view = bytearray(56)
+        view[0:20] = ipv4(56 - trunc, 1, 0, src4, local4)
+        view[20:28] = bytes([3, code, 0, 0, 0xde, 0xad, 0xbe, 0xef])
+        view[28:48] = ipv4(100, 10, fo, local4, remote4)
+        for i in range(48, 56):
+            view[i] = i & 0xFF
+        rows.append({"name": "ipv4/" + name, "packet": bytes(view[:56 - trunc]).hex(), "verdict": verdict,
+                     "expected_count": count, "source": "network/ip_test.go:293-398"})
+
+    local6 = b"\x0a" + bytes(14) + b"\x01"
+    remote6 = b"\x0a" + bytes(14) + b"\x02"
+    outer6 = b"\x0a" + bytes(14) + b"\xaa"
+
+    def ipv6(pl, nh, src, dst):  # IPv6Fields: hop limit 20
+        return bytes([0x60, 0, 0, 0]) + (pl & 0xFFFF).to_bytes(2, "big") + bytes([nh, 20]) + src + dst
+
+    for name, count, fo, typ, code, trunc, verdict in (
+            ("PacketTooBig", 1, None, 2, 0, 0, 1), ("Truncated (10 bytes missing)", 0, None, 2, 0, 10, 0),
+            ("Truncated (missing IPv6 header)", 0, None, 2, 0, 48, 0),
+            ("Truncated PacketTooBig (missing 'extra info')", 0, None, 2, 0, 52, 3),
+            ("Truncated (missing ICMP header)", 0, None, 2, 0, 56, 3), ("Port unreachable", 1, None, 1, 4, 0, 1),
+            ("Truncated DstUnreachable (missing 'extra info')", 0, None, 1, 4, 52, 3),
+            ("Fragmented, zero offset", 1, 0, 1, 4, 0, 1), ("Non-zero fragment offset", 0, 100, 1, 4, 0, 1),
+            ("Zero-length packet", 0, None, 1, 4, 96, 3)):
+        data_at = 88 + (8 if fo is not None else 0)
+        view = bytearray(data_at + 8)
+        view[0:40] = ipv6(len(view) - 40 - trunc, 58, outer6, local6)
+        view[40:48] = bytes([typ, code, 0, 0, 0xde, 0xad, 0xbe, 0xef])
+        view[48:88] = ipv6(100, 10 if fo is None else 44, local6, remote6)
+        if fo is not None:  # IPv6FragmentFields: NextHeader 10, M, Identification 0x12345678
+            view[88:96] = bytes([10, 0]) + ((fo << 3) | 1).to_bytes(2, "big") + (0x12345678).to_bytes(4, "big")
+        for i in range(data_at, len(view)):
+            view[i] = i & 0xFF
+        msg = bytes(view[40:])  # ICMPv6Checksum over the whole message, before the cut
+        pseudo = _sum16(outer6 + local6 + len(msg).to_bytes(4, "big") + bytes([0, 0, 0, 58]))
+        view[42:44] = (~_sum16(msg, pseudo) & 0xFFFF).to_bytes(2, "big")
+        pkt = bytes(view[:len(view) - trunc])
+        if verdict == 0:  # a cut message no longer matches its checksum
+            m = pkt[40:]
+            ps = _sum16(outer6 + local6 + len(m).to_bytes(4, "big") + bytes([0, 0, 0, 58]))
+            assert _sum16(m, ps) != 0xFFFF, name
+        rows.append({"name": "ipv6/" + name, "packet": pkt.hex(), "verdict": verdict, "expected_count": count,
+                     "source": "network/ip_test.go:534-650"})
+    assert all(r["verdict"] in (1, 2) for r in rows if r["expected_count"])
+    return rows
+
+
 def main():
     out = {"invalid_fragments": invalid_fragments(), "holes": holes(), "process": process(),
            "fragmentation": fragmentation(), "incorrect_checksum": incorrect_checksum(),
-           "ipv6_receive": ipv6_receive()}
+           "ipv6_receive": ipv6_receive(), "receive_control": receive_control()}
     with open(os.path.join(HERE, "rx_fixtures.json"), "w") as f:
         json.dump(out, f, indent=1)
         f.write("\n")

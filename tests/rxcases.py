@@ -132,3 +132,10 @@ def ipv6_rows(fx):
         rows.append((c["name"] + "/bad", bytes(bad), P.UNCHECKED if b[6] == 17 else P.INVALID))
     return rows
 
+
+
+def control_rows(fx):
+    """tests/golden/rx_fixtures.json receive_control: TestIPv4ReceiveControl's
+    and TestIPv6ReceiveControl's ICMP errors at each case's cut, with the
+    verdict each owes (network/ip_test.go:293-398, :534-650)."""
+    return [(c["name"], bytes.fromhex(c["packet"]), c["verdict"]) for c in fx["receive_control"]]

@@ -142,18 +142,20 @@ def test_reference_packet_fixtures(engine):
 
 
 @pytest.mark.parametrize("link_hdr,first_view", [(0, 0), (0, 128), (14, 128), (14, 0)])
-def test_ipv6_receive_fixtures(engine, link_hdr, first_view):
-    """tests/golden/rx_fixtures.json ipv6_receive: the IPv6 packets
+def test_ipv6_and_control_fixtures(engine, link_hdr, first_view):
+    """tests/golden/rx_fixtures.json ipv6_receive — the IPv6 packets
     network/ipv6's tests inject (ipv6_test.go testReceiveICMP/testReceiveUDP,
     ndp_test.go's NDP hop-limit and RA validation: 8-B, 15-B and 64-B ICMPv6
-    messages, an 8-B UDP), intact and with a flipped checksum bit, in a ring
-    and through ns_csum_packet_buffers: the fixture's verdicts, the oracle's
-    sums."""
+    messages, an 8-B UDP), intact and with a flipped checksum bit — and
+    receive_control — network/ip_test.go's IPv4/IPv6 ReceiveControl ICMP
+    errors at every cut, down to empty packets — in a ring and through
+    ns_csum_packet_buffers: the fixture's verdicts, the oracle's sums."""
     import rxcases
 
     from netstack_amd.packet import PacketBuffer, verify_packet_buffers
 
-    rows = rxcases.ipv6_rows(rxcases.fixtures())
+    fx = rxcases.fixtures()
+    rows = rxcases.ipv6_rows(fx) + rxcases.control_rows(fx)
     frames = [ethernet(b) if link_hdr else b for _, b, _ in rows]
     got = _check(engine, frames, 128, link_hdr=link_hdr, first_view=first_view, seed=4)
     assert got == [w for _, _, w in rows]

@@ -215,16 +215,39 @@ def test_ipv6_receive_packets_verify(fx):
     validation — odd-length and 8-B ICMPv6 among them) get the fixture's
     verdict from both restatements, as one view, in the link's BufConfig
     views (TUN and Ethernet), and the link's sums as the Python oracle's."""
+    import packets as P
+
+    rows = R.ipv6_rows(fx)
+    assert len(rows) == 42 and {r[2] for r in rows} == {P.VALID, P.INVALID, P.UNCHECKED}
+    _both_restatements(rows)
+
+
+def test_receive_control_packets_verify(fx):
+    """TestIPv4ReceiveControl / TestIPv6ReceiveControl (network/ip_test.go:
+    293-398, :534-650): ICMP errors cut 10 B short, at the inner header, at
+    the 'extra info', at the ICMP header, to nothing.  An ICMP message under
+    8 B is dropped before any checksum (MALFORMED), a cut ICMPv6 message
+    fails its checksum (INVALID), a non-echo ICMPv4 one is never checked
+    (UNCHECKED); every packet the reference hands on is VALID or UNCHECKED."""
+    import packets as P
+
+    rows = R.control_rows(fx)
+    assert len(rows) == 18 and {r[2] for r in rows} == {P.VALID, P.INVALID, P.UNCHECKED, P.MALFORMED}
+    _both_restatements(rows)
+
+
+def _both_restatements(rows):
+    """packets.verify on the packet as one view; packets.verify_frame and the
+    C oracle_rx_ring on TUN and Ethernet rings (first view 128): the row's
+    verdict, and the same sums from both."""
     import numpy as np
 
     import oracle as O
     import packets as P
     from pktgen import ethernet
 
-    rows = R.ipv6_rows(fx)
-    assert len(rows) == 42 and {r[2] for r in rows} == {P.VALID, P.INVALID, P.UNCHECKED}
     for name, b, want in rows:
-        assert P.verify(b"", [b], len(b))[0] == want, name
+        assert P.verify(b"", [b] if b else [], len(b))[0] == want, name
     for link_hdr in (0, 14):
         frames = [ethernet(b) if link_hdr else b for _, b, _ in rows]
         stride = 128
