@@ -160,6 +160,16 @@ struct RxGeo {
   // from `ring` (< 4 GiB); nullptr: the ring's slots.
   const uint32_t* off;
   uint64_t limit;
+  // Timing variants only (tools/rx_ring_variants.hip 30-34; zero in the
+  // product): a buffer list sorted into bk_nb buckets of 2^bk_shift arena
+  // bytes first (bk_tup[j] = (off, len, list index, 0), bucket by bucket),
+  // the parse then run over bk_tup (LIST = 2).  bk_total (bk_nb words) is
+  // zero before the sort and left zero by the parse; bk_wgoff holds bk_nb
+  // words per 4,096 list entries.
+  uint4* bk_tup;
+  uint32_t* bk_total;
+  uint32_t* bk_wgoff;
+  uint32_t bk_shift, bk_nb;
 };
 hipError_t launch_rx_ring(const RxGeo& g, hipStream_t stream);
 

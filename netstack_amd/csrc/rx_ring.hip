@@ -138,6 +138,10 @@ __device__ __forceinline__ uint4 rx_load(__amdgpu_buffer_rsrc_t r, uint32_t off)
 // group g reads line 2 + (k - 2 + 3 g) mod (NB - 2), so the eight groups of
 // a wave do not all ask for line k of their slots at once (the same lines
 // are loaded and summed whole: the sums do not change).
+// LIST = 2 (timing variant, tools/rx_ring_variants.hip 30-32): a buffer list
+// already sorted into address buckets (g.bk_tup: off, len, list index), the
+// outputs written at the list index; 3: at the sorted position (timing only);
+// 4: 2 with the index loaded with the entry.  It lost.
 // LL = 1 (timing variant, tools/rx_ring_variants.hip): the packet's last
 // line (the one it may share with the next buffer) with the default cache
 // policy, its other lines >= 1 with AN, through two predicated loads of which
@@ -158,14 +162,22 @@ __global__ __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(OCC))) 
   // net header) and the link header.  A slot longer than the ring's stride is
   // malformed and counted (ns_csum_sync), a frame of no more than its link
   // header is dropped by the link (packet_dispatchers.go:268-270).
-  uint32_t rlen = live ? g.len[s] : 0u;
+  if constexpr (LIST >= 2) {  // leave the bucket totals zero for the next sort
+    if (blockIdx.x == 0 && threadIdx.x < g.bk_nb) g.bk_total[threadIdx.x] = 0u;
+  }
+  // LIST = 2: (off, len) from the sorted list; its list index (where the
+  // outputs go) is read again at the end rather than held
+  const uint32_t* tup32 = reinterpret_cast<const uint32_t*>(g.bk_tup);
+  uint32_t rlen = live ? (LIST >= 2 ? tup32[4 * s + 1] : g.len[s]) : 0u;
+  // LIST = 4 (timing): the list index read with the entry
+  const uint32_t idx4 = LIST == 4 && live ? tup32[4 * s + 2] : 0u;
   const uint32_t pre = g.frame_at + g.link;
   uint64_t slot;
   uint64_t wbase;
   uint32_t nrec;
   bool bad = false;  // LIST: a buffer not 16-B aligned or not inside the arena
   if constexpr (LIST) {
-    const uint32_t o = live ? g.off[s] : 0u;
+    const uint32_t o = live ? (LIST >= 2 ? tup32[4 * s] : g.off[s]) : 0u;
     bad = live && ((o & 15u) || (uint64_t)o + g.stride > g.limit);
     if (bad) rlen = 0;  // parsed as an empty frame: malformed
     slot = g.ring + (bad ? 0u : o);
@@ -410,6 +422,8 @@ __global__ __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(OCC))) 
   const uint32_t addr = (uint32_t)__builtin_amdgcn_mov_dpp((int)rs, 0x55, 0xF, 0xF, false);  // lane 1's
 
   if (li == 0 && live) {
+    // LIST = 3 (timing only: outputs in sorted order, not the list's)
+    const uint64_t os = LIST == 2 ? (uint64_t)tup32[4 * s + 2] : LIST == 4 ? (uint64_t)idx4 : s;
     uint32_t tr = 0;
     if (kind == 1) {  // PseudoHeaderChecksum (checksum.go:112-122), then xsum == 0xffff (segment.go:180)
       tr = rx_fold(rx_fold(rx_class(addr) + (tsize & 0xFFFFu) + 6u) + rx_class(w));
@@ -421,10 +435,10 @@ __global__ __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(OCC))) 
       tr = rx_fold(rx_fold(rx_class(addr) + tsize + 58u) + rx_class(w));
       verdict = (~tr & 0xFFFFu) == want ? kValid : kInvalid;
     }
-    if (g.verdict) g.verdict[s] = (uint8_t)verdict;
+    if (g.verdict) g.verdict[os] = (uint8_t)verdict;
     if (g.sums) {
-      g.sums[2 * s] = (uint16_t)(v4 ? rx_class(rs) : 0u);
-      g.sums[2 * s + 1] = (uint16_t)tr;
+      g.sums[2 * os] = (uint16_t)(v4 ? rx_class(rs) : 0u);
+      g.sums[2 * os + 1] = (uint16_t)tr;
     }
     if (over || bad) atomicAdd(g.err, 1ull);
   }

@@ -30,14 +30,18 @@ NAMES = {0: "product", 1: "all_default", 2: "all_nt", 3: "wg2", 4: "wg8", 5: "wg
          8: "occ6", 9: "nb12", 10: "checked_f0", 11: "f1_nb8", 12: "spec_line0", 13: "spec_lines01",
          14: "rotated_lines", 20: "bufs_product", 21: "bufs_nt_sc1", 22: "bufs_all_default", 23: "bufs_sc1",
          24: "bufs_lastline_default", 25: "bufs_lastline_default_nt_sc1", 26: "bufs_ll_sc0_nt",
-         27: "bufs_ll_sc0_sc1", 28: "bufs_ll_sc0_nt_sc1", 29: "bufs_ll_sc0"}
+         27: "bufs_ll_sc0_sc1", 28: "bufs_ll_sc0_nt_sc1", 29: "bufs_ll_sc0",
+         30: "bufs_sorted", 31: "bufs_sorted_outputs_in_sorted_order", 32: "bufs_sorted_index_early",
+         33: "sort_only", 34: "count_only"}
 
 
 class RxGeo(ctypes.Structure):
     _fields_ = [("ring", ctypes.c_uint64), ("stride", ctypes.c_uint64), ("len", ctypes.c_void_p),
                 ("sums", ctypes.c_void_p), ("verdict", ctypes.c_void_p), ("err", ctypes.c_void_p),
                 ("n", ctypes.c_uint32), ("frame_at", ctypes.c_uint32), ("link", ctypes.c_uint32),
-                ("view0", ctypes.c_uint32), ("off", ctypes.c_void_p), ("limit", ctypes.c_uint64)]
+                ("view0", ctypes.c_uint32), ("off", ctypes.c_void_p), ("limit", ctypes.c_uint64),
+                ("bk_tup", ctypes.c_void_p), ("bk_total", ctypes.c_void_p), ("bk_wgoff", ctypes.c_void_p),
+                ("bk_shift", ctypes.c_uint32), ("bk_nb", ctypes.c_uint32)]
 
 
 def main():
@@ -54,6 +58,8 @@ def main():
     ap.add_argument("--bufs", default="", choices=("", "shuffled", "ring"),
                     help="the frames as a buffer list (ns_csum_rx_bufs) in shuffled or ring order; variants "
                          "20-23 then (the ring variants need no list)")
+    ap.add_argument("--bk-shift", type=int, default=0,
+                    help="variant 30: bucket size 2^shift bytes (0: the arena over at most 128 buckets)")
     ap.add_argument("--trend", type=int, default=0,
                     help="then time this many back-to-back launches of the product one by one (run-long drift)")
     args = ap.parse_args()
@@ -91,8 +97,16 @@ def main():
     # two rings of the same frames, alternating (3.2 GB > the MALL), as
     # bench.py runs it
     arena2 = spread(W.rx_ring_batch(n, 9, dev, corrupt_every=1000)[0]) if args.rotate else arena
+    limit = arena.numel()
+    shift = args.bk_shift or max(12, (limit - 1).bit_length() - 7)
+    nb = (limit + (1 << shift) - 1) >> shift
+    assert nb <= 128, nb
+    tup = torch.empty(n * 4, dtype=torch.int32, device=dev)
+    total = torch.zeros(128, dtype=torch.int32, device=dev)
+    wgoff = torch.empty(((n + 4095) // 4096) * nb, dtype=torch.int32, device=dev)
     gs = [RxGeo(a.data_ptr(), stride, lens.data_ptr(), sums.data_ptr(), verdict.data_ptr(), err.data_ptr(),
-                n, 0, 0, 0, offs.data_ptr() if offs is not None else None, a.numel() if offs is not None else 0)
+                n, 0, 0, 0, offs.data_ptr() if offs is not None else None, a.numel() if offs is not None else 0,
+                tup.data_ptr(), total.data_ptr(), wgoff.data_ptr(), shift, nb)
           for a in (arena, arena2)]
     g = gs[0]
     algo = n * (W.RX_PKT + 9)
@@ -114,7 +128,7 @@ def main():
         sums.fill_(0x1234)
         assert libs[k].rxv_launch(ctypes.byref(g), stream.cuda_stream, max(k, 0)) == 0
         torch.cuda.synchronize()
-        ok[k] = bool(torch.equal(verdict, v0) and torch.equal(sums, s0))
+        ok[k] = bool(torch.equal(verdict, v0) and torch.equal(sums, s0)) if k not in (31, 33, 34) else None
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     for _ in range(args.rounds):
         for k in ks:

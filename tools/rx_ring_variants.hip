@@ -16,8 +16,107 @@
 //  24-29 buffer lists with each packet's last line at the default policy
 //        (LL), the other lines >= 1 nt / nt sc1 / sc0 nt / sc0 sc1 /
 //        sc0 nt sc1 / sc0
-// Every variant computes the same verdicts and sums.  Not part of the ABI.
+//  30    buffer lists sorted into address buckets first (rx_bk_count,
+//        rx_bk_place, then the parse over the sorted list: LIST = 2)
+//  31    30 with the outputs written in sorted order (timing only: wrong
+//        places)   32  30 with the list index loaded with the entry
+//  33    the sort alone (rx_bk_count + rx_bk_place)   34  rx_bk_count alone
+// Every variant but 31, 33 and 34 computes the product's verdicts and sums.
+// Not part of the ABI.
 #include "../netstack_amd/csrc/rx_ring.hip"
+
+namespace nsk {
+// Sorting a buffer list into address buckets (variants 30-34, LIST = 2).
+// A pool hands its buffers out in any order; verified in that order,
+// neighbouring buffers' shared edge lines are read twice and the reads
+// scatter over the whole pool.
+// Two passes over the list, 4,096 entries per workgroup, bring it into
+// bucket order (bucket = off >> bk_shift; order inside a bucket arbitrary):
+// rx_bk_count histograms its entries in LDS and reserves each bucket's run
+// with one atomic per bucket (bk_wgoff: where its run starts in the bucket);
+// rx_bk_place turns the bucket totals into starts and writes each entry's
+// (off, len, index) at start + run offset + its LDS rank.
+constexpr uint32_t kBkChunk = 4096, kBkMax = 128, kBkPer = kBkChunk / 256;
+
+__device__ __forceinline__ uint32_t rx_bk_of(const RxGeo& g, uint32_t o) {
+  const uint32_t b = o >> g.bk_shift;
+  return b < g.bk_nb ? b : g.bk_nb - 1u;
+}
+
+__global__ __launch_bounds__(256) void rx_bk_count(RxGeo g) {
+  __shared__ uint32_t h[kBkMax];
+  const uint32_t t = threadIdx.x;
+  if (t < kBkMax) h[t] = 0u;
+  __syncthreads();
+  const uint64_t c0 = (uint64_t)blockIdx.x * kBkChunk;
+  uint32_t o[kBkPer];
+#pragma unroll
+  for (uint32_t j = 0; j < kBkPer; ++j) {
+    const uint64_t i = c0 + t + 256u * j;
+    o[j] = i < g.n ? g.off[i] : 0u;
+  }
+#pragma unroll
+  for (uint32_t j = 0; j < kBkPer; ++j)
+    if (c0 + t + 256u * j < g.n) atomicAdd(&h[rx_bk_of(g, o[j])], 1u);
+  __syncthreads();
+  if (t < g.bk_nb) {
+    const uint32_t c = h[t];
+    g.bk_wgoff[(uint64_t)blockIdx.x * g.bk_nb + t] = c ? atomicAdd(&g.bk_total[t], c) : 0u;
+  }
+}
+
+__global__ __launch_bounds__(256) void rx_bk_place(RxGeo g) {
+  __shared__ uint32_t sc[kBkMax], cur[kBkMax];
+  const uint32_t t = threadIdx.x;
+  const uint64_t c0 = (uint64_t)blockIdx.x * kBkChunk;
+  uint32_t o[kBkPer], l[kBkPer];
+#pragma unroll
+  for (uint32_t j = 0; j < kBkPer; ++j) {
+    const uint64_t i = c0 + t + 256u * j;
+    o[j] = i < g.n ? g.off[i] : 0u;
+    l[j] = i < g.n ? g.len[i] : 0u;
+  }
+  const uint32_t tot = t < g.bk_nb ? g.bk_total[t] : 0u;
+  if (t < kBkMax) sc[t] = tot;
+  __syncthreads();
+  for (uint32_t d = 1; d < kBkMax; d <<= 1) {  // inclusive scan of the totals
+    const uint32_t x = t < kBkMax && t >= d ? sc[t - d] : 0u;
+    __syncthreads();
+    if (t < kBkMax) sc[t] += x;
+    __syncthreads();
+  }
+  if (t < g.bk_nb) cur[t] = sc[t] - tot + g.bk_wgoff[(uint64_t)blockIdx.x * g.bk_nb + t];
+  __syncthreads();
+#pragma unroll
+  for (uint32_t j = 0; j < kBkPer; ++j) {
+    const uint64_t i = c0 + t + 256u * j;
+    if (i < g.n) {
+      const uint32_t at = atomicAdd(&cur[rx_bk_of(g, o[j])], 1u);
+      g.bk_tup[at] = make_uint4(o[j], l[j], (uint32_t)i, 0u);
+    }
+  }
+}
+
+// The sorted list's parse: the product shape over bk_tup.
+template <int NB, int L = 2>
+static hipError_t launch_rx_bufs_sorted_t(const RxGeo& g, hipStream_t stream) {
+  const uint32_t wgs = (uint32_t)((g.n + kBkChunk - 1) / kBkChunk);
+  hipLaunchKernelGGL(rx_bk_count, dim3(wgs), dim3(256), 0, stream, g);
+  hipLaunchKernelGGL(rx_bk_place, dim3(wgs), dim3(256), 0, stream, g);
+  return launch_rx_ring_t<NB, 0, 2, kWaves, 1, 1, 0, L>(g, stream);
+}
+
+static hipError_t launch_rx_bufs_sorted(const RxGeo& g, hipStream_t stream) {
+  if (g.n == 0) return hipSuccess;
+  switch (rx_batch_lines(g)) {
+    case 2: return launch_rx_bufs_sorted_t<2>(g, stream);
+    case 4: return launch_rx_bufs_sorted_t<4>(g, stream);
+    case 8: return launch_rx_bufs_sorted_t<8>(g, stream);
+    default: return launch_rx_bufs_sorted_t<13>(g, stream);
+  }
+}
+
+}  // namespace nsk
 
 extern "C" int rxv_launch(const nsk::RxGeo* g, void* stream, int k) {
   hipStream_t s = (hipStream_t)stream;
@@ -46,6 +145,16 @@ extern "C" int rxv_launch(const nsk::RxGeo* g, void* stream, int k) {
     case 27: return (int)nsk::launch_rx_ring_t<13, 0, 17, 4, 1, 1, 0, 1, 0, 1>(*g, s);
     case 28: return (int)nsk::launch_rx_ring_t<13, 0, 19, 4, 1, 1, 0, 1, 0, 1>(*g, s);
     case 29: return (int)nsk::launch_rx_ring_t<13, 0, 1, 4, 1, 1, 0, 1, 0, 1>(*g, s);
+    case 30: return (int)nsk::launch_rx_bufs_sorted(*g, s);
+    case 31: return (int)nsk::launch_rx_bufs_sorted_t<13, 3>(*g, s);
+    case 32: return (int)nsk::launch_rx_bufs_sorted_t<13, 4>(*g, s);
+    case 33: case 34: {
+      const uint32_t wgs = (uint32_t)((g->n + nsk::kBkChunk - 1) / nsk::kBkChunk);
+      hipLaunchKernelGGL(nsk::rx_bk_count, dim3(wgs), dim3(256), 0, s, *g);
+      if (k == 33) hipLaunchKernelGGL(nsk::rx_bk_place, dim3(wgs), dim3(256), 0, s, *g);
+      hipMemsetAsync(g->bk_total, 0, 4 * g->bk_nb, s);
+      return (int)hipGetLastError();
+    }
     default: return (int)nsk::launch_rx_ring_t<13>(*g, s);
   }
 }
