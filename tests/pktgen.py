@@ -247,3 +247,56 @@ def min_size_frames(rng, link_hdr: int):
     if link_hdr:
         frames = [ethernet(bytes(f)) for f in frames]
     return [bytes(f) for f in frames], want
+
+
+def fuzz_fields(rng, p: bytearray) -> bytearray:
+    """One header field of a packet set to a boundary or random value: the
+    fields the receive rules read (IPv4 version/IHL, TotalLength, flags and
+    fragment offset, protocol; IPv6 PayloadLength and NextHeader; the TCP
+    data offset, the ICMP type, the transport checksum field).  Checksums are
+    left as they were, so most results are INVALID or MALFORMED, and the
+    boundaries sit where a rule changes its mind."""
+    p = bytearray(p)
+    if len(p) < 1:
+        return p
+    n = len(p)
+    v6 = (p[0] >> 4) == 6
+    ipl = 40 if v6 else 4 * (p[0] & 15)
+    pick = lambda *vals: int(vals[int(rng.integers(0, len(vals)))])  # noqa: E731
+    f = int(rng.integers(0, 6))
+    if not v6 and f == 0:
+        p[0] = pick(0x40, 0x44, 0x45, 0x46, 0x4F, 0x60, 0x00, int(rng.integers(0, 256)))
+    elif not v6 and f == 1 and n >= 4:
+        struct.pack_into(">H", p, 2, pick(0, 19, 20, ipl, ipl + 7, ipl + 8, ipl + 19, ipl + 20, n - 1, n, n + 1,
+                                          0xFFFF, int(rng.integers(0, 65536))) & 0xFFFF)
+    elif not v6 and f == 2 and n >= 8:
+        struct.pack_into(">H", p, 6, pick(0x2000, 0x1FFF, 0x3FFF, 0x4000, 0x0001, 0x2001, int(rng.integers(0, 65536))))
+    elif v6 and f in (0, 1) and n >= 6:
+        struct.pack_into(">H", p, 4, pick(0, 7, 8, 19, 20, n - 41, n - 40, n - 39, 0xFFFF,
+                                          int(rng.integers(0, 65536))) & 0xFFFF)
+    elif f == 3 and n > (6 if v6 else 9):
+        p[6 if v6 else 9] = pick(1, 6, 17, 58, 0, 44, int(rng.integers(0, 256)))
+    elif f == 4 and n > ipl + 12:
+        proto = p[6] if v6 else p[9]
+        if proto == 6:
+            p[ipl + 12] = pick(0x00, 0x40, 0x50, 0x60, 0xF0, 0x80, int(rng.integers(0, 256)))
+        else:
+            p[ipl] = pick(0, 3, 8, 128, 129, 133, 136, int(rng.integers(0, 256)))
+    elif n > ipl + 18:
+        proto = p[6] if v6 else p[9]
+        at = ipl + (16 if proto == 6 else 6 if proto == 17 else 2)
+        p[at + int(rng.integers(0, 2))] ^= 1 << int(rng.integers(0, 8))
+    return p
+
+
+def fuzzed_packets(rng, count: int, max_payload: int = 3000):
+    """valid_packet / random_packet bytes, each with one field fuzzed."""
+    out = []
+    for _ in range(count):
+        if rng.random() < 0.7:
+            kind = ("tcp4", "tcp6", "icmp4", "icmp6", "udp4")[int(rng.integers(0, 5))]
+            p = valid_packet(rng, kind, int(rng.choice([0, 1, 7, 8, 20, int(rng.integers(0, max_payload))])))
+        else:
+            p = random_packet(rng, max_payload)
+        out.append(bytes(fuzz_fields(rng, p)))
+    return out

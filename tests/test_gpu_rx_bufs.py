@@ -102,6 +102,23 @@ def test_minimum_sizes(engine, link_hdr, first_view):
     assert verdict.tolist() == want
 
 
+@pytest.mark.parametrize("link_hdr,first_view", [(0, 128), (14, 128)])
+def test_fuzzed_header_fields(engine, link_hdr, first_view):
+    """Header fields at their boundaries (pktgen.fuzz_fields) from a shuffled
+    pool: the oracle's verdicts and sums."""
+    from pktgen import ethernet, fuzzed_packets
+
+    rng = np.random.default_rng(5970 + link_hdr)
+    frames = [ethernet(p) if link_hdr else p for p in fuzzed_packets(rng, 2000)]
+    cap = (max(len(f) for f in frames) + 15) // 16 * 16
+    arena, offs, lens = _pool(frames, cap, seed=5971, ring_off=32)
+    ring = dict(ring_off=32, stride=cap, n=len(frames), link_hdr=link_hdr, first_view=first_view)
+    verdict, sums = _run_bufs(engine, arena, offs, lens, ring)
+    wv, ws = _want(arena, offs, lens, ring)
+    assert np.array_equal(verdict, wv) and np.array_equal(sums, ws)
+    assert {0, 1, 2, 3} <= set(verdict.tolist())
+
+
 def test_bad_buffers_are_malformed_and_counted(engine):
     rng = np.random.default_rng(5800)
     _, frames = _frames(rng, 64, 14, max_payload=1400)

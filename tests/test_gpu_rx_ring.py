@@ -164,6 +164,38 @@ def test_ipv6_and_control_fixtures(engine, link_hdr, first_view):
     assert list(v2) == got
 
 
+@pytest.mark.parametrize("link_hdr,first_view", [(0, 0), (0, 128), (14, 128), (0, 64), (14, 78)])
+def test_fuzzed_header_fields(engine, link_hdr, first_view):
+    """Every header field the receive rules read set to its boundaries or a
+    random value (pktgen.fuzz_fields: version/IHL, TotalLength, fragment
+    field, protocol, IPv6 PayloadLength and NextHeader, TCP data offset, ICMP
+    type, the checksum field): the ring's verdicts and sums equal the
+    oracle's, and ns_csum_packet_buffers gives the same over the link's
+    views."""
+    from pktgen import fuzzed_packets
+
+    from netstack_amd.packet import PacketBuffer, verify_packet_buffers
+
+    rng = np.random.default_rng(6100 + link_hdr + first_view)
+    pk = fuzzed_packets(rng, 3000)
+    frames = [ethernet(p) if link_hdr else p for p in pk]
+    stride = (max(len(f) for f in frames) + 15) // 16 * 16
+    got = _check(engine, frames, stride, link_hdr=link_hdr, first_view=first_view, seed=6)
+    assert {0, 1, 2, 3} <= set(got)
+    if first_view in (0, 128):  # the views ns_csum_packet_buffers is given are BufConfig's (or one)
+        ip = [k for k, p in enumerate(pk) if p and (p[0] >> 4) in (4, 6)]
+        pkts = [PacketBuffer(Data=views_bufconfig(pk[k], link_hdr)) if first_view else
+                PacketBuffer(Data=_one_view(pk[k])) for k in ip]
+        v2, _ = verify_packet_buffers(pkts, engine)
+        assert list(v2) == [got[k] for k in ip]
+
+
+def _one_view(b: bytes):
+    from netstack_amd.buffer import NewVectorisedView, View
+
+    return NewVectorisedView(len(b), [View(bytearray(b))])
+
+
 @pytest.mark.parametrize("link_hdr,first_view", [(0, 0), (0, 128), (0, 64), (14, 128), (14, 0), (14, 78)])
 def test_minimum_sizes(engine, link_hdr, first_view):
     """Every transport message from 0 to its minimum + 2 bytes (TCP 20, UDP 8,

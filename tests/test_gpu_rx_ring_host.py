@@ -71,6 +71,23 @@ def test_minimum_sizes(engine, link_hdr, first_view, ring_off):
     assert verdict.tolist() == want
 
 
+@pytest.mark.parametrize("link_hdr,first_view", [(0, 0), (14, 128)])
+def test_fuzzed_header_fields(engine, link_hdr, first_view):
+    """Header fields at their boundaries (pktgen.fuzz_fields) in a host ring:
+    the oracle's verdicts and sums, and the device ring's."""
+    from pktgen import ethernet, fuzzed_packets
+
+    rng = np.random.default_rng(5980 + link_hdr)
+    frames = [ethernet(p) if link_hdr else p for p in fuzzed_packets(rng, 2000)]
+    stride = (max(len(f) for f in frames) + 15) // 16 * 16
+    arena, ln = _ring(frames, stride, ring_off=3)
+    ring = dict(ring_off=3, stride=stride, n=len(frames), link_hdr=link_hdr, first_view=first_view)
+    verdict, sums = engine.rx_ring_host(arena, ring, ln)
+    wv, ws = _want(arena, ln, ring)
+    assert np.array_equal(verdict, wv) and np.array_equal(sums, ws)
+    assert {0, 1, 2, 3} <= set(verdict.tolist())
+
+
 @pytest.mark.parametrize("ring_off", [0, 3, 1000])
 def test_small_staging_and_unaligned_ring(oracle_mod, ring_off):
     """A staging budget of 7 slots: the ring goes up in chunks that cycle

@@ -61,3 +61,23 @@ def test_verify_frame_is_verify_over_the_links_views(link_hdr):
         vv = views_bufconfig(p, link_hdr)
         want = P.verify(b"", [bytes(v) for v in vv.Views()], vv.Size())
         assert P.verify_frame(frame, len(frame), 0, link_hdr, 128) == want
+
+
+@pytest.mark.parametrize("link_hdr,first_view", [(0, 0), (0, 128), (14, 128), (0, 64)])
+def test_c_ring_matches_verify_frame_on_fuzzed_fields(link_hdr, first_view):
+    """Every header field the receive rules read, set to its boundaries
+    (pktgen.fuzz_fields): both restatements give the same verdicts and sums."""
+    from pktgen import fuzzed_packets
+
+    rng = np.random.default_rng(900 + link_hdr + first_view)
+    pk = fuzzed_packets(rng, 1500)
+    frames = [ethernet(p) if link_hdr else p for p in pk]
+    stride = (max(len(f) for f in frames) + 15) // 16 * 16
+    arena, lens = _ring(frames, stride, 0, 2)
+    v, s = O.c_rx_ring(arena, lens, stride, len(frames), link_hdr=link_hdr, first_view=first_view, nthreads=3)
+    seen = set()
+    for k in range(len(frames)):
+        want = P.verify_frame(bytes(arena[k * stride:(k + 1) * stride]), int(lens[k]), 0, link_hdr, first_view)
+        assert (int(v[k]), int(s[2 * k]), int(s[2 * k + 1])) == want, (k, pk[k][:64].hex())
+        seen.add(want[0])
+    assert seen == {P.INVALID, P.VALID, P.UNCHECKED, P.MALFORMED}
