@@ -139,3 +139,19 @@ def control_rows(fx):
     and TestIPv6ReceiveControl's ICMP errors at each case's cut, with the
     verdict each owes (network/ip_test.go:293-398, :534-650)."""
     return [(c["name"], bytes.fromhex(c["packet"]), c["verdict"]) for c in fx["receive_control"]]
+
+
+def fill_rows(fx):
+    """The packets of rx_fixtures.json whose checksum the reference's own
+    tests computed (ipv6_test.go / ndp_test.go: ICMPv6Checksum over the
+    message, UDP's ^CalculateChecksum over the pseudo-header; ip_test.go
+    TestIPv6ReceiveControl's uncut ICMPv6 errors), each with that field
+    zeroed: (name, zeroed packet, the packet as the test built it)."""
+    rows = []
+    for c in fx["ipv6_receive"] + [c for c in fx["receive_control"] if c["name"].startswith("ipv6/") and c["verdict"] == 1]:
+        b = bytes.fromhex(c["packet"])
+        at = 40 + (6 if b[6] == 17 else 2)
+        z = bytearray(b)
+        z[at:at + 2] = b"\0\0"
+        rows.append((c["name"], bytes(z), b))
+    return rows

@@ -306,3 +306,22 @@ def test_acquired_stage_is_read_in_place(engine, big):
         engine.stage_release(st)
     st2 = engine.stage_acquire(nbytes)
     engine.stage_release(st2)
+
+
+def test_fill_reproduces_the_reference_tests_checksums(engine):
+    """ns_csum_packet_buffers (NS_PKB_FILL) writes into each fixture packet of
+    tests/rxcases.py fill_rows, its checksum field zeroed, the checksum the
+    reference's own test computed (ICMPv6Checksum over NDP messages and
+    ICMPv6 errors, UDP's ^CalculateChecksum over an 8-B datagram)."""
+    import rxcases
+
+    from netstack_amd.buffer import NewPrependableFromView, NewVectorisedView, View
+    from netstack_amd.packet import PacketBuffer, fill_packet_buffers
+
+    rows = rxcases.fill_rows(rxcases.fixtures())
+    pkts = [PacketBuffer(Data=NewVectorisedView(0, []), Header=NewPrependableFromView(View(bytearray(z))))
+            for _, z, _ in rows]
+    fill_packet_buffers(pkts, engine)
+    for (name, _, want), pk in zip(rows, pkts):
+        assert bytes(pk.Header.View()) == want, name
+

@@ -260,3 +260,17 @@ def _both_restatements(rows):
         for k, (name, _, want) in enumerate(rows):
             py = P.verify_frame(bytes(arena[k * stride:(k + 1) * stride]), int(lens[k]), 0, link_hdr, 128)
             assert py[0] == want and (int(v[k]), int(s[2 * k]), int(s[2 * k + 1])) == py, (name, link_hdr)
+
+
+def test_fill_reproduces_the_reference_tests_checksums(fx):
+    """The transmit restatement (packets.fill: sendUDP's and ICMPv6Checksum's
+    rules) writes into each fixture packet, its checksum field zeroed, the
+    very checksum the reference's own test computed for it (ipv6_test.go,
+    ndp_test.go, ip_test.go; tests/rxcases.py fill_rows)."""
+    import packets as P
+
+    rows = R.fill_rows(fx)
+    assert len(rows) == 21 + 4
+    for name, zeroed, want in rows:
+        assert P.fill(zeroed, [], 0)[0] == want, name
+
