@@ -31,7 +31,8 @@ ipv6_receive      — the IPv6 packets network/ipv6's tests inject and expect to
     TestReceiveOnSolicitedNodeAddr (:160-225) send them; ndp_test.go:75-184
     TestHopLimitValidation (each NDP type at its table size, lladdr0 ->
     lladdr1, hop limit 254 and 255) and :189-372 TestRouterAdvertValidation
-    (its seven RAs to ff02::1, 15-B NDPPayloadTooSmall among them).  Each
+    (its seven RAs to ff02::1, 15-B NDPPayloadTooSmall among them);
+    stack/ndp_test.go:361-420 TestDADFail's NS from :: and NA.  Each
     row: the packet, the verdict the receive path owes it (VALID; UNCHECKED
     for UDP) and what the reference's test then expects — the drops these
     tests count (hop limit, code, source, RA size) all come after the
@@ -190,7 +191,22 @@ def ipv6_receive():
                      "reference": "ICMP.V6PacketsReceived.RouterAdvert + 1" if ok
                      else "ICMP.V6PacketsReceived.Invalid + 1 (after the checksum)",
                      "source": "network/ipv6/ndp_test.go:189-372"})
-    assert len(rows) == 4 + 10 + 7
+    # stack/ndp_test.go:361-420 TestDADFail: a DAD probe (NS from the
+    # unspecified address to the target's solicited-node group) and an
+    # NA with the S and O flags, both for addr1
+    any6 = bytes(16)
+    snmc1 = b"\xff\x02" + bytes(9) + b"\x01\xff" + addr1[-3:]
+    ns = bytearray(24)
+    ns[0], ns[8:24] = 135, addr1
+    rows.append({"name": "dad_rx_solicit", "packet": _ipv6(any6, snmc1, 58, 255, ns, 2), "verdict": 1,
+                 "reference": "ICMP.V6PacketsReceived.NeighborSolicit + 1 (DAD fails)",
+                 "source": "stack/ndp_test.go:361-420"})
+    na = bytearray(32)
+    na[0], na[4], na[8:24] = 136, 0x60, addr1
+    rows.append({"name": "dad_rx_advert", "packet": _ipv6(addr1, all_nodes, 58, 255, na, 2), "verdict": 1,
+                 "reference": "ICMP.V6PacketsReceived.NeighborAdvert + 1 (DAD fails)",
+                 "source": "stack/ndp_test.go:361-420"})
+    assert len(rows) == 4 + 10 + 7 + 2
     return rows
 
 

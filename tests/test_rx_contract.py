@@ -218,7 +218,7 @@ def test_ipv6_receive_packets_verify(fx):
     import packets as P
 
     rows = R.ipv6_rows(fx)
-    assert len(rows) == 42 and {r[2] for r in rows} == {P.VALID, P.INVALID, P.UNCHECKED}
+    assert len(rows) == 46 and {r[2] for r in rows} == {P.VALID, P.INVALID, P.UNCHECKED}
     _both_restatements(rows)
 
 
@@ -270,7 +270,7 @@ def test_fill_reproduces_the_reference_tests_checksums(fx):
     import packets as P
 
     rows = R.fill_rows(fx)
-    assert len(rows) == 21 + 4
+    assert len(rows) == 23 + 4
     for name, zeroed, want in rows:
         assert P.fill(zeroed, [], 0)[0] == want, name
 
