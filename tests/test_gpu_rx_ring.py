@@ -387,17 +387,20 @@ def test_invalid_geometry(engine):
 
 
 @pytest.mark.slow
-def test_full_size_ring(engine):
-    """BASELINE cfg2's shape as a receive ring (1M x 1500-B IPv4/TCP packets
-    at stride 1504, every 997th with one corrupted byte): exactly those fail;
-    every IPv4 header sums to 0xffff; 256 random slots against the oracle."""
+@pytest.mark.parametrize("v6", [False, True])
+def test_full_size_ring(engine, v6):
+    """BASELINE cfg2's shape as a receive ring (1M x 1500-B IPv4/TCP, or
+    IPv6/TCP, packets at stride 1504, every 997th with one corrupted byte):
+    exactly those fail; every IPv4 header sums to 0xffff (IPv6: no IP sum,
+    0); 256 random slots against the oracle."""
     import torch
 
     from netstack_amd import workloads as W
 
     n = 1 << 20
     dev = torch.device("cuda", 0)
-    arena, lens, bad = W.rx_ring_batch(n, 9, dev, corrupt_every=997)
+    make = W.rx_ring_batch_v6 if v6 else W.rx_ring_batch
+    arena, lens, bad = make(n, 9, dev, corrupt_every=997)
     ring = dict(stride=W.RX_STRIDE, n=n)
     verdict, sums = engine.rx_ring(arena, ring, lens)
     torch.cuda.synchronize()
@@ -406,7 +409,7 @@ def test_full_size_ring(engine):
     want[bad] = 0
     assert (v == want).all()
     s = sums.cpu().numpy().view(np.uint16)
-    assert (s[0::2] == 0xFFFF).all()
+    assert (s[0::2] == (0 if v6 else 0xFFFF)).all()
     rng = np.random.default_rng(29)
     pick = np.sort(rng.choice(n, 256, replace=False))
     a = arena.view(n, W.RX_STRIDE)[torch.from_numpy(pick).to(dev)].cpu().numpy()

@@ -58,6 +58,7 @@ def main():
     ap.add_argument("--bufs", default="", choices=("", "shuffled", "ring"),
                     help="the frames as a buffer list (ns_csum_rx_bufs) in shuffled or ring order; variants "
                          "20-23 then (the ring variants need no list)")
+    ap.add_argument("--ipv6", action="store_true", help="IPv6/TCP frames instead of IPv4/TCP")
     ap.add_argument("--bk-shift", type=int, default=0,
                     help="variant 30: bucket size 2^shift bytes (0: the arena over at most 128 buckets)")
     ap.add_argument("--trend", type=int, default=0,
@@ -79,7 +80,8 @@ def main():
         b[:, :W.RX_STRIDE] = a.view(n, W.RX_STRIDE)
         return b.view(-1)
 
-    arena, lens, bad = W.rx_ring_batch(n, 9, dev, corrupt_every=1000)
+    make = W.rx_ring_batch_v6 if args.ipv6 else W.rx_ring_batch
+    arena, lens, bad = make(n, 9, dev, corrupt_every=1000)
     arena = spread(arena)
     ring = dict(stride=stride, n=n)
     offs = None
@@ -96,7 +98,13 @@ def main():
     sums = torch.empty(2 * n, dtype=torch.int16, device=dev)
     # two rings of the same frames, alternating (3.2 GB > the MALL), as
     # bench.py runs it
-    arena2 = spread(W.rx_ring_batch(n, 9, dev, corrupt_every=1000)[0]) if args.rotate else arena
+    # the product's verdicts: VALID but for the corrupted packets (INVALID)
+    want = torch.ones(n, dtype=torch.uint8, device=dev)
+    want[torch.from_numpy(bad).to(dev)] = 0
+    if args.bufs:
+        want = want[torch.from_numpy(perm).to(dev)]
+    product_ok = bool(torch.equal(v0, want))
+    arena2 = spread(make(n, 9, dev, corrupt_every=1000)[0]) if args.rotate else arena
     limit = arena.numel()
     shift = args.bk_shift or max(12, (limit - 1).bit_length() - 7)
     nb = (limit + (1 << shift) - 1) >> shift
@@ -157,7 +165,8 @@ def main():
         q = max(1, args.trend // 10)
         trend = {"per_launch_us": [round(x, 1) for x in t],
                  "first_decile_us": round(float(np.median(t[:q])), 2), "last_decile_us": round(float(np.median(t[-q:])), 2)}
-    print(json.dumps({"workload": f"1M x 1500-B IPv4/TCP in {stride}-B slots" + (", 2 rotating rings" if args.rotate else ", one ring re-read") + (f", a buffer list in {args.bufs} order" if args.bufs else ""), "algo_bytes": algo, "variants": out,
+    print(json.dumps({"product_verdicts_as_generated": product_ok,
+                      "workload": f"1M x 1500-B {'IPv6' if args.ipv6 else 'IPv4'}/TCP in {stride}-B slots" + (", 2 rotating rings" if args.rotate else ", one ring re-read") + (f", a buffer list in {args.bufs} order" if args.bufs else ""), "algo_bytes": algo, "variants": out,
                       "trend": trend}, indent=1))
 
 
