@@ -189,12 +189,16 @@ def test_fields_only_stores(engine, oracle_mod):
 
 def test_many_segments_full_tiles(engine, oracle_mod):
     """Batches large enough for the launcher's own tiles, MSS 1460 (102 MB:
-    two passes by size) and MSS 16 (one pass; up to two segment ends per
-    window per lane row), with and without d_out."""
+    two passes by size), the same over an IPv6 route (74-B slots: the header
+    pass's 64-slot tile would pass 4 KiB, so the launcher picks another) and
+    MSS 16 (one pass; up to two segment ends per window per lane row), with
+    and without d_out."""
     import torch
 
-    for size, mss in ((1460 * 70_000 - 3, 1460), (16 * 70_000 + 9, 16)):
-        geo, total = _geo(size, mss, hdr_off=7)
+    for size, mss, v6 in ((1460 * 70_000 - 3, 1460, False), (1440 * 72_000 - 5, 1440, True),
+                          (16 * 70_000 + 9, 16, False)):
+        geo, total = (_geo(size, mss, slot=74, ip_len=0, tcp_at=54, src=V6S, dst=V6D, hdr_off=7) if v6
+                      else _geo(size, mss, hdr_off=7))
         a = _arena(total, geo, seed=mss)
         wa, ws = _want(oracle_mod, a, geo)
         ga, gs = _run(engine, a, geo)
