@@ -742,18 +742,24 @@ static hipError_t launch_header_pass(TxGeo h, hipStream_t stream, uint32_t per_c
   uint32_t grid = 0;
   hipError_t e = tx_shape(h, 2, &grid);
   if (e != hipSuccess) return e;
-  // the persistent kernel's conditions (tcp_tx_hdr): full TCP mode with whole
-  // write-back, tiles of <= 64 segments starting 16-B aligned, <= 4 KiB of
-  // slots each, d_out 4-B aligned
-  if (h.tile > 64 || (uint64_t)h.tile * h.slot > 4096 || ((uint64_t)h.tile * h.slot) % 16 || (h.hdr & 15) ||
-      !(h.mode & kTxTcpFull) || (h.mode & kTxFieldsOnly) || ((uintptr_t)h.out & 3) || h.xs == nullptr)
+  // tcp_tx_hdr's conditions: full TCP mode with whole write-back, tiles of
+  // <= 64 segments starting 16-B aligned, <= 8 KiB of slots each (CPL = 4,
+  // 5, 6 or 8 chunks per lane: IPv4's 54-B slots take 4, an IPv6 route's
+  // 74-B slots 5), d_out 4-B aligned
+  const uint64_t region = (uint64_t)h.tile * h.slot;
+  if (h.tile > 64 || region > 8192 || region % 16 || (h.hdr & 15) || !(h.mode & kTxTcpFull) ||
+      (h.mode & kTxFieldsOnly) || ((uintptr_t)h.out & 3) || h.xs == nullptr)
     return launch_tcp_tx_t<16, 2, SP, 1, 0, 2>(h, stream);
   const uint64_t tiles = (h.n + h.tile - 1) / h.tile;
   if (DEP == 1 && per_cu >= 1 && per_cu <= 4) h.wpg = per_cu;  // one-shot: per_cu = waves per workgroup (A/B)
   const uint64_t waves = DEP == 1 ? tiles : std::min<uint64_t>(tiles, (uint64_t)tx_cu_count() * (per_cu ? per_cu : 24u));
   const uint32_t wgs = (uint32_t)((waves + h.wpg - 1) / h.wpg);
-  hipLaunchKernelGGL((tcp_tx_hdr<4, SP, DEP>), dim3(wgs), dim3(64 * h.wpg), (size_t)h.lds_wave * h.wpg, stream, h,
-                     (uint32_t)tiles);
+  const size_t lds = (size_t)h.lds_wave * h.wpg;
+  const uint32_t cpl = (uint32_t)((region + 1023) / 1024);
+  if (cpl <= 4) hipLaunchKernelGGL((tcp_tx_hdr<4, SP, DEP>), dim3(wgs), dim3(64 * h.wpg), lds, stream, h, (uint32_t)tiles);
+  else if (cpl == 5) hipLaunchKernelGGL((tcp_tx_hdr<5, SP, DEP>), dim3(wgs), dim3(64 * h.wpg), lds, stream, h, (uint32_t)tiles);
+  else if (cpl == 6) hipLaunchKernelGGL((tcp_tx_hdr<6, SP, DEP>), dim3(wgs), dim3(64 * h.wpg), lds, stream, h, (uint32_t)tiles);
+  else hipLaunchKernelGGL((tcp_tx_hdr<8, SP, DEP>), dim3(wgs), dim3(64 * h.wpg), lds, stream, h, (uint32_t)tiles);
   return hipGetLastError();
 }
 

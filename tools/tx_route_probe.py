@@ -1,0 +1,98 @@
+#!/usr/bin/env python3
+"""ns_csum_tcp_tx over an IPv4 route and an IPv6 route: 1M segments of one
+1500-B MTU each (IPv4: MSS 1460, 54-B slots; IPv6: MSS 1440, 74-B slots, no
+IPv4 header checksum, 16-B addresses in the pseudo-header), sendTCPBatch's
+layout (slots, then the payload view), random bytes, two rotating batches.
+Median of `--rounds` rounds of `--reps` back-to-back calls; algorithmic
+bytes per segment = payload + IP and TCP headers read + the 2-B fields
+written (IPv4 1,504, IPv6 1,502).  The first `--check` segments of batch 0,
+filled by the two-pass call, must equal the same segments filled by
+ns_csum_tcp_tx_multi (another kernel: the fused per-tile shape); parity with
+the oracle is tests/test_gpu_tx_struct.py's (test_many_segments_full_tiles
+runs the IPv6 route at this size class).
+
+  python tools/tx_route_probe.py [--rounds 5] [--reps 20] [--check 4096]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+from netstack_amd import Engine  # noqa: E402
+from netstack_amd import workloads as W  # noqa: E402
+
+ROUTES = {
+    "ipv4": dict(mss=1460, slot=54, ip_at=14, ip_len=20, tcp_at=34, tcp_len=20,
+                 src=bytes([10, 0, 0, 1]), dst=bytes([10, 0, 0, 2])),
+    "ipv6": dict(mss=1440, slot=74, ip_at=14, ip_len=0, tcp_at=54, tcp_len=20,
+                 src=bytes(range(0x20, 0x30)), dst=bytes(range(0xF0, 0x100))),
+}
+
+
+def geometry(route: str, n: int, gap: int = 4096) -> tuple[dict, int]:
+    r = ROUTES[route]
+    hdr = n * r["slot"]
+    pay_off = (hdr + gap + 255) // 256 * 256
+    size = n * r["mss"]
+    return dict(hdr_off=0, pay_off=pay_off, size=size, protocol=6, **r), pay_off + size + 64
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--n", type=int, default=1 << 20)
+    ap.add_argument("--check", type=int, default=4096)
+    args = ap.parse_args()
+    n = args.n
+    dev = torch.device("cuda", 0)
+    eng = Engine(0)
+    print(json.dumps({"start": True, "n": n}), flush=True)
+    res = {}
+    for route in ROUTES:
+        geo, total = geometry(route, n)
+        batches = [W.random_bytes_torch(7100 + b, total, dev) for b in range(2)]
+        # cross-check: the first K segments as their own call through
+        # ns_csum_tcp_tx_multi, on a copy of batch 0
+        k = args.check
+        ref = batches[0].clone()
+        small = dict(geo, size=k * geo["mss"])
+        eng.tcp_tx_multi(ref, [small])
+        eng.tcp_tx(batches[0], geo)
+        torch.cuda.synchronize()
+        ok = bool(torch.equal(batches[0][:k * geo["slot"]], ref[:k * geo["slot"]]))
+        del ref
+        stream = torch.cuda.current_stream(dev)
+        times = []
+        for _ in range(args.rounds):
+            for i in range(3):
+                eng.tcp_tx(batches[i % 2], geo, stream=stream)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for i in range(args.reps):
+                eng.tcp_tx(batches[i % 2], geo, stream=stream)
+            e1.record(stream)
+            torch.cuda.synchronize()
+            times.append(e0.elapsed_time(e1) * 1e3 / args.reps)
+        us = float(np.median(times))
+        per = geo["mss"] + (geo["ip_len"] or 0) + geo["tcp_len"] + (4 if geo["ip_len"] else 2)
+        res[route] = {"us": round(us, 2), "min_us": round(min(times), 2), "algo_bytes_per_segment": per,
+                      "frac_of_8TBs": round(n * per / us / 1e3 / 8000, 4), "first_segments_bit_exact": ok}
+        print(json.dumps({route: res[route]}), flush=True)
+        del batches
+        torch.cuda.empty_cache()
+    print(json.dumps({"workload": f"{n} segments per call, one MTU each, 2 rotating batches", "routes": res}),
+          flush=True)
+
+
+if __name__ == "__main__":
+    main()
