@@ -29,7 +29,9 @@
 // A buffer list (ns_csum_rx_bufs, LIST = 1) is the same parse over buffers at
 // per-packet offsets in one arena (a NIC's buffer pool) instead of slots.
 //
-// Shape.  A wave owns 8 consecutive slots, one 8-lane group per packet.  The
+// Shape.  A wave owns 8 consecutive slots, one 8-lane group per packet (16
+// slots and 4-lane groups reading 64-B units on rings of short slots, G = 4:
+// there the per-packet parse, not memory, is the cost).  The
 // group's instruction k reads the packet's k-th 128-B HBM line whole (lane i:
 // 16 B at line + 16 i), so every load instruction reads exactly one line per
 // group: line 0 with the default cache policy (its first bytes may belong to
@@ -148,12 +150,17 @@ __device__ __forceinline__ uint4 rx_load(__amdgpu_buffer_rsrc_t r, uint32_t off)
 // one reads nothing; only lines NB - 2 and NB - 1 (where an MTU frame ends)
 // get the pair.
 template <int NB, int A0 = 0, int AN = 2, int WV = kWaves, int OCC = 1, int F = 1, int SPEC = 0, int LIST = 0,
-          int ROT = 0, int LL = 0>
+          int ROT = 0, int LL = 0, int G = 8>
 __global__ __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(OCC))) void rx_ring(RxGeo g) {
-  __shared__ uint4 rx_lds[WV * kPerWave * kRowBytes / 16];
-  const uint32_t lane = threadIdx.x & 63u, grp = lane >> 3, li = lane & 7u;
+  // G lanes per packet: a load unit of U = 16 G bytes per group instruction
+  // (G = 8: a 128-B line), KR units holding the LDS row, PW packets per wave
+  static_assert(G == 8 || (G == 4 && LIST == 0 && ROT == 0 && LL == 0 && SPEC == 0 && F == 1 && NB >= 3),
+                "4-lane groups: rings only, the product shape");
+  constexpr uint32_t U = 16u * G, US = G == 8 ? 7u : 6u, KR = G == 8 ? 2u : 3u, PW = 64u / G;
+  __shared__ uint4 rx_lds[WV * PW * kRowBytes / 16];
+  const uint32_t lane = threadIdx.x & 63u, grp = lane / G, li = lane & (G - 1u);
   const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint64_t s0 = ((uint64_t)blockIdx.x * WV + wv) * kPerWave;  // the wave's first slot
+  const uint64_t s0 = ((uint64_t)blockIdx.x * WV + wv) * PW;  // the wave's first slot
   if (s0 >= g.n) return;  // a whole wave leaves together
   const uint64_t s = s0 + grp;
   const bool live = s < g.n;
@@ -189,13 +196,13 @@ __global__ __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(OCC))) 
     // Wave-relative 32-bit coordinates: one buffer resource from the 128-B
     // line of the wave's first packet over its slots (< 8 strides + a line).
     wbase = (g.ring + s0 * g.stride + pre) & ~127ull;
-    const uint64_t s_end = s0 + kPerWave < g.n ? s0 + kPerWave : g.n;
+    const uint64_t s_end = s0 + PW < g.n ? s0 + PW : g.n;
     nrec = (uint32_t)(g.ring + s_end * g.stride - wbase);
   }
   const __amdgpu_buffer_rsrc_t rsrc = rx_srd(wbase, nrec);
   const uint32_t pa = (uint32_t)(slot + pre - wbase);  // the IP packet's first byte
   const uint32_t po = pa & 15u;                         // its offset in its 16-B chunk (even)
-  const uint32_t cl = (pa & ~127u) + 16u * li;          // lane li's chunk of line 0
+  const uint32_t cl = (pa & ~(U - 1u)) + 16u * li;      // lane li's chunk of line (unit) 0
   uint4 v[NB];
   // SPEC (timing variants): line 0 (1: and line 1, 2) loaded before the
   // length arrives: bytes past the frame only ever reach the LDS row, whose
@@ -214,8 +221,8 @@ __global__ __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(OCC))) 
   // it starts before pe: k <= klast.  The voffset is cl (or nrec) and the
   // line's 128 k goes in the instruction's offset field.
   const uint32_t pe = pa + Pl;
-  const uint32_t klast = Pl && pe > cl ? (pe - 1u - cl) >> 7 : 0u;
-  const bool any1 = Pl && pe > cl + 128u;  // some line k >= 1 holds packet bytes for this lane
+  const uint32_t klast = Pl && pe > cl ? (pe - 1u - cl) >> US : 0u;
+  const bool any1 = Pl && pe > cl + U;  // some line k >= 1 holds packet bytes for this lane
   const uint32_t cl1 = any1 ? cl : nrec;
 
   if constexpr (SPEC < 1 && LIST && A0 == 0) {
@@ -250,8 +257,8 @@ __global__ __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(OCC))) 
         return;
       }
     }
-    if constexpr (F) v[k] = rx_load<AN>(rsrc, ((uint32_t)k <= klast ? cl1 : nrec) + 128u * k);
-    else v[k] = rx_load<AN>(rsrc, off_of(cl + 128u * k));
+    if constexpr (F) v[k] = rx_load<AN>(rsrc, ((uint32_t)k <= klast ? cl1 : nrec) + U * k);
+    else v[k] = rx_load<AN>(rsrc, off_of(cl + U * k));
   };
   if constexpr (SPEC < 2) line(1);
   // The EtherType (the link header's bytes 12-13, pa - 2): a buffer load on
@@ -265,10 +272,10 @@ __global__ __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(OCC))) 
   }
 #pragma unroll
   for (int k = 2; k < NB; ++k) line(k);
-  uint32_t w2 = 0;  // F: every loaded chunk of lines >= 2
+  uint32_t w2 = 0;  // F: every loaded chunk of lines >= KR
   if constexpr (F) {
 #pragma unroll
-    for (int k = 2; k < NB; ++k) {
+    for (int k = KR; k < NB; ++k) {
       w2 = __builtin_amdgcn_sad_u16(v[k].x, 0u, w2);
       w2 = __builtin_amdgcn_sad_u16(v[k].y, 0u, w2);
       w2 = __builtin_amdgcn_sad_u16(v[k].z, 0u, w2);
@@ -277,11 +284,11 @@ __global__ __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(OCC))) 
   }
 
   // The first 96 B from the packet's 16-B chunk into the group's LDS row.
-  uint8_t* row = reinterpret_cast<uint8_t*>(rx_lds) + (wv * kPerWave + grp) * kRowBytes;
+  uint8_t* row = reinterpret_cast<uint8_t*>(rx_lds) + (wv * PW + grp) * kRowBytes;
   const uint32_t f16 = pa & ~15u;
 #pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    const uint32_t o = cl + 128u * k - f16;
+  for (int k = 0; k < (int)KR; ++k) {
+    const uint32_t o = cl + U * k - f16;
     if (o < kRowBytes) *reinterpret_cast<uint4*>(row + o) = v[k];
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -353,7 +360,7 @@ __global__ __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(OCC))) 
   }
   // The last loaded chunk (its offset from pa) and the first of line 2.
   const uint32_t rl = Pl ? ((pa + Pl - 1u) & ~15u) - pa : 0u;
-  const uint32_t r2 = (pa & ~127u) + 256u - pa;
+  const uint32_t r2 = (pa & ~(U - 1u)) + KR * U - pa;
   // F: a frame padded past its transport's end with loaded chunks beyond the
   // transport's last chunk in lines >= 2 (their bytes are in w2; the chunk at
   // B is corrected below only if it holds transport bytes): the whole wave
@@ -376,27 +383,27 @@ __global__ __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(OCC))) 
   uint32_t w = (li == 2 ? rs : 0u) + tail;
   const uint32_t d = cl - pa - A;
 #pragma unroll
-  for (int k = 0; k < (F ? 2 : NB); ++k) {
+  for (int k = 0; k < (F ? (int)KR : NB); ++k) {
     const uint32_t t = rx_wsum4(v[k]);
-    w += (d + 128u * k) < span ? t : 0u;
+    w += (d + U * k) < span ? t : 0u;
   }
   if constexpr (F) {
     // (both loops below take 4 lines at a time: their registers are not the
     // kernel's peak, and they run only for long or padded frames)
     if (wslow) {  // a padded frame in this wave: lines >= 2 re-read, range-checked
       w2 = 0;
-      for (uint32_t k0 = 2; __builtin_amdgcn_ballot_w64((d + 128u * k0) < span) != 0; k0 += 4) {
+      for (uint32_t k0 = KR; __builtin_amdgcn_ballot_w64((d + U * k0) < span) != 0; k0 += 4) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-          const uint32_t t = rx_wsum4(rx_load<AN>(rsrc, off_of(cl + 128u * (k0 + k))));
-          w2 += (d + 128u * (k0 + k)) < span ? t : 0u;
+          const uint32_t t = rx_wsum4(rx_load<AN>(rsrc, off_of(cl + U * (k0 + k))));
+          w2 += (d + U * (k0 + k)) < span ? t : 0u;
         }
       }
     } else {
       for (uint32_t k0 = NB; __builtin_amdgcn_ballot_w64(k0 <= klast && kind) != 0; k0 += 4) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-          const uint4 x4 = rx_load<AN>(rsrc, ((k0 + k) <= klast ? cl1 : nrec) + 128u * (k0 + k));
+          const uint4 x4 = rx_load<AN>(rsrc, ((k0 + k) <= klast ? cl1 : nrec) + U * (k0 + k));
           w2 = __builtin_amdgcn_sad_u16(x4.x, 0u, w2);
           w2 = __builtin_amdgcn_sad_u16(x4.y, 0u, w2);
           w2 = __builtin_amdgcn_sad_u16(x4.z, 0u, w2);
@@ -406,19 +413,19 @@ __global__ __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(OCC))) 
     }
     w += w2;
   } else {
-    for (uint32_t k0 = NB; __builtin_amdgcn_ballot_w64((d + 128u * k0) < span) != 0; k0 += NB) {
+    for (uint32_t k0 = NB; __builtin_amdgcn_ballot_w64((d + U * k0) < span) != 0; k0 += NB) {
 #pragma unroll
-      for (int k = 0; k < NB; ++k) v[k] = rx_load<AN>(rsrc, off_of(cl + 128u * (k0 + k)));
+      for (int k = 0; k < NB; ++k) v[k] = rx_load<AN>(rsrc, off_of(cl + U * (k0 + k)));
 #pragma unroll
       for (int k = 0; k < NB; ++k) {
         const uint32_t t = rx_wsum4(v[k]);
-        w += (d + 128u * (k0 + k)) < span ? t : 0u;
+        w += (d + U * (k0 + k)) < span ? t : 0u;
       }
     }
   }
   w += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)w, 0xB1, 0xF, 0xF, false);   // quad_perm 1,0,3,2
   w += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)w, 0x4E, 0xF, 0xF, false);   // quad_perm 2,3,0,1
-  w += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)w, 0x141, 0xF, 0xF, false);  // row_half_mirror
+  if constexpr (G == 8) w += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)w, 0x141, 0xF, 0xF, false);  // row_half_mirror
   const uint32_t addr = (uint32_t)__builtin_amdgcn_mov_dpp((int)rs, 0x55, 0xF, 0xF, false);  // lane 1's
 
   if (li == 0 && live) {
@@ -460,13 +467,24 @@ static int rx_batch_lines(const RxGeo& g) {
 }
 
 template <int NB, int A0 = 0, int AN = 2, int WV = kWaves, int OCC = 1, int F = 1, int SPEC = 0, int LIST = 0,
-          int ROT = 0, int LL = 0>
+          int ROT = 0, int LL = 0, int G = 8>
 static hipError_t launch_rx_ring_t(const RxGeo& g, hipStream_t stream) {
   if (g.n == 0) return hipSuccess;
-  const uint64_t per_wg = (uint64_t)WV * kPerWave;
-  hipLaunchKernelGGL((rx_ring<NB, A0, AN, WV, OCC, F, SPEC, LIST, ROT, LL>),
+  const uint64_t per_wg = (uint64_t)WV * (64u / G);
+  hipLaunchKernelGGL((rx_ring<NB, A0, AN, WV, OCC, F, SPEC, LIST, ROT, LL, G>),
                      dim3((uint32_t)((g.n + per_wg - 1) / per_wg)), dim3(64 * WV), 0, stream, g);
   return hipGetLastError();
+}
+
+// 4-lane groups (G = 4: 16 packets per wave, 64-B load units) for a ring
+// whose frames span at most 8 units: the per-packet parse is the kernel's
+// cost below a few hundred bytes, and a wave then parses twice the packets.
+// 0: not eligible (a longer stride or a buffer list).
+static int rx_batch_units4(const RxGeo& g) {
+  if (g.off) return 0;
+  const uint64_t longest = g.stride < (uint64_t)kMaxIp + g.frame_at + g.link ? g.stride : (uint64_t)kMaxIp + g.frame_at + g.link;
+  const uint64_t units = (longest + 62 + 63) / 64;
+  return units <= 4 ? 4 : units <= 8 ? 8 : 0;
 }
 
 template <int LIST, int A0 = 0>
@@ -485,8 +503,17 @@ static hipError_t launch_rx_ring_l(const RxGeo& g, hipStream_t stream) {
 // start in their slot's first line shares no line between slots: line 0
 // goes nontemporal too (1536-B slots: 236.5 -> 234.2 us per 1M frames,
 // tools/rx_ring_probe.py --stride 1536).
+// Rings of short slots take 4-lane groups (rx_batch_units4; tools/
+// rx_size_probe.py --variants 40,41, profiles/r06/rxg4/: per ring of ~1.5 GB,
+// 64-B frames 903.9 -> 509.5 us, 128-B 665.3 -> 424.2, 256-B 369.9 -> 332.7;
+// 576-B frames lose, 315.5 against 241.7, and keep 8-lane groups).
 hipError_t launch_rx_ring(const RxGeo& g, hipStream_t stream) {
   if (g.off) return launch_rx_ring_l<1>(g, stream);
+  switch (rx_batch_units4(g)) {
+    case 4: return launch_rx_ring_t<4, 0, 2, kWaves, 1, 1, 0, 0, 0, 0, 4>(g, stream);
+    case 8: return launch_rx_ring_t<8, 0, 2, kWaves, 1, 1, 0, 0, 0, 0, 4>(g, stream);
+    default: break;
+  }
   if ((g.ring & 127) == 0 && (g.stride & 127) == 0 && g.frame_at + g.link < 128) return launch_rx_ring_l<0, 2>(g, stream);
   return launch_rx_ring_l<0>(g, stream);
 }

@@ -368,6 +368,58 @@ def rx_ring_batch_v6(n: int, seed: int, device, corrupt_every: int = 0):
     return arena, lens, bad
 
 
+def rx_ring_batch_sized(n: int, frame: int, seed: int, device, v6: bool = False, corrupt_every: int = 0):
+    """rx_ring_batch / rx_ring_batch_v6 at any frame length (IPv4 or IPv6
+    TCP packets of `frame` bytes, e.g. 9000-B jumbo frames), one per slot of
+    stride round_up(frame, 16) + 16.  Returns (arena, lens, bad, stride)."""
+    import torch
+
+    stride = (frame + 15) // 16 * 16 + 16
+    arena = random_bytes_torch(seed, n * stride, device)
+    p = arena.view(n, stride)[:, :frame]
+    ipl = 40 if v6 else RX_IHL
+    tl = frame - ipl
+    if v6:
+        p[:, 0] = 0x60
+        p[:, 1:4] = 0
+        p[:, 4] = tl >> 8
+        p[:, 5] = tl & 0xFF
+        p[:, 6] = 6
+        p[:, 7] = 64
+    else:
+        p[:, 0] = 0x45
+        p[:, 1] = 0
+        p[:, 2] = frame >> 8
+        p[:, 3] = frame & 0xFF
+        p[:, 6] = 0x40
+        p[:, 7] = 0
+        p[:, 8] = 64
+        p[:, 9] = 6
+        p[:, 10:12] = 0
+    p[:, ipl + 12] = 0x50
+    p[:, ipl + 13] = 0x18
+    p[:, ipl + 16:ipl + 20] = 0
+
+    def be_sum(lo, hi):
+        w = p[:, lo:hi].to(torch.int64)
+        return (w[:, 0::2] * 256 + w[:, 1::2]).sum(dim=1)
+
+    if not v6:
+        ip = (~_fold_np(be_sum(0, RX_IHL))) & 0xFFFF
+        p[:, 10] = (ip >> 8).to(torch.uint8)
+        p[:, 11] = (ip & 0xFF).to(torch.uint8)
+    addr = be_sum(8, 40) if v6 else be_sum(12, 20)
+    tcp = (~_fold_np(_fold_np(be_sum(ipl, frame) + addr + tl + 6))) & 0xFFFF
+    p[:, ipl + 16] = (tcp >> 8).to(torch.uint8)
+    p[:, ipl + 17] = (tcp & 0xFF).to(torch.uint8)
+    bad = np.arange(0, n, corrupt_every, dtype=np.int64) if corrupt_every > 0 else np.zeros(0, np.int64)
+    if bad.size:
+        idx = torch.from_numpy(bad).to(device)
+        p[idx, frame - 3] ^= 0x5A
+    lens = torch.full((n,), frame, dtype=torch.int32, device=device)
+    return arena, lens, bad, stride
+
+
 TX_IP_CSUM = 10   # header.IPv4 checksum field (ipv4.go:35 checksum offset)
 TX_TCP_CSUM = 16  # header.TCP checksum field, from the TCP header start
 

@@ -196,6 +196,24 @@ def _one_view(b: bytes):
     return NewVectorisedView(len(b), [View(bytearray(b))])
 
 
+@pytest.mark.parametrize("link_hdr,first_view,frame_at", [(0, 0, 0), (0, 128, 0), (14, 128, 0), (14, 128, 10),
+                                                           (14, 0, 4), (0, 64, 2)])
+@pytest.mark.parametrize("cap", [80, 128, 192, 256])
+def test_short_frame_rings(engine, link_hdr, first_view, frame_at, cap):
+    """Rings of short slots (80-256 B, the strides the 4-lane group shape
+    takes, rx_ring.hip rx_batch_units4): random packets and fuzzed headers
+    cut to the slot, every verdict and sum equal to the oracle's."""
+    from pktgen import fuzzed_packets
+
+    rng = np.random.default_rng(6300 + cap + link_hdr + frame_at)
+    pk = [random_packet(rng, cap) for _ in range(500)] + fuzzed_packets(rng, 500, max_payload=cap)
+    frames = [ethernet(p) if link_hdr else bytes(p) for p in pk]
+    stride = cap
+    lens = [min(len(f) + frame_at, stride) for f in frames]
+    got = _check(engine, frames, stride, frame_at, link_hdr, first_view, lens=lens, seed=cap)
+    assert {1, 3} <= set(got)
+
+
 @pytest.mark.parametrize("link_hdr,first_view", [(0, 0), (0, 128), (0, 64), (14, 128), (14, 0), (14, 78)])
 def test_minimum_sizes(engine, link_hdr, first_view):
     """Every transport message from 0 to its minimum + 2 bytes (TCP 20, UDP 8,
