@@ -12,6 +12,9 @@ the oracle is tests/test_gpu_tx_struct.py's (test_many_segments_full_tiles
 runs the IPv6 route at this size class).
 
   python tools/tx_route_probe.py [--rounds 5] [--reps 20] [--check 4096]
+                                  [--mss 64,256,536,1460,8960]
+--mss: the IPv4 route at those segment sizes instead, ~1.5 GB of payload per
+call (n = 1.5 GB / MSS, at most 16M segments).
 """
 from __future__ import annotations
 
@@ -38,8 +41,10 @@ ROUTES = {
 }
 
 
-def geometry(route: str, n: int, gap: int = 4096) -> tuple[dict, int]:
-    r = ROUTES[route]
+def geometry(route: str, n: int, gap: int = 4096, mss: int = 0) -> tuple[dict, int]:
+    r = dict(ROUTES[route])
+    if mss:
+        r["mss"] = mss
     hdr = n * r["slot"]
     pay_off = (hdr + gap + 255) // 256 * 256
     size = n * r["mss"]
@@ -52,14 +57,17 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--n", type=int, default=1 << 20)
     ap.add_argument("--check", type=int, default=4096)
+    ap.add_argument("--mss", default="")
     args = ap.parse_args()
     n = args.n
     dev = torch.device("cuda", 0)
     eng = Engine(0)
     print(json.dumps({"start": True, "n": n}), flush=True)
     res = {}
-    for route in ROUTES:
-        geo, total = geometry(route, n)
+    cases = [(r, 0, n) for r in ROUTES] if not args.mss else \
+        [("ipv4", int(m), min(16 << 20, int(1.5e9 // int(m)))) for m in args.mss.split(",")]
+    for route, mss, n in cases:
+        geo, total = geometry(route, n, mss=mss)
         batches = [W.random_bytes_torch(7100 + b, total, dev) for b in range(2)]
         # cross-check: the first K segments as their own call through
         # ns_csum_tcp_tx_multi, on a copy of batch 0
@@ -85,13 +93,13 @@ def main():
             times.append(e0.elapsed_time(e1) * 1e3 / args.reps)
         us = float(np.median(times))
         per = geo["mss"] + (geo["ip_len"] or 0) + geo["tcp_len"] + (4 if geo["ip_len"] else 2)
-        res[route] = {"us": round(us, 2), "min_us": round(min(times), 2), "algo_bytes_per_segment": per,
+        key = f"{route}_mss{geo['mss']}"
+        res[key] = {"segments": n, "us": round(us, 2), "min_us": round(min(times), 2), "algo_bytes_per_segment": per,
                       "frac_of_8TBs": round(n * per / us / 1e3 / 8000, 4), "first_segments_bit_exact": ok}
-        print(json.dumps({route: res[route]}), flush=True)
+        print(json.dumps({key: res[key]}), flush=True)
         del batches
         torch.cuda.empty_cache()
-    print(json.dumps({"workload": f"{n} segments per call, one MTU each, 2 rotating batches", "routes": res}),
-          flush=True)
+    print(json.dumps({"workload": "2 rotating batches per case", "cases": res}), flush=True)
 
 
 if __name__ == "__main__":
