@@ -368,15 +368,23 @@ def rx_ring_batch_v6(n: int, seed: int, device, corrupt_every: int = 0):
     return arena, lens, bad
 
 
-def rx_ring_batch_sized(n: int, frame: int, seed: int, device, v6: bool = False, corrupt_every: int = 0):
+def rx_ring_batch_sized(n: int, frame: int, seed: int, device, v6: bool = False, corrupt_every: int = 0,
+                        eth: bool = False):
     """rx_ring_batch / rx_ring_batch_v6 at any frame length (IPv4 or IPv6
     TCP packets of `frame` bytes, e.g. 9000-B jumbo frames), one per slot of
-    stride round_up(frame, 16) + 16.  Returns (arena, lens, bad, stride)."""
+    stride round_up(frame [+ 14], 16) + 16; eth: each packet behind a 14-B
+    Ethernet header (EtherType 0x0800 / 0x86DD; ring link_hdr 14, lengths
+    frame + 14).  Returns (arena, lens, bad, stride)."""
     import torch
 
-    stride = (frame + 15) // 16 * 16 + 16
+    lh = 14 if eth else 0
+    stride = (frame + lh + 15) // 16 * 16 + 16
     arena = random_bytes_torch(seed, n * stride, device)
-    p = arena.view(n, stride)[:, :frame]
+    if eth:
+        e = arena.view(n, stride)[:, :14]
+        e[:, 12] = 0x86 if v6 else 0x08
+        e[:, 13] = 0xDD if v6 else 0x00
+    p = arena.view(n, stride)[:, lh:lh + frame]
     ipl = 40 if v6 else RX_IHL
     tl = frame - ipl
     if v6:
@@ -416,7 +424,7 @@ def rx_ring_batch_sized(n: int, frame: int, seed: int, device, v6: bool = False,
     if bad.size:
         idx = torch.from_numpy(bad).to(device)
         p[idx, frame - 3] ^= 0x5A
-    lens = torch.full((n,), frame, dtype=torch.int32, device=device)
+    lens = torch.full((n,), frame + lh, dtype=torch.int32, device=device)
     return arena, lens, bad, stride
 
 

@@ -35,6 +35,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--frames", default="64,256,576,1500,4000,9000")
     ap.add_argument("--v6", action="store_true")
+    ap.add_argument("--eth", action="store_true", help="frames behind a 14-B Ethernet header (link_hdr 14)")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--bytes", type=float, default=1.5e9)
@@ -53,9 +54,10 @@ def main():
     print(json.dumps({"start": True, "v6": args.v6}), flush=True)
     for fr in (int(x) for x in args.frames.split(",")):
         n = min(16 << 20, int(args.bytes // fr))
-        rings = [W.rx_ring_batch_sized(n, fr, 9 + r, dev, v6=args.v6, corrupt_every=1000) for r in range(2)]
+        rings = [W.rx_ring_batch_sized(n, fr, 9 + r, dev, v6=args.v6, corrupt_every=1000, eth=args.eth)
+                 for r in range(2)]
         arena0, lens, bad, stride = rings[0]
-        ring = dict(stride=stride, n=n)
+        ring = dict(stride=stride, n=n, link_hdr=14 if args.eth else 0)
         v, _ = eng.rx_ring(arena0, ring, lens)
         torch.cuda.synchronize()
         want = torch.ones(n, dtype=torch.uint8, device=dev)
@@ -68,7 +70,7 @@ def main():
         verdict = torch.empty(n, dtype=torch.uint8, device=dev)
         sums = torch.empty(2 * n, dtype=torch.int16, device=dev)
         geos = [RxGeo(r[0].data_ptr(), stride, lens.data_ptr(), sums.data_ptr(), verdict.data_ptr(), err.data_ptr(),
-                      n, 0, 0, 0, None, 0) for r in rings] if ks else []
+                      n, 0, 14 if args.eth else 0, 0, None, 0) for r in rings] if ks else []
 
         def launcher(k):
             if k < 0:
@@ -96,11 +98,11 @@ def main():
                 torch.cuda.synchronize()
                 times.append(e0.elapsed_time(e1) * 1e3 / args.reps)
             us = float(np.median(times))
-            algo = n * (fr + 9)
+            algo = n * (fr + (14 if args.eth else 0) + 9)
             out["product" if k < 0 else f"variant_{k}"] = {"us": round(us, 2),
                                                            "frac_of_8TBs": round(algo / us / 1e3 / 8000, 4),
                                                            "same_as_product": same}
-        print(json.dumps({"frame": fr, "ipv6": args.v6, "slots": n, "stride": stride,
+        print(json.dumps({"frame": fr, "ipv6": args.v6, "ethernet": args.eth, "slots": n, "stride": stride,
                           "verdicts_as_generated": ok, "shapes": out}), flush=True)
         del rings, arena0, lens, v, want, s0, verdict, sums
         torch.cuda.empty_cache()
