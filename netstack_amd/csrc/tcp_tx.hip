@@ -745,7 +745,7 @@ static hipError_t launch_header_pass(TxGeo h, hipStream_t stream, uint32_t per_c
   // tcp_tx_hdr's conditions: full TCP mode with whole write-back, tiles of
   // <= 64 segments starting 16-B aligned, <= 8 KiB of slots each (CPL = 4,
   // 5, 6 or 8 chunks per lane: IPv4's 54-B slots take 4, an IPv6 route's
-  // 74-B slots 5), d_out 4-B aligned
+  // 74-B slots 5; 6 and 8 on the one-shot grid only), d_out 4-B aligned
   const uint64_t region = (uint64_t)h.tile * h.slot;
   if (h.tile > 64 || region > 8192 || region % 16 || (h.hdr & 15) || !(h.mode & kTxTcpFull) ||
       (h.mode & kTxFieldsOnly) || ((uintptr_t)h.out & 3) || h.xs == nullptr)
@@ -756,10 +756,16 @@ static hipError_t launch_header_pass(TxGeo h, hipStream_t stream, uint32_t per_c
   const uint32_t wgs = (uint32_t)((waves + h.wpg - 1) / h.wpg);
   const size_t lds = (size_t)h.lds_wave * h.wpg;
   const uint32_t cpl = (uint32_t)((region + 1023) / 1024);
-  if (cpl <= 4) hipLaunchKernelGGL((tcp_tx_hdr<4, SP, DEP>), dim3(wgs), dim3(64 * h.wpg), lds, stream, h, (uint32_t)tiles);
-  else if (cpl == 5) hipLaunchKernelGGL((tcp_tx_hdr<5, SP, DEP>), dim3(wgs), dim3(64 * h.wpg), lds, stream, h, (uint32_t)tiles);
-  else if (cpl == 6) hipLaunchKernelGGL((tcp_tx_hdr<6, SP, DEP>), dim3(wgs), dim3(64 * h.wpg), lds, stream, h, (uint32_t)tiles);
-  else hipLaunchKernelGGL((tcp_tx_hdr<8, SP, DEP>), dim3(wgs), dim3(64 * h.wpg), lds, stream, h, (uint32_t)tiles);
+  if (cpl <= 4) {
+    hipLaunchKernelGGL((tcp_tx_hdr<4, SP, DEP>), dim3(wgs), dim3(64 * h.wpg), lds, stream, h, (uint32_t)tiles);
+  } else if (cpl == 5) {
+    hipLaunchKernelGGL((tcp_tx_hdr<5, SP, DEP>), dim3(wgs), dim3(64 * h.wpg), lds, stream, h, (uint32_t)tiles);
+  } else if constexpr (DEP == 1) {  // (2-3 tiles in flight at 6-8 chunks per lane: 5 waves per SIMD or fewer)
+    if (cpl == 6) hipLaunchKernelGGL((tcp_tx_hdr<6, SP, 1>), dim3(wgs), dim3(64 * h.wpg), lds, stream, h, (uint32_t)tiles);
+    else hipLaunchKernelGGL((tcp_tx_hdr<8, SP, 1>), dim3(wgs), dim3(64 * h.wpg), lds, stream, h, (uint32_t)tiles);
+  } else {
+    return launch_tcp_tx_t<16, 2, SP, 1, 0, 2>(h, stream);
+  }
   return hipGetLastError();
 }
 
