@@ -21,8 +21,8 @@
 //  31    30 with the outputs written in sorted order (timing only: wrong
 //        places)   32  30 with the list index loaded with the entry
 //  33    the sort alone (rx_bk_count + rx_bk_place)   34  rx_bk_count alone
-//  40 / 41  4-lane groups (16 packets per wave, 64-B units), 4 / 8 units per
-//        batch (rings of short frames)
+//  40 / 41 / 42  4-lane groups (16 packets per wave, 64-B units), 4 / 8 / 16
+//        units per batch (rings of short frames)
 // Every variant but 31, 33 and 34 computes the product's verdicts and sums.
 // Not part of the ABI.
 #include "../netstack_amd/csrc/rx_ring.hip"
@@ -149,6 +149,7 @@ extern "C" int rxv_launch(const nsk::RxGeo* g, void* stream, int k) {
     case 29: return (int)nsk::launch_rx_ring_t<13, 0, 1, 4, 1, 1, 0, 1, 0, 1>(*g, s);
     case 40: return (int)nsk::launch_rx_ring_t<4, 0, 2, 4, 1, 1, 0, 0, 0, 0, 4>(*g, s);
     case 41: return (int)nsk::launch_rx_ring_t<8, 0, 2, 4, 1, 1, 0, 0, 0, 0, 4>(*g, s);
+    case 42: return (int)nsk::launch_rx_ring_t<16, 0, 2, 4, 1, 1, 0, 0, 0, 0, 4>(*g, s);
     case 30: return (int)nsk::launch_rx_bufs_sorted(*g, s);
     case 31: return (int)nsk::launch_rx_bufs_sorted_t<13, 3>(*g, s);
     case 32: return (int)nsk::launch_rx_bufs_sorted_t<13, 4>(*g, s);
