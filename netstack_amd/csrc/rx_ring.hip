@@ -502,7 +502,9 @@ static hipError_t launch_rx_ring_l(const RxGeo& g, hipStream_t stream) {
 // slot before's last ones.  A ring of line-aligned slots whose IP packets
 // start in their slot's first line shares no line between slots: line 0
 // goes nontemporal too (1536-B slots: 236.5 -> 234.2 us per 1M frames,
-// tools/rx_ring_probe.py --stride 1536).
+// tools/rx_ring_probe.py --stride 1536) -- but not where the stride is a
+// multiple of 1 KiB (2048-B slots: 233.3-240.1 us nontemporal against
+// 221.0-229.4 default; 1024, 3072, 4096 no better; profiles/r06/rxpow2/).
 // Rings of short slots take 4-lane groups (rx_batch_units4; tools/
 // rx_size_probe.py --variants 40,41, profiles/r06/rxg4/: per ring of ~1.5 GB,
 // 64-B frames 903.9 -> 509.5 us, 128-B 665.3 -> 424.2, 256-B 369.9 -> 332.7;
@@ -514,7 +516,8 @@ hipError_t launch_rx_ring(const RxGeo& g, hipStream_t stream) {
     case 8: return launch_rx_ring_t<8, 0, 2, kWaves, 1, 1, 0, 0, 0, 0, 4>(g, stream);
     default: break;
   }
-  if ((g.ring & 127) == 0 && (g.stride & 127) == 0 && g.frame_at + g.link < 128) return launch_rx_ring_l<0, 2>(g, stream);
+  if ((g.ring & 127) == 0 && (g.stride & 127) == 0 && (g.stride & 1023) != 0 && g.frame_at + g.link < 128)
+    return launch_rx_ring_l<0, 2>(g, stream);
   return launch_rx_ring_l<0>(g, stream);
 }
 
