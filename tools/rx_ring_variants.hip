@@ -21,6 +21,8 @@
 //  31    30 with the outputs written in sorted order (timing only: wrong
 //        places)   32  30 with the list index loaded with the entry
 //  33    the sort alone (rx_bk_count + rx_bk_place)   34  rx_bk_count alone
+//  50    the layout's read floor (rx_floor: the frames' lines, no parse;
+//        timing only)
 //  40 / 41 / 42  4-lane groups (16 packets per wave, 64-B units), 4 / 8 / 16
 //        units per batch (rings of short frames)
 // Every variant but 31, 33 and 34 computes the product's verdicts and sums.
@@ -118,6 +120,40 @@ static hipError_t launch_rx_bufs_sorted(const RxGeo& g, hipStream_t stream) {
   }
 }
 
+// Variant 50: the read floor of a ring layout -- each 8-lane group reads the
+// lines holding its slot's received bytes (len[s] from the slot's start),
+// sums them and writes one byte; no parse.  Timing only.
+template <int NB>
+__global__ __launch_bounds__(256) void rx_floor(RxGeo g) {
+  const uint32_t lane = threadIdx.x & 63u, grp = lane >> 3, li = lane & 7u;
+  const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t s0 = ((uint64_t)blockIdx.x * 4u + wv) * 8u;
+  if (s0 >= g.n) return;
+  const uint64_t s = s0 + grp;
+  const uint64_t wbase = (g.ring + s0 * g.stride) & ~127ull;
+  const uint64_t s_end = s0 + 8u < g.n ? s0 + 8u : g.n;
+  const uint32_t nrec = (uint32_t)(g.ring + s_end * g.stride - wbase);
+  const __amdgpu_buffer_rsrc_t r = rx_srd(wbase, nrec);
+  const uint32_t len = s < g.n ? g.len[s] : 0u;
+  const uint32_t pa = (uint32_t)(g.ring + s * g.stride - wbase);
+  const uint32_t cl = (pa & ~127u) + 16u * li;
+  uint32_t w = 0;
+  for (uint32_t k0 = 0; __builtin_amdgcn_ballot_w64(s < g.n && 128u * k0 < len + (pa & 127u)) != 0; k0 += NB) {
+    uint4 v[NB];
+#pragma unroll
+    for (int k = 0; k < NB; ++k) {
+      const uint32_t o = cl + 128u * (k0 + k);
+      v[k] = rx_load<2>(r, s < g.n && o + 16u > pa && o < pa + len ? o : nrec);
+    }
+#pragma unroll
+    for (int k = 0; k < NB; ++k) w = rx_wsum4(v[k]) + w;
+  }
+  w += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)w, 0xB1, 0xF, 0xF, false);
+  w += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)w, 0x4E, 0xF, 0xF, false);
+  w += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)w, 0x141, 0xF, 0xF, false);
+  if (li == 0 && s < g.n) g.verdict[s] = (uint8_t)w;
+}
+
 }  // namespace nsk
 
 extern "C" int rxv_launch(const nsk::RxGeo* g, void* stream, int k) {
@@ -151,6 +187,10 @@ extern "C" int rxv_launch(const nsk::RxGeo* g, void* stream, int k) {
     case 41: return (int)nsk::launch_rx_ring_t<8, 0, 2, 4, 1, 1, 0, 0, 0, 0, 4>(*g, s);
     case 42: return (int)nsk::launch_rx_ring_t<16, 0, 2, 4, 1, 1, 0, 0, 0, 0, 4>(*g, s);
     case 30: return (int)nsk::launch_rx_bufs_sorted(*g, s);
+    case 50: {
+      hipLaunchKernelGGL(nsk::rx_floor<13>, dim3((uint32_t)((g->n + 31) / 32)), dim3(256), 0, s, *g);
+      return (int)hipGetLastError();
+    }
     case 31: return (int)nsk::launch_rx_bufs_sorted_t<13, 3>(*g, s);
     case 32: return (int)nsk::launch_rx_bufs_sorted_t<13, 4>(*g, s);
     case 33: case 34: {
