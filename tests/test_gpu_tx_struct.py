@@ -51,6 +51,11 @@ CASES = {
     "jumbo_9000": _geo(9000 * 9 + 17, 9000, hdr_off=8),
     "gso_64k": _geo(65535 * 3 + 1, 65535, gap=1),
     "ip_header_with_options": _geo(1460 * 12, 1460, slot=78, ip_len=44, tcp_at=58),
+    # IPv6 with TCP options: 86-B and 114-B slots, whose 64-slot header tiles
+    # take 6 and 8 chunks per lane
+    "ipv6_tcp_options": _geo(1408 * 70 + 5, 1408, slot=86, ip_len=0, tcp_at=54, tcp_len=32, src=V6S, dst=V6D),
+    "ipv6_max_tcp_options": _geo(1380 * 66 + 1, 1380, slot=114, ip_len=0, tcp_at=54, tcp_len=60, src=V6S,
+                                 dst=V6D),
 }
 
 
@@ -134,8 +139,9 @@ def test_forced_tiles(engine, oracle_mod, tile):
 def test_header_pass_tiles(engine, oracle_mod, htile):
     """The header pass's tile (ns_csum_set_tx_tuning htile): up to 256 segments per wave,
     each lane looping over every 64th; with and without d_out (payload values
-    parked in d_out or in per-stream scratch)."""
-    for name in ("short_last_odd", "odd_slots_odd_mss", "ipv6_route"):
+    parked in d_out or in per-stream scratch).  At 64 segments the IPv6
+    geometries' tiles take 5, 6 and 8 chunks per lane."""
+    for name in ("short_last_odd", "odd_slots_odd_mss", "ipv6_route", "ipv6_tcp_options", "ipv6_max_tcp_options"):
         geo, total = CASES[name]
         if htile * geo["slot"] > 12 << 10:
             continue
