@@ -819,7 +819,7 @@ def packet_mode(args, dist, eng, dev, tx: bool):
                    "packets_per_gpu": RX_N, "descriptors_per_gpu": n_desc, "rotating_batches": 2},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
-                     "kernel": ("nsk::tcp_tx_pay<13,0> (payload pass, 8-lane groups) + nsk::tcp_tx_hdr<4,4,1> "
+                     "kernel": ("nsk::tcp_tx_pay<13,0,8> (payload pass, 8-lane groups) + nsk::tcp_tx_hdr<4,4,1> "
                                 "(header pass, one tile per wave, nt sc1 slot stores)"
                                 if struct else kernel_name(arena.numel(), n_desc, chained=chained, store=tx or split)
                                 + (" + nsk::fold_scan" if chained else "")),

@@ -633,11 +633,16 @@ __device__ __forceinline__ uint32_t tx_bytes_from(const uint4 v, int c) {  // W 
   return wsum4(make_uint4(v.x & ~below(c), v.y & ~below(c - 4), v.z & ~below(c - 8), v.w & ~below(c - 12)), 0u);
 }
 
-template <int NB, int A0 = 0>
+// G lanes per segment: 8 (a 128-B line per group instruction) or 4 (64-B
+// units, 16 segments per wave: short segments, where the per-segment work and
+// not memory is the cost).
+template <int NB, int A0 = 0, int G = 8>
 __global__ __launch_bounds__(256) void tcp_tx_pay(TxGeo g) {
-  const uint32_t lane = threadIdx.x & 63u, grp = lane >> 3, li = lane & 7u;
+  static_assert(G == 8 || G == 4, "8- or 4-lane groups");
+  constexpr uint32_t U = 16u * G, US = G == 8 ? 7u : 6u, PW = 64u / G;
+  const uint32_t lane = threadIdx.x & 63u, grp = lane / G, li = lane & (G - 1u);
   const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint64_t s0 = ((uint64_t)blockIdx.x * 4u + wv) * 8u;  // the wave's first segment
+  const uint64_t s0 = ((uint64_t)blockIdx.x * 4u + wv) * PW;  // the wave's first segment
   if (s0 >= g.n) return;  // a whole wave leaves together
   const uint64_t s = s0 + grp;
   const uint64_t tail0 = (g.n - 1) * (uint64_t)g.mss;  // where the last segment starts
@@ -648,33 +653,33 @@ __global__ __launch_bounds__(256) void tcp_tx_pay(TxGeo g) {
   // byte must lie inside it (its bytes past the end are in the same aligned
   // chunk, never another page)
   const uint64_t wbase = (g.pay + s0 * g.mss) & ~127ull;
-  const uint64_t s_end = s0 + 8u < g.n ? s0 + 8u : g.n;
+  const uint64_t s_end = s0 + PW < g.n ? s0 + PW : g.n;
   const uint64_t w_end = g.pay + (s_end < g.n ? s_end * (uint64_t)g.mss : g.size);
   const uint32_t nrec = (uint32_t)((w_end - wbase + 15u) & ~15ull);
   const __amdgpu_buffer_rsrc_t r = tx_srd(wbase, nrec);
   const uint32_t pa = sz ? (uint32_t)(g.pay + s * g.mss - wbase) : 0u;  // the segment's first byte
   const uint32_t pe = pa + sz;
-  const uint32_t cl = (pa & ~127u) + 16u * li;  // lane li's chunk of line 0
+  const uint32_t cl = (pa & ~(U - 1u)) + 16u * li;  // lane li's chunk of line (unit) 0
   // lines k >= 1 start past pa: the lane's chunk there holds segment bytes
   // iff it starts before pe (k <= klast)
-  const uint32_t klast = sz && pe > cl ? (pe - 1u - cl) >> 7 : 0u;
-  const uint32_t cl1 = sz && pe > cl + 128u ? cl : nrec;
+  const uint32_t klast = sz && pe > cl ? (pe - 1u - cl) >> US : 0u;
+  const uint32_t cl1 = sz && pe > cl + U ? cl : nrec;
   const bool in0 = sz && cl + 16u > pa && cl < pe;
   // the chunk holding the last byte, re-read by the lane that loads it
   const uint32_t tc = (pe - 1u) & ~15u;
-  const bool owner = sz && ((tc >> 4) & 7u) == li;
+  const bool owner = sz && ((tc >> 4) & (G - 1u)) == li;
   uint4 v[NB];
   v[0] = tx_load<A0>(r, in0 ? cl : nrec);
   const uint4 t = tx_load<0>(r, owner ? tc : nrec);
 #pragma unroll
-  for (int k = 1; k < NB; ++k) v[k] = tx_load<2>(r, ((uint32_t)k <= klast ? cl1 : nrec) + 128u * k);
+  for (int k = 1; k < NB; ++k) v[k] = tx_load<2>(r, ((uint32_t)k <= klast ? cl1 : nrec) + U * k);
   uint32_t w = tx_bytes_from(v[0], pa > cl ? (int)(pa - cl) : 0);
 #pragma unroll
   for (int k = 1; k < NB; ++k) w = wsum4(v[k], w);
   // segments longer than NB lines: the rest in batches of 4 lines
   for (uint32_t k0 = NB; __builtin_amdgcn_ballot_w64(k0 <= klast) != 0; k0 += 4) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) w = wsum4(tx_load<2>(r, ((k0 + k) <= klast ? cl1 : nrec) + 128u * (k0 + k)), w);
+    for (int k = 0; k < 4; ++k) w = wsum4(tx_load<2>(r, ((k0 + k) <= klast ? cl1 : nrec) + U * (k0 + k)), w);
   }
   // the bytes [pe, tc + 16) were summed whole with the last chunk (none when
   // pe ends a chunk); the first chunk's bytes below pa were masked, so if it
@@ -682,7 +687,7 @@ __global__ __launch_bounds__(256) void tcp_tx_pay(TxGeo g) {
   if (owner) w -= tx_bytes_from(t, (int)(pe - tc));
   w += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)w, 0xB1, 0xF, 0xF, false);   // quad_perm 1,0,3,2
   w += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)w, 0x4E, 0xF, 0xF, false);   // quad_perm 2,3,0,1
-  w += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)w, 0x141, 0xF, 0xF, false);  // row_half_mirror
+  if constexpr (G == 8) w += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)w, 0x141, 0xF, 0xF, false);  // row_half_mirror
   if (li == 0 && s < g.n) g.xs[s * g.xstride] = (uint16_t)tx_class(w, (uint32_t)((g.pay + s * g.mss) & 1u));
 }
 
@@ -692,10 +697,11 @@ static int tx_pay_lines(uint32_t mss) {
   return lines <= 2 ? 2 : lines <= 4 ? 4 : lines <= 8 ? 8 : lines <= 13 ? 13 : 16;
 }
 
-template <int NB, int A0>
+template <int NB, int A0, int G = 8>
 static hipError_t launch_tx_pay_t(const TxGeo& g, hipStream_t stream) {
-  const uint64_t wgs = (g.n + 31) / 32;  // 4 waves x 8 segments
-  hipLaunchKernelGGL((tcp_tx_pay<NB, A0>), dim3((uint32_t)wgs), dim3(256), 0, stream, g);
+  const uint64_t per = 4u * (64u / G);  // 4 waves x 8 (16) segments
+  const uint64_t wgs = (g.n + per - 1) / per;
+  hipLaunchKernelGGL((tcp_tx_pay<NB, A0, G>), dim3((uint32_t)wgs), dim3(256), 0, stream, g);
   return hipGetLastError();
 }
 

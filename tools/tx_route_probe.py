@@ -14,7 +14,8 @@ runs the IPv6 route at this size class).
   python tools/tx_route_probe.py [--rounds 5] [--reps 20] [--check 4096]
                                   [--mss 64,256,536,1460,8960]
 --mss: the IPv4 route at those segment sizes instead, ~1.5 GB of payload per
-call (n = 1.5 GB / MSS, at most 16M segments).
+call (n = 1.5 GB / MSS, at most 16M segments).  --split: also time the two
+passes one by one (tools/tx_variants.hip 28 and 92 through libns_txv.so).
 """
 from __future__ import annotations
 
@@ -58,6 +59,8 @@ def main():
     ap.add_argument("--n", type=int, default=1 << 20)
     ap.add_argument("--check", type=int, default=4096)
     ap.add_argument("--mss", default="")
+    ap.add_argument("--split", action="store_true")
+    ap.add_argument("--pay-variant", type=int, default=28, help="--split: the payload pass variant (93: 4-lane)")
     args = ap.parse_args()
     n = args.n
     dev = torch.device("cuda", 0)
@@ -92,9 +95,50 @@ def main():
             torch.cuda.synchronize()
             times.append(e0.elapsed_time(e1) * 1e3 / args.reps)
         us = float(np.median(times))
+        split = None
+        if args.split:
+            import ctypes
+
+            sys.path.insert(0, os.path.join(ROOT, "tools"))
+            from tx_drain_probe import TxGeo
+            from netstack_amd.engine import addr_sum
+
+            txv = ctypes.CDLL(os.path.join(ROOT, "netstack_amd", "lib", "libns_txv.so"))
+            txv.txv_launch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+            xs = torch.zeros(n, dtype=torch.int16, device=dev)
+
+            def tg(a):
+                return TxGeo(hdr=a.data_ptr() + geo["hdr_off"], pay=a.data_ptr() + geo["pay_off"], size=geo["size"],
+                             n=n, mss=geo["mss"], slot=geo["slot"], ip_at=geo["ip_at"], ip_len=geo["ip_len"],
+                             tcp_at=geo["tcp_at"], tcp_len=geo["tcp_len"],
+                             addr_sum=addr_sum(geo["src"], geo["dst"]), proto=6, mode=3 if geo["ip_len"] else 2,
+                             xs=xs.data_ptr(), xstride=1)
+
+            tgs = [tg(b) for b in batches]
+            pt, ht = [], []
+            for i in range(4 + args.reps):
+                e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+                e[0].record(stream)
+                assert txv.txv_launch(ctypes.byref(tgs[i % 2]), stream.cuda_stream, args.pay_variant) == 0
+                e[1].record(stream)
+                assert txv.txv_launch(ctypes.byref(tgs[i % 2]), stream.cuda_stream, 92) == 0
+                e[2].record(stream)
+                torch.cuda.synchronize()
+                if i >= 4:
+                    pt.append(e[0].elapsed_time(e[1]) * 1e3)
+                    ht.append(e[1].elapsed_time(e[2]) * 1e3)
+            # the split fill must equal the product's (batch 0, refilled by both)
+            ref = batches[0].clone()
+            eng.tcp_tx(ref, geo)
+            assert txv.txv_launch(ctypes.byref(tgs[0]), stream.cuda_stream, args.pay_variant) == 0
+            assert txv.txv_launch(ctypes.byref(tgs[0]), stream.cuda_stream, 92) == 0
+            torch.cuda.synchronize()
+            split = {"payload_variant": args.pay_variant, "payload_pass_us": round(float(np.median(pt)), 2),
+                     "header_pass_us": round(float(np.median(ht)), 2), "same_fill": bool(torch.equal(ref, batches[0]))}
+            del ref
         per = geo["mss"] + (geo["ip_len"] or 0) + geo["tcp_len"] + (4 if geo["ip_len"] else 2)
         key = f"{route}_mss{geo['mss']}"
-        res[key] = {"segments": n, "us": round(us, 2), "min_us": round(min(times), 2), "algo_bytes_per_segment": per,
+        res[key] = {"segments": n, "us": round(us, 2), "split": split, "min_us": round(min(times), 2), "algo_bytes_per_segment": per,
                       "frac_of_8TBs": round(n * per / us / 1e3 / 8000, 4), "first_segments_bit_exact": ok}
         print(json.dumps({key: res[key]}), flush=True)
         del batches

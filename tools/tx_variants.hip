@@ -16,7 +16,8 @@
 //   copied onto themselves (read + write), read only, written only (16-B
 //   lane accesses, 4 per lane, one-shot grid); 22-24 / 25-27 = written only /
 //   copied with store cache policy 1 / 2 / 3; 28 / 29 = the payload pass
-//   alone, in 8-lane groups (product) / windowed (round 4); 30 / 31 / 32 =
+//   alone, in 8-lane groups (product) / windowed (round 4); 93 = the payload
+//   pass alone in 4-lane groups (16 segments per wave); 30 / 31 / 32 =
 //   both passes with the group payload pass all nontemporal / with
 //   nontemporal header stores / both; 33 = the all-nontemporal group
 //   payload pass alone; 34 / 35 = both passes, windowed / group payload
@@ -270,6 +271,12 @@ extern "C" int txv_launch(const nsk::TxGeo* g, void* stream, int k) {
     case 26: e = launch_floor<0, 2>(*g, s); break;
     case 27: e = launch_floor<0, 3>(*g, s); break;
     case 28: e = nsk::launch_payload_pass<16, 2, 0, 1, 1>(*g, s); break;
+    case 93: {  // the payload pass in 4-lane groups (16 segments per wave, 64-B units)
+      const uint32_t u = (g->mss + 63u + 63u) / 64u;
+      e = u <= 2 ? nsk::launch_tx_pay_t<2, 0, 4>(*g, s) : u <= 4 ? nsk::launch_tx_pay_t<4, 0, 4>(*g, s)
+        : u <= 8 ? nsk::launch_tx_pay_t<8, 0, 4>(*g, s) : nsk::launch_tx_pay_t<16, 0, 4>(*g, s);
+      break;
+    }
     case 29: e = nsk::launch_payload_pass<16, 2, 0, 1, 0>(*g, s); break;
     case 30: e = nsk::launch_passes<16, 2, 0, 1, 1, 2>(*g, s); break;
     case 31: e = nsk::launch_passes<16, 2, 1, 1, 1, 1>(*g, s); break;
