@@ -335,50 +335,24 @@ def rx_ring_batch(n: int, seed: int, device, corrupt_every: int = 0):
 def rx_ring_batch_v6(n: int, seed: int, device, corrupt_every: int = 0):
     """rx_ring_batch over IPv6: n 1500-B IPv6/TCP packets (a 40-B header,
     PayloadLength 1460, NextHeader 6, random addresses) with valid TCP
-    checksums (the pseudo-header of ipv6: src, dst, length, protocol), one
-    per RX_STRIDE slot; with corrupt_every = k > 0 one payload byte of every
-    k-th packet is flipped.  Returns (arena, lens, bad indices)."""
-    import torch
-
-    arena = random_bytes_torch(seed, n * RX_STRIDE, device)
-    p = arena.view(n, RX_STRIDE)[:, :RX_PKT]
-    tl = RX_PKT - 40
-    p[:, 0] = 0x60
-    p[:, 1:4] = 0
-    p[:, 4] = tl >> 8
-    p[:, 5] = tl & 0xFF
-    p[:, 6] = 6
-    p[:, 7] = 64
-    p[:, 52] = 0x50  # data offset 5 words
-    p[:, 53] = 0x18  # PSH | ACK
-    p[:, 56:60] = 0  # checksum, urgent pointer
-
-    def be_sum(lo, hi):
-        w = p[:, lo:hi].to(torch.int64)
-        return (w[:, 0::2] * 256 + w[:, 1::2]).sum(dim=1)
-
-    tcp = (~_fold_np(_fold_np(be_sum(40, RX_PKT) + be_sum(8, 40) + tl + 6))) & 0xFFFF
-    p[:, 56] = (tcp >> 8).to(torch.uint8)
-    p[:, 57] = (tcp & 0xFF).to(torch.uint8)
-    bad = np.arange(0, n, corrupt_every, dtype=np.int64) if corrupt_every > 0 else np.zeros(0, np.int64)
-    if bad.size:
-        idx = torch.from_numpy(bad).to(device)
-        p[idx, 100] ^= 0x5A
-    lens = torch.full((n,), RX_PKT, dtype=torch.int32, device=device)
+    checksums, one per RX_STRIDE slot; with corrupt_every = k > 0 one payload
+    byte of every k-th packet is flipped.  Returns (arena, lens, bad)."""
+    arena, lens, bad, _ = rx_ring_batch_sized(n, RX_PKT, seed, device, v6=True, corrupt_every=corrupt_every,
+                                              stride=RX_STRIDE)
     return arena, lens, bad
 
 
 def rx_ring_batch_sized(n: int, frame: int, seed: int, device, v6: bool = False, corrupt_every: int = 0,
-                        eth: bool = False):
+                        eth: bool = False, stride: int = 0):
     """rx_ring_batch / rx_ring_batch_v6 at any frame length (IPv4 or IPv6
     TCP packets of `frame` bytes, e.g. 9000-B jumbo frames), one per slot of
-    stride round_up(frame [+ 14], 16) + 16; eth: each packet behind a 14-B
-    Ethernet header (EtherType 0x0800 / 0x86DD; ring link_hdr 14, lengths
-    frame + 14).  Returns (arena, lens, bad, stride)."""
+    `stride` bytes (0: round_up(frame [+ 14], 16) + 16); eth: each packet
+    behind a 14-B Ethernet header (EtherType 0x0800 / 0x86DD; ring link_hdr
+    14, lengths frame + 14).  Returns (arena, lens, bad, stride)."""
     import torch
 
     lh = 14 if eth else 0
-    stride = (frame + lh + 15) // 16 * 16 + 16
+    stride = stride or (frame + lh + 15) // 16 * 16 + 16
     arena = random_bytes_torch(seed, n * stride, device)
     if eth:
         e = arena.view(n, stride)[:, :14]
